@@ -1,0 +1,130 @@
+/*
+ * mfgp.h — C ABI of the MI355X-native multi-fidelity GP engine (libmfgp.so).
+ *
+ * This is the drop-in boundary below the Python mirror of the reference's
+ * GPflow-facing API.  The reference (qezlou/multi_fidelity_gpflow) is pure
+ * Python and has no FFI of its own; each entry point below names the reference
+ * interface whose arithmetic it replaces.  The Python side binds it with ctypes
+ * (multi_fidelity_gpflow_amd/_lib.py).
+ *
+ * Conventions
+ *   - Every array argument is a caller-owned DEVICE pointer (fp64, row-major,
+ *     leading dimensions in elements).  The library never allocates or frees in
+ *     a compute call; scratch comes from a caller-provided workspace whose size
+ *     is queried with the matching *_workspace_size function.
+ *   - theta (device, fp64, constrained values) has the layout
+ *         [vL, lL[0..d-1], vD, lD[0..d-1], rho0, noise]      (2d + 4 entries)
+ *     i.e. kernel_L (variance, lengthscales), kernel_delta (variance,
+ *     lengthscales), rho[0,0] and the Gaussian likelihood variance.
+ *   - X rows hold d input columns followed by the fidelity flag (0.0 / 1.0);
+ *     rows whose flag is neither exactly 0 nor 1 produce zero kernel rows
+ *     (mfgpflow/linear.py:67-70).
+ *   - Calls are asynchronous and ordered on the handle's stream (default: the
+ *     null stream); none synchronises, so they can be captured in a hipGraph.
+ *   - Return value: 0 = ok, < 0 = bad argument / launch error (see
+ *     mfgp_error_string).  A Cholesky that meets a non-positive pivot writes a
+ *     LAPACK-style info > 0 (1-based row) into the caller's device int; the
+ *     Python layer raises the analogue of TF's InvalidArgumentError.
+ *   - Threading: a handle must not be used by two host threads at once.
+ */
+#ifndef MFGP_H_
+#define MFGP_H_
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mfgp_handle_s* mfgp_handle_t;
+
+#define MFGP_OK 0
+#define MFGP_ERR_ARG (-1)
+#define MFGP_ERR_WORKSPACE (-2)
+#define MFGP_ERR_LAUNCH (-3)
+#define MFGP_ERR_DIM (-4)
+#define MFGP_MAX_D 32
+
+int mfgp_version(void);
+const char* mfgp_error_string(int code);
+
+/* Handle: device + stream + tile size (32 or 64).  No reference analogue
+ * (TensorFlow's implicit device context). */
+int mfgp_create(int device, mfgp_handle_t* out);
+int mfgp_destroy(mfgp_handle_t h);
+int mfgp_set_stream(mfgp_handle_t h, void* hip_stream);
+int mfgp_set_tile(mfgp_handle_t h, int nb);
+int mfgp_get_tile(mfgp_handle_t h);
+
+/* gpflow.kernels.SquaredExponential.K(X1, X2) (GPflow 2.9 stationaries.py via
+ * utilities/ops.py:square_distance).  params = [variance, lengthscales[d]]. */
+int mfgp_rbf_gram(mfgp_handle_t h, int n1, int n2, int d, const double* X1, int ldx1, const double* X2, int ldx2,
+                  const double* params, double* K, int ldk);
+
+/* LinearMultiFidelityKernel.K(X, X2) — mfgpflow/linear.py:55-104.
+ * diag_add is added to K[i][i] (use only for X2 == X). */
+int mfgp_mf_gram(mfgp_handle_t h, int n1, int n2, int d, const double* X1, int ldx1, const double* X2, int ldx2,
+                 const double* theta, double diag_add, double* K, int ldk);
+
+/* LinearMultiFidelityKernel.K_diag(X) — mfgpflow/linear.py:106-136. */
+int mfgp_mf_kdiag(mfgp_handle_t h, int n, int d, const double* X, int ldx, const double* theta, double* out);
+
+/* GPR.log_marginal_likelihood() of MultiFidelityGPModel (mfgpflow/linear.py:138-156;
+ * GPflow models/gpr.py) and, with want_grad, its gradient w.r.t. theta (the
+ * GradientTape of linear.py:205-207).  out[0] = LML, out[1 + q] = dLML/dtheta[q].
+ * Y is [n, p]: all p columns share the one Gram / Cholesky (linear.py:90). */
+int mfgp_gpr_workspace_size(mfgp_handle_t h, int n, int p, int d, size_t* bytes);
+int mfgp_gpr_lml(mfgp_handle_t h, int n, int p, int d, const double* X, int ldx, const double* Y, int ldy,
+                 const double* theta, int want_grad, void* ws, size_t ws_bytes, double* out, int* info);
+
+/* One iteration of MultiFidelityGPModel.optimize(use_adam=True) (linear.py:200-214):
+ * value+grad at theta, loss_hist[*step] = -LML, Keras-Adam update of the
+ * unconstrained vector u for entries with trainable[q] != 0 (entries with equal
+ * tie[q] share one variable and its summed gradient; tie may be NULL), theta refreshed
+ * (Softplus; Shift(1e-6)+Softplus for the noise entry), ++*step.  lr / beta1 /
+ * beta2 are passed already rounded as the caller wants them (TF 2.10 keeps them
+ * as float32 hyper variables). */
+int mfgp_gpr_adam_step(mfgp_handle_t h, int n, int p, int d, const double* X, int ldx, const double* Y, int ldy,
+                       double* theta, double* u, double* m, double* v, const unsigned char* trainable,
+                       const int* tie, int* step, double lr, double beta1, double beta2, double eps,
+                       double* loss_hist, void* ws, size_t ws_bytes, double* out, int* info);
+
+/* theta[q] = softplus(u[q]) (+1e-6 for q == noise_index); GPflow positive(). */
+int mfgp_theta_from_u(mfgp_handle_t h, const double* u, double* theta, int g, int noise_index);
+
+/* GPR.predict_f(Xnew, full_cov=False) (GPflow models/gpr.py -> base_conditional;
+ * mirror at mfgpflow/linear.py:237-286).  mean [nstar, p]; var [nstar] (the
+ * reference tiles it over the p outputs). */
+int mfgp_gpr_predict_workspace_size(mfgp_handle_t h, int n, int p, int d, int nstar, size_t* bytes);
+int mfgp_gpr_predict(mfgp_handle_t h, int n, int p, int d, int nstar, const double* X, int ldx, const double* Y,
+                     int ldy, const double* Xs, int ldxs, const double* theta, void* ws, size_t ws_bytes,
+                     double* mean, int ldm, double* var, int* info);
+
+/* Batched Cholesky factor inverse of SPD matrices (tf.linalg.cholesky +
+ * triangular_solve(L, I) as used by GPflow's conditionals): Linv = chol(A)^{-1},
+ * ldiag = diag(chol(A)).  A, Linv: [batch][n][n] with strides sA / sL elements. */
+int mfgp_potrf_inv_workspace_size(mfgp_handle_t h, int n, int batch, size_t* bytes);
+int mfgp_potrf_inv(mfgp_handle_t h, int n, int batch, const double* A, int lda, long sA, void* ws, size_t ws_bytes,
+                   double* Linv, int ldl, long sL, double* ldiag, int* info);
+
+/* SVGP ELBO value (GPflow SVGP.elbo, whiten=True, Gaussian likelihood) for the
+ * latent LinearCoregionalization model (mfgpflow/linear_svgp.py:64-203) and the
+ * SingleBinSVGP (SeparateIndependent, mfgpflow/singlebin_svgp.py:13-97, W = I):
+ *   thetas [L][2d+4] per-latent constrained kernel parameters (noise entry unused),
+ *   Z [M, d+1], q_mu [M, L], q_sqrt [L, M, M] (lower used), W [P, L] or NULL
+ *   (identity mixing; requires L == P).  out = [elbo, KL, VE]; g_mu / g_var
+ *   [L][N] receive the latent predictive moments. */
+int mfgp_svgp_workspace_size(mfgp_handle_t h, int n, int m, int l, int p, int d, size_t* bytes);
+int mfgp_svgp_elbo(mfgp_handle_t h, int n, int m, int l, int p, int d, const double* X, int ldx, const double* Y,
+                   int ldy, const double* Z, int ldz, const double* thetas, const double* q_mu,
+                   const double* q_sqrt, const double* W, double noise, double scale, double jitter, void* ws,
+                   size_t ws_bytes, double* out, double* g_mu, double* g_var, int* info);
+
+/* Diagnostic: one v_mfma_f64_16x16x4_f64 with A[i][k] = 4i+k+1, B[k][j] = 100k+j;
+ * writes C (16x16 row-major, device). */
+int mfgp_selftest_mfma(mfgp_handle_t h, double* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MFGP_H_ */

@@ -1,0 +1,101 @@
+"""ctypes binding of libmfgp.so — the C-ABI declared in include/mfgp.h.
+
+The shared library is built in-tree (``multi_fidelity_gpflow_amd/libmfgp.so``)
+by :func:`multi_fidelity_gpflow_amd.build.build_lib`.  There is no CPU
+fallback: if the library or a GPU is missing, every compute entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmfgp.so")
+
+_p = C.c_void_p
+_i = C.c_int
+_l = C.c_long
+_d = C.c_double
+_sz = C.c_size_t
+
+# name -> argtypes (restype is int everywhere except noted)
+SIGNATURES = {
+    "mfgp_version": [],
+    "mfgp_error_string": [_i],
+    "mfgp_create": [_i, C.POINTER(_p)],
+    "mfgp_destroy": [_p],
+    "mfgp_set_stream": [_p, _p],
+    "mfgp_set_tile": [_p, _i],
+    "mfgp_get_tile": [_p],
+    "mfgp_rbf_gram": [_p, _i, _i, _i, _p, _i, _p, _i, _p, _p, _i],
+    "mfgp_mf_gram": [_p, _i, _i, _i, _p, _i, _p, _i, _p, _d, _p, _i],
+    "mfgp_mf_kdiag": [_p, _i, _i, _p, _i, _p, _p],
+    "mfgp_gpr_workspace_size": [_p, _i, _i, _i, C.POINTER(_sz)],
+    "mfgp_gpr_lml": [_p, _i, _i, _i, _p, _i, _p, _i, _p, _i, _p, _sz, _p, _p],
+    "mfgp_gpr_adam_step": [_p, _i, _i, _i, _p, _i, _p, _i, _p, _p, _p, _p, _p, _p, _p, _d, _d, _d, _d, _p, _p,
+                           _sz, _p, _p],
+    "mfgp_theta_from_u": [_p, _p, _p, _i, _i],
+    "mfgp_gpr_predict_workspace_size": [_p, _i, _i, _i, _i, C.POINTER(_sz)],
+    "mfgp_gpr_predict": [_p, _i, _i, _i, _i, _p, _i, _p, _i, _p, _i, _p, _p, _sz, _p, _i, _p, _p],
+    "mfgp_potrf_inv_workspace_size": [_p, _i, _i, C.POINTER(_sz)],
+    "mfgp_potrf_inv": [_p, _i, _i, _p, _i, _l, _p, _sz, _p, _i, _l, _p, _p],
+    "mfgp_svgp_workspace_size": [_p, _i, _i, _i, _i, _i, C.POINTER(_sz)],
+    "mfgp_svgp_elbo": [_p, _i, _i, _i, _i, _i, _p, _i, _p, _i, _p, _i, _p, _p, _p, _p, _d, _d, _d, _p, _sz, _p,
+                       _p, _p, _p],
+    "mfgp_selftest_mfma": [_p, _p],
+}
+
+_lib = None
+_lock = threading.Lock()
+_handles = {}
+
+
+class MFGPError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    """Load libmfgp.so (no compute; safe without a GPU)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(path):
+                raise MFGPError(
+                    f"libmfgp.so not found at {path}: build it with "
+                    "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950)")
+            lib = C.CDLL(path)
+            for name, args in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.argtypes = args
+                fn.restype = C.c_char_p if name == "mfgp_error_string" else C.c_int
+            _lib = lib
+    return _lib
+
+
+def check(code: int, what: str):
+    if code != 0:
+        msg = load().mfgp_error_string(code).decode()
+        raise MFGPError(f"{what} failed: {msg} ({code})")
+
+
+def handle(device_index: int):
+    """Per-(thread, device) library handle bound to torch's current stream."""
+    import torch
+
+    lib = load()
+    key = (threading.get_ident(), device_index)
+    h = _handles.get(key)
+    if h is None:
+        hp = _p()
+        check(lib.mfgp_create(device_index, C.byref(hp)), "mfgp_create")
+        h = hp
+        _handles[key] = h
+    stream = torch.cuda.current_stream(device_index).cuda_stream
+    check(lib.mfgp_set_stream(h, _p(stream)), "mfgp_set_stream")
+    return h
+
+
+def ptr(t) -> int:
+    """Device address of a torch tensor (None -> NULL)."""
+    return None if t is None else t.data_ptr()

@@ -1,0 +1,482 @@
+// C-ABI entry points of libmfgp.so (declared in include/mfgp.h).
+//
+// Host-side orchestration only: workspace carving, argument blocks, kernel
+// launch sequences on the handle's stream.  No allocation, no synchronisation
+// (every sequence is hipGraph-capturable).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/mfgp.h"
+#include "mfgp_device.h"
+#include "mfgp_internal.h"
+
+struct mfgp_handle_s {
+    int device;
+    hipStream_t stream;
+    int nb;
+};
+
+namespace mfgp {
+
+static inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
+
+struct Carve {
+    char* base;
+    size_t off = 0;
+    explicit Carve(void* b) : base((char*)b) {}
+    template <class T>
+    T* take(size_t count) {
+        off = (off + 255) & ~(size_t)255;
+        T* p = base ? reinterpret_cast<T*>(base + off) : nullptr;
+        off += count * sizeof(T);
+        return p;
+    }
+};
+
+struct GprLayout {
+    int nb, npad, T, ppad, Tp, G, gstride, ng;
+    double *A, *R, *Xo, *Dd, *ldiag, *alpha, *zpart, *gpart;
+    size_t bytes;
+};
+
+static GprLayout gpr_layout(int nb, int n, int p, int d, void* ws) {
+    GprLayout L;
+    L.nb = nb;
+    L.T = ceil_div(n, nb);
+    L.npad = L.T * nb;
+    L.Tp = ceil_div(p > 0 ? p : 1, nb);
+    L.ppad = L.Tp * nb;
+    L.G = theta_size(d);
+    L.gstride = (L.G + 3) & ~3;
+    L.ng = grad_tasks(L.T);
+    Carve c(ws);
+    const size_t ldr = (size_t)L.npad + L.ppad;
+    L.A = c.take<double>((size_t)L.npad * L.npad);
+    L.R = c.take<double>((size_t)L.npad * ldr);
+    L.Xo = c.take<double>((size_t)L.npad * ldr);
+    L.Dd = c.take<double>((size_t)L.T * nb * nb);
+    L.ldiag = c.take<double>(L.npad);
+    L.alpha = c.take<double>((size_t)L.npad * L.ppad);
+    L.zpart = c.take<double>((size_t)L.T * L.Tp);
+    L.gpart = c.take<double>((size_t)L.ng * L.gstride);
+    L.bytes = c.off + 256;
+    return L;
+}
+
+static inline hipError_t last() { return hipGetLastError(); }
+
+template <int NB>
+static void gram_lml_and_factor(hipStream_t s, const GprLayout& L, int n, int p, int d, const double* X, int ldx,
+                                const double* Y, int ldy, const double* theta, int* info) {
+    const long ldr = L.npad + L.ppad;
+    {
+        const long total = (long)L.npad * ldr;
+        const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
+        hipLaunchKernelGGL(k_rhs_init, dim3(blocks), dim3(256), 0, s, L.R, ldr, 0L, L.npad, L.ppad, Y, (long)ldy,
+                           0L, n, p);
+    }
+    GramArgs g{};
+    g.X1 = X; g.ldx1 = ldx; g.sx1 = 0; g.n1 = n;
+    g.X2 = X; g.ldx2 = ldx; g.sx2 = 0; g.n2 = n;
+    g.theta = theta; g.stheta = 0; g.D = d; g.rbf_only = 0;
+    g.out = L.A; g.ldo = L.npad; g.so = 0;
+    g.padded = 1; g.npad = L.npad; g.tiles_c = L.T; g.add_noise = 1; g.diag_add = 0.0;
+    g.Dd = L.Dd; g.sD = 0; g.ldiag = L.ldiag; g.sL = 0; g.info = info;
+    launch_gram<NB>(g, L.T * (L.T + 1) / 2, 1, s);
+    CholArgs c{};
+    c.A = L.A; c.lda = L.npad; c.sA = 0;
+    c.R = L.R; c.ldr = ldr; c.sR = 0;
+    c.Xo = L.Xo; c.ldx = ldr; c.sX = 0;
+    c.Dd = L.Dd; c.sD = 0; c.ldiag = L.ldiag; c.sL = 0; c.info = info;
+    c.T = L.T; c.Tp = L.Tp; c.k = 0;
+    launch_chol_steps<NB>(c, 1, s);
+}
+
+template <int NB>
+static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X, int ldx, const double* Y, int ldy,
+                          double* theta, int want_grad, void* ws, size_t ws_bytes, double* out, int* info,
+                          const FinArgs* adam) {
+    const GprLayout L = gpr_layout(NB, n, p, d, ws);
+    if (ws_bytes < L.bytes) return MFGP_ERR_WORKSPACE;
+    hipStream_t s = h->stream;
+    (void)hipMemsetAsync(info, 0, sizeof(int), s);
+    gram_lml_and_factor<NB>(s, L, n, p, d, X, ldx, Y, ldy, theta, info);
+    const long ldr = L.npad + L.ppad;
+    AlphaArgs aa{L.Xo, ldr, L.alpha, (long)L.ppad, L.zpart, L.T, L.Tp, n, p};
+    launch_alpha<NB>(aa, s);
+    if (want_grad) {
+        GradArgs ga{L.Xo, ldr, L.alpha, (long)L.ppad, X, (long)ldx, theta, L.gpart, L.gstride, L.T, L.Tp, n, p, d};
+        launch_grad<NB>(ga, s);
+    }
+    FinArgs f{};
+    if (adam) f = *adam;
+    f.zpart = L.zpart; f.nz = L.T * L.Tp;
+    f.ldiag = L.ldiag; f.n = n;
+    f.gpart = L.gpart; f.ng = L.ng; f.gstride = L.gstride;
+    f.info = info; f.P = p; f.D = d; f.want_grad = want_grad;
+    f.out = out;
+    f.adam = adam != nullptr;
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(NTHREADS), 0, s, f);
+    return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;
+}
+
+// ---------------------------------------------------------------- potrf_inv
+template <int NB>
+__global__ void k_pad_copy(const double* A, long lda, long sA, double* Ap, int n, int npad) {
+    const int b = blockIdx.z;
+    const long total = (long)npad * npad;
+    for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const int r = (int)(e / npad), c = (int)(e % npad);
+        double v = (r == c) ? 1.0 : 0.0;
+        if (r < n && c < n) v = A[b * sA + (long)r * lda + c];
+        Ap[b * total + e] = v;
+    }
+}
+
+template <int NB>
+__global__ __launch_bounds__(NTHREADS) void k_factor_first(double* Ap, int npad, double* Dd, long sD, double* ldiag,
+                                                           int* info) {
+    constexpr int E = TileCfg<NB>::ELEMS;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    double* T0 = smem;
+    double* R0 = T0 + E;
+    double* dg = R0 + E;
+    __shared__ int bad;
+    const int b = blockIdx.z;
+    tile_load<NB>(T0, Ap + (long)b * npad * npad, npad);
+    __syncthreads();
+    tile_potrf_inv<NB>(T0, R0, dg, &bad);
+    tile_store<NB>(Dd + b * sD, NB, R0);
+    for (int r = threadIdx.x; r < NB; r += NTHREADS) ldiag[(long)b * npad + r] = dg[r];
+    if (threadIdx.x == 0 && bad && info[b] == 0) info[b] = bad;
+}
+
+__global__ void k_copy_lower_out(const double* Xo, long ldx, long sX, double* Linv, long ldl, long sL, int n) {
+    const int b = blockIdx.z;
+    const long total = (long)n * n;
+    for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const int r = (int)(e / n), c = (int)(e % n);
+        Linv[b * sL + (long)r * ldl + c] = (c <= r) ? Xo[b * sX + (long)r * ldx + c] : 0.0;
+    }
+}
+
+__global__ void k_copy_vec(const double* src, long ss, double* dst, long sd, int n) {
+    const int b = blockIdx.z;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        dst[b * sd + i] = src[b * ss + i];
+}
+
+struct PotrfLayout {
+    int npad, T;
+    double *A, *R, *Xo, *Dd, *ldiag;
+    size_t bytes;
+};
+
+static PotrfLayout potrf_layout(int nb, int n, int batch, void* ws) {
+    PotrfLayout L;
+    L.T = ceil_div(n, nb);
+    L.npad = L.T * nb;
+    const size_t mat = (size_t)L.npad * L.npad;
+    Carve c(ws);
+    L.A = c.take<double>(mat * batch);
+    L.R = c.take<double>(mat * batch);
+    L.Xo = c.take<double>(mat * batch);
+    L.Dd = c.take<double>((size_t)L.T * nb * nb * batch);
+    L.ldiag = c.take<double>((size_t)L.npad * batch);
+    L.bytes = c.off + 256;
+    return L;
+}
+
+template <int NB>
+static int potrf_inv_impl(mfgp_handle_t h, int n, int batch, const double* A, int lda, long sA, void* ws,
+                          size_t ws_bytes, double* Linv, int ldl, long sLo, double* ldiag, int* info) {
+    const PotrfLayout L = potrf_layout(NB, n, batch, ws);
+    if (ws_bytes < L.bytes) return MFGP_ERR_WORKSPACE;
+    hipStream_t s = h->stream;
+    const long mat = (long)L.npad * L.npad;
+    const int blocks = (int)std::min<long>((mat + 255) / 256, 2048);
+    (void)hipMemsetAsync(info, 0, sizeof(int) * batch, s);
+    hipLaunchKernelGGL(k_pad_copy<NB>, dim3(blocks, 1, batch), dim3(256), 0, s, A, (long)lda, sA, L.A, n, L.npad);
+    hipLaunchKernelGGL(k_rhs_init, dim3(blocks, 1, batch), dim3(256), 0, s, L.R, (long)L.npad, mat, L.npad, 0,
+                       (const double*)nullptr, 0L, 0L, n, 0);
+    hipLaunchKernelGGL(k_factor_first<NB>, dim3(1, 1, batch), dim3(NTHREADS),
+                       sizeof(double) * (2 * NB * (NB + 2) + NB), s, L.A, L.npad, L.Dd, (long)L.T * NB * NB,
+                       L.ldiag, info);
+    CholArgs c{};
+    c.A = L.A; c.lda = L.npad; c.sA = mat;
+    c.R = L.R; c.ldr = L.npad; c.sR = mat;
+    c.Xo = L.Xo; c.ldx = L.npad; c.sX = mat;
+    c.Dd = L.Dd; c.sD = (long)L.T * NB * NB; c.ldiag = L.ldiag; c.sL = L.npad; c.info = info;
+    c.T = L.T; c.Tp = 0; c.k = 0;
+    launch_chol_steps<NB>(c, batch, s);
+    const long tot = (long)n * n;
+    const int b2 = (int)std::min<long>((tot + 255) / 256, 2048);
+    hipLaunchKernelGGL(k_copy_lower_out, dim3(b2, 1, batch), dim3(256), 0, s, L.Xo, (long)L.npad, mat, Linv,
+                       (long)ldl, sLo, n);
+    if (ldiag)
+        hipLaunchKernelGGL(k_copy_vec, dim3(ceil_div(n, 256), 1, batch), dim3(256), 0, s, L.ldiag, (long)L.npad,
+                           ldiag, (long)n, n);
+    return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;
+}
+
+// ---------------------------------------------------------------- predict
+struct PredLayout {
+    GprLayout g;
+    int nspad, Ts;
+    double *Kmn, *Am, *kdiag;
+    size_t bytes;
+};
+
+static PredLayout pred_layout(int nb, int n, int p, int d, int nstar, void* ws) {
+    PredLayout P;
+    P.g = gpr_layout(nb, n, p, d, ws);
+    P.Ts = ceil_div(nstar > 0 ? nstar : 1, nb);
+    P.nspad = P.Ts * nb;
+    Carve c(ws);
+    c.off = P.g.bytes;
+    P.Kmn = c.take<double>((size_t)P.g.npad * P.nspad);
+    P.Am = c.take<double>((size_t)P.g.npad * P.nspad);
+    P.kdiag = c.take<double>(P.nspad);
+    P.bytes = c.off + 256;
+    return P;
+}
+
+template <int NB>
+static int predict_impl(mfgp_handle_t h, int n, int p, int d, int nstar, const double* X, int ldx, const double* Y,
+                        int ldy, const double* Xs, int ldxs, const double* theta, void* ws, size_t ws_bytes,
+                        double* mean, int ldm, double* var, int* info) {
+    const PredLayout P = pred_layout(NB, n, p, d, nstar, ws);
+    if (ws_bytes < P.bytes) return MFGP_ERR_WORKSPACE;
+    hipStream_t s = h->stream;
+    const GprLayout& L = P.g;
+    (void)hipMemsetAsync(info, 0, sizeof(int), s);
+    gram_lml_and_factor<NB>(s, L, n, p, d, X, ldx, Y, ldy, theta, info);
+    (void)hipMemsetAsync(P.Kmn, 0, sizeof(double) * (size_t)L.npad * P.nspad, s);
+    GramArgs g{};
+    g.X1 = X; g.ldx1 = ldx; g.n1 = n;
+    g.X2 = Xs; g.ldx2 = ldxs; g.n2 = nstar;
+    g.theta = theta; g.D = d; g.rbf_only = 0;
+    g.out = P.Kmn; g.ldo = P.nspad; g.padded = 0; g.tiles_c = P.Ts; g.diag_add = 0.0;
+    launch_gram<NB>(g, L.T * P.Ts, 1, s);
+    hipLaunchKernelGGL(k_kdiag, dim3(ceil_div(nstar, 256)), dim3(256), 0, s, Xs, (long)ldxs, nstar, d, theta,
+                       P.kdiag);
+    const long ldr = L.npad + L.ppad;
+    PredAArgs pa{L.Xo, ldr, P.Kmn, (long)P.nspad, P.Am, (long)P.nspad, P.Ts};
+    PredOutArgs po{P.Am, (long)P.nspad, L.Xo, ldr, P.kdiag, mean, (long)ldm, var, L.T, L.Tp, nstar, p};
+    launch_pred<NB>(pa, po, L.T, s);
+    return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;
+}
+
+size_t svgp_workspace_bytes(int nb, int n, int m, int l, int p, int d);
+int svgp_elbo_impl(hipStream_t s, int nb, int n, int m, int l, int p, int d, const double* X, int ldx,
+                   const double* Y, int ldy, const double* Z, int ldz, const double* thetas, const double* q_mu,
+                   const double* q_sqrt, const double* W, double noise, double scale, double jitter, void* ws,
+                   size_t ws_bytes, double* out, double* g_mu, double* g_var, int* info);
+
+}  // namespace mfgp
+
+using namespace mfgp;
+
+#define CHECK_H(h) \
+    if ((h) == nullptr) return MFGP_ERR_ARG
+#define CHECK_D(d) \
+    if ((d) < 1 || (d) > MFGP_MAX_D) return MFGP_ERR_DIM
+
+extern "C" {
+
+int mfgp_version(void) { return 100; }
+
+const char* mfgp_error_string(int code) {
+    switch (code) {
+        case MFGP_OK: return "ok";
+        case MFGP_ERR_ARG: return "invalid argument";
+        case MFGP_ERR_WORKSPACE: return "workspace too small";
+        case MFGP_ERR_LAUNCH: return "kernel launch failed";
+        case MFGP_ERR_DIM: return "unsupported input dimension (1 <= d <= 32)";
+        default: return "unknown error";
+    }
+}
+
+int mfgp_create(int device, mfgp_handle_t* out) {
+    if (!out) return MFGP_ERR_ARG;
+    mfgp_handle_s* h = (mfgp_handle_s*)calloc(1, sizeof(mfgp_handle_s));
+    if (!h) return MFGP_ERR_ARG;
+    h->device = device;
+    h->stream = nullptr;
+    h->nb = 32;
+    const char* env = getenv("MFGP_TILE");
+    if (env && atoi(env) == 64) h->nb = 64;
+    *out = h;
+    return MFGP_OK;
+}
+
+int mfgp_destroy(mfgp_handle_t h) {
+    free(h);
+    return MFGP_OK;
+}
+
+int mfgp_set_stream(mfgp_handle_t h, void* stream) {
+    CHECK_H(h);
+    h->stream = (hipStream_t)stream;
+    return MFGP_OK;
+}
+
+int mfgp_set_tile(mfgp_handle_t h, int nb) {
+    CHECK_H(h);
+    if (nb != 32 && nb != 64) return MFGP_ERR_ARG;
+    h->nb = nb;
+    return MFGP_OK;
+}
+
+int mfgp_get_tile(mfgp_handle_t h) { return h ? h->nb : MFGP_ERR_ARG; }
+
+static int gram_common(mfgp_handle_t h, int n1, int n2, int d, const double* X1, int ldx1, const double* X2,
+                       int ldx2, const double* params, double diag_add, double* K, int ldk, int rbf) {
+    CHECK_H(h);
+    CHECK_D(d);
+    if (n1 < 0 || n2 < 0 || !X1 || !X2 || !params || !K) return MFGP_ERR_ARG;
+    if (n1 == 0 || n2 == 0) return MFGP_OK;
+    GramArgs g{};
+    g.X1 = X1; g.ldx1 = ldx1; g.n1 = n1;
+    g.X2 = X2; g.ldx2 = ldx2; g.n2 = n2;
+    g.theta = params; g.D = d; g.rbf_only = rbf;
+    g.out = K; g.ldo = ldk; g.padded = 0; g.diag_add = diag_add;
+    const int nb = h->nb;
+    g.tiles_c = ceil_div(n2, nb);
+    const int blocks = ceil_div(n1, nb) * g.tiles_c;
+    if (nb == 64) launch_gram<64>(g, blocks, 1, h->stream);
+    else launch_gram<32>(g, blocks, 1, h->stream);
+    return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;
+}
+
+int mfgp_rbf_gram(mfgp_handle_t h, int n1, int n2, int d, const double* X1, int ldx1, const double* X2, int ldx2,
+                  const double* params, double* K, int ldk) {
+    return gram_common(h, n1, n2, d, X1, ldx1, X2, ldx2, params, 0.0, K, ldk, 1);
+}
+
+int mfgp_mf_gram(mfgp_handle_t h, int n1, int n2, int d, const double* X1, int ldx1, const double* X2, int ldx2,
+                 const double* theta, double diag_add, double* K, int ldk) {
+    return gram_common(h, n1, n2, d, X1, ldx1, X2, ldx2, theta, diag_add, K, ldk, 0);
+}
+
+int mfgp_mf_kdiag(mfgp_handle_t h, int n, int d, const double* X, int ldx, const double* theta, double* out) {
+    CHECK_H(h);
+    CHECK_D(d);
+    if (n < 0 || !X || !theta || !out) return MFGP_ERR_ARG;
+    if (n == 0) return MFGP_OK;
+    hipLaunchKernelGGL(k_kdiag, dim3(ceil_div(n, 256)), dim3(256), 0, h->stream, X, (long)ldx, n, d, theta, out);
+    return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;
+}
+
+int mfgp_gpr_workspace_size(mfgp_handle_t h, int n, int p, int d, size_t* bytes) {
+    CHECK_H(h);
+    CHECK_D(d);
+    if (n < 1 || p < 1 || !bytes) return MFGP_ERR_ARG;
+    *bytes = gpr_layout(h->nb, n, p, d, nullptr).bytes;
+    return MFGP_OK;
+}
+
+int mfgp_gpr_lml(mfgp_handle_t h, int n, int p, int d, const double* X, int ldx, const double* Y, int ldy,
+                 const double* theta, int want_grad, void* ws, size_t ws_bytes, double* out, int* info) {
+    CHECK_H(h);
+    CHECK_D(d);
+    if (n < 1 || p < 1 || !X || !Y || !theta || !ws || !out || !info) return MFGP_ERR_ARG;
+    if (h->nb == 64)
+        return gpr_value_grad<64>(h, n, p, d, X, ldx, Y, ldy, (double*)theta, want_grad, ws, ws_bytes, out, info,
+                                  nullptr);
+    return gpr_value_grad<32>(h, n, p, d, X, ldx, Y, ldy, (double*)theta, want_grad, ws, ws_bytes, out, info,
+                              nullptr);
+}
+
+int mfgp_gpr_adam_step(mfgp_handle_t h, int n, int p, int d, const double* X, int ldx, const double* Y, int ldy,
+                       double* theta, double* u, double* m, double* v, const unsigned char* trainable,
+                       const int* tie, int* step, double lr, double beta1, double beta2, double eps,
+                       double* loss_hist, void* ws, size_t ws_bytes, double* out, int* info) {
+    CHECK_H(h);
+    CHECK_D(d);
+    if (n < 1 || p < 1 || !X || !Y || !theta || !u || !m || !v || !trainable || !step || !loss_hist || !ws ||
+        !out || !info)
+        return MFGP_ERR_ARG;
+    FinArgs f{};
+    f.theta = theta; f.u = u; f.m = m; f.v = v; f.trainable = trainable; f.tie = tie; f.step = step;
+    f.lr = lr; f.b1 = beta1; f.b2 = beta2; f.eps = eps; f.loss_hist = loss_hist;
+    f.noise_index = theta_size(d) - 1;
+    if (h->nb == 64) return gpr_value_grad<64>(h, n, p, d, X, ldx, Y, ldy, theta, 1, ws, ws_bytes, out, info, &f);
+    return gpr_value_grad<32>(h, n, p, d, X, ldx, Y, ldy, theta, 1, ws, ws_bytes, out, info, &f);
+}
+
+int mfgp_theta_from_u(mfgp_handle_t h, const double* u, double* theta, int g, int noise_index) {
+    CHECK_H(h);
+    if (!u || !theta || g < 1 || g > 256) return MFGP_ERR_ARG;
+    hipLaunchKernelGGL(k_theta_from_u, dim3(1), dim3(256), 0, h->stream, u, theta, g, noise_index);
+    return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;
+}
+
+int mfgp_gpr_predict_workspace_size(mfgp_handle_t h, int n, int p, int d, int nstar, size_t* bytes) {
+    CHECK_H(h);
+    CHECK_D(d);
+    if (n < 1 || p < 1 || nstar < 0 || !bytes) return MFGP_ERR_ARG;
+    *bytes = pred_layout(h->nb, n, p, d, nstar, nullptr).bytes;
+    return MFGP_OK;
+}
+
+int mfgp_gpr_predict(mfgp_handle_t h, int n, int p, int d, int nstar, const double* X, int ldx, const double* Y,
+                     int ldy, const double* Xs, int ldxs, const double* theta, void* ws, size_t ws_bytes,
+                     double* mean, int ldm, double* var, int* info) {
+    CHECK_H(h);
+    CHECK_D(d);
+    if (n < 1 || p < 1 || nstar < 0 || !X || !Y || !theta || !ws || !info) return MFGP_ERR_ARG;
+    if (nstar == 0) return MFGP_OK;
+    if (!Xs || !mean || !var) return MFGP_ERR_ARG;
+    if (h->nb == 64)
+        return predict_impl<64>(h, n, p, d, nstar, X, ldx, Y, ldy, Xs, ldxs, theta, ws, ws_bytes, mean, ldm, var,
+                                info);
+    return predict_impl<32>(h, n, p, d, nstar, X, ldx, Y, ldy, Xs, ldxs, theta, ws, ws_bytes, mean, ldm, var, info);
+}
+
+int mfgp_potrf_inv_workspace_size(mfgp_handle_t h, int n, int batch, size_t* bytes) {
+    CHECK_H(h);
+    if (n < 1 || batch < 1 || !bytes) return MFGP_ERR_ARG;
+    *bytes = potrf_layout(h->nb, n, batch, nullptr).bytes;
+    return MFGP_OK;
+}
+
+int mfgp_potrf_inv(mfgp_handle_t h, int n, int batch, const double* A, int lda, long sA, void* ws, size_t ws_bytes,
+                   double* Linv, int ldl, long sL, double* ldiag, int* info) {
+    CHECK_H(h);
+    if (n < 1 || batch < 1 || !A || !ws || !Linv || !info) return MFGP_ERR_ARG;
+    if (h->nb == 64) return potrf_inv_impl<64>(h, n, batch, A, lda, sA, ws, ws_bytes, Linv, ldl, sL, ldiag, info);
+    return potrf_inv_impl<32>(h, n, batch, A, lda, sA, ws, ws_bytes, Linv, ldl, sL, ldiag, info);
+}
+
+int mfgp_svgp_workspace_size(mfgp_handle_t h, int n, int m, int l, int p, int d, size_t* bytes) {
+    CHECK_H(h);
+    CHECK_D(d);
+    if (n < 1 || m < 1 || l < 1 || p < 1 || !bytes) return MFGP_ERR_ARG;
+    *bytes = (size_t)svgp_workspace_bytes(h->nb, n, m, l, p, d);
+    return MFGP_OK;
+}
+
+int mfgp_svgp_elbo(mfgp_handle_t h, int n, int m, int l, int p, int d, const double* X, int ldx, const double* Y,
+                   int ldy, const double* Z, int ldz, const double* thetas, const double* q_mu,
+                   const double* q_sqrt, const double* W, double noise, double scale, double jitter, void* ws,
+                   size_t ws_bytes, double* out, double* g_mu, double* g_var, int* info) {
+    CHECK_H(h);
+    CHECK_D(d);
+    if (n < 1 || m < 1 || l < 1 || p < 1 || !X || !Y || !Z || !thetas || !q_mu || !q_sqrt || !ws || !out || !info)
+        return MFGP_ERR_ARG;
+    if (!W && l != p) return MFGP_ERR_ARG;
+    return svgp_elbo_impl(h->stream, h->nb, n, m, l, p, d, X, ldx, Y, ldy, Z, ldz, thetas, q_mu, q_sqrt, W, noise,
+                          scale, jitter, ws, ws_bytes, out, g_mu, g_var, info);
+}
+
+int mfgp_selftest_mfma(mfgp_handle_t h, double* out) {
+    CHECK_H(h);
+    if (!out) return MFGP_ERR_ARG;
+    hipLaunchKernelGGL(k_selftest_mfma, dim3(1), dim3(64), 0, h->stream, out);
+    return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;
+}
+
+}  // extern "C"

@@ -1,0 +1,106 @@
+// Internal (host<->device) argument blocks and launchers of the MI355X GP kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+namespace mfgp {
+
+struct GramArgs {
+    const double* X1; long ldx1; long sx1; int n1;
+    const double* X2; long ldx2; long sx2; int n2;
+    const double* theta; long stheta;         // per-batch theta stride (doubles)
+    int D;
+    int rbf_only;                             // 1: plain SquaredExponential on all D columns
+    double* out; long ldo; long so;
+    int padded;                               // 1: LML layout (square, lower tiles, identity pad)
+    int npad;                                 // padded size (LML layout)
+    int tiles_c;                              // number of column tiles (dense layout)
+    int add_noise;                            // add theta noise on i==j<n (LML layout)
+    double diag_add;                          // extra constant on i==j<n (jitter)
+    // fused factor of tile (0,0) (LML layout only)
+    double* Dd; long sD; double* ldiag; long sL; int* info;
+};
+
+struct CholArgs {
+    double* A; long lda; long sA;        // SPD matrix, lower tiles, updated in place
+    double* R; long ldr; long sR;        // RHS [I | Y] (identity tiles 0..T-1, Y tiles T..T+Tp-1)
+    double* Xo; long ldx; long sX;       // output [L^{-1} | Z]
+    double* Dd; long sD;                 // T inverse diagonal factors (NB x NB each)
+    double* ldiag; long sL;              // diag(L)
+    int* info;
+    int T, Tp, k;
+};
+
+struct AlphaArgs {
+    const double* Xo; long ldx;           // [L^{-1} | Z]
+    double* alpha; long lda;              // Npad x Ppad
+    double* zpart;                        // T*Tp partial sums of Z^2 (valid region)
+    int T, Tp, n, p;
+};
+
+struct GradArgs {
+    const double* Xo; long ldx;           // [L^{-1} | Z]
+    const double* alpha; long lda;        // Npad x Ppad
+    const double* X; long ldxx;           // inputs [n, D+1]
+    const double* theta;
+    double* gpart; int gstride;           // per task partial gradient
+    int T, Tp, n, P, D;
+};
+
+struct FinArgs {
+    const double* zpart; int nz;
+    const double* ldiag; int n;
+    const double* gpart; int ng; int gstride;
+    const int* info;
+    int P, D, want_grad;
+    double* out;                      // [lml, grad(G)]
+    // Adam (optional, unconstrained parameters)
+    int adam;
+    double* theta;                    // constrained theta, refreshed after the step
+    double* u; double* m; double* v;
+    const unsigned char* trainable;
+    const int* tie;                   // tie[q]: entries sharing one variable (isotropic lengthscales)
+    int* step;
+    double lr, b1, b2, eps;
+    double* loss_hist;                // loss_hist[step] = -lml (pre-step)
+    int noise_index;                  // theta entry using Shift(1e-6) o Softplus
+};
+
+struct PredAArgs {
+    const double* Xo; long ldx;       // [L^{-1} | Z]
+    const double* Kmn; long ldk;      // Npad x Nspad
+    double* Am; long ldam;            // Npad x Nspad   A = L^{-1} Kmn
+    int Ts;
+};
+
+struct PredOutArgs {
+    const double* Am; long ldam;
+    const double* Xo; long ldx;
+    const double* kdiag;              // nstar
+    double* mean; long ldm;           // nstar x p
+    double* var;                      // nstar
+    int T, Tp, nstar, p;
+};
+
+constexpr int MAXD_HOST = 32;
+
+size_t gram_smem_bytes(int nb);
+size_t chol_smem_bytes(int nb);
+size_t grad_smem_bytes(int nb);
+int chol_step_blocks(int T, int Tp, int k);
+int grad_tasks(int T);
+
+template <int NB> void launch_gram(const GramArgs& g, int nblocks, int batch, hipStream_t s);
+template <int NB> void launch_chol_steps(CholArgs c, int batch, hipStream_t s);
+template <int NB> void launch_alpha(const AlphaArgs& a, hipStream_t s);
+template <int NB> void launch_grad(const GradArgs& g, hipStream_t s);
+template <int NB> void launch_pred(const PredAArgs& pa, const PredOutArgs& po, int T, hipStream_t s);
+
+__global__ void k_rhs_init(double* R, long ldr, long sR, int npad, int ppad, const double* Y, long ldy, long sY,
+                           int n, int p);
+__global__ void k_finalize(FinArgs a);
+__global__ void k_theta_from_u(const double* u, double* theta, int G, int noise_index);
+__global__ void k_kdiag(const double* X, long ldx, int n, int D, const double* theta, double* out);
+__global__ void k_selftest_mfma(double* out);
+
+}  // namespace mfgp

@@ -1,0 +1,661 @@
+// MI355X-native kernels for the multi-fidelity GPR hot path (fp64).
+//
+//   K1  k_gram            per-fidelity RBF distance + rho-scaled block assembly
+//                         (mfgpflow/linear.py:55-104, GPflow SquaredExponential.K)
+//   K2  k_chol_step       right-looking tile Cholesky fused with the inverse
+//                         factor L^{-1} and the forward solve Z = L^{-1} Y
+//   K3  k_alpha           alpha = L^{-T} Z  (+ sum Z^2 partials for the LML)
+//   K5  k_grad            W = alpha alpha^T - P K^{-1} contracted with dK/dtheta,
+//                         K^{-1} = L^{-T} L^{-1} formed tile-by-tile, never stored
+//   K4  k_finalize        LML reduction, gradient reduction, optional Adam step
+//   K6  k_pred_a / k_pred_out   posterior mean / variance (GPflow base_conditional)
+//
+// Every kernel runs 256-thread workgroups on NB x NB fp64 tiles; tile products
+// go through v_mfma_f64_16x16x4_f64 (mfgp_device.h).
+#include "mfgp_device.h"
+#include "mfgp_internal.h"
+
+namespace mfgp {
+
+constexpr int MAXD = 32;
+
+// ============================================================ K1: gram
+
+template <int NB>
+__device__ __forceinline__ void stage_rows(double* aL, double* aD, double* nL, double* nD, double* f,
+                                           const double* X, long ldx, int n, int r0, int D,
+                                           const MFTheta& th, int rbf_only) {
+    // aL[r*MAXD + d] = X[r][d] / lL[d] ; nL[r] = sum aL^2 (GPflow square_distance)
+    for (int e = threadIdx.x; e < NB * D; e += NTHREADS) {
+        const int r = e / D, d = e % D;
+        const int gr = r0 + r;
+        const double x = (gr < n) ? X[(long)gr * ldx + d] : 0.0;
+        aL[r * MAXD + d] = x / th.lL(d);
+        if (!rbf_only) aD[r * MAXD + d] = x / th.lD(d);
+    }
+    __syncthreads();
+    for (int r = threadIdx.x; r < NB; r += NTHREADS) {
+        double sL = 0.0, sD = 0.0;
+        for (int d = 0; d < D; ++d) {
+            const double a = aL[r * MAXD + d];
+            sL += a * a;
+            if (!rbf_only) { const double b = aD[r * MAXD + d]; sD += b * b; }
+        }
+        nL[r] = sL;
+        nD[r] = sD;
+        const int gr = r0 + r;
+        f[r] = (gr < n) ? (rbf_only ? 0.0 : X[(long)gr * ldx + D]) : -1.0;
+    }
+}
+
+// one Gram entry from staged rows (GPflow: dist = -2 a.b + (|a|^2 + |b|^2); k = v exp(-dist/2))
+__device__ __forceinline__ double gram_entry(const double* aL1, const double* aD1, double nL1, double nD1, double f1,
+                                             const double* aL2, const double* aD2, double nL2, double nD2, double f2,
+                                             int D, const MFTheta& th, int rbf_only) {
+    if (rbf_only) {
+        if (f1 < 0.0 || f2 < 0.0) return 0.0;
+        double dot = 0.0;
+        for (int d = 0; d < D; ++d) dot += aL1[d] * aL2[d];
+        const double r2 = -2.0 * dot + (nL1 + nL2);
+        return th.vL() * exp(-0.5 * r2);
+    }
+    const bool L1 = (f1 == 0.0), H1 = (f1 == 1.0), L2 = (f2 == 0.0), H2 = (f2 == 1.0);
+    if (!(L1 || H1) || !(L2 || H2)) return 0.0;        // linear.py:67-70 exact masks
+    double dot = 0.0;
+    for (int d = 0; d < D; ++d) dot += aL1[d] * aL2[d];
+    const double kL = th.vL() * exp(-0.5 * (-2.0 * dot + (nL1 + nL2)));
+    const double rho = th.rho();
+    if (L1 && L2) return kL;                           // K_LL
+    if (!(H1 && H2)) return kL * rho;                  // K_LH, K_HL
+    double dotD = 0.0;
+    for (int d = 0; d < D; ++d) dotD += aD1[d] * aD2[d];
+    const double kD = th.vD() * exp(-0.5 * (-2.0 * dotD + (nD1 + nD2)));
+    return kL * (rho * rho) + kD;                      // K_HH (linear.py:96)
+}
+
+template <int NB>
+__global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
+    constexpr int S = TileCfg<NB>::S;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    double* aL1 = smem;
+    double* aD1 = aL1 + NB * MAXD;
+    double* aL2 = aD1 + NB * MAXD;
+    double* aD2 = aL2 + NB * MAXD;
+    double* nL1 = aD2 + NB * MAXD;
+    double* nD1 = nL1 + NB;
+    double* f1 = nD1 + NB;
+    double* nL2 = f1 + NB;
+    double* nD2 = nL2 + NB;
+    double* f2 = nD2 + NB;
+    double* tile = f2 + NB;                    // NB x S
+    double* rtile = tile + TileCfg<NB>::ELEMS; // NB x S (factor scratch)
+    double* dg = rtile + TileCfg<NB>::ELEMS;   // NB
+    __shared__ int bad;
+
+    const int b = blockIdx.z;
+    int ti, tj;
+    if (a.padded) {   // lower tiles: t -> (ti, tj), ti >= tj
+        const int t = blockIdx.x;
+        ti = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+        while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+        while (ti * (ti + 1) / 2 > t) --ti;
+        tj = t - ti * (ti + 1) / 2;
+    } else {
+        ti = blockIdx.x / a.tiles_c;
+        tj = blockIdx.x % a.tiles_c;
+    }
+    const MFTheta th{a.theta + b * a.stheta, a.D};
+    const double* X1 = a.X1 + b * a.sx1;
+    const double* X2 = a.X2 + b * a.sx2;
+    stage_rows<NB>(aL1, aD1, nL1, nD1, f1, X1, a.ldx1, a.n1, ti * NB, a.D, th, a.rbf_only);
+    stage_rows<NB>(aL2, aD2, nL2, nD2, f2, X2, a.ldx2, a.n2, tj * NB, a.D, th, a.rbf_only);
+    __syncthreads();
+
+    const double noise = a.add_noise ? th.noise() : 0.0;
+    double* out = a.out + b * a.so;
+    for (int e = threadIdx.x; e < NB * NB; e += NTHREADS) {
+        const int r = e / NB, c = e % NB;
+        const int gi = ti * NB + r, gj = tj * NB + c;
+        double v = gram_entry(aL1 + r * MAXD, aD1 + r * MAXD, nL1[r], nD1[r], f1[r],
+                              aL2 + c * MAXD, aD2 + c * MAXD, nL2[c], nD2[c], f2[c], a.D, th, a.rbf_only);
+        if (a.padded) {
+            if (gi == gj) v = (gi < a.n1) ? v + noise + a.diag_add : 1.0;   // identity padding
+            tile[r * S + c] = v;
+        } else {
+            if (gi == gj) v += a.diag_add;
+            if (gi < a.n1 && gj < a.n2) out[(long)gi * a.ldo + gj] = v;
+        }
+    }
+    if (!a.padded) return;
+    __syncthreads();
+    tile_store<NB>(out + (long)ti * NB * a.ldo + tj * NB, a.ldo, tile);
+    if (a.Dd != nullptr && ti == 0 && tj == 0) {
+        // fused factor of the first diagonal tile (step "-1" of the tile Cholesky)
+        __syncthreads();
+        tile_potrf_inv<NB>(tile, rtile, dg, &bad);
+        tile_store<NB>(a.Dd + b * a.sD, NB, rtile);
+        for (int r = threadIdx.x; r < NB; r += NTHREADS) a.ldiag[b * a.sL + r] = dg[r];
+        if (threadIdx.x == 0 && bad && a.info[b] == 0) a.info[b] = bad;
+    }
+}
+
+size_t gram_smem_bytes(int nb) {
+    const size_t tile = (size_t)nb * (nb + 2);
+    return sizeof(double) * (4 * (size_t)nb * MAXD + 6 * (size_t)nb + 2 * tile + nb);
+}
+
+// ============================================================ K2: tile Cholesky step
+
+__device__ __forceinline__ void tri_decode(int t, int& i, int& j) {
+    int r = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+    while ((r + 1) * (r + 2) / 2 <= t) ++r;
+    while (r * (r + 1) / 2 > t) --r;
+    i = r;
+    j = t - r * (r + 1) / 2;
+}
+
+template <int NB>
+__global__ __launch_bounds__(NTHREADS) void k_chol_step(CholArgs a) {
+    constexpr int S = TileCfg<NB>::S;
+    constexpr int E = TileCfg<NB>::ELEMS;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    double* Ds = smem;           // D_k
+    double* T0 = Ds + E;         // scratch / A tile / X tile
+    double* Pi = T0 + E;         // L_ik = A_ik D_k^T
+    double* Pj = Pi + E;         // L_jk
+    double* dg = Pj + E;         // NB
+    __shared__ int bad;
+
+    const int b = blockIdx.z;
+    const int k = a.k, T = a.T, Tp = a.Tp;
+    double* A = a.A + b * a.sA;
+    double* R = a.R + b * a.sR;
+    double* Xo = a.Xo + b * a.sX;
+    const long lda = a.lda, ldr = a.ldr, ldx = a.ldx;
+    auto At = [&](int i, int j) { return A + (long)i * NB * lda + (long)j * NB; };
+    auto Rt = [&](int i, int c) { return R + (long)i * NB * ldr + (long)c * NB; };
+    auto Xt = [&](int i, int c) { return Xo + (long)i * NB * ldx + (long)c * NB; };
+
+    const int rem = T - k - 1;
+    const int nA = rem * (rem + 1) / 2;
+    const int ncol = k + 1 + Tp;               // active RHS column tiles
+    const int nR = rem * ncol;
+    int t = blockIdx.x;
+
+    tile_load<NB>(Ds, a.Dd + b * a.sD + (long)k * NB * NB, NB);
+
+    if (t < nA) {
+        // ---- trailing update A_ij -= L_ik L_jk^T, i >= j > k
+        int ii, jj;
+        tri_decode(t, ii, jj);
+        const int i = k + 1 + ii, j = k + 1 + jj;
+        tile_load<NB>(T0, At(i, k), lda);
+        __syncthreads();
+        Acc<NB> acc;
+        acc_zero(acc);
+        tile_mma<NB, false, true>(acc, T0, Ds, 1.0);     // P_i = A_ik D_k^T
+        acc_to_lds(acc, Pi);
+        const double* PJ = Pi;
+        if (j != i) {
+            __syncthreads();
+            tile_load<NB>(T0, At(j, k), lda);
+            __syncthreads();
+            acc_zero(acc);
+            tile_mma<NB, false, true>(acc, T0, Ds, 1.0);
+            acc_to_lds(acc, Pj);
+            PJ = Pj;
+        }
+        __syncthreads();
+        acc_load(acc, At(i, j), lda);
+        tile_mma<NB, false, true>(acc, Pi, PJ, -1.0);    // A_ij -= P_i P_j^T
+        if (i == j && i == k + 1) {
+            // next diagonal tile is final: factor it and publish D_{k+1}
+            acc_to_lds(acc, T0);
+            __syncthreads();
+            tile_potrf_inv<NB>(T0, Pj, dg, &bad);
+            tile_store<NB>(a.Dd + b * a.sD + (long)(k + 1) * NB * NB, NB, Pj);
+            for (int r = threadIdx.x; r < NB; r += NTHREADS) a.ldiag[b * a.sL + (k + 1) * NB + r] = dg[r];
+            if (threadIdx.x == 0 && bad && a.info[b] == 0) a.info[b] = (k + 1) * NB + bad;
+        } else {
+            acc_store(acc, At(i, j), lda);
+        }
+        return;
+    }
+    t -= nA;
+    if (t < nR) {
+        // ---- RHS update R_ic -= L_ik X_kc, X_kc = D_k R_kc (row k of [L^{-1} | Z])
+        const int i = k + 1 + t / ncol;
+        const int cc = t % ncol;
+        const int c = (cc <= k) ? cc : T + (cc - k - 1);
+        tile_load<NB>(T0, Rt(k, c), ldr);
+        __syncthreads();
+        Acc<NB> acc;
+        acc_zero(acc);
+        tile_mma<NB, false, false>(acc, Ds, T0, 1.0);    // X_kc
+        acc_to_lds(acc, Pj);
+        if (i == k + 1) acc_store(acc, Xt(k, c), ldx);
+        __syncthreads();
+        tile_load<NB>(T0, At(i, k), lda);
+        __syncthreads();
+        acc_zero(acc);
+        tile_mma<NB, false, true>(acc, T0, Ds, 1.0);     // P_i
+        acc_to_lds(acc, Pi);
+        __syncthreads();
+        acc_load(acc, Rt(i, c), ldr);
+        tile_mma<NB, false, false>(acc, Pi, Pj, -1.0);
+        acc_store(acc, Rt(i, c), ldr);
+        return;
+    }
+    t -= nR;
+    // ---- last step writers: X_{T-1,c} = D_{T-1} R_{T-1,c}
+    {
+        const int c = t;   // 0..T-1 identity tiles, T..T+Tp-1 Y tiles
+        tile_load<NB>(T0, Rt(k, c), ldr);
+        __syncthreads();
+        Acc<NB> acc;
+        acc_zero(acc);
+        tile_mma<NB, false, false>(acc, Ds, T0, 1.0);
+        acc_store(acc, Xt(k, c), ldx);
+    }
+}
+
+int chol_step_blocks(int T, int Tp, int k) {
+    const int rem = T - k - 1;
+    return rem * (rem + 1) / 2 + rem * (k + 1 + Tp) + ((k == T - 1) ? (T + Tp) : 0);
+}
+
+size_t chol_smem_bytes(int nb) { return sizeof(double) * (4 * (size_t)nb * (nb + 2) + nb); }
+
+// RHS init: identity tiles on the diagonal, zeros strictly below, Y (zero padded)
+__global__ void k_rhs_init(double* R, long ldr, long sR, int npad, int ppad, const double* Y, long ldy, long sY,
+                           int n, int p) {
+    const int b = blockIdx.z;
+    const long total = (long)npad * (npad + ppad);
+    for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const int r = (int)(e / (npad + ppad)), c = (int)(e % (npad + ppad));
+        double v;
+        if (c < npad) v = (r == c) ? 1.0 : 0.0;
+        else {
+            const int pc = c - npad;
+            v = (Y != nullptr && r < n && pc < p) ? Y[b * sY + (long)r * ldy + pc] : 0.0;
+        }
+        R[b * sR + (long)r * ldr + c] = v;
+    }
+}
+
+// ============================================================ K3: alpha = L^{-T} Z
+
+template <int NB>
+__global__ __launch_bounds__(NTHREADS) void k_alpha(AlphaArgs a) {
+    constexpr int E = TileCfg<NB>::ELEMS;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    double* Ls = smem;
+    double* Zs = Ls + E;
+    __shared__ double red[4];
+    const int i = blockIdx.x / a.Tp, cy = blockIdx.x % a.Tp;
+    auto Xt = [&](int r, int c) { return a.Xo + (long)r * NB * a.ldx + (long)c * NB; };
+    Acc<NB> acc;
+    acc_zero(acc);
+    double z2 = 0.0;
+    for (int m = i; m < a.T; ++m) {
+        tile_load<NB>(Ls, Xt(m, i), a.ldx);
+        tile_load<NB>(Zs, Xt(m, a.T + cy), a.ldx);
+        __syncthreads();
+        if (m == i) {   // sum of squares of Z_i (rows < n, cols < p)
+            for (int e = threadIdx.x; e < NB * NB; e += NTHREADS) {
+                const int r = e / NB, c = e % NB;
+                if (i * NB + r < a.n && cy * NB + c < a.p) {
+                    const double z = Zs[r * TileCfg<NB>::S + c];
+                    z2 += z * z;
+                }
+            }
+        }
+        tile_mma<NB, true, false>(acc, Ls, Zs, 1.0);
+        __syncthreads();
+    }
+    acc_store(acc, a.alpha + (long)i * NB * a.lda + (long)cy * NB, a.lda);
+    z2 = block_sum(z2, red);
+    if (threadIdx.x == 0) a.zpart[blockIdx.x] = z2;
+}
+
+// ============================================================ K5: gradient
+constexpr int GRAD_CH = 8;   // m-range chunk per task (load balance)
+
+__host__ __device__ inline int grad_row_chunks(int T, int i) { return (T - i + GRAD_CH - 1) / GRAD_CH; }
+
+int grad_tasks(int T) {
+    int s = 0;
+    for (int i = 0; i < T; ++i) s += (i + 1) * grad_row_chunks(T, i);
+    return s;
+}
+
+
+template <int NB>
+__global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
+    constexpr int S = TileCfg<NB>::S;
+    constexpr int E = TileCfg<NB>::ELEMS;
+    constexpr int NE = TileCfg<NB>::NBLK * 4;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    double* As = smem;
+    double* Bs = As + E;
+    double* xi = Bs + E;              // NB x MAXD raw rows of tile i
+    double* xj = xi + NB * MAXD;      // NB x MAXD raw rows of tile j
+    double* fi = xj + NB * MAXD;      // NB
+    double* fj = fi + NB;             // NB
+    double* red = fj + NB;            // 4 x (2*MAXD+4)
+    const int G = theta_size(a.D);
+    const MFTheta th{a.theta, a.D};
+
+    // decode task -> (i, j, m0, m1)
+    int t = blockIdx.x, i = 0;
+    for (;; ++i) {
+        const int cnt = (i + 1) * grad_row_chunks(a.T, i);
+        if (t < cnt) break;
+        t -= cnt;
+    }
+    const int nch = grad_row_chunks(a.T, i);
+    const int j = t / nch, ch = t % nch;
+    const int m0 = i + ch * GRAD_CH;
+    const int m1 = min(a.T, m0 + GRAD_CH);
+    auto Xt = [&](int r, int c) { return a.Xo + (long)r * NB * a.ldx + (long)c * NB; };
+
+    // stage raw inputs of the two row tiles
+    for (int e = threadIdx.x; e < NB * (a.D + 1); e += NTHREADS) {
+        const int r = e / (a.D + 1), d = e % (a.D + 1);
+        const int gi = i * NB + r, gj = j * NB + r;
+        const double vi = (gi < a.n) ? a.X[(long)gi * a.ldxx + d] : 0.0;
+        const double vj = (gj < a.n) ? a.X[(long)gj * a.ldxx + d] : 0.0;
+        if (d < a.D) { xi[r * MAXD + d] = vi; xj[r * MAXD + d] = vj; }
+        else { fi[r] = (gi < a.n) ? vi : -1.0; fj[r] = (gj < a.n) ? vj : -1.0; }
+    }
+
+    // W_ij (tile) = [alpha_i alpha_j^T] - P * sum_m Linv_mi^T Linv_mj
+    Acc<NB> acc;
+    acc_zero(acc);
+    const double negP = -(double)a.P;
+    for (int m = m0; m < m1; ++m) {
+        __syncthreads();
+        tile_load<NB>(As, Xt(m, i), a.ldx);
+        tile_load<NB>(Bs, Xt(m, j), a.ldx);
+        __syncthreads();
+        tile_mma<NB, true, false>(acc, As, Bs, negP);
+    }
+    if (ch == 0) {
+        for (int cy = 0; cy < a.Tp; ++cy) {
+            __syncthreads();
+            tile_load<NB>(As, a.alpha + (long)i * NB * a.lda + cy * NB, a.lda);
+            tile_load<NB>(Bs, a.alpha + (long)j * NB * a.lda + cy * NB, a.lda);
+            __syncthreads();
+            tile_mma<NB, false, true>(acc, As, Bs, 1.0);
+        }
+    }
+    __syncthreads();
+
+    // epilogue: contract with dK/dtheta recomputed from the inputs
+    const double wscale = (i == j) ? 0.5 : 1.0;   // 1/2 * (2 for the mirrored tile)
+    const double rho = th.rho();
+    double cL[NE], cD[NE];
+    double gvL = 0.0, gvD = 0.0, grho = 0.0, gnoise = 0.0;
+#pragma unroll
+    for (int q = 0; q < TileCfg<NB>::NBLK; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int e = q * 4 + r;
+            const int ri = acc_row<NB>(q, r), cj = acc_col<NB>(q);
+            const double f1 = fi[ri], f2 = fj[cj];
+            const bool L1 = f1 == 0.0, H1 = f1 == 1.0, L2 = f2 == 0.0, H2 = f2 == 1.0;
+            const double w = acc.v[q][r] * wscale;
+            double kL = 0.0, kD = 0.0;
+            if ((L1 || H1) && (L2 || H2)) {
+                double s2 = 0.0, s2d = 0.0;
+                for (int d = 0; d < a.D; ++d) {
+                    const double df = xi[ri * MAXD + d] - xj[cj * MAXD + d];
+                    const double d2 = df * df;
+                    const double ql = th.lL(d);
+                    s2 += d2 / (ql * ql);
+                    if (H1 && H2) { const double qd = th.lD(d); s2d += d2 / (qd * qd); }
+                }
+                kL = th.vL() * exp(-0.5 * s2);
+                if (H1 && H2) kD = th.vD() * exp(-0.5 * s2d);
+            }
+            const double si = L1 ? 1.0 : (H1 ? rho : 0.0), sj = L2 ? 1.0 : (H2 ? rho : 0.0);
+            const double hi = H1 ? 1.0 : 0.0, hj = H2 ? 1.0 : 0.0;
+            cL[e] = w * si * sj * kL;
+            cD[e] = w * hi * hj * kD;
+            gvL += cL[e];
+            gvD += cD[e];
+            grho += w * (hi * sj + si * hj) * kL;
+            if (i == j && ri == cj && i * NB + ri < a.n) gnoise += w;
+        }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    auto put = [&](int qidx, double v) {
+        v = wave_sum(v);
+        if (lane == 0) red[wv * (2 * MAXD + 4) + qidx] = v;
+    };
+    put(0, gvL);
+    put(1 + a.D, gvD);
+    put(2 + 2 * a.D, grho);
+    put(3 + 2 * a.D, gnoise);
+    for (int d = 0; d < a.D; ++d) {
+        double tl = 0.0, td = 0.0;
+#pragma unroll
+        for (int q = 0; q < TileCfg<NB>::NBLK; ++q)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int e = q * 4 + r;
+                const double df = xi[acc_row<NB>(q, r) * MAXD + d] - xj[acc_col<NB>(q) * MAXD + d];
+                tl += cL[e] * df * df;
+                td += cD[e] * df * df;
+            }
+        put(1 + d, tl);
+        put(2 + a.D + d, td);
+    }
+    __syncthreads();
+    for (int qx = threadIdx.x; qx < G; qx += NTHREADS) {
+        const int st = 2 * MAXD + 4;
+        double v = (red[qx] + red[st + qx]) + (red[2 * st + qx] + red[3 * st + qx]);
+        if (qx == 0) v /= th.vL();
+        else if (qx <= a.D) { const double l = th.lL(qx - 1); v /= l * l * l; }
+        else if (qx == 1 + a.D) v /= th.vD();
+        else if (qx <= 1 + 2 * a.D) { const double l = th.lD(qx - 2 - a.D); v /= l * l * l; }
+        a.gpart[(long)blockIdx.x * a.gstride + qx] = v;
+    }
+}
+
+size_t grad_smem_bytes(int nb) {
+    return sizeof(double) * (2 * (size_t)nb * (nb + 2) + 2 * (size_t)nb * MAXD + 2 * nb + 4 * (2 * MAXD + 4));
+}
+
+// ============================================================ K4: finalize (+Adam)
+
+__device__ __forceinline__ double tf_softplus(double x) {
+    // tensorflow/core/kernels/softplus_op.h
+    const double thr = -34.04365338911715;   // log(DBL_EPSILON) + 2
+    if (x > -thr) return x;
+    if (x < thr) return exp(x);
+    return log(exp(x) + 1.0);
+}
+
+__global__ __launch_bounds__(NTHREADS) void k_finalize(FinArgs a) {
+    __shared__ double red[4];
+    __shared__ double gsh[2 * MAXD + 4];
+    __shared__ double lml_sh;
+    const int G = theta_size(a.D);
+    double z2 = 0.0, ld = 0.0;
+    for (int e = threadIdx.x; e < a.nz; e += NTHREADS) z2 += a.zpart[e];
+    for (int e = threadIdx.x; e < a.n; e += NTHREADS) ld += log(a.ldiag[e]);
+    z2 = block_sum(z2, red);
+    ld = block_sum(ld, red);
+    const double LOG2PI = 1.8378770664093453;
+    double lml = -0.5 * z2 - (double)a.P * ld - 0.5 * (double)a.n * (double)a.P * LOG2PI;
+    if (a.info[0] != 0) lml = NAN;
+    if (a.want_grad) {
+        for (int q = 0; q < G; ++q) {
+            double s = 0.0;
+            for (int e = threadIdx.x; e < a.ng; e += NTHREADS) s += a.gpart[(long)e * a.gstride + q];
+            s = block_sum(s, red);
+            if (threadIdx.x == 0) gsh[q] = s;
+        }
+    }
+    if (threadIdx.x == 0) {
+        lml_sh = lml;
+        a.out[0] = lml;
+    }
+    __syncthreads();
+    if (a.want_grad)
+        for (int q = threadIdx.x; q < G; q += NTHREADS) a.out[1 + q] = gsh[q];
+    if (!a.adam) return;
+    __syncthreads();
+    const int s = *a.step;
+    if (threadIdx.x == 0) a.loss_hist[s] = -lml_sh;
+    if (a.info[0] != 0) return;   // non-PD: leave parameters untouched (host raises)
+    const double t = (double)(s + 1);
+    const double alpha = a.lr * sqrt(1.0 - pow(a.b2, t)) / (1.0 - pow(a.b1, t));
+    for (int q = threadIdx.x; q < G; q += NTHREADS) {
+        if (a.trainable[q]) {
+            const double uq = a.u[q];
+            double gc = gsh[q];
+            if (a.tie) {   // a variable shared by several theta entries gets the summed gradient
+                gc = 0.0;
+                for (int r = 0; r < G; ++r)
+                    if (a.tie[r] == a.tie[q]) gc += gsh[r];
+            }
+            const double g = -gc * (1.0 / (exp(-uq) + 1.0));   // loss = -lml, chain through softplus
+            double mq = a.m[q], vq = a.v[q];
+            mq += (g - mq) * (1.0 - a.b1);
+            vq += (g * g - vq) * (1.0 - a.b2);
+            const double un = uq - (mq * alpha) / (sqrt(vq) + a.eps);
+            a.m[q] = mq;
+            a.v[q] = vq;
+            a.u[q] = un;
+            a.theta[q] = tf_softplus(un) + (q == a.noise_index ? 1e-6 : 0.0);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) *a.step = s + 1;
+}
+
+__global__ void k_theta_from_u(const double* u, double* theta, int G, int noise_index) {
+    const int q = threadIdx.x;
+    if (q < G) theta[q] = tf_softplus(u[q]) + (q == noise_index ? 1e-6 : 0.0);
+}
+
+// ============================================================ K6: predict
+
+template <int NB>
+__global__ __launch_bounds__(NTHREADS) void k_pred_a(PredAArgs a) {
+    constexpr int E = TileCfg<NB>::ELEMS;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    double* Ls = smem;
+    double* Ks = Ls + E;
+    const int i = blockIdx.x / a.Ts, cs = blockIdx.x % a.Ts;
+    Acc<NB> acc;
+    acc_zero(acc);
+    for (int m = 0; m <= i; ++m) {
+        tile_load<NB>(Ls, a.Xo + (long)i * NB * a.ldx + (long)m * NB, a.ldx);
+        tile_load<NB>(Ks, a.Kmn + (long)m * NB * a.ldk + (long)cs * NB, a.ldk);
+        __syncthreads();
+        tile_mma<NB, false, false>(acc, Ls, Ks, 1.0);
+        __syncthreads();
+    }
+    acc_store(acc, a.Am + (long)i * NB * a.ldam + (long)cs * NB, a.ldam);
+}
+
+
+template <int NB>
+__global__ __launch_bounds__(NTHREADS) void k_pred_out(PredOutArgs a) {
+    constexpr int S = TileCfg<NB>::S;
+    constexpr int E = TileCfg<NB>::ELEMS;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    double* As = smem;
+    double* Zs = As + E;
+    double* vs = Zs + E;              // NB
+    const int cs = blockIdx.x / a.Tp, cy = blockIdx.x % a.Tp;
+    Acc<NB> acc;
+    acc_zero(acc);
+    double vpart = 0.0;               // thread c < NB accumulates column c
+    for (int i = 0; i < a.T; ++i) {
+        tile_load<NB>(As, a.Am + (long)i * NB * a.ldam + (long)cs * NB, a.ldam);
+        tile_load<NB>(Zs, a.Xo + (long)i * NB * a.ldx + (long)(a.T + cy) * NB, a.ldx);
+        __syncthreads();
+        if (cy == 0 && threadIdx.x < NB)
+            for (int r = 0; r < NB; ++r) { const double v = As[r * S + threadIdx.x]; vpart += v * v; }
+        tile_mma<NB, true, false>(acc, As, Zs, 1.0);   // mean tile = sum_i A_i^T Z_i
+        __syncthreads();
+    }
+#pragma unroll
+    for (int q = 0; q < TileCfg<NB>::NBLK; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int s = cs * NB + acc_row<NB>(q, r), c = cy * NB + acc_col<NB>(q);
+            if (s < a.nstar && c < a.p) a.mean[(long)s * a.ldm + c] = acc.v[q][r];
+        }
+    if (cy == 0 && threadIdx.x < NB) {
+        const int s = cs * NB + threadIdx.x;
+        if (s < a.nstar) a.var[s] = a.kdiag[s] - vpart;
+    }
+    (void)vs;
+}
+
+// K_diag (linear.py:106-136)
+__global__ void k_kdiag(const double* X, long ldx, int n, int D, const double* theta, double* out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const MFTheta th{theta, D};
+    const double f = X[(long)i * ldx + D];
+    const double rho = th.rho();
+    out[i] = (f == 0.0) ? th.vL() : ((f == 1.0) ? th.vL() * (rho * rho) + th.vD() : 0.0);
+}
+
+// ============================================================ MFMA self-test
+// C = A B for one 16x16x4 f64 MFMA with A[i][k] = i*4+k+1, B[k][j] = 100*k + j (asymmetric).
+__global__ void k_selftest_mfma(double* out /* 16x16 */) {
+    const int l = threadIdx.x;
+    const double a = (double)((l & 15) * 4 + (l >> 4) + 1);
+    const double b = (double)(100 * (l >> 4) + (l & 15));
+    f64x4 c = {0.0, 0.0, 0.0, 0.0};
+    c = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+    for (int r = 0; r < 4; ++r) out[((l >> 4) + 4 * r) * 16 + (l & 15)] = c[r];
+}
+
+// ============================================================ launch helpers
+template <int NB>
+void launch_gram(const GramArgs& g, int nblocks, int batch, hipStream_t s) {
+    hipLaunchKernelGGL(k_gram<NB>, dim3(nblocks, 1, batch), dim3(NTHREADS), gram_smem_bytes(NB), s, g);
+}
+template <int NB>
+void launch_chol_steps(CholArgs c, int batch, hipStream_t s) {
+    for (int k = 0; k < c.T; ++k) {
+        c.k = k;
+        const int nb = chol_step_blocks(c.T, c.Tp, k);
+        if (nb > 0)
+            hipLaunchKernelGGL(k_chol_step<NB>, dim3(nb, 1, batch), dim3(NTHREADS), chol_smem_bytes(NB), s, c);
+    }
+}
+template <int NB>
+void launch_alpha(const AlphaArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_alpha<NB>, dim3(a.T * a.Tp), dim3(NTHREADS), 2 * sizeof(double) * NB * (NB + 2), s, a);
+}
+template <int NB>
+void launch_grad(const GradArgs& g, hipStream_t s) {
+    hipLaunchKernelGGL(k_grad<NB>, dim3(grad_tasks(g.T)), dim3(NTHREADS), grad_smem_bytes(NB), s, g);
+}
+template <int NB>
+void launch_pred(const PredAArgs& pa, const PredOutArgs& po, int T, hipStream_t s) {
+    hipLaunchKernelGGL(k_pred_a<NB>, dim3(T * pa.Ts), dim3(NTHREADS), 2 * sizeof(double) * NB * (NB + 2), s, pa);
+    hipLaunchKernelGGL(k_pred_out<NB>, dim3(pa.Ts * po.Tp), dim3(NTHREADS),
+                       sizeof(double) * (2 * NB * (NB + 2) + NB), s, po);
+}
+
+template void launch_gram<32>(const GramArgs&, int, int, hipStream_t);
+template void launch_gram<64>(const GramArgs&, int, int, hipStream_t);
+template void launch_chol_steps<32>(CholArgs, int, hipStream_t);
+template void launch_chol_steps<64>(CholArgs, int, hipStream_t);
+template void launch_alpha<32>(const AlphaArgs&, hipStream_t);
+template void launch_alpha<64>(const AlphaArgs&, hipStream_t);
+template void launch_grad<32>(const GradArgs&, hipStream_t);
+template void launch_grad<64>(const GradArgs&, hipStream_t);
+template void launch_pred<32>(const PredAArgs&, const PredOutArgs&, int, hipStream_t);
+template void launch_pred<64>(const PredAArgs&, const PredOutArgs&, int, hipStream_t);
+
+}  // namespace mfgp

@@ -1,0 +1,337 @@
+// SVGP hot path (value): batched K_uu factor, the K_uf K_uu^{-1} products of the
+// whitened conditional, output mixing, Gaussian variational expectations and KL.
+//
+// Reference: mfgpflow/linear_svgp.py:64-203 (LinearCoregionalization over L
+// per-latent LinearMultiFidelityKernels, SharedIndependentInducingVariables,
+// whiten=True) and mfgpflow/singlebin_svgp.py:13-97 (SeparateIndependent, W = I),
+// both through GPflow 2.9 SVGP.elbo -> posteriors / base_conditional_with_lm /
+// gauss_kl / Gaussian.variational_expectations.
+//
+// Per latent l:  Lm = chol(Kuu_l),  A = Lm^{-1} Kuf_l,  B = tril(q_sqrt_l)^T A,
+//   g_mu = A^T q_mu[:, l],  g_var = Kff_l - colsum(A^2) + colsum(B^2).
+// B is formed as (Lq^T Lm^{-1}) Kuf so that A and B come out of ONE fused tile
+// loop over Kuf (K6 below) and neither is ever written to HBM.
+#include "mfgp_device.h"
+#include "mfgp_internal.h"
+
+namespace mfgp {
+
+static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+struct SvgpLayout {
+    int nb, Tm, mpad, Tn, npad, G;
+    double *Kuu, *R, *Xo, *Dd, *ldiag, *Lq, *C, *Kuf, *pa, *pb, *pm, *ve_part, *kl_part;
+    size_t bytes;
+};
+
+static SvgpLayout svgp_layout(int nb, int n, int m, int l, int p, int d, void* ws) {
+    SvgpLayout S;
+    S.nb = nb;
+    S.Tm = cdiv(m, nb);
+    S.mpad = S.Tm * nb;
+    S.Tn = cdiv(n, nb);
+    S.npad = S.Tn * nb;
+    S.G = theta_size(d);
+    const size_t mm = (size_t)S.mpad * S.mpad;
+    size_t off = 0;
+    char* base = (char*)ws;
+    auto take = [&](size_t count) {
+        off = (off + 255) & ~(size_t)255;
+        double* ptr = base ? reinterpret_cast<double*>(base + off) : nullptr;
+        off += count * sizeof(double);
+        return ptr;
+    };
+    S.Kuu = take(mm * l);
+    S.R = take(mm * l);
+    S.Xo = take(mm * l);
+    S.Dd = take((size_t)S.Tm * nb * nb * l);
+    S.ldiag = take((size_t)S.mpad * l);
+    S.Lq = take(mm * l);
+    S.C = take(mm * l);
+    S.Kuf = take((size_t)S.mpad * S.npad * l);
+    S.pa = take((size_t)l * S.Tm * S.npad);
+    S.pb = take((size_t)l * S.Tm * S.npad);
+    S.pm = take((size_t)l * S.Tm * S.npad);
+    S.ve_part = take(1024);
+    S.kl_part = take((size_t)l + 8);
+    S.bytes = off + 256;
+    return S;
+}
+
+size_t svgp_workspace_bytes(int nb, int n, int m, int l, int p, int d) {
+    return svgp_layout(nb, n, m, l, p, d, nullptr).bytes;
+}
+
+// tril(q_sqrt_l) into a zero-padded Mpad x Mpad buffer
+__global__ void k_lq_pad(const double* q_sqrt, int m, int mpad, double* Lq) {
+    const int l = blockIdx.z;
+    const long tot = (long)mpad * mpad;
+    for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < tot; e += (long)gridDim.x * blockDim.x) {
+        const int r = (int)(e / mpad), c = (int)(e % mpad);
+        Lq[l * tot + e] = (r < m && c <= r) ? q_sqrt[(long)l * m * m + (long)r * m + c] : 0.0;
+    }
+}
+
+// C_l = Lq_l^T Linv_l  (tile (i, j): sum over m >= max(i, j))
+template <int NB>
+__global__ __launch_bounds__(NTHREADS) void k_lqt_linv(const double* Lq, const double* Xo, double* C, int Tm) {
+    constexpr int E = TileCfg<NB>::ELEMS;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    double* As = smem;
+    double* Bs = As + E;
+    const int l = blockIdx.z;
+    const int i = blockIdx.x / Tm, j = blockIdx.x % Tm;
+    const long mp = (long)Tm * NB, mm = mp * mp;
+    const double* lq = Lq + l * mm;
+    const double* xo = Xo + l * mm;
+    Acc<NB> acc;
+    acc_zero(acc);
+    for (int mt = max(i, j); mt < Tm; ++mt) {
+        tile_load<NB>(As, lq + (long)mt * NB * mp + (long)i * NB, mp);
+        tile_load<NB>(Bs, xo + (long)mt * NB * mp + (long)j * NB, mp);
+        __syncthreads();
+        tile_mma<NB, true, false>(acc, As, Bs, 1.0);
+        __syncthreads();
+    }
+    acc_store(acc, C + l * mm + (long)i * NB * mp + (long)j * NB, mp);
+}
+
+// Fused conditional: task (l, i, tn): A_i = sum_{m<=i} Linv_im Kuf_m ; B_i = sum_m C_im Kuf_m
+template <int NB>
+__global__ __launch_bounds__(NTHREADS) void k_svgp_cond(const double* Xo, const double* C, const double* Kuf,
+                                                        const double* q_mu, int L, int m, int Tm, int npad,
+                                                        double* pa, double* pb, double* pm) {
+    constexpr int S = TileCfg<NB>::S;
+    constexpr int E = TileCfg<NB>::ELEMS;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    double* Ls = smem;
+    double* Ks = Ls + E;
+    double* As = Ks + E;
+    double* red = As + E;   // 3 x 4 x NB
+    const int l = blockIdx.z;
+    const int Tn = npad / NB;
+    const int i = blockIdx.x / Tn, tn = blockIdx.x % Tn;
+    const long mp = (long)Tm * NB, mm = mp * mp;
+    const double* xo = Xo + l * mm;
+    const double* cc = C + l * mm;
+    const double* kuf = Kuf + (long)l * mp * npad;
+    Acc<NB> accA, accB;
+    acc_zero(accA);
+    acc_zero(accB);
+    for (int mt = 0; mt < Tm; ++mt) {
+        tile_load<NB>(Ks, kuf + (long)mt * NB * npad + (long)tn * NB, npad);
+        if (mt <= i) tile_load<NB>(Ls, xo + (long)i * NB * mp + (long)mt * NB, mp);
+        tile_load<NB>(As, cc + (long)i * NB * mp + (long)mt * NB, mp);
+        __syncthreads();
+        if (mt <= i) tile_mma<NB, false, false>(accA, Ls, Ks, 1.0);
+        tile_mma<NB, false, false>(accB, As, Ks, 1.0);
+        __syncthreads();
+    }
+    // column reductions: thread owns (row, col) elements; reduce over rows via LDS
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double qm[TileCfg<NB>::NBLK * 4];
+#pragma unroll
+    for (int q = 0; q < TileCfg<NB>::NBLK; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int gr = i * NB + acc_row<NB>(q, r);
+            qm[q * 4 + r] = (gr < m) ? q_mu[(long)gr * L + l] : 0.0;
+        }
+    // per-thread partial column sums (each thread owns NBLK distinct columns)
+    for (int e = threadIdx.x; e < 3 * 4 * NB; e += NTHREADS) red[e] = 0.0;
+    __syncthreads();
+    // each column is shared by 4 lane-groups x (wave row halves); accumulate with LDS atomics-free passes
+#pragma unroll
+    for (int q = 0; q < TileCfg<NB>::NBLK; ++q) {
+        double sa = 0.0, sb = 0.0, sm = 0.0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const double a = accA.v[q][r], b = accB.v[q][r];
+            sa += a * a;
+            sb += b * b;
+            sm += a * qm[q * 4 + r];
+        }
+        // lanes l, l+16, l+32, l+48 share a column: reduce across lane>>4
+        sa += __shfl_xor(sa, 16, 64); sa += __shfl_xor(sa, 32, 64);
+        sb += __shfl_xor(sb, 16, 64); sb += __shfl_xor(sb, 32, 64);
+        sm += __shfl_xor(sm, 16, 64); sm += __shfl_xor(sm, 32, 64);
+        if (lane < 16) {
+            // waves w and w^2 share columns (w>>1 selects the row half)
+            const int col = acc_col<NB>(q);
+            const int slot = (w >> 1);
+            red[(0 * 4 + slot) * NB + col] += sa;   // distinct (slot, col) per writer
+            red[(1 * 4 + slot) * NB + col] += sb;
+            red[(2 * 4 + slot) * NB + col] += sm;
+        }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < NB; c += NTHREADS) {
+        const long o = ((long)l * Tm + i) * npad + (long)tn * NB + c;
+        double sa = 0.0, sb = 0.0, sm = 0.0;
+        for (int slot = 0; slot < 4; ++slot) {
+            sa += red[(0 * 4 + slot) * NB + c];
+            sb += red[(1 * 4 + slot) * NB + c];
+            sm += red[(2 * 4 + slot) * NB + c];
+        }
+        pa[o] = sa;
+        pb[o] = sb;
+        pm[o] = sm;
+    }
+    (void)S;
+}
+
+// g_mu[l][n], g_var[l][n] from the partials (+ Kff = K_diag_l(X))
+__global__ void k_svgp_moments(const double* pa, const double* pb, const double* pm, const double* X, long ldx,
+                               const double* thetas, int G, int D, int n, int npad, int Tm, double* g_mu,
+                               double* g_var) {
+    const int l = blockIdx.z;
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    double sa = 0.0, sb = 0.0, sm = 0.0;
+    for (int i = 0; i < Tm; ++i) {
+        const long o = ((long)l * Tm + i) * npad + c;
+        sa += pa[o];
+        sb += pb[o];
+        sm += pm[o];
+    }
+    const MFTheta th{thetas + (long)l * G, D};
+    const double f = X[(long)c * ldx + D];
+    const double rho = th.rho();
+    const double kff = (f == 0.0) ? th.vL() : ((f == 1.0) ? th.vL() * (rho * rho) + th.vD() : 0.0);
+    g_mu[(long)l * n + c] = sm;
+    g_var[(long)l * n + c] = kff - sa + sb;
+}
+
+// Gaussian variational expectations summed over (n, p); mixing f = g W^T, f_var = g_var (W o W)^T
+__global__ __launch_bounds__(NTHREADS) void k_svgp_ve(const double* g_mu, const double* g_var, const double* W,
+                                                      const double* Y, long ldy, int n, int p, int L, double noise,
+                                                      double* ve_part) {
+    __shared__ double red[4];
+    const double LOG2PI = 1.8378770664093453;
+    const double c0 = -0.5 * LOG2PI - 0.5 * log(noise);
+    const double inv = 1.0 / noise;
+    double acc = 0.0;
+    const long tot = (long)n * p;
+    for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < tot; e += (long)gridDim.x * blockDim.x) {
+        const int r = (int)(e / p), c = (int)(e % p);
+        double fm, fv;
+        if (W) {
+            fm = 0.0;
+            fv = 0.0;
+            for (int l = 0; l < L; ++l) {
+                const double w = W[(long)c * L + l];
+                fm += g_mu[(long)l * n + r] * w;
+                fv += g_var[(long)l * n + r] * (w * w);
+            }
+        } else {
+            fm = g_mu[(long)c * n + r];
+            fv = g_var[(long)c * n + r];
+        }
+        const double dy = Y[(long)r * ldy + c] - fm;
+        acc += c0 - 0.5 * (dy * dy + fv) * inv;
+    }
+    acc = block_sum(acc, red);
+    if (threadIdx.x == 0) ve_part[blockIdx.x] = acc;
+}
+
+// gauss_kl(q_mu, q_sqrt, K=None) per latent (whitened prior)
+__global__ __launch_bounds__(NTHREADS) void k_svgp_kl(const double* q_mu, const double* q_sqrt, int m, int L,
+                                                      double* kl_part) {
+    __shared__ double red[4];
+    const int l = blockIdx.x;
+    double maha = 0.0, tr = 0.0, ld = 0.0;
+    for (int r = threadIdx.x; r < m; r += NTHREADS) {
+        const double q = q_mu[(long)r * L + l];
+        maha += q * q;
+        const double* row = q_sqrt + (long)l * m * m + (long)r * m;
+        for (int c = 0; c <= r; ++c) tr += row[c] * row[c];
+        ld += log(row[r] * row[r]);
+    }
+    maha = block_sum(maha, red);
+    tr = block_sum(tr, red);
+    ld = block_sum(ld, red);
+    if (threadIdx.x == 0) kl_part[l] = 0.5 * (maha - (double)m + tr - ld);
+}
+
+__global__ void k_svgp_final(const double* ve_part, int nve, const double* kl_part, int L, double scale,
+                             const int* info, double* out) {
+    if (threadIdx.x != 0) return;
+    double ve = 0.0, kl = 0.0;
+    for (int i = 0; i < nve; ++i) ve += ve_part[i];
+    for (int l = 0; l < L; ++l) kl += kl_part[l];
+    double elbo = ve * scale - kl;
+    if (info[0] != 0) elbo = NAN;
+    out[0] = elbo;
+    out[1] = kl;
+    out[2] = ve;
+}
+
+template <int NB>
+static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const double* X, int ldx, const double* Y,
+                    int ldy, const double* Z, int ldz, const double* thetas, const double* q_mu,
+                    const double* q_sqrt, const double* W, double noise, double scale, double jitter, void* ws,
+                    size_t ws_bytes, double* out, double* g_mu, double* g_var, int* info) {
+    const SvgpLayout S = svgp_layout(NB, n, m, L, p, d, ws);
+    if (ws_bytes < S.bytes) return -2;
+    const long mm = (long)S.mpad * S.mpad;
+    (void)hipMemsetAsync(info, 0, sizeof(int) * L, s);
+    // Kuu_l (+ jitter) with fused factor of tile 0; RHS = I
+    {
+        const int blocks = (int)std::min<long>((mm + 255) / 256, 2048);
+        hipLaunchKernelGGL(k_rhs_init, dim3(blocks, 1, L), dim3(256), 0, s, S.R, (long)S.mpad, mm, S.mpad, 0,
+                           (const double*)nullptr, 0L, 0L, m, 0);
+        GramArgs g{};
+        g.X1 = Z; g.ldx1 = ldz; g.sx1 = 0; g.n1 = m;
+        g.X2 = Z; g.ldx2 = ldz; g.sx2 = 0; g.n2 = m;
+        g.theta = thetas; g.stheta = S.G; g.D = d; g.rbf_only = 0;
+        g.out = S.Kuu; g.ldo = S.mpad; g.so = mm;
+        g.padded = 1; g.npad = S.mpad; g.tiles_c = S.Tm; g.add_noise = 0; g.diag_add = jitter;
+        g.Dd = S.Dd; g.sD = (long)S.Tm * NB * NB; g.ldiag = S.ldiag; g.sL = S.mpad; g.info = info;
+        launch_gram<NB>(g, S.Tm * (S.Tm + 1) / 2, L, s);
+        CholArgs c{};
+        c.A = S.Kuu; c.lda = S.mpad; c.sA = mm;
+        c.R = S.R; c.ldr = S.mpad; c.sR = mm;
+        c.Xo = S.Xo; c.ldx = S.mpad; c.sX = mm;
+        c.Dd = S.Dd; c.sD = (long)S.Tm * NB * NB; c.ldiag = S.ldiag; c.sL = S.mpad; c.info = info;
+        c.T = S.Tm; c.Tp = 0; c.k = 0;
+        launch_chol_steps<NB>(c, L, s);
+        hipLaunchKernelGGL(k_lq_pad, dim3(blocks, 1, L), dim3(256), 0, s, q_sqrt, m, S.mpad, S.Lq);
+        hipLaunchKernelGGL(k_lqt_linv<NB>, dim3(S.Tm * S.Tm, 1, L), dim3(NTHREADS),
+                           2 * sizeof(double) * NB * (NB + 2), s, S.Lq, S.Xo, S.C, S.Tm);
+    }
+    // Kuf_l = K_l(Z, X), zero padded to Mpad x Npad
+    {
+        (void)hipMemsetAsync(S.Kuf, 0, sizeof(double) * (size_t)S.mpad * S.npad * L, s);
+        GramArgs g{};
+        g.X1 = Z; g.ldx1 = ldz; g.sx1 = 0; g.n1 = m;
+        g.X2 = X; g.ldx2 = ldx; g.sx2 = 0; g.n2 = n;
+        g.theta = thetas; g.stheta = S.G; g.D = d; g.rbf_only = 0;
+        g.out = S.Kuf; g.ldo = S.npad; g.so = (long)S.mpad * S.npad;
+        g.padded = 0; g.tiles_c = S.Tn; g.diag_add = 0.0;
+        launch_gram<NB>(g, S.Tm * S.Tn, L, s);
+    }
+    hipLaunchKernelGGL(k_svgp_cond<NB>, dim3(S.Tm * S.Tn, 1, L), dim3(NTHREADS),
+                       sizeof(double) * (3 * NB * (NB + 2) + 12 * NB), s, S.Xo, S.C, S.Kuf, q_mu, L, m, S.Tm,
+                       S.npad, S.pa, S.pb, S.pm);
+    hipLaunchKernelGGL(k_svgp_moments, dim3(cdiv(n, 256), 1, L), dim3(256), 0, s, S.pa, S.pb, S.pm, X, (long)ldx,
+                       thetas, S.G, d, n, S.npad, S.Tm, g_mu, g_var);
+    const int nve = 512;
+    hipLaunchKernelGGL(k_svgp_ve, dim3(nve), dim3(NTHREADS), 0, s, g_mu, g_var, W, Y, (long)ldy, n, p, L, noise,
+                       S.ve_part);
+    hipLaunchKernelGGL(k_svgp_kl, dim3(L), dim3(NTHREADS), 0, s, q_mu, q_sqrt, m, L, S.kl_part);
+    hipLaunchKernelGGL(k_svgp_final, dim3(1), dim3(64), 0, s, S.ve_part, nve, S.kl_part, L, scale, info, out);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+int svgp_elbo_impl(hipStream_t s, int nb, int n, int m, int l, int p, int d, const double* X, int ldx,
+                   const double* Y, int ldy, const double* Z, int ldz, const double* thetas, const double* q_mu,
+                   const double* q_sqrt, const double* W, double noise, double scale, double jitter, void* ws,
+                   size_t ws_bytes, double* out, double* g_mu, double* g_var, int* info) {
+    if (nb == 64)
+        return svgp_run<64>(s, n, m, l, p, d, X, ldx, Y, ldy, Z, ldz, thetas, q_mu, q_sqrt, W, noise, scale, jitter,
+                            ws, ws_bytes, out, g_mu, g_var, info);
+    return svgp_run<32>(s, n, m, l, p, d, X, ldx, Y, ldy, Z, ldz, thetas, q_mu, q_sqrt, W, noise, scale, jitter, ws,
+                        ws_bytes, out, g_mu, g_var, info);
+}
+
+}  // namespace mfgp

@@ -1,0 +1,201 @@
+"""Device engine: torch-ROCm buffers + calls into libmfgp.so (include/mfgp.h).
+
+PyTorch only provides device memory, streams and graphs here; every FLOP of the
+hot path runs in the hand-written HIP kernels of ``csrc/``.  There is no CPU
+fallback — on a machine without a GPU every compute call raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import MFGPError, check, ptr
+
+
+def theta_size(d: int) -> int:
+    return 2 * d + 4
+
+
+def default_device() -> torch.device:
+    if not torch.cuda.is_available():
+        raise MFGPError("no GPU visible: the MI355X engine has no CPU fallback")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def to_dev(x, device: torch.device) -> torch.Tensor:
+    """float64, contiguous, on `device` (numpy / list / torch accepted)."""
+    if isinstance(x, torch.Tensor):
+        t = x.detach()
+    else:
+        t = torch.as_tensor(np.asarray(x, dtype=np.float64))
+    return t.to(device=device, dtype=torch.float64).contiguous()
+
+
+class Engine:
+    """One per device: owns the library handle binding and grow-only workspaces."""
+
+    _engines: dict = {}
+
+    def __init__(self, device: torch.device):
+        self.device = device
+        self.index = device.index if device.index is not None else torch.cuda.current_device()
+        self._ws: dict = {}
+        self.lib = _lib.load()
+
+    @classmethod
+    def get(cls, device=None) -> "Engine":
+        device = torch.device(device) if device is not None else default_device()
+        if device.type != "cuda":
+            raise MFGPError(f"MI355X engine needs a GPU device, got {device}")
+        key = device.index if device.index is not None else torch.cuda.current_device()
+        eng = cls._engines.get(key)
+        if eng is None:
+            eng = cls(torch.device("cuda", key))
+            cls._engines[key] = eng
+        return eng
+
+    # ------------------------------------------------------------ plumbing
+    @property
+    def h(self):
+        return _lib.handle(self.index)
+
+    def workspace(self, key: str, nbytes: int) -> torch.Tensor:
+        buf = self._ws.get(key)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(int(nbytes), dtype=torch.uint8, device=self.device)
+            self._ws[key] = buf
+        return buf
+
+    def _size(self, fn, *args) -> int:
+        out = C.c_size_t(0)
+        check(fn(self.h, *args, C.byref(out)), fn.__name__)
+        return out.value
+
+    def tile(self) -> int:
+        return self.lib.mfgp_get_tile(self.h)
+
+    def set_tile(self, nb: int):
+        check(self.lib.mfgp_set_tile(self.h, nb), "mfgp_set_tile")
+
+    # ------------------------------------------------------------ kernels
+    def rbf_gram(self, X1: torch.Tensor, X2: torch.Tensor, params: torch.Tensor) -> torch.Tensor:
+        n1, d = X1.shape
+        n2 = X2.shape[0]
+        K = torch.empty((n1, n2), dtype=torch.float64, device=self.device)
+        check(self.lib.mfgp_rbf_gram(self.h, n1, n2, d, ptr(X1), d, ptr(X2), X2.shape[1], ptr(params), ptr(K), n2),
+              "mfgp_rbf_gram")
+        return K
+
+    def mf_gram(self, X1: torch.Tensor, X2: torch.Tensor, theta: torch.Tensor, diag_add: float = 0.0) -> torch.Tensor:
+        n1, dp1 = X1.shape
+        n2 = X2.shape[0]
+        K = torch.empty((n1, n2), dtype=torch.float64, device=self.device)
+        check(self.lib.mfgp_mf_gram(self.h, n1, n2, dp1 - 1, ptr(X1), dp1, ptr(X2), X2.shape[1], ptr(theta),
+                                    float(diag_add), ptr(K), n2), "mfgp_mf_gram")
+        return K
+
+    def mf_kdiag(self, X: torch.Tensor, theta: torch.Tensor) -> torch.Tensor:
+        n, dp1 = X.shape
+        out = torch.empty((n,), dtype=torch.float64, device=self.device)
+        check(self.lib.mfgp_mf_kdiag(self.h, n, dp1 - 1, ptr(X), dp1, ptr(theta), ptr(out)), "mfgp_mf_kdiag")
+        return out
+
+    def gpr_lml(self, X, Y, theta, want_grad=False):
+        n, dp1 = X.shape
+        p = Y.shape[1]
+        d = dp1 - 1
+        nbytes = self._size(self.lib.mfgp_gpr_workspace_size, n, p, d)
+        ws = self.workspace("gpr", nbytes)
+        out = torch.empty((1 + theta_size(d),), dtype=torch.float64, device=self.device)
+        info = torch.empty((1,), dtype=torch.int32, device=self.device)
+        check(self.lib.mfgp_gpr_lml(self.h, n, p, d, ptr(X), dp1, ptr(Y), p, ptr(theta), int(want_grad), ptr(ws),
+                                    ws.numel(), ptr(out), ptr(info)), "mfgp_gpr_lml")
+        return out, info
+
+    def gpr_adam_step(self, X, Y, st: "AdamState", loss_hist: torch.Tensor, out: torch.Tensor, info: torch.Tensor):
+        n, dp1 = X.shape
+        p = Y.shape[1]
+        d = dp1 - 1
+        nbytes = self._size(self.lib.mfgp_gpr_workspace_size, n, p, d)
+        ws = self.workspace("gpr", nbytes)
+        check(self.lib.mfgp_gpr_adam_step(self.h, n, p, d, ptr(X), dp1, ptr(Y), p, ptr(st.theta), ptr(st.u),
+                                          ptr(st.m), ptr(st.v), ptr(st.trainable), ptr(st.tie), ptr(st.step), st.lr, st.b1,
+                                          st.b2, st.eps, ptr(loss_hist), ptr(ws), ws.numel(), ptr(out), ptr(info)),
+              "mfgp_gpr_adam_step")
+
+    def theta_from_u(self, u: torch.Tensor, theta: torch.Tensor, noise_index: int):
+        check(self.lib.mfgp_theta_from_u(self.h, ptr(u), ptr(theta), u.numel(), noise_index), "mfgp_theta_from_u")
+
+    def gpr_predict(self, X, Y, Xs, theta):
+        n, dp1 = X.shape
+        p = Y.shape[1]
+        d = dp1 - 1
+        ns = Xs.shape[0]
+        nbytes = self._size(self.lib.mfgp_gpr_predict_workspace_size, n, p, d, ns)
+        ws = self.workspace("pred", nbytes)
+        mean = torch.empty((ns, p), dtype=torch.float64, device=self.device)
+        var = torch.empty((ns,), dtype=torch.float64, device=self.device)
+        info = torch.empty((1,), dtype=torch.int32, device=self.device)
+        check(self.lib.mfgp_gpr_predict(self.h, n, p, d, ns, ptr(X), dp1, ptr(Y), p, ptr(Xs), Xs.shape[1],
+                                        ptr(theta), ptr(ws), ws.numel(), ptr(mean), p, ptr(var), ptr(info)),
+              "mfgp_gpr_predict")
+        return mean, var, info
+
+    def potrf_inv(self, A: torch.Tensor):
+        """A: [n, n] or [b, n, n] SPD -> (Linv, diag(L), info[b])."""
+        batched = A.dim() == 3
+        A3 = A if batched else A.unsqueeze(0)
+        A3 = A3.contiguous()
+        b, n, _ = A3.shape
+        nbytes = self._size(self.lib.mfgp_potrf_inv_workspace_size, n, b)
+        ws = self.workspace("potrf", nbytes)
+        Linv = torch.empty_like(A3)
+        ld = torch.empty((b, n), dtype=torch.float64, device=self.device)
+        info = torch.empty((b,), dtype=torch.int32, device=self.device)
+        check(self.lib.mfgp_potrf_inv(self.h, n, b, ptr(A3), n, n * n, ptr(ws), ws.numel(), ptr(Linv), n, n * n,
+                                      ptr(ld), ptr(info)), "mfgp_potrf_inv")
+        if not batched:
+            return Linv[0], ld[0], info
+        return Linv, ld, info
+
+    def svgp_elbo(self, X, Y, Z, thetas, q_mu, q_sqrt, W, noise, scale, jitter=1e-6):
+        n, dp1 = X.shape
+        d = dp1 - 1
+        p = Y.shape[1]
+        m = Z.shape[0]
+        L = thetas.shape[0]
+        nbytes = self._size(self.lib.mfgp_svgp_workspace_size, n, m, L, p, d)
+        ws = self.workspace("svgp", nbytes)
+        out = torch.empty((3,), dtype=torch.float64, device=self.device)
+        g_mu = torch.empty((L, n), dtype=torch.float64, device=self.device)
+        g_var = torch.empty((L, n), dtype=torch.float64, device=self.device)
+        info = torch.empty((L,), dtype=torch.int32, device=self.device)
+        check(self.lib.mfgp_svgp_elbo(self.h, n, m, L, p, d, ptr(X), dp1, ptr(Y), p, ptr(Z), Z.shape[1],
+                                      ptr(thetas), ptr(q_mu), ptr(q_sqrt), ptr(W), float(noise), float(scale),
+                                      float(jitter), ptr(ws), ws.numel(), ptr(out), ptr(g_mu), ptr(g_var),
+                                      ptr(info)), "mfgp_svgp_elbo")
+        return out, g_mu, g_var, info
+
+    def selftest_mfma(self) -> np.ndarray:
+        out = torch.zeros((16, 16), dtype=torch.float64, device=self.device)
+        check(self.lib.mfgp_selftest_mfma(self.h, ptr(out)), "mfgp_selftest_mfma")
+        return out.cpu().numpy()
+
+
+class AdamState:
+    """Device-resident Keras-Adam state over the unconstrained theta vector."""
+
+    def __init__(self, device, u: np.ndarray, trainable: np.ndarray, tie: np.ndarray, lr: float, b1=0.9, b2=0.999,
+                 eps=1e-7):
+        f32 = lambda x: float(np.float32(x))   # TF 2.10 OptimizerV2 hyper variables are float32
+        self.u = torch.tensor(u, dtype=torch.float64, device=device)
+        self.theta = torch.empty_like(self.u)
+        self.m = torch.zeros_like(self.u)
+        self.v = torch.zeros_like(self.u)
+        self.trainable = torch.tensor(trainable.astype(np.uint8), device=device)
+        self.tie = torch.tensor(tie.astype(np.int32), device=device)
+        self.step = torch.zeros((1,), dtype=torch.int32, device=device)
+        self.lr, self.b1, self.b2, self.eps = f32(lr), f32(b1), f32(b2), float(eps)

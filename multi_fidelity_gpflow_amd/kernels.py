@@ -1,0 +1,143 @@
+"""GPflow-compatible kernels whose arithmetic runs in libmfgp.so.
+
+* ``SquaredExponential`` / ``RBF`` — gpflow.kernels.SquaredExponential (K1, rbf mode).
+* ``LinearMultiFidelityKernel`` — mfgpflow/linear.py:12-136 (K1, multi-fidelity mode):
+  ``K(X, X2=None, ith_output_dim=0)`` and ``K_diag(X, ith_output_dim=0)``.
+* ``LinearCoregionalization`` / ``SeparateIndependent`` — the multi-output
+  containers of GPflow used by mfgpflow/linear_svgp.py:122 and
+  mfgpflow/singlebin_svgp.py:47.
+"""
+from __future__ import annotations
+
+import copy
+
+import numpy as np
+import torch
+
+from .engine import Engine, theta_size, to_dev
+from .params import Module, Parameter, as_result, positive, set_trainable
+
+
+class Kernel(Module):
+    """gpflow.kernels.Kernel call protocol: ``kernel(X, X2=None, full_cov=True)``."""
+
+    def __call__(self, X, X2=None, *, full_cov: bool = True, presliced: bool = False):
+        if not full_cov:
+            if X2 is not None:
+                raise ValueError("Ambiguous inputs: `not full_cov` and `X2` are not compatible.")
+            return self.K_diag(X)
+        return self.K(X, X2)
+
+
+class SquaredExponential(Kernel):
+    """gpflow.kernels.SquaredExponential: k(x, x') = variance * exp(-|x - x'|^2 / (2 l^2))."""
+
+    def __init__(self, variance=1.0, lengthscales=1.0, active_dims=None):
+        self.variance = Parameter(variance, transform=positive())
+        self.lengthscales = Parameter(lengthscales, transform=positive())
+        self.active_dims = active_dims
+
+    @property
+    def ard(self) -> bool:
+        return self.lengthscales.shape != ()
+
+    def lengthscale_vector(self, d: int) -> np.ndarray:
+        ls = self.lengthscales.numpy()
+        return np.broadcast_to(ls, (d,)).astype(np.float64) if ls.ndim == 0 else ls.astype(np.float64)
+
+    def _params(self, d, device):
+        return torch.tensor(np.concatenate([[float(self.variance.numpy())], self.lengthscale_vector(d)]),
+                            dtype=torch.float64, device=device)
+
+    def K(self, X, X2=None):
+        eng = Engine.get()
+        X1 = to_dev(X, eng.device)
+        X2d = X1 if X2 is None else to_dev(X2, eng.device)
+        return as_result(eng.rbf_gram(X1, X2d, self._params(X1.shape[1], eng.device)))
+
+    def K_diag(self, X):
+        eng = Engine.get()
+        n = np.shape(X)[0]
+        return as_result(torch.full((n,), float(self.variance.numpy()), dtype=torch.float64, device=eng.device))
+
+
+RBF = SquaredExponential
+
+
+class LinearMultiFidelityKernel(Kernel):
+    """Kennedy–O'Hagan AR(1) multi-fidelity kernel (mfgpflow/linear.py:12-136).
+
+    f_H(x) = rho f_L(x) + delta(x):  K = [K_LL, rho K_LH; rho K_HL, rho^2 K_HH + K_delta].
+    The last input column is the fidelity flag (0.0 = LF, 1.0 = HF; anything else
+    gives zero rows, linear.py:67-70).  ``rho`` has shape (num_output_dims, 1) but
+    the model-level calls only ever use rho[0] (linear.py:90).
+    """
+
+    def __init__(self, kernel_L, kernel_delta, num_output_dims, use_rho=True):
+        self.kernel_L = kernel_L
+        self.kernel_delta = kernel_delta
+        self.rho = Parameter(np.ones((num_output_dims, 1)), transform=positive())
+        if not use_rho:
+            set_trainable(self.rho, False)
+
+    # -- theta layout of include/mfgp.h: [vL, lL(d), vD, lD(d), rho, noise]
+    def theta_vector(self, d: int, ith_output_dim: int = 0, noise: float = 0.0) -> np.ndarray:
+        return np.concatenate([
+            [float(self.kernel_L.variance.numpy())], self.kernel_L.lengthscale_vector(d),
+            [float(self.kernel_delta.variance.numpy())], self.kernel_delta.lengthscale_vector(d),
+            [float(self.rho.numpy()[ith_output_dim, 0])], [noise]])
+
+    def theta(self, d: int, device, ith_output_dim: int = 0, noise: float = 0.0) -> torch.Tensor:
+        return torch.tensor(self.theta_vector(d, ith_output_dim, noise), dtype=torch.float64, device=device)
+
+    def K(self, X, X2=None, ith_output_dim=0):
+        eng = Engine.get()
+        X1 = to_dev(X, eng.device)
+        X2d = X1 if X2 is None else to_dev(X2, eng.device)
+        d = X1.shape[1] - 1
+        return as_result(eng.mf_gram(X1, X2d, self.theta(d, eng.device, ith_output_dim)))
+
+    def K_diag(self, X, ith_output_dim=0):
+        eng = Engine.get()
+        X1 = to_dev(X, eng.device)
+        d = X1.shape[1] - 1
+        return as_result(eng.mf_kdiag(X1, self.theta(d, eng.device, ith_output_dim)))
+
+
+class Combination(Kernel):
+    def __init__(self, kernels):
+        self.kernels = list(kernels)
+
+    @property
+    def num_latent_gps(self) -> int:
+        return len(self.kernels)
+
+    def latent_thetas(self, d: int, device) -> torch.Tensor:
+        return torch.tensor(np.stack([k.theta_vector(d) for k in self.kernels]), dtype=torch.float64, device=device)
+
+
+class SeparateIndependent(Combination):
+    """gpflow.kernels.SeparateIndependent (singlebin_svgp.py:47)."""
+
+    def K(self, X, X2=None, full_output_cov=False):
+        return as_result(torch.stack([torch.Tensor(k.K(X, X2)) for k in self.kernels], dim=0))
+
+    def K_diag(self, X, full_output_cov=False):
+        return as_result(torch.stack([torch.Tensor(k.K_diag(X)) for k in self.kernels], dim=1))
+
+
+class LinearCoregionalization(Combination):
+    """gpflow.kernels.LinearCoregionalization (linear_svgp.py:122): f = W g."""
+
+    def __init__(self, kernels, W):
+        super().__init__(kernels)
+        self.W = W if isinstance(W, Parameter) else Parameter(W)
+
+    @property
+    def num_latent_gps(self) -> int:
+        return self.W.shape[-1]
+
+
+def deepcopy_kernel(k):
+    """copy.deepcopy of a kernel (linear_svgp.py:121 deep-copies per latent)."""
+    return copy.deepcopy(k)

@@ -1,0 +1,312 @@
+"""MultiFidelityGPModel — drop-in for mfgpflow.linear.MultiFidelityGPModel.
+
+Reference: mfgpflow/linear.py:138-234 (constructor, optimize) plus the GPflow 2.9
+GPR methods it inherits (log_marginal_likelihood, training_loss, predict_f,
+predict_y).  Every evaluation runs on the GPU through libmfgp.so:
+
+  log_marginal_likelihood  -> mfgp_gpr_lml           (K1 gram, K2 tile Cholesky, K3, K4)
+  optimize(use_adam=True)  -> mfgp_gpr_adam_step     (value + analytic grad + Keras Adam on
+                                                      device, captured in a hipGraph)
+  optimize(use_adam=False) -> scipy L-BFGS-B on the host, value+grad on the device
+  predict_f                -> mfgp_gpr_predict       (K1, K2, K6)
+
+Behavioural quirks of the reference that are reproduced:
+  * one Gram / Cholesky shared by all P outputs; only rho[0] is used;
+  * the likelihood noise starts at 1e-3, fixed; ``unfix_noise_after`` has no
+    effect in the Adam path (the reference's tf.function traced the variable list
+    before set_trainable), but the L-BFGS path does train it in its second pass;
+  * ``loss_history`` records the pre-step loss (-LML) of every iteration.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ._lib import MFGPError
+from .engine import AdamState, Engine, theta_size, to_dev
+from .kernels import LinearMultiFidelityKernel
+from .params import Module, Parameter, as_result, positive, set_trainable
+
+
+class CholeskyError(MFGPError):
+    """Analogue of TF's InvalidArgumentError('Cholesky decomposition was not successful')."""
+
+
+class Gaussian(Module):
+    """gpflow.likelihoods.Gaussian: variance >= 1e-6 via Shift(1e-6) o Softplus."""
+
+    DEFAULT_VARIANCE_LOWER_BOUND = 1e-6
+
+    def __init__(self, variance=1.0, variance_lower_bound=DEFAULT_VARIANCE_LOWER_BOUND):
+        self.variance = Parameter(variance, transform=positive(lower=variance_lower_bound))
+
+
+class _ThetaMap:
+    """Maps the model's Parameters onto the device theta vector
+    [vL, lL(d), vD, lD(d), rho0, noise] of include/mfgp.h."""
+
+    def __init__(self, model: "MultiFidelityGPModel", d: int):
+        k = model.kernel
+        self.d = d
+        self.entries = []   # (Parameter, index tuple or None)
+        self.entries.append((k.kernel_L.variance, None))
+        for i in range(d):
+            self.entries.append((k.kernel_L.lengthscales, None if k.kernel_L.lengthscales.shape == () else (i,)))
+        self.entries.append((k.kernel_delta.variance, None))
+        for i in range(d):
+            self.entries.append((k.kernel_delta.lengthscales,
+                                 None if k.kernel_delta.lengthscales.shape == () else (i,)))
+        self.entries.append((k.rho, (0, 0)))
+        self.entries.append((model.likelihood.variance, None))
+        assert len(self.entries) == theta_size(d)
+        self.noise_index = theta_size(d) - 1
+
+    def _get(self, p: Parameter, idx, which: str):
+        arr = p.numpy() if which == "c" else p.unconstrained_variable
+        return float(arr if idx is None else arr[idx])
+
+    def theta(self) -> np.ndarray:
+        return np.array([self._get(p, i, "c") for p, i in self.entries])
+
+    def u(self) -> np.ndarray:
+        return np.array([self._get(p, i, "u") for p, i in self.entries])
+
+    def trainable(self) -> np.ndarray:
+        return np.array([p.trainable for p, _ in self.entries], dtype=bool)
+
+    def tie(self) -> np.ndarray:
+        ids, out = {}, []
+        for p, i in self.entries:
+            key = (id(p), i)
+            out.append(ids.setdefault(key, len(ids)))
+        return np.array(out, dtype=np.int32)
+
+    def set_u(self, u: np.ndarray):
+        for (p, idx), val in zip(self.entries, u):
+            if idx is None:
+                p.unconstrained_variable = np.full(p.shape, val)
+            else:
+                arr = p.unconstrained_variable.copy()
+                arr[idx] = val
+                p.unconstrained_variable = arr
+
+    def grad_to_params(self, g: np.ndarray, with_noise: bool):
+        """Constrained theta-gradient -> unconstrained gradient per trainable variable
+        (sum over tied entries, chain through Softplus)."""
+        groups = {}
+        for (p, idx), gq in zip(self.entries, g):
+            key = (id(p), idx)
+            if key not in groups:
+                groups[key] = [p, idx, 0.0]
+            groups[key][2] += gq
+        return groups
+
+
+class MultiFidelityGPModel(Module):
+    """GPR with the linear multi-fidelity kernel and a shared Gram over P outputs."""
+
+    def __init__(self, X, Y, kernel_L, kernel_delta):
+        Xh = np.asarray(X.cpu().numpy() if isinstance(X, torch.Tensor) else X, dtype=np.float64)
+        Yh = np.asarray(Y.cpu().numpy() if isinstance(Y, torch.Tensor) else Y, dtype=np.float64)
+        if Yh.ndim == 1:
+            Yh = Yh[:, None]
+        num_output_dims = Yh.shape[1]
+        self.kernel = LinearMultiFidelityKernel(kernel_L, kernel_delta, num_output_dims)
+        self.likelihood = Gaussian(variance=1e-3)
+        set_trainable(self.likelihood.variance, False)
+        self.num_output_dims = num_output_dims
+        self.mean_function = None
+        self._Xh, self._Yh = Xh, Yh
+        self._dev = None
+        self.loss_history = []
+
+    # ------------------------------------------------------------ data
+    @property
+    def data(self):
+        return self._Xh, self._Yh
+
+    def _device_data(self):
+        eng = Engine.get()
+        if self._dev is None or self._dev[0].device != eng.device:
+            self._dev = (to_dev(self._Xh, eng.device), to_dev(self._Yh, eng.device))
+        return eng, self._dev[0], self._dev[1]
+
+    @property
+    def input_dim(self) -> int:
+        return self._Xh.shape[1] - 1
+
+    def _theta_map(self) -> _ThetaMap:
+        return _ThetaMap(self, self.input_dim)
+
+    @staticmethod
+    def _raise_info(info: torch.Tensor, what: str):
+        v = int(info.reshape(-1)[0].item())
+        if v != 0:
+            raise CholeskyError(f"{what}: Cholesky decomposition was not successful "
+                                f"(non-positive pivot at row {v}); the input might not be valid.")
+
+    # ------------------------------------------------------------ GPR surface
+    def log_marginal_likelihood(self):
+        eng, X, Y = self._device_data()
+        theta = torch.tensor(self._theta_map().theta(), dtype=torch.float64, device=eng.device)
+        out, info = eng.gpr_lml(X, Y, theta, want_grad=False)
+        self._raise_info(info, "log_marginal_likelihood")
+        return as_result(out[0].clone())
+
+    def maximum_log_likelihood_objective(self):
+        return self.log_marginal_likelihood()
+
+    def training_loss(self):
+        return as_result(-self.log_marginal_likelihood())
+
+    def log_marginal_likelihood_and_grad(self):
+        """(LML, dLML/dtheta) with theta in the include/mfgp.h layout (numpy)."""
+        eng, X, Y = self._device_data()
+        theta = torch.tensor(self._theta_map().theta(), dtype=torch.float64, device=eng.device)
+        out, info = eng.gpr_lml(X, Y, theta, want_grad=True)
+        self._raise_info(info, "log_marginal_likelihood")
+        o = out.cpu().numpy()
+        return float(o[0]), o[1:]
+
+    def predict_f(self, Xnew, full_cov: bool = False, full_output_cov: bool = False):
+        if full_cov or full_output_cov:
+            raise NotImplementedError("predict_f(full_cov=True) is not provided by the MI355X engine yet")
+        eng, X, Y = self._device_data()
+        Xs = to_dev(Xnew, eng.device)
+        theta = torch.tensor(self._theta_map().theta(), dtype=torch.float64, device=eng.device)
+        mean, var, info = eng.gpr_predict(X, Y, Xs, theta)
+        self._raise_info(info, "predict_f")
+        return as_result(mean), as_result(var[:, None].expand(-1, Y.shape[1]).contiguous())
+
+    def predict_y(self, Xnew, full_cov: bool = False, full_output_cov: bool = False):
+        mean, var = self.predict_f(Xnew, full_cov, full_output_cov)
+        return mean, as_result(var + float(self.likelihood.variance.numpy()))
+
+    # ------------------------------------------------------------ training
+    def optimize(self, max_iters=1000, learning_rate=0.01, use_adam=True, unfix_noise_after=500, verbose=True,
+                 graph=True, graph_chunk=50):
+        """mfgpflow/linear.py:190-234."""
+        self.loss_history = []
+        if use_adam:
+            if verbose:
+                print("Optimizing with Adam...")
+            self._optimize_adam(max_iters, learning_rate, unfix_noise_after, verbose, graph, graph_chunk)
+        else:
+            if verbose:
+                print("Optimizing with L-BFGS (Scipy)...")
+            self._optimize_lbfgs(max_iters)
+
+    def _optimize_adam(self, max_iters, lr, unfix_noise_after, verbose, graph, chunk):
+        eng, X, Y = self._device_data()
+        tm = self._theta_map()
+        st = AdamState(eng.device, tm.u(), tm.trainable(), tm.tie(), lr)
+        eng.theta_from_u(st.u, st.theta, tm.noise_index)
+        hist = torch.zeros((max(max_iters, 1),), dtype=torch.float64, device=eng.device)
+        out = torch.empty((1 + theta_size(tm.d),), dtype=torch.float64, device=eng.device)
+        info = torch.zeros((1,), dtype=torch.int32, device=eng.device)
+        # pre-size the workspace outside any capture
+        eng.gpr_lml(X, Y, st.theta, want_grad=False)
+
+        def step():
+            eng.gpr_adam_step(X, Y, st, hist, out, info)
+
+        runner = _StepRunner(step, chunk if graph else 0)
+        report = set(range(0, max_iters, 100)) if verbose else set()
+        done = 0
+        while done < max_iters:
+            n = min(max_iters - done, runner.chunk or 1)
+            nxt = min((r for r in report if r >= done), default=None)
+            if nxt is not None and nxt < done + n:
+                n = nxt - done + 1
+            runner.run(n)
+            done += n
+            if nxt is not None and nxt == done - 1:
+                torch.cuda.current_stream(eng.device).synchronize()
+                i = nxt
+                if i == unfix_noise_after:
+                    print(f"🔹 Unfixing noise at iteration {i}")
+                print(f"🔹 Iteration {i}: Loss = {-float(hist[i].item())}")
+            if verbose and unfix_noise_after < max_iters and done - n <= unfix_noise_after < done \
+                    and unfix_noise_after % 100 != 0:
+                print(f"🔹 Unfixing noise at iteration {unfix_noise_after}")
+        torch.cuda.current_stream(eng.device).synchronize()
+        h = hist[:max_iters].cpu().numpy()
+        self.loss_history = [np.float64(v) for v in h]
+        if int(info.item()) != 0 or not np.all(np.isfinite(h)):
+            bad = int(np.argmax(~np.isfinite(h))) if not np.all(np.isfinite(h)) else max_iters - 1
+            self.loss_history = self.loss_history[:bad + 1]
+            tm.set_u(st.u.cpu().numpy())
+            raise CholeskyError(f"optimize: Cholesky failed at iteration {bad}")
+        tm.set_u(st.u.cpu().numpy())
+
+    def _optimize_lbfgs(self, max_iters):
+        """gpflow.optimizers.Scipy().minimize twice: noise fixed, then trainable
+        (linear.py:230-234).  Value+grad on the device; L-BFGS-B on the host."""
+        from scipy.optimize import minimize
+
+        for phase in (0, 1):
+            if phase == 1:
+                set_trainable(self.likelihood.variance, True)
+            tm = self._theta_map()
+            train = tm.trainable()
+            tie = tm.tie()
+            u_full = tm.u()
+            # one unconstrained variable per trainable tie group
+            groups = []
+            for q in range(len(u_full)):
+                if train[q] and tie[q] not in [tie[g] for g in groups]:
+                    groups.append(q)
+            x0 = np.array([u_full[q] for q in groups])
+
+            def expand(x):
+                u = u_full.copy()
+                for gq, val in zip(groups, x):
+                    u[tie == tie[gq]] = val
+                return u
+
+            def fg(x):
+                u = expand(x)
+                tm.set_u(u)
+                lml, g = self.log_marginal_likelihood_and_grad()
+                sig = 1.0 / (np.exp(-u) + 1.0)
+                gu = np.array([-np.sum(g[tie == tie[gq]]) * sig[gq] for gq in groups])
+                self.loss_history.append(np.float64(-lml))
+                return -lml, gu
+
+            res = minimize(fg, x0, jac=True, method="L-BFGS-B", options={"maxiter": max_iters})
+            tm.set_u(expand(res.x))
+
+
+class _StepRunner:
+    """Runs a step function n times: eagerly, or replaying a hipGraph of `chunk`
+    captured steps (torch.cuda.CUDAGraph is the HIP graph API on ROCm)."""
+
+    def __init__(self, step, chunk: int):
+        self.step = step
+        self.chunk = chunk
+        self.graphs = {}
+
+    def _graph(self, n):
+        g = self.graphs.get(n)
+        if g is None:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(n):
+                    self.step()
+            self.graphs[n] = g
+        return g
+
+    def run(self, n: int):
+        if self.chunk <= 0 or n < 4:
+            for _ in range(n):
+                self.step()
+            return
+        full, rem = divmod(n, self.chunk)
+        for _ in range(full):
+            self._graph(self.chunk).replay()
+        if rem:
+            if rem < 4:
+                for _ in range(rem):
+                    self.step()
+            else:
+                self._graph(rem).replay()
