@@ -1,0 +1,258 @@
+#!/usr/bin/env python
+"""Benchmark: Goku z=0 P(k) 1128LF/36HF multi-bin GPR on MI355X.
+
+Metric (BASELINE.json): LML evals/sec + train+predict wall-clock, Goku multi-bin.
+
+  step      = one MultiFidelityGPModel.optimize(use_adam=True) iteration on the
+              Goku training set: LML value + analytic gradient + Keras-Adam update
+              (mfgpflow/linear.py:203-214), executed by libmfgp.so from a hipGraph.
+  value     = Goku LML value+grad evaluations per second, whole job.  With N GPUs
+              the 64 k-bins are sharded into N contiguous blocks, one independent
+              per-shard-theta model per rank (SURVEY §8(e) "embarrassing mode"):
+              one step = every rank evaluates its block, so one step covers the
+              whole 64-bin Goku LML -> value = steps / max-over-ranks time
+              ("scaling": "strong": total work fixed; the Gram/Cholesky is
+              replicated per rank, so efficiency is Amdahl-limited by design).
+  inputs    = rank 0 reads the reference's Goku txt files (tests/golden/data) and
+              RCCL-broadcasts them once; no collective inside the timed loop.
+  extras    = train_predict_s: the notebook protocol optimize(1000, lr=0.1) +
+              predict_f(X_test) wall-clock (max over ranks); roofline of the
+              dominant kernel family from live hipEvent phase times; cpu_baseline:
+              the fp64 oracle (oracle/mfgp_oracle.py) timed on this host (rank 0, N=1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+GOKU = os.path.join(ROOT, "tests", "golden", "data", "matter_power_1128_Box1000_Part750_36_Box1000_Part3000_z0")
+FP64_PEAK_TFLOPS = 78.6   # MI355X dense FP64 (vector = matrix on gfx950), MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0
+
+
+def load_goku():
+    from multi_fidelity_gpflow_amd.data import PowerSpecs, multifidelity_training_set
+    ps = PowerSpecs()
+    ps.read_from_txt(GOKU)
+    return multifidelity_training_set(ps)
+
+
+def broadcast_inputs(rank, world, device):
+    """Rank 0 reads the txt files; one RCCL broadcast of the packed inputs."""
+    if rank == 0:
+        X, Y, Xt, Yt = load_goku()
+        hdr = torch.tensor([X.shape[0], X.shape[1], Y.shape[1], Xt.shape[0]], dtype=torch.int64, device=device)
+    else:
+        hdr = torch.zeros(4, dtype=torch.int64, device=device)
+    if world > 1:
+        dist.broadcast(hdr, 0)
+    n, dx, p, ns = [int(v) for v in hdr.tolist()]
+    size = n * dx + n * p + ns * dx + ns * p
+    if rank == 0:
+        buf = torch.tensor(np.concatenate([X.ravel(), Y.ravel(), Xt.ravel(), Yt.ravel()]), dtype=torch.float64,
+                           device=device)
+    else:
+        buf = torch.empty(size, dtype=torch.float64, device=device)
+    if world > 1:
+        dist.broadcast(buf, 0)
+    h = buf.cpu().numpy()
+    o = 0
+    X = h[o:o + n * dx].reshape(n, dx); o += n * dx
+    Y = h[o:o + n * p].reshape(n, p); o += n * p
+    Xt = h[o:o + ns * dx].reshape(ns, dx); o += ns * dx
+    Yt = h[o:o + ns * p].reshape(ns, p)
+    return X, Y, Xt, Yt
+
+
+def bin_block(p, rank, world):
+    edges = np.linspace(0, p, world + 1).round().astype(int)
+    return int(edges[rank]), int(edges[rank + 1])
+
+
+def make_model(X, Yr):
+    import multi_fidelity_gpflow_amd as M
+    d = X.shape[1] - 1
+    return M.MultiFidelityGPModel(X, Yr, M.SquaredExponential(lengthscales=np.ones(d), variance=1.0),
+                                  M.SquaredExponential(lengthscales=np.ones(d), variance=1.0))
+
+
+def step_flops(n, p, d):
+    """one LML value+grad evaluation (fp64)."""
+    gram = (n * (n + 1) / 2) * (3 * d + 6)
+    return gram + n ** 3 / 3 + n * n * p + 2 * n ** 3 / 3 + 2 * n * n * p + n * (n + 1) / 2 * (4 * d + 10)
+
+
+def roofline(model, n, p, d, reps=10):
+    """Dominant kernel family from live hipEvent phase times (launch stream)."""
+    from multi_fidelity_gpflow_amd.engine import gpr_phase_times
+    eng, X, Y = model._device_data()
+    theta = torch.tensor(model._theta_map().theta(), dtype=torch.float64, device=eng.device)
+    gpr_phase_times(eng, X, Y, theta)   # warm
+    acc = np.zeros(6)
+    for _ in range(reps):
+        acc += np.array(gpr_phase_times(eng, X, Y, theta))
+    ms = acc / reps
+    names = ["rhs_init", "gram", "chol_steps", "alpha", "grad", "finalize"]
+    nb = eng.tile()
+    T = -(-n // nb)
+    # algorithmic work per phase (SURVEY §8(d) figures)
+    flops = {
+        "gram": (n * (n + 1) / 2) * (3 * d + 6),
+        "chol_steps": n ** 3 / 3 + n ** 3 / 3 + n * n * p,   # potrf + L^{-1} (trtri) + Z = L^{-1} Y
+        "alpha": n * n * p,
+        "grad": n ** 3 / 3 + n * n * p + n * (n + 1) / 2 * (4 * d + 10),
+    }
+    launches = {"gram": 1, "chol_steps": T, "alpha": 1, "grad": 1}
+    dom = max(flops, key=lambda k: ms[names.index(k)])
+    t_ms = ms[names.index(dom)]
+    per_launch_ms = t_ms / launches[dom]
+    per_launch_flop = flops[dom] / launches[dom]
+    achieved = per_launch_flop / (per_launch_ms * 1e-3) / 1e12
+    return {
+        "kernel": {"chol_steps": "k_chol_step", "gram": "k_gram", "alpha": "k_alpha", "grad": "k_grad"}[dom],
+        "bound": "mfma",
+        "achieved": round(achieved, 4),
+        "peak": FP64_PEAK_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": round(achieved / FP64_PEAK_TFLOPS, 5),
+        "traffic": None,
+        "launches_per_step": launches[dom],
+        "avg_launch_us": round(per_launch_ms * 1e3, 3),
+        "flop_per_launch": per_launch_flop,
+        "phase_ms": {k: round(float(v), 4) for k, v in zip(names, ms)},
+    }
+
+
+def cpu_baseline(X, Y, budget_s=20.0):
+    """fp64 oracle (CPU restatement of the reference path) on this host's cores."""
+    from oracle import mfgp_oracle as O
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:
+        cores = os.cpu_count() or 1
+    p0 = O.MFParams.initial(X.shape[1] - 1, Y.shape[1])
+    O.gpr_lml_and_grad(X, Y, p0)   # warm
+    t0 = time.perf_counter()
+    k = 0
+    while time.perf_counter() - t0 < budget_s or k < 3:
+        O.gpr_lml_and_grad(X, Y, p0)
+        k += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(k / dt, 4), "unit": "LML value+grad evals/s", "cores": int(cores), "kind": "port",
+            "sample": f"{k} Goku LML value+grad evaluations (oracle/mfgp_oracle.py gpr_lml_and_grad, fp64 "
+                      f"NumPy/SciPy) at the initial theta, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--tile", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-train-predict", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    from multi_fidelity_gpflow_amd.engine import Engine
+    eng = Engine.get(device)
+    if args.tile:
+        eng.set_tile(args.tile)
+
+    X, Y, Xt, Yt = broadcast_inputs(rank, world, device)
+    n, d, P = X.shape[0], X.shape[1] - 1, Y.shape[1]
+    b0, b1 = bin_block(P, rank, world)
+    Yr = np.ascontiguousarray(Y[:, b0:b1])
+
+    model = make_model(X, Yr)
+    K, W = args.steps, args.warmup
+    sess = model.adam_session(0.1, K + W, graph=True, graph_chunk=50)
+    sess.run(W)
+    sess.sync()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sess.run(K)
+    sess.sync()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([dt], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    sess.finish()
+
+    # train + predict wall-clock (notebook protocol, fresh model)
+    tp = None
+    if not args.no_train_predict:
+        m2 = make_model(X, Yr)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        m2.optimize(max_iters=1000, learning_rate=0.1, use_adam=True, unfix_noise_after=500, verbose=False)
+        mean, var = m2.predict_f(Xt)
+        torch.cuda.synchronize()
+        tp = time.perf_counter() - t1
+        if world > 1:
+            t = torch.tensor([tp], dtype=torch.float64, device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            tp = float(t.item())
+
+    roof = roofline(model, n, Yr.shape[1], d)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(X, Y)
+
+    if rank == 0:
+        value = K / dt
+        line = {
+            "metric": "LML evals/sec (Goku 1128LF/36HF multi-bin, value+grad+Adam step)",
+            "value": round(value, 3),
+            "unit": "evals/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": W,
+            "ms_per_step": round(dt / K * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "Goku z=0 P(k) (reference data files, tests/golden/data), RCCL-broadcast from rank 0",
+            "config": {"workload": "goku_multibin_adam_step", "n_lf": 1128, "n_hf": 36, "d": d, "p": P,
+                       "bins_per_rank": Yr.shape[1], "tile": eng.tile(),
+                       "parallelism": f"bins{world}" if world > 1 else "single"},
+            "train_predict_s": None if tp is None else round(tp, 4),
+            "step_tflops": round(step_flops(n, P, d) * value / 1e12, 4),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "published_m1_cpu": {"train_1000_adam_s": 142.36, "evals_per_s": 7.02,
+                                 "source": "notebooks/demo: goku power spectra.ipynb:120"},
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

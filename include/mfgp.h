@@ -89,6 +89,14 @@ int mfgp_gpr_adam_step(mfgp_handle_t h, int n, int p, int d, const double* X, in
                        const int* tie, int* step, double lr, double beta1, double beta2, double eps,
                        double* loss_hist, void* ws, size_t ws_bytes, double* out, int* info);
 
+/* Diagnostic: the mfgp_gpr_lml(want_grad=1) sequence with hipEvents recorded on
+ * the handle's stream between its phases; synchronises and writes the elapsed
+ * milliseconds of [rhs init, gram+first factor, tile Cholesky steps, alpha,
+ * gradient, finalize] into the HOST array ms[6]. */
+int mfgp_gpr_lml_phase_times(mfgp_handle_t h, int n, int p, int d, const double* X, int ldx, const double* Y,
+                             int ldy, const double* theta, void* ws, size_t ws_bytes, double* out, int* info,
+                             float* ms);
+
 /* theta[q] = softplus(u[q]) (+1e-6 for q == noise_index); GPflow positive(). */
 int mfgp_theta_from_u(mfgp_handle_t h, const double* u, double* theta, int g, int noise_index);
 

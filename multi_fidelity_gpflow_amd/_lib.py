@@ -35,6 +35,7 @@ SIGNATURES = {
     "mfgp_gpr_lml": [_p, _i, _i, _i, _p, _i, _p, _i, _p, _i, _p, _sz, _p, _p],
     "mfgp_gpr_adam_step": [_p, _i, _i, _i, _p, _i, _p, _i, _p, _p, _p, _p, _p, _p, _p, _d, _d, _d, _d, _p, _p,
                            _sz, _p, _p],
+    "mfgp_gpr_lml_phase_times": [_p, _i, _i, _i, _p, _i, _p, _i, _p, _p, _sz, _p, _p, C.POINTER(C.c_float)],
     "mfgp_theta_from_u": [_p, _p, _p, _i, _i],
     "mfgp_gpr_predict_workspace_size": [_p, _i, _i, _i, _i, C.POINTER(_sz)],
     "mfgp_gpr_predict": [_p, _i, _i, _i, _i, _p, _i, _p, _i, _p, _i, _p, _p, _sz, _p, _i, _p, _p],

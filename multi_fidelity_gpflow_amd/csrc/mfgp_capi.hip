@@ -94,22 +94,59 @@ static void gram_lml_and_factor(hipStream_t s, const GprLayout& L, int n, int p,
     launch_chol_steps<NB>(c, 1, s);
 }
 
+// Optional per-phase event marks (diagnostic timing; never used on the hot path).
+struct PhaseMarks {
+    hipEvent_t ev[8];
+    int count = 0;
+    void mark(hipStream_t s) { (void)hipEventRecord(ev[count++], s); }
+};
+
 template <int NB>
 static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X, int ldx, const double* Y, int ldy,
                           double* theta, int want_grad, void* ws, size_t ws_bytes, double* out, int* info,
-                          const FinArgs* adam) {
+                          const FinArgs* adam, PhaseMarks* pm = nullptr) {
     const GprLayout L = gpr_layout(NB, n, p, d, ws);
     if (ws_bytes < L.bytes) return MFGP_ERR_WORKSPACE;
     hipStream_t s = h->stream;
-    (void)hipMemsetAsync(info, 0, sizeof(int), s);
-    gram_lml_and_factor<NB>(s, L, n, p, d, X, ldx, Y, ldy, theta, info);
     const long ldr = L.npad + L.ppad;
+    if (pm) pm->mark(s);
+    (void)hipMemsetAsync(info, 0, sizeof(int), s);
+    {
+        const long total = (long)L.npad * ldr;
+        const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
+        hipLaunchKernelGGL(k_rhs_init, dim3(blocks), dim3(256), 0, s, L.R, ldr, 0L, L.npad, L.ppad, Y, (long)ldy,
+                           0L, n, p);
+    }
+    if (pm) pm->mark(s);
+    {
+        GramArgs g{};
+        g.X1 = X; g.ldx1 = ldx; g.sx1 = 0; g.n1 = n;
+        g.X2 = X; g.ldx2 = ldx; g.sx2 = 0; g.n2 = n;
+        g.theta = theta; g.stheta = 0; g.D = d; g.rbf_only = 0;
+        g.out = L.A; g.ldo = L.npad; g.so = 0;
+        g.padded = 1; g.npad = L.npad; g.tiles_c = L.T; g.add_noise = 1; g.diag_add = 0.0;
+        g.Dd = L.Dd; g.sD = 0; g.ldiag = L.ldiag; g.sL = 0; g.info = info;
+        launch_gram<NB>(g, L.T * (L.T + 1) / 2, 1, s);
+    }
+    if (pm) pm->mark(s);
+    {
+        CholArgs c{};
+        c.A = L.A; c.lda = L.npad; c.sA = 0;
+        c.R = L.R; c.ldr = ldr; c.sR = 0;
+        c.Xo = L.Xo; c.ldx = ldr; c.sX = 0;
+        c.Dd = L.Dd; c.sD = 0; c.ldiag = L.ldiag; c.sL = 0; c.info = info;
+        c.T = L.T; c.Tp = L.Tp; c.k = 0;
+        launch_chol_steps<NB>(c, 1, s);
+    }
+    if (pm) pm->mark(s);
     AlphaArgs aa{L.Xo, ldr, L.alpha, (long)L.ppad, L.zpart, L.T, L.Tp, n, p};
     launch_alpha<NB>(aa, s);
+    if (pm) pm->mark(s);
     if (want_grad) {
         GradArgs ga{L.Xo, ldr, L.alpha, (long)L.ppad, X, (long)ldx, theta, L.gpart, L.gstride, L.T, L.Tp, n, p, d};
         launch_grad<NB>(ga, s);
     }
+    if (pm) pm->mark(s);
     FinArgs f{};
     if (adam) f = *adam;
     f.zpart = L.zpart; f.nz = L.T * L.Tp;
@@ -119,6 +156,7 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
     f.out = out;
     f.adam = adam != nullptr;
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(NTHREADS), 0, s, f);
+    if (pm) pm->mark(s);
     return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;
 }
 
@@ -405,6 +443,27 @@ int mfgp_gpr_adam_step(mfgp_handle_t h, int n, int p, int d, const double* X, in
     f.noise_index = theta_size(d) - 1;
     if (h->nb == 64) return gpr_value_grad<64>(h, n, p, d, X, ldx, Y, ldy, theta, 1, ws, ws_bytes, out, info, &f);
     return gpr_value_grad<32>(h, n, p, d, X, ldx, Y, ldy, theta, 1, ws, ws_bytes, out, info, &f);
+}
+
+int mfgp_gpr_lml_phase_times(mfgp_handle_t h, int n, int p, int d, const double* X, int ldx, const double* Y,
+                             int ldy, const double* theta, void* ws, size_t ws_bytes, double* out, int* info,
+                             float* ms) {
+    CHECK_H(h);
+    CHECK_D(d);
+    if (n < 1 || p < 1 || !X || !Y || !theta || !ws || !out || !info || !ms) return MFGP_ERR_ARG;
+    PhaseMarks pm;
+    for (int i = 0; i < 7; ++i) (void)hipEventCreate(&pm.ev[i]);
+    int rc = (h->nb == 64)
+                 ? gpr_value_grad<64>(h, n, p, d, X, ldx, Y, ldy, (double*)theta, 1, ws, ws_bytes, out, info,
+                                      nullptr, &pm)
+                 : gpr_value_grad<32>(h, n, p, d, X, ldx, Y, ldy, (double*)theta, 1, ws, ws_bytes, out, info,
+                                      nullptr, &pm);
+    if (rc == MFGP_OK) {
+        (void)hipEventSynchronize(pm.ev[pm.count - 1]);
+        for (int i = 0; i + 1 < pm.count; ++i) (void)hipEventElapsedTime(&ms[i], pm.ev[i], pm.ev[i + 1]);
+    }
+    for (int i = 0; i < 7; ++i) (void)hipEventDestroy(pm.ev[i]);
+    return rc;
 }
 
 int mfgp_theta_from_u(mfgp_handle_t h, const double* u, double* theta, int g, int noise_index) {

@@ -199,3 +199,19 @@ class AdamState:
         self.tie = torch.tensor(tie.astype(np.int32), device=device)
         self.step = torch.zeros((1,), dtype=torch.int32, device=device)
         self.lr, self.b1, self.b2, self.eps = f32(lr), f32(b1), f32(b2), float(eps)
+
+
+def gpr_phase_times(eng: Engine, X, Y, theta):
+    """Per-phase device times (ms) of one value+grad evaluation, measured with
+    hipEvents on the launch stream: [rhs_init, gram, chol_steps, alpha, grad, finalize]."""
+    n, dp1 = X.shape
+    p = Y.shape[1]
+    d = dp1 - 1
+    nbytes = eng._size(eng.lib.mfgp_gpr_workspace_size, n, p, d)
+    ws = eng.workspace("gpr", nbytes)
+    out = torch.empty((1 + theta_size(d),), dtype=torch.float64, device=eng.device)
+    info = torch.empty((1,), dtype=torch.int32, device=eng.device)
+    ms = (C.c_float * 6)()
+    check(eng.lib.mfgp_gpr_lml_phase_times(eng.h, n, p, d, ptr(X), dp1, ptr(Y), p, ptr(theta), ptr(ws), ws.numel(),
+                                           ptr(out), ptr(info), ms), "mfgp_gpr_lml_phase_times")
+    return [float(v) for v in ms]

@@ -196,48 +196,26 @@ class MultiFidelityGPModel(Module):
                 print("Optimizing with L-BFGS (Scipy)...")
             self._optimize_lbfgs(max_iters)
 
+    def adam_session(self, learning_rate: float, max_iters: int, graph: bool = True, graph_chunk: int = 50):
+        """Device-resident Adam training state (used by optimize() and bench.py)."""
+        return AdamSession(self, learning_rate, max_iters, graph, graph_chunk)
+
     def _optimize_adam(self, max_iters, lr, unfix_noise_after, verbose, graph, chunk):
-        eng, X, Y = self._device_data()
-        tm = self._theta_map()
-        st = AdamState(eng.device, tm.u(), tm.trainable(), tm.tie(), lr)
-        eng.theta_from_u(st.u, st.theta, tm.noise_index)
-        hist = torch.zeros((max(max_iters, 1),), dtype=torch.float64, device=eng.device)
-        out = torch.empty((1 + theta_size(tm.d),), dtype=torch.float64, device=eng.device)
-        info = torch.zeros((1,), dtype=torch.int32, device=eng.device)
-        # pre-size the workspace outside any capture
-        eng.gpr_lml(X, Y, st.theta, want_grad=False)
-
-        def step():
-            eng.gpr_adam_step(X, Y, st, hist, out, info)
-
-        runner = _StepRunner(step, chunk if graph else 0)
-        report = set(range(0, max_iters, 100)) if verbose else set()
+        sess = self.adam_session(lr, max_iters, graph, chunk)
+        report = list(range(0, max_iters, 100)) if verbose else []
         done = 0
-        while done < max_iters:
-            n = min(max_iters - done, runner.chunk or 1)
-            nxt = min((r for r in report if r >= done), default=None)
-            if nxt is not None and nxt < done + n:
-                n = nxt - done + 1
-            runner.run(n)
-            done += n
-            if nxt is not None and nxt == done - 1:
-                torch.cuda.current_stream(eng.device).synchronize()
-                i = nxt
-                if i == unfix_noise_after:
-                    print(f"🔹 Unfixing noise at iteration {i}")
-                print(f"🔹 Iteration {i}: Loss = {-float(hist[i].item())}")
-            if verbose and unfix_noise_after < max_iters and done - n <= unfix_noise_after < done \
-                    and unfix_noise_after % 100 != 0:
-                print(f"🔹 Unfixing noise at iteration {unfix_noise_after}")
-        torch.cuda.current_stream(eng.device).synchronize()
-        h = hist[:max_iters].cpu().numpy()
-        self.loss_history = [np.float64(v) for v in h]
-        if int(info.item()) != 0 or not np.all(np.isfinite(h)):
-            bad = int(np.argmax(~np.isfinite(h))) if not np.all(np.isfinite(h)) else max_iters - 1
-            self.loss_history = self.loss_history[:bad + 1]
-            tm.set_u(st.u.cpu().numpy())
-            raise CholeskyError(f"optimize: Cholesky failed at iteration {bad}")
-        tm.set_u(st.u.cpu().numpy())
+        for r in report + [max_iters - 1]:
+            if r < done:
+                continue
+            sess.run(r + 1 - done)
+            done = r + 1
+            if verbose and r in report:
+                sess.sync()
+                if r == unfix_noise_after:
+                    # reference prints this; the traced tf.function never sees the noise (Appendix C-2)
+                    print(f"🔹 Unfixing noise at iteration {r}")
+                print(f"🔹 Iteration {r}: Loss = {-sess.loss_at(r)}")
+        sess.finish()
 
     def _optimize_lbfgs(self, max_iters):
         """gpflow.optimizers.Scipy().minimize twice: noise fixed, then trainable
@@ -275,6 +253,58 @@ class MultiFidelityGPModel(Module):
 
             res = minimize(fg, x0, jac=True, method="L-BFGS-B", options={"maxiter": max_iters})
             tm.set_u(expand(res.x))
+
+
+class AdamSession:
+    """Runs MultiFidelityGPModel Adam iterations on the device.
+
+    State (unconstrained u, moments, step counter, loss history) lives in HBM; each
+    iteration is ONE mfgp_gpr_adam_step call (≈T+6 kernel launches), replayed from
+    hipGraphs of `graph_chunk` iterations on a dedicated stream.  The host only
+    syncs when asked (progress prints, finish)."""
+
+    def __init__(self, model: "MultiFidelityGPModel", lr: float, max_iters: int, graph: bool, chunk: int):
+        self.model = model
+        self.eng, self.X, self.Y = model._device_data()
+        self.tm = model._theta_map()
+        self.stream = torch.cuda.Stream(self.eng.device)
+        self.max_iters = max(int(max_iters), 1)
+        with torch.cuda.stream(self.stream):
+            self.st = AdamState(self.eng.device, self.tm.u(), self.tm.trainable(), self.tm.tie(), lr)
+            self.hist = torch.zeros((self.max_iters,), dtype=torch.float64, device=self.eng.device)
+            self.out = torch.empty((1 + theta_size(self.tm.d),), dtype=torch.float64, device=self.eng.device)
+            self.info = torch.zeros((1,), dtype=torch.int32, device=self.eng.device)
+            self.eng.theta_from_u(self.st.u, self.st.theta, self.tm.noise_index)
+            self.eng.gpr_lml(self.X, self.Y, self.st.theta, want_grad=False)   # sizes the workspace
+        self.done = 0
+        self.runner = _StepRunner(self._step, chunk if graph else 0)
+
+    def _step(self):
+        self.eng.gpr_adam_step(self.X, self.Y, self.st, self.hist, self.out, self.info)
+
+    def run(self, n: int):
+        if self.done + n > self.max_iters:
+            raise ValueError("AdamSession: more iterations than max_iters")
+        with torch.cuda.stream(self.stream):
+            self.runner.run(n)
+        self.done += n
+
+    def sync(self):
+        self.stream.synchronize()
+
+    def loss_at(self, i: int) -> float:
+        self.sync()
+        return float(self.hist[i].item())
+
+    def finish(self):
+        self.sync()
+        h = self.hist[:self.done].cpu().numpy()
+        self.model.loss_history = [np.float64(v) for v in h]
+        self.tm.set_u(self.st.u.cpu().numpy())
+        if int(self.info.item()) != 0 or not np.all(np.isfinite(h)):
+            bad = int(np.argmax(~np.isfinite(h))) if not np.all(np.isfinite(h)) else len(h) - 1
+            self.model.loss_history = self.model.loss_history[:bad + 1]
+            raise CholeskyError(f"optimize: Cholesky failed at iteration {bad}")
 
 
 class _StepRunner:
