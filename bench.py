@@ -49,34 +49,9 @@ def load_goku():
 
 def broadcast_inputs(rank, world, device):
     """Rank 0 reads the txt files; one RCCL broadcast of the packed inputs."""
-    if rank == 0:
-        X, Y, Xt, Yt = load_goku()
-        hdr = torch.tensor([X.shape[0], X.shape[1], Y.shape[1], Xt.shape[0]], dtype=torch.int64, device=device)
-    else:
-        hdr = torch.zeros(4, dtype=torch.int64, device=device)
-    if world > 1:
-        dist.broadcast(hdr, 0)
-    n, dx, p, ns = [int(v) for v in hdr.tolist()]
-    size = n * dx + n * p + ns * dx + ns * p
-    if rank == 0:
-        buf = torch.tensor(np.concatenate([X.ravel(), Y.ravel(), Xt.ravel(), Yt.ravel()]), dtype=torch.float64,
-                           device=device)
-    else:
-        buf = torch.empty(size, dtype=torch.float64, device=device)
-    if world > 1:
-        dist.broadcast(buf, 0)
-    h = buf.cpu().numpy()
-    o = 0
-    X = h[o:o + n * dx].reshape(n, dx); o += n * dx
-    Y = h[o:o + n * p].reshape(n, p); o += n * p
-    Xt = h[o:o + ns * dx].reshape(ns, dx); o += ns * dx
-    Yt = h[o:o + ns * p].reshape(ns, p)
-    return X, Y, Xt, Yt
-
-
-def bin_block(p, rank, world):
-    edges = np.linspace(0, p, world + 1).round().astype(int)
-    return int(edges[rank]), int(edges[rank + 1])
+    from multi_fidelity_gpflow_amd.distributed import broadcast_arrays
+    arrays = list(load_goku()) if rank == 0 else None
+    return broadcast_arrays(arrays, rank, world, device)
 
 
 def make_model(X, Yr):
@@ -179,6 +154,7 @@ def main():
 
     X, Y, Xt, Yt = broadcast_inputs(rank, world, device)
     n, d, P = X.shape[0], X.shape[1] - 1, Y.shape[1]
+    from multi_fidelity_gpflow_amd.distributed import bin_block
     b0, b1 = bin_block(P, rank, world)
     Yr = np.ascontiguousarray(Y[:, b0:b1])
 

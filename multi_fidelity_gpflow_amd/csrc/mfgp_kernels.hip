@@ -520,7 +520,7 @@ __global__ __launch_bounds__(NTHREADS) void k_finalize(FinArgs a) {
                 for (int r = 0; r < G; ++r)
                     if (a.tie[r] == a.tie[q]) gc += gsh[r];
             }
-            const double g = -gc * (1.0 / (exp(-uq) + 1.0));   // loss = -lml, chain through softplus
+            const double g = (-gc) / (exp(-uq) + 1.0);   // loss = -lml; TF SoftplusGrad form
             double mq = a.m[q], vq = a.v[q];
             mq += (g - mq) * (1.0 - a.b1);
             vq += (g * g - vq) * (1.0 - a.b2);

@@ -90,17 +90,6 @@ class _ThetaMap:
                 arr[idx] = val
                 p.unconstrained_variable = arr
 
-    def grad_to_params(self, g: np.ndarray, with_noise: bool):
-        """Constrained theta-gradient -> unconstrained gradient per trainable variable
-        (sum over tied entries, chain through Softplus)."""
-        groups = {}
-        for (p, idx), gq in zip(self.entries, g):
-            key = (id(p), idx)
-            if key not in groups:
-                groups[key] = [p, idx, 0.0]
-            groups[key][2] += gq
-        return groups
-
 
 class MultiFidelityGPModel(Module):
     """GPR with the linear multi-fidelity kernel and a shared Gram over P outputs."""
@@ -219,40 +208,49 @@ class MultiFidelityGPModel(Module):
 
     def _optimize_lbfgs(self, max_iters):
         """gpflow.optimizers.Scipy().minimize twice: noise fixed, then trainable
-        (linear.py:230-234).  Value+grad on the device; L-BFGS-B on the host."""
+        (linear.py:230-234).  GPflow semantics: the optimisation vector is the
+        concatenation of the trainable Parameters' UNCONSTRAINED values in
+        tf.Module attribute order (kernel_L.lengthscales, kernel_L.variance,
+        kernel_delta.lengthscales, kernel_delta.variance, rho (all P entries),
+        likelihood.variance); value + gradient come from the device, L-BFGS-B
+        (scipy, jac=True) runs on the host."""
         from scipy.optimize import minimize
 
         for phase in (0, 1):
             if phase == 1:
                 set_trainable(self.likelihood.variance, True)
             tm = self._theta_map()
-            train = tm.trainable()
-            tie = tm.tie()
-            u_full = tm.u()
-            # one unconstrained variable per trainable tie group
-            groups = []
-            for q in range(len(u_full)):
-                if train[q] and tie[q] not in [tie[g] for g in groups]:
-                    groups.append(q)
-            x0 = np.array([u_full[q] for q in groups])
+            params = [p for _, p in self.parameters_with_names() if p.trainable]
+            sizes = [int(np.prod(p.shape)) if p.shape else 1 for p in params]
 
-            def expand(x):
-                u = u_full.copy()
-                for gq, val in zip(groups, x):
-                    u[tie == tie[gq]] = val
-                return u
+            def pack():
+                return np.concatenate([np.asarray(p.unconstrained_variable, dtype=np.float64).ravel() for p in params])
+
+            def unpack(x):
+                o = 0
+                for p, n in zip(params, sizes):
+                    p.unconstrained_variable = x[o:o + n].reshape(p.shape)
+                    o += n
 
             def fg(x):
-                u = expand(x)
-                tm.set_u(u)
+                unpack(x)
                 lml, g = self.log_marginal_likelihood_and_grad()
-                sig = 1.0 / (np.exp(-u) + 1.0)
-                gu = np.array([-np.sum(g[tie == tie[gq]]) * sig[gq] for gq in groups])
+                grads = {id(p): np.zeros(p.shape) for p in params}
+                for (p, idx), gq in zip(tm.entries, g):
+                    if id(p) not in grads:
+                        continue
+                    if idx is None:
+                        grads[id(p)] = grads[id(p)] + gq
+                    else:
+                        grads[id(p)][idx] += gq
+                # TF SoftplusGrad: upstream / (exp(-u) + 1), applied to the loss (-LML) gradient
+                gu = np.concatenate([(-grads[id(p)] / (np.exp(-p.unconstrained_variable) + 1.0)).ravel()
+                                     for p in params])
                 self.loss_history.append(np.float64(-lml))
                 return -lml, gu
 
-            res = minimize(fg, x0, jac=True, method="L-BFGS-B", options={"maxiter": max_iters})
-            tm.set_u(expand(res.x))
+            res = minimize(fg, pack(), jac=True, method="L-BFGS-B", options={"maxiter": max_iters})
+            unpack(res.x)
 
 
 class AdamSession:

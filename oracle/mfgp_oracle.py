@@ -256,12 +256,16 @@ def unpack_unconstrained(u, template: MFParams, with_noise=False):
     return q
 
 
+def softplus_backprop(g, u):
+    """TF SoftplusGrad as autodiff applies it: upstream / (exp(-u) + 1)."""
+    return g / (np.exp(-np.asarray(u, dtype=np.float64)) + 1.0)
+
+
 def grad_unconstrained(u, g, with_noise=False):
-    """Chain rule through Softplus: dθ/du = sigmoid(u)."""
-    D = len(g["lL"])
+    """Chain rule through Softplus (TF SoftplusGrad form)."""
     gc = np.concatenate([[g["vL"]], g["lL"], [g["vD"]], g["lD"], [g["rho0"]]]
                         + ([[g["noise"]]] if with_noise else []))
-    return gc * softplus_grad(u)
+    return softplus_backprop(gc, u)
 
 
 # ---------------------------------------------------------------- optimisers
@@ -319,25 +323,53 @@ def adam_train(X, Y, p0: MFParams, max_iters=1000, learning_rate=0.1, record=Non
         p = unpack_unconstrained(u, p0)
         lml, g = gpr_lml_and_grad(X, Y, p)
         hist.append(-lml)
-        u = opt.step(u, -grad_unconstrained(u, g))
+        u = opt.step(u, grad_unconstrained(u, {k: -np.asarray(v) for k, v in g.items()}))
     return unpack_unconstrained(u, p0), np.array(hist)
 
 
-def lbfgs_train(X, Y, p0: MFParams, max_iters=1000):
-    """optimize(use_adam=False) — linear.py:223-234: gpflow.optimizers.Scipy
-    (L-BFGS-B, jac=True) over the trainables with the noise fixed, then again with
-    the noise trainable."""
+def lbfgs_train(X, Y, p0: MFParams, max_iters=1000, return_trace=False):
+    """optimize(use_adam=False) — linear.py:223-234 through gpflow.optimizers.Scipy:
+    L-BFGS-B (jac=True) over the concatenated UNCONSTRAINED trainables in tf.Module
+    attribute order [lL(D), vL, lD(D), vD, rho (all P), (noise)], first with the
+    noise fixed, then again with it trainable.  The unconstrained values persist
+    between the two passes; the noise is always Shift(1e-6) o Softplus of its
+    variable (so its initial value is softplus(softplus_inverse(1e-3 - 1e-6)) + 1e-6).
+    The objective is degenerate (the noise runs to its 1e-6 floor), so the end
+    point is sensitive to 1e-16-level arithmetic differences."""
     from scipy.optimize import minimize
 
-    p = p0.copy()
-    for with_noise in (False, True):
-        u0 = pack_unconstrained(p, with_noise)
+    D = len(p0.lL)
+    P = np.asarray(p0.rho).reshape(-1).size
+    u = {"lL": softplus_inverse(p0.lL), "vL": np.atleast_1d(softplus_inverse(p0.vL)),
+         "lD": softplus_inverse(p0.lD), "vD": np.atleast_1d(softplus_inverse(p0.vD)),
+         "rho": softplus_inverse(np.asarray(p0.rho, dtype=np.float64).reshape(-1)),
+         "noise": np.atleast_1d(softplus_inverse(p0.noise - NOISE_SHIFT))}
 
-        def fg(u, wn=with_noise, tmpl=p):
-            q = unpack_unconstrained(u, tmpl, wn)
-            lml, g = gpr_lml_and_grad(X, Y, q)
-            return -lml, -grad_unconstrained(u, g, wn)
+    def params():
+        return MFParams(float(softplus(u["vL"][0])), softplus(u["lL"]), float(softplus(u["vD"][0])),
+                        softplus(u["lD"]), softplus(u["rho"]).reshape(P, 1),
+                        float(softplus(u["noise"][0]) + NOISE_SHIFT))
 
-        res = minimize(fg, u0, jac=True, method="L-BFGS-B", options={"maxiter": max_iters})
-        p = unpack_unconstrained(res.x, p, with_noise)
-    return p
+    trace = []
+    for phase in (0, 1):
+        keys = ["lL", "vL", "lD", "vD", "rho"] + (["noise"] if phase else [])
+        sizes = [u[k].size for k in keys]
+
+        def unpack(x):
+            o = 0
+            for k, n in zip(keys, sizes):
+                u[k] = np.array(x[o:o + n])
+                o += n
+
+        def fg(x):
+            unpack(x)
+            lml, g = gpr_lml_and_grad(X, Y, params())
+            gd = {"lL": g["lL"], "vL": [g["vL"]], "lD": g["lD"], "vD": [g["vD"]],
+                  "rho": np.r_[g["rho0"], np.zeros(P - 1)], "noise": [g["noise"]]}
+            trace.append(-lml)
+            return -lml, np.concatenate([softplus_backprop(-np.asarray(gd[k], dtype=np.float64), u[k]) for k in keys])
+
+        res = minimize(fg, np.concatenate([u[k] for k in keys]), jac=True, method="L-BFGS-B",
+                       options={"maxiter": max_iters})
+        unpack(res.x)
+    return (params(), np.array(trace)) if return_trace else params()

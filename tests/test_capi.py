@@ -1,0 +1,54 @@
+"""The C-ABI library loads and exports every symbol include/mfgp.h declares (no GPU needed)."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "mfgp.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(mfgp_[a-z0-9_]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from multi_fidelity_gpflow_amd import _lib
+    from multi_fidelity_gpflow_amd.build import build_lib
+    build_lib()
+    return _lib.load()
+
+
+def test_exports_every_declared_symbol(lib):
+    names = _declared()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(lib, n), f"{n} declared in include/mfgp.h but not exported"
+
+
+def test_python_binding_covers_header(lib):
+    from multi_fidelity_gpflow_amd._lib import SIGNATURES
+    assert set(SIGNATURES) == set(_declared())
+
+
+def test_host_only_entry_points(lib):
+    assert lib.mfgp_version() >= 100
+    assert lib.mfgp_error_string(-2).decode() == "workspace too small"
+    h = C.c_void_p()
+    assert lib.mfgp_create(0, C.byref(h)) == 0
+    assert lib.mfgp_get_tile(h) in (32, 64)
+    assert lib.mfgp_set_tile(h, 48) == -1
+    assert lib.mfgp_set_tile(h, 64) == 0 and lib.mfgp_get_tile(h) == 64
+    sz = C.c_size_t()
+    assert lib.mfgp_gpr_workspace_size(h, 1164, 64, 10, C.byref(sz)) == 0
+    # A (npad^2) + R + Xo (npad x (npad+ppad)) dominate: > 30 MB at Goku
+    assert sz.value > 30e6
+    assert lib.mfgp_gpr_workspace_size(h, 1164, 64, 33, C.byref(sz)) == -4    # d > 32 rejected
+    assert lib.mfgp_svgp_workspace_size(h, 1164, 300, 15, 64, 10, C.byref(sz)) == 0
+    # argument validation happens before any device work
+    assert lib.mfgp_gpr_lml(h, 0, 1, 1, None, 2, None, 1, None, 0, None, 0, None, None) == -1
+    assert lib.mfgp_mf_gram(h, 4, 4, 1, None, 2, None, 2, None, 0.0, None, 4) == -1
+    assert lib.mfgp_destroy(h) == 0

@@ -1,0 +1,241 @@
+"""HIP path (libmfgp.so through the C-ABI) vs. the CPU oracle and the reference KATs.
+
+Tolerances (fp64): Gram entries 1e-13 abs; LML 1e-11 rel; gradient 1e-8 rel (of the
+largest component); posterior mean/var 1e-9 abs; Adam trajectories 1e-10 rel through
+iteration 500 (the reference dynamics turn chaotic after ~520).  The north-star bar is
+1e-5 relative for posteriors."""
+import numpy as np
+import pytest
+import torch
+
+import multi_fidelity_gpflow_amd as M
+from multi_fidelity_gpflow_amd.engine import Engine
+from oracle import mfgp_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from multi_fidelity_gpflow_amd.build import build_lib
+    build_lib()
+    e = Engine.get()
+    yield e
+    e.set_tile(32)
+
+
+@pytest.fixture(params=[32, 64], ids=["nb32", "nb64"])
+def tile(request, eng):
+    eng.set_tile(request.param)
+    yield request.param
+    eng.set_tile(32)
+
+
+def _params(D, P, seed=0, scale=1.0):
+    rng = np.random.default_rng(seed)
+    return O.MFParams(1.0 + 0.5 * rng.random() * scale, 0.5 + 1.5 * rng.random(D) * scale, 0.3 + rng.random() * scale,
+                      0.5 + rng.random(D) * scale, np.full((P, 1), 0.7 + 0.6 * rng.random() * scale), 1e-3)
+
+
+def _model(X, Y, p: O.MFParams):
+    D = X.shape[1] - 1
+    m = M.MultiFidelityGPModel(X, Y, M.SquaredExponential(lengthscales=np.ones(D)),
+                               M.SquaredExponential(lengthscales=np.ones(D)))
+    m.kernel.kernel_L.variance.assign(p.vL)
+    m.kernel.kernel_L.lengthscales.assign(p.lL)
+    m.kernel.kernel_delta.variance.assign(p.vD)
+    m.kernel.kernel_delta.lengthscales.assign(p.lD)
+    m.kernel.rho.assign(p.rho)
+    m.likelihood.variance.assign(p.noise)
+    return m
+
+
+def _oracle_params(m) -> O.MFParams:
+    k = m.kernel
+    D = m.input_dim
+    return O.MFParams(float(k.kernel_L.variance.numpy()), k.kernel_L.lengthscale_vector(D),
+                      float(k.kernel_delta.variance.numpy()), k.kernel_delta.lengthscale_vector(D),
+                      k.rho.numpy(), float(m.likelihood.variance.numpy()))
+
+
+def test_mfma_f64_layout(eng):
+    A = np.arange(16)[:, None] * 4 + np.arange(4)[None, :] + 1.0
+    B = 100.0 * np.arange(4)[:, None] + np.arange(16)[None, :]
+    np.testing.assert_array_equal(eng.selftest_mfma(), A @ B)
+
+
+@pytest.mark.parametrize("which", ["hbs", "goku"])
+def test_mf_gram(which, tile, hbs, goku):
+    d = hbs if which == "hbs" else goku
+    X = d["X"]
+    p = _params(X.shape[1] - 1, d["Y"].shape[1], seed=1)
+    m = _model(X, d["Y"], p)
+    np.testing.assert_allclose(m.kernel.K(X).numpy(), O.mf_K(X, None, p), rtol=0, atol=1e-13)
+    # rectangular, mixed fidelities on both sides, LF+HF test rows
+    X2 = np.vstack([d["Xtest"], np.hstack([d["Xtest"][:, :-1], np.zeros((len(d["Xtest"]), 1))])])
+    np.testing.assert_allclose(m.kernel.K(X, X2).numpy(), O.mf_K(X, X2, p), rtol=0, atol=1e-13)
+    np.testing.assert_allclose(m.kernel.K_diag(X2).numpy(), O.mf_Kdiag(X2, p), rtol=0, atol=1e-15)
+
+
+def test_fractional_fidelity_rows_are_zero(eng, hbs):
+    """linear.py:67-70 exact masks: a KMeans centre with fidelity 0.9999999999999999 gets a zero row."""
+    X = hbs["X"][:20].copy()
+    X[3, -1] = 0.9999999999999999
+    X[7, -1] = 0.5
+    p = _params(5, 1, seed=2)
+    m = _model(X, np.zeros((20, 1)), p)
+    K = m.kernel.K(X).numpy()
+    np.testing.assert_array_equal(K[3], 0.0)
+    np.testing.assert_array_equal(K[:, 7], 0.0)
+    np.testing.assert_allclose(K, O.mf_K(X, None, p), rtol=0, atol=1e-14)
+    assert m.kernel.K_diag(X).numpy()[3] == 0.0
+
+
+def test_rbf_gram(eng):
+    rng = np.random.default_rng(3)
+    A, B = rng.random((70, 4)), rng.random((33, 4))
+    k = M.SquaredExponential(variance=1.7, lengthscales=np.array([0.3, 0.8, 1.1, 2.0]))
+    np.testing.assert_allclose(k.K(A, B).numpy(), O.rbf_K(A, B, 1.7, [0.3, 0.8, 1.1, 2.0]), rtol=0, atol=1e-14)
+    k2 = M.SquaredExponential(variance=0.5, lengthscales=0.7)       # isotropic
+    np.testing.assert_allclose(k2(A).numpy(), O.rbf_K(A, A, 0.5, 0.7), rtol=0, atol=1e-14)
+    np.testing.assert_allclose(k2(A, full_cov=False).numpy(), np.full(70, 0.5))
+
+
+@pytest.mark.parametrize("n,batch", [(1, 1), (5, 2), (32, 1), (33, 3), (64, 1), (65, 2), (300, 2)])
+def test_potrf_inv(n, batch, tile, eng):
+    rng = np.random.default_rng(n)
+    G = rng.standard_normal((batch, n, n))
+    A = G @ G.transpose(0, 2, 1) / n + np.eye(n) * 0.5
+    Linv, ld, info = eng.potrf_inv(torch.tensor(A, device=eng.device))
+    assert info.cpu().numpy().tolist() == [0] * batch
+    for b in range(batch):
+        L = np.linalg.cholesky(A[b])
+        np.testing.assert_allclose(Linv[b].cpu().numpy() @ L, np.eye(n), atol=1e-11)
+        np.testing.assert_allclose(ld[b].cpu().numpy(), np.diag(L), rtol=1e-13)
+        assert np.all(np.triu(Linv[b].cpu().numpy(), 1) == 0)
+
+
+def test_non_pd_reports_info_and_raises(eng, hbs):
+    A = np.eye(40)
+    A[17, 17] = -1.0
+    _, _, info = eng.potrf_inv(torch.tensor(A, device=eng.device))
+    assert int(info.item()) == 18                 # LAPACK-style 1-based row
+    bad = _model(hbs["X"], hbs["Y"], _params(5, 49))
+    bad.kernel.kernel_L.variance.assign(1e300)    # overflowing trailing updates -> non-finite pivot
+    with pytest.raises(M.CholeskyError):
+        bad.log_marginal_likelihood()
+
+
+@pytest.mark.parametrize("which,seed", [("hbs", None), ("hbs", 4), ("goku", None), ("goku", 5), ("forrester", 6)])
+def test_lml_and_grad(which, seed, tile, hbs, goku):
+    if which == "forrester":
+        from conftest import forrester_test_data
+        X, Y = forrester_test_data()
+    else:
+        d = hbs if which == "hbs" else goku
+        X, Y = d["X"], d["Y"]
+    D, P = X.shape[1] - 1, Y.shape[1]
+    p = O.MFParams.initial(D, P) if seed is None else _params(D, P, seed=seed)
+    m = _model(X, Y, p)
+    po = _oracle_params(m)
+    lo, go = O.gpr_lml_and_grad(X, Y, po)
+    assert abs(float(m.log_marginal_likelihood()) - lo) < 1e-11 * abs(lo)
+    l, g = m.log_marginal_likelihood_and_grad()
+    gov = np.concatenate([[go["vL"]], go["lL"], [go["vD"]], go["lD"], [go["rho0"]], [go["noise"]]])
+    assert abs(l - lo) < 1e-11 * abs(lo)
+    np.testing.assert_allclose(g, gov, rtol=0, atol=1e-8 * np.abs(gov).max())
+
+
+def test_lml_kats(hbs, goku, kats, eng):
+    for d, key in ((hbs, "hbs_lml_initial"), (goku, "goku_lml_initial")):
+        m = _model(d["X"], d["Y"], O.MFParams.initial(d["X"].shape[1] - 1, d["Y"].shape[1]))
+        v = float(m.log_marginal_likelihood())
+        assert abs(v - kats[key]["value"]) < 1e-12 * abs(v)
+
+
+@pytest.mark.parametrize("which", ["hbs", "goku"])
+def test_predict_f(which, tile, hbs, goku):
+    d = hbs if which == "hbs" else goku
+    p = _params(d["X"].shape[1] - 1, d["Y"].shape[1], seed=7)
+    m = _model(d["X"], d["Y"], p)
+    po = _oracle_params(m)
+    for Xs in (d["Xtest"], d["X"][::7]):
+        mean, var = m.predict_f(Xs)
+        mo, vo = O.gpr_predict_f(d["X"], d["Y"], Xs, po)
+        assert mean.shape == mo.shape and var.shape == vo.shape
+        np.testing.assert_allclose(mean.numpy(), mo, rtol=0, atol=1e-9 * max(1, np.abs(mo).max()))
+        np.testing.assert_allclose(var.numpy(), vo, rtol=0, atol=1e-9)
+
+
+def test_tile_size_invariance(eng, goku):
+    m = _model(goku["X"], goku["Y"], _params(10, 64, seed=8))
+    vals = []
+    for nb in (32, 64):
+        eng.set_tile(nb)
+        vals.append(m.log_marginal_likelihood_and_grad())
+    eng.set_tile(32)
+    assert abs(vals[0][0] - vals[1][0]) < 1e-12 * abs(vals[0][0])
+    np.testing.assert_allclose(vals[0][1], vals[1][1], rtol=0, atol=1e-9 * np.abs(vals[0][1]).max())
+
+
+@pytest.mark.parametrize("which", ["hbs", "goku"])
+def test_adam_trajectory_kats(which, hbs, goku, kats, eng):
+    d = hbs if which == "hbs" else goku
+    key = "hbs_adam_lr0.1_lml" if which == "hbs" else "goku_adam_lr0.1_lml"
+    D = d["X"].shape[1] - 1
+    m = M.MultiFidelityGPModel(d["X"], d["Y"], M.SquaredExponential(lengthscales=np.ones(D)),
+                               M.SquaredExponential(lengthscales=np.ones(D)))
+    m.optimize(max_iters=1000, use_adam=True, learning_rate=0.1, unfix_noise_after=500, verbose=False)
+    assert len(m.loss_history) == 1000
+    for k, v in kats[key]["values"].items():
+        k = int(k)
+        assert abs(-m.loss_history[k] - v) < (1e-10 if k <= 500 else 1e-4) * abs(v), (k, -m.loss_history[k], v)
+    # noise never trained in the Adam path (Appendix C-2)
+    assert float(m.likelihood.variance.numpy()) == pytest.approx(1e-3, rel=1e-12)
+
+
+def test_graph_and_eager_agree(hbs, eng):
+    hs = []
+    for graph in (True, False):
+        m = M.MultiFidelityGPModel(hbs["X"], hbs["Y"], M.SquaredExponential(lengthscales=np.ones(5)),
+                                   M.SquaredExponential(lengthscales=np.ones(5)))
+        m.optimize(max_iters=120, learning_rate=0.1, verbose=False, graph=graph)
+        hs.append(np.array(m.loss_history))
+    np.testing.assert_array_equal(hs[0], hs[1])
+
+
+def test_lbfgs_forrester_kat(kats, eng):
+    """L-BFGS on this objective is degenerate once the noise reaches its 1e-6 floor:
+    1-ulp changes move the stopping point along a flat valley (the bit-identical host
+    driver fed by the fp64 oracle stops at rho 1.9998815, 5.6e-5 from the recorded
+    1.99976989).  The KAT is therefore checked at 1e-4, the noise floor exactly, and
+    the GPU objective along the first L-BFGS evaluations against the oracle driver."""
+    from conftest import forrester_demo_data
+    X, Y = forrester_demo_data()
+    m = M.MultiFidelityGPModel(X, Y, M.SquaredExponential(), M.SquaredExponential())
+    m.optimize(max_iters=1000, learning_rate=0.01, use_adam=False, unfix_noise_after=500, verbose=False)
+    rho = float(m.kernel.rho.numpy()[0, 0])
+    assert abs(rho - kats["forrester_lbfgs"]["rho"]) < 1e-4 * kats["forrester_lbfgs"]["rho"]
+    assert float(m.likelihood.variance.numpy()) == pytest.approx(kats["forrester_lbfgs"]["noise"], rel=1e-3)
+    _, trace = O.lbfgs_train(X, Y, O.MFParams.initial(1, 1), max_iters=1000, return_trace=True)
+    np.testing.assert_allclose(m.loss_history[:8], trace[:8], rtol=1e-9)
+
+
+def test_large_synthetic_properties(eng):
+    """N = 4096 (T = 128 tiles): additivity of the shared-Gram LML over output
+    columns, and agreement of the full value with the fp64 oracle."""
+    rng = np.random.default_rng(20251015)
+    nl, nh, D, P = 3584, 512, 10, 8
+    X = np.vstack([np.hstack([rng.random((nl, D)), np.zeros((nl, 1))]),
+                   np.hstack([rng.random((nh, D)), np.ones((nh, 1))])])
+    Y = rng.standard_normal((nl + nh, P))
+    p = O.MFParams(1.0, np.full(D, 1.0), 1.0, np.full(D, 1.0), np.ones((P, 1)), 1e-2)
+    m = _model(X, Y, p)
+    full = float(m.log_marginal_likelihood())
+    parts = 0.0
+    for i in range(0, P, 2):
+        q = p.copy()
+        q.rho = np.ones((2, 1))
+        parts += float(_model(X, Y[:, i:i + 2], q).log_marginal_likelihood())
+    assert abs(full - parts) < 1e-9 * abs(full)
+    assert abs(full - O.gpr_lml(X, Y, _oracle_params(m))) < 1e-9 * abs(full)
