@@ -128,6 +128,14 @@ int mfgp_svgp_elbo(mfgp_handle_t h, int n, int m, int l, int p, int d, const dou
                    const double* q_sqrt, const double* W, double noise, double scale, double jitter, void* ws,
                    size_t ws_bytes, double* out, double* g_mu, double* g_var, int* info);
 
+/* SVGP.predict_f(Xnew, full_cov=False) of the same models (GPflow posteriors with
+ * mix_latent_gp): latent moments g_mu / g_var [L][nstar] and mixed f_mu / f_var
+ * [nstar][P].  Workspace: mfgp_svgp_workspace_size(h, nstar, m, l, p, d). */
+int mfgp_svgp_predict(mfgp_handle_t h, int nstar, int m, int l, int p, int d, const double* Xs, int ldxs,
+                      const double* Z, int ldz, const double* thetas, const double* q_mu, const double* q_sqrt,
+                      const double* W, double jitter, void* ws, size_t ws_bytes, double* g_mu, double* g_var,
+                      double* f_mu, double* f_var, int* info);
+
 /* Diagnostic: one v_mfma_f64_16x16x4_f64 with A[i][k] = 4i+k+1, B[k][j] = 100k+j;
  * writes C (16x16 row-major, device). */
 int mfgp_selftest_mfma(mfgp_handle_t h, double* out);

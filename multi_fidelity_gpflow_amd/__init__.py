@@ -9,6 +9,8 @@ from .params import Parameter, positive, set_trainable, parameter_dict, multiple
 from .kernels import (SquaredExponential, RBF, LinearMultiFidelityKernel,  # noqa: F401
                       LinearCoregionalization, SeparateIndependent)
 from .models import MultiFidelityGPModel, Gaussian, CholeskyError  # noqa: F401
+from .svgp import LatentMFCoregionalizationSVGP, SingleBinSVGP, initialize_W  # noqa: F401
+from .data import PowerSpecs  # noqa: F401
 from ._lib import MFGPError  # noqa: F401
 
 __version__ = "0.1.0"

@@ -44,6 +44,8 @@ SIGNATURES = {
     "mfgp_svgp_workspace_size": [_p, _i, _i, _i, _i, _i, C.POINTER(_sz)],
     "mfgp_svgp_elbo": [_p, _i, _i, _i, _i, _i, _p, _i, _p, _i, _p, _i, _p, _p, _p, _p, _d, _d, _d, _p, _sz, _p,
                        _p, _p, _p],
+    "mfgp_svgp_predict": [_p, _i, _i, _i, _i, _i, _p, _i, _p, _i, _p, _p, _p, _p, _d, _p, _sz, _p, _p, _p, _p,
+                          _p],
     "mfgp_selftest_mfma": [_p, _p],
 }
 

@@ -313,6 +313,11 @@ int svgp_elbo_impl(hipStream_t s, int nb, int n, int m, int l, int p, int d, con
                    const double* q_sqrt, const double* W, double noise, double scale, double jitter, void* ws,
                    size_t ws_bytes, double* out, double* g_mu, double* g_var, int* info);
 
+int svgp_predict_impl(hipStream_t s, int nb, int n, int m, int l, int p, int d, const double* Xs, int ldx,
+                      const double* Z, int ldz, const double* thetas, const double* q_mu, const double* q_sqrt,
+                      const double* W, double jitter, void* ws, size_t ws_bytes, double* g_mu, double* g_var,
+                      double* f_mu, double* f_var, int* info);
+
 }  // namespace mfgp
 
 using namespace mfgp;
@@ -529,6 +534,20 @@ int mfgp_svgp_elbo(mfgp_handle_t h, int n, int m, int l, int p, int d, const dou
     if (!W && l != p) return MFGP_ERR_ARG;
     return svgp_elbo_impl(h->stream, h->nb, n, m, l, p, d, X, ldx, Y, ldy, Z, ldz, thetas, q_mu, q_sqrt, W, noise,
                           scale, jitter, ws, ws_bytes, out, g_mu, g_var, info);
+}
+
+int mfgp_svgp_predict(mfgp_handle_t h, int nstar, int m, int l, int p, int d, const double* Xs, int ldxs,
+                      const double* Z, int ldz, const double* thetas, const double* q_mu, const double* q_sqrt,
+                      const double* W, double jitter, void* ws, size_t ws_bytes, double* g_mu, double* g_var,
+                      double* f_mu, double* f_var, int* info) {
+    CHECK_H(h);
+    CHECK_D(d);
+    if (nstar < 1 || m < 1 || l < 1 || p < 1 || !Xs || !Z || !thetas || !q_mu || !q_sqrt || !ws || !g_mu ||
+        !g_var || !f_mu || !f_var || !info)
+        return MFGP_ERR_ARG;
+    if (!W && l != p) return MFGP_ERR_ARG;
+    return svgp_predict_impl(h->stream, h->nb, nstar, m, l, p, d, Xs, ldxs, Z, ldz, thetas, q_mu, q_sqrt, W, jitter,
+                             ws, ws_bytes, g_mu, g_var, f_mu, f_var, info);
 }
 
 int mfgp_selftest_mfma(mfgp_handle_t h, double* out) {

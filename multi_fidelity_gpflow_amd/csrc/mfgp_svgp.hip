@@ -234,6 +234,28 @@ __global__ __launch_bounds__(NTHREADS) void k_svgp_ve(const double* g_mu, const 
     if (threadIdx.x == 0) ve_part[blockIdx.x] = acc;
 }
 
+// posteriors mix_latent_gp (full_cov=False): f_mu = g_mu W^T, f_var = g_var (W o W)^T  (W NULL: identity)
+__global__ void k_svgp_mix(const double* g_mu, const double* g_var, const double* W, int n, int p, int L,
+                           double* f_mu, double* f_var) {
+    const long tot = (long)n * p;
+    for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < tot; e += (long)gridDim.x * blockDim.x) {
+        const int r = (int)(e / p), c = (int)(e % p);
+        double fm = 0.0, fv = 0.0;
+        if (W) {
+            for (int l = 0; l < L; ++l) {
+                const double w = W[(long)c * L + l];
+                fm += g_mu[(long)l * n + r] * w;
+                fv += g_var[(long)l * n + r] * (w * w);
+            }
+        } else {
+            fm = g_mu[(long)c * n + r];
+            fv = g_var[(long)c * n + r];
+        }
+        f_mu[e] = fm;
+        f_var[e] = fv;
+    }
+}
+
 // gauss_kl(q_mu, q_sqrt, K=None) per latent (whitened prior)
 __global__ __launch_bounds__(NTHREADS) void k_svgp_kl(const double* q_mu, const double* q_sqrt, int m, int L,
                                                       double* kl_part) {
@@ -270,7 +292,8 @@ template <int NB>
 static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const double* X, int ldx, const double* Y,
                     int ldy, const double* Z, int ldz, const double* thetas, const double* q_mu,
                     const double* q_sqrt, const double* W, double noise, double scale, double jitter, void* ws,
-                    size_t ws_bytes, double* out, double* g_mu, double* g_var, int* info) {
+                    size_t ws_bytes, double* out, double* g_mu, double* g_var, int* info, double* f_mu = nullptr,
+                    double* f_var = nullptr) {
     const SvgpLayout S = svgp_layout(NB, n, m, L, p, d, ws);
     if (ws_bytes < S.bytes) return -2;
     const long mm = (long)S.mpad * S.mpad;
@@ -315,6 +338,11 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
                        S.npad, S.pa, S.pb, S.pm);
     hipLaunchKernelGGL(k_svgp_moments, dim3(cdiv(n, 256), 1, L), dim3(256), 0, s, S.pa, S.pb, S.pm, X, (long)ldx,
                        thetas, S.G, d, n, S.npad, S.Tm, g_mu, g_var);
+    if (f_mu) {   // predict: mixed moments only
+        hipLaunchKernelGGL(k_svgp_mix, dim3(std::min(cdiv(n * p, 256), 2048)), dim3(256), 0, s, g_mu, g_var, W, n, p, L,
+                           f_mu, f_var);
+        return hipGetLastError() == hipSuccess ? 0 : -3;
+    }
     const int nve = 512;
     hipLaunchKernelGGL(k_svgp_ve, dim3(nve), dim3(NTHREADS), 0, s, g_mu, g_var, W, Y, (long)ldy, n, p, L, noise,
                        S.ve_part);
@@ -332,6 +360,17 @@ int svgp_elbo_impl(hipStream_t s, int nb, int n, int m, int l, int p, int d, con
                             ws, ws_bytes, out, g_mu, g_var, info);
     return svgp_run<32>(s, n, m, l, p, d, X, ldx, Y, ldy, Z, ldz, thetas, q_mu, q_sqrt, W, noise, scale, jitter, ws,
                         ws_bytes, out, g_mu, g_var, info);
+}
+
+int svgp_predict_impl(hipStream_t s, int nb, int n, int m, int l, int p, int d, const double* Xs, int ldx,
+                      const double* Z, int ldz, const double* thetas, const double* q_mu, const double* q_sqrt,
+                      const double* W, double jitter, void* ws, size_t ws_bytes, double* g_mu, double* g_var,
+                      double* f_mu, double* f_var, int* info) {
+    if (nb == 64)
+        return svgp_run<64>(s, n, m, l, p, d, Xs, ldx, Xs, 0, Z, ldz, thetas, q_mu, q_sqrt, W, 1.0, 1.0, jitter, ws,
+                            ws_bytes, nullptr, g_mu, g_var, info, f_mu, f_var);
+    return svgp_run<32>(s, n, m, l, p, d, Xs, ldx, Xs, 0, Z, ldz, thetas, q_mu, q_sqrt, W, 1.0, 1.0, jitter, ws,
+                        ws_bytes, nullptr, g_mu, g_var, info, f_mu, f_var);
 }
 
 }  // namespace mfgp

@@ -179,6 +179,24 @@ class Engine:
                                       ptr(info)), "mfgp_svgp_elbo")
         return out, g_mu, g_var, info
 
+    def svgp_predict(self, Xs, Z, thetas, q_mu, q_sqrt, W, p, jitter=1e-6):
+        ns, dp1 = Xs.shape
+        d = dp1 - 1
+        m = Z.shape[0]
+        L = thetas.shape[0]
+        nbytes = self._size(self.lib.mfgp_svgp_workspace_size, ns, m, L, p, d)
+        ws = self.workspace("svgp_pred", nbytes)
+        g_mu = torch.empty((L, ns), dtype=torch.float64, device=self.device)
+        g_var = torch.empty((L, ns), dtype=torch.float64, device=self.device)
+        f_mu = torch.empty((ns, p), dtype=torch.float64, device=self.device)
+        f_var = torch.empty((ns, p), dtype=torch.float64, device=self.device)
+        info = torch.empty((L,), dtype=torch.int32, device=self.device)
+        check(self.lib.mfgp_svgp_predict(self.h, ns, m, L, p, d, ptr(Xs), dp1, ptr(Z), Z.shape[1], ptr(thetas),
+                                         ptr(q_mu), ptr(q_sqrt), ptr(W), float(jitter), ptr(ws), ws.numel(),
+                                         ptr(g_mu), ptr(g_var), ptr(f_mu), ptr(f_var), ptr(info)),
+              "mfgp_svgp_predict")
+        return f_mu, f_var, g_mu, g_var, info
+
     def selftest_mfma(self) -> np.ndarray:
         out = torch.zeros((16, 16), dtype=torch.float64, device=self.device)
         check(self.lib.mfgp_selftest_mfma(self.h, ptr(out)), "mfgp_selftest_mfma")

@@ -151,4 +151,4 @@ class SingleBinTrainer:
                 self.m[k] += (g - self.m[k]) * (1.0 - self.b1)
                 self.v[k] += (g * g - self.v[k]) * (1.0 - self.b2)
                 var -= (self.m[k] * alpha) / (torch.sqrt(self.v[k]) + self.eps)
-        return float(loss)
+        return float(loss.detach())
