@@ -181,7 +181,7 @@ __global__ __launch_bounds__(NTHREADS) void k_factor_first(double* Ap, int npad,
     double* T0 = smem;
     double* R0 = T0 + E;
     double* dg = R0 + E;
-    __shared__ int bad;
+    int& bad = *reinterpret_cast<int*>(dg + NB);
     const int b = blockIdx.z;
     tile_load<NB>(T0, Ap + (long)b * npad * npad, npad);
     __syncthreads();
@@ -240,7 +240,7 @@ static int potrf_inv_impl(mfgp_handle_t h, int n, int batch, const double* A, in
     hipLaunchKernelGGL(k_rhs_init, dim3(blocks, 1, batch), dim3(256), 0, s, L.R, (long)L.npad, mat, L.npad, 0,
                        (const double*)nullptr, 0L, 0L, n, 0);
     hipLaunchKernelGGL(k_factor_first<NB>, dim3(1, 1, batch), dim3(NTHREADS),
-                       sizeof(double) * (2 * NB * (NB + 2) + NB), s, L.A, L.npad, L.Dd, (long)L.T * NB * NB,
+                       sizeof(double) * (2 * NB * (NB + 2) + NB + 2), s, L.A, L.npad, L.Dd, (long)L.T * NB * NB,
                        L.ldiag, info);
     CholArgs c{};
     c.A = L.A; c.lda = L.npad; c.sA = mat;

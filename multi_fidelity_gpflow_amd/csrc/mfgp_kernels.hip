@@ -90,7 +90,8 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
     double* tile = f2 + NB;                    // NB x S
     double* rtile = tile + TileCfg<NB>::ELEMS; // NB x S (factor scratch)
     double* dg = rtile + TileCfg<NB>::ELEMS;   // NB
-    __shared__ int bad;
+    int& bad = *reinterpret_cast<int*>(dg + NB);   // keep ALL LDS dynamic: a static __shared__
+                                                   // would shift the dynamic base off 16 B (G17)
 
     const int b = blockIdx.z;
     int ti, tj;
@@ -141,7 +142,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
 
 size_t gram_smem_bytes(int nb) {
     const size_t tile = (size_t)nb * (nb + 2);
-    return sizeof(double) * (4 * (size_t)nb * MAXD + 6 * (size_t)nb + 2 * tile + nb);
+    return sizeof(double) * (4 * (size_t)nb * MAXD + 6 * (size_t)nb + 2 * tile + nb + 2);
 }
 
 // ============================================================ K2: tile Cholesky step
@@ -164,7 +165,7 @@ __global__ __launch_bounds__(NTHREADS) void k_chol_step(CholArgs a) {
     double* Pi = T0 + E;         // L_ik = A_ik D_k^T
     double* Pj = Pi + E;         // L_jk
     double* dg = Pj + E;         // NB
-    __shared__ int bad;
+    int& bad = *reinterpret_cast<int*>(dg + NB);
 
     const int b = blockIdx.z;
     const int k = a.k, T = a.T, Tp = a.Tp;
@@ -264,7 +265,7 @@ int chol_step_blocks(int T, int Tp, int k) {
     return rem * (rem + 1) / 2 + rem * (k + 1 + Tp) + ((k == T - 1) ? (T + Tp) : 0);
 }
 
-size_t chol_smem_bytes(int nb) { return sizeof(double) * (4 * (size_t)nb * (nb + 2) + nb); }
+size_t chol_smem_bytes(int nb) { return sizeof(double) * (4 * (size_t)nb * (nb + 2) + nb + 2); }
 
 // RHS init: identity tiles on the diagonal, zeros strictly below, Y (zero padded)
 __global__ void k_rhs_init(double* R, long ldr, long sR, int npad, int ppad, const double* Y, long ldy, long sY,
@@ -291,7 +292,7 @@ __global__ __launch_bounds__(NTHREADS) void k_alpha(AlphaArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     double* Ls = smem;
     double* Zs = Ls + E;
-    __shared__ double red[4];
+    double* red = Zs + E;
     const int i = blockIdx.x / a.Tp, cy = blockIdx.x % a.Tp;
     auto Xt = [&](int r, int c) { return a.Xo + (long)r * NB * a.ldx + (long)c * NB; };
     Acc<NB> acc;
@@ -634,7 +635,8 @@ void launch_chol_steps(CholArgs c, int batch, hipStream_t s) {
 }
 template <int NB>
 void launch_alpha(const AlphaArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_alpha<NB>, dim3(a.T * a.Tp), dim3(NTHREADS), 2 * sizeof(double) * NB * (NB + 2), s, a);
+    hipLaunchKernelGGL(k_alpha<NB>, dim3(a.T * a.Tp), dim3(NTHREADS), sizeof(double) * (2 * NB * (NB + 2) + 4), s,
+                       a);
 }
 template <int NB>
 void launch_grad(const GradArgs& g, hipStream_t s) {
