@@ -16,6 +16,7 @@ struct mfgp_handle_s {
     int device;
     hipStream_t stream;
     int nb;
+    int grad_chunk;
 };
 
 namespace mfgp {
@@ -37,11 +38,11 @@ struct Carve {
 
 struct GprLayout {
     int nb, npad, T, ppad, Tp, G, gstride, ng;
-    double *A, *R, *Xo, *Dd, *ldiag, *alpha, *zpart, *gpart;
+    double *A, *R, *Xo, *Dd, *ldiag, *alpha, *zpart, *gpart, *apart, *items;
     size_t bytes;
 };
 
-static GprLayout gpr_layout(int nb, int n, int p, int d, void* ws) {
+static GprLayout gpr_layout(int nb, int n, int p, int d, void* ws, int grad_chunk) {
     GprLayout L;
     L.nb = nb;
     L.T = ceil_div(n, nb);
@@ -50,7 +51,7 @@ static GprLayout gpr_layout(int nb, int n, int p, int d, void* ws) {
     L.ppad = L.Tp * nb;
     L.G = theta_size(d);
     L.gstride = (L.G + 3) & ~3;
-    L.ng = grad_tasks(L.T);
+    L.ng = grad_tasks(L.T, grad_chunk);
     Carve c(ws);
     const size_t ldr = (size_t)L.npad + L.ppad;
     L.A = c.take<double>((size_t)L.npad * L.npad);
@@ -61,6 +62,8 @@ static GprLayout gpr_layout(int nb, int n, int p, int d, void* ws) {
     L.alpha = c.take<double>((size_t)L.npad * L.ppad);
     L.zpart = c.take<double>((size_t)L.T * L.Tp);
     L.gpart = c.take<double>((size_t)L.ng * L.gstride);
+    L.apart = c.take<double>((size_t)((L.T + 3) / 4) * L.npad * L.ppad);
+    L.items = c.take<double>((size_t)L.G + 8);
     L.bytes = c.off + 256;
     return L;
 }
@@ -71,13 +74,8 @@ template <int NB>
 static void gram_lml_and_factor(hipStream_t s, const GprLayout& L, int n, int p, int d, const double* X, int ldx,
                                 const double* Y, int ldy, const double* theta, int* info) {
     const long ldr = L.npad + L.ppad;
-    {
-        const long total = (long)L.npad * ldr;
-        const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
-        hipLaunchKernelGGL(k_rhs_init, dim3(blocks), dim3(256), 0, s, L.R, ldr, 0L, L.npad, L.ppad, Y, (long)ldy,
-                           0L, n, p);
-    }
     GramArgs g{};
+    g.R = L.R; g.ldr = ldr; g.sR = 0; g.Y = Y; g.ldy = ldy; g.sY = 0; g.p = p; g.ppad = L.ppad;
     g.X1 = X; g.ldx1 = ldx; g.sx1 = 0; g.n1 = n;
     g.X2 = X; g.ldx2 = ldx; g.sx2 = 0; g.n2 = n;
     g.theta = theta; g.stheta = 0; g.D = d; g.rbf_only = 0;
@@ -105,21 +103,15 @@ template <int NB>
 static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X, int ldx, const double* Y, int ldy,
                           double* theta, int want_grad, void* ws, size_t ws_bytes, double* out, int* info,
                           const FinArgs* adam, PhaseMarks* pm = nullptr) {
-    const GprLayout L = gpr_layout(NB, n, p, d, ws);
+    const GprLayout L = gpr_layout(NB, n, p, d, ws, h->grad_chunk);
     if (ws_bytes < L.bytes) return MFGP_ERR_WORKSPACE;
     hipStream_t s = h->stream;
     const long ldr = L.npad + L.ppad;
     if (pm) pm->mark(s);
-    (void)hipMemsetAsync(info, 0, sizeof(int), s);
-    {
-        const long total = (long)L.npad * ldr;
-        const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
-        hipLaunchKernelGGL(k_rhs_init, dim3(blocks), dim3(256), 0, s, L.R, ldr, 0L, L.npad, L.ppad, Y, (long)ldy,
-                           0L, n, p);
-    }
     if (pm) pm->mark(s);
     {
         GramArgs g{};
+        g.R = L.R; g.ldr = ldr; g.sR = 0; g.Y = Y; g.ldy = ldy; g.sY = 0; g.p = p; g.ppad = L.ppad;
         g.X1 = X; g.ldx1 = ldx; g.sx1 = 0; g.n1 = n;
         g.X2 = X; g.ldx2 = ldx; g.sx2 = 0; g.n2 = n;
         g.theta = theta; g.stheta = 0; g.D = d; g.rbf_only = 0;
@@ -139,11 +131,12 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
         launch_chol_steps<NB>(c, 1, s);
     }
     if (pm) pm->mark(s);
-    AlphaArgs aa{L.Xo, ldr, L.alpha, (long)L.ppad, L.zpart, L.T, L.Tp, n, p};
+    AlphaArgs aa{L.Xo, ldr, L.alpha, (long)L.ppad, L.zpart, L.T, L.Tp, n, p, L.apart, L.npad};
     launch_alpha<NB>(aa, s);
     if (pm) pm->mark(s);
     if (want_grad) {
-        GradArgs ga{L.Xo, ldr, L.alpha, (long)L.ppad, X, (long)ldx, theta, L.gpart, L.gstride, L.T, L.Tp, n, p, d};
+        GradArgs ga{L.Xo, ldr, L.alpha, (long)L.ppad, X, (long)ldx, theta, L.gpart, L.gstride, L.T, L.Tp, n, p, d,
+                    h->grad_chunk};
         launch_grad<NB>(ga, s);
     }
     if (pm) pm->mark(s);
@@ -155,7 +148,9 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
     f.info = info; f.P = p; f.D = d; f.want_grad = want_grad;
     f.out = out;
     f.adam = adam != nullptr;
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(NTHREADS), 0, s, f);
+    f.items = L.items;
+    hipLaunchKernelGGL(k_reduce_items, dim3(2 + (want_grad ? L.G : 0)), dim3(NTHREADS), 0, s, f);
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, f);
     if (pm) pm->mark(s);
     return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;
 }
@@ -267,9 +262,9 @@ struct PredLayout {
     size_t bytes;
 };
 
-static PredLayout pred_layout(int nb, int n, int p, int d, int nstar, void* ws) {
+static PredLayout pred_layout(int nb, int n, int p, int d, int nstar, void* ws, int grad_chunk) {
     PredLayout P;
-    P.g = gpr_layout(nb, n, p, d, ws);
+    P.g = gpr_layout(nb, n, p, d, ws, grad_chunk);
     P.Ts = ceil_div(nstar > 0 ? nstar : 1, nb);
     P.nspad = P.Ts * nb;
     Carve c(ws);
@@ -285,11 +280,10 @@ template <int NB>
 static int predict_impl(mfgp_handle_t h, int n, int p, int d, int nstar, const double* X, int ldx, const double* Y,
                         int ldy, const double* Xs, int ldxs, const double* theta, void* ws, size_t ws_bytes,
                         double* mean, int ldm, double* var, int* info) {
-    const PredLayout P = pred_layout(NB, n, p, d, nstar, ws);
+    const PredLayout P = pred_layout(NB, n, p, d, nstar, ws, h->grad_chunk);
     if (ws_bytes < P.bytes) return MFGP_ERR_WORKSPACE;
     hipStream_t s = h->stream;
     const GprLayout& L = P.g;
-    (void)hipMemsetAsync(info, 0, sizeof(int), s);
     gram_lml_and_factor<NB>(s, L, n, p, d, X, ldx, Y, ldy, theta, info);
     (void)hipMemsetAsync(P.Kmn, 0, sizeof(double) * (size_t)L.npad * P.nspad, s);
     GramArgs g{};
@@ -349,6 +343,8 @@ int mfgp_create(int device, mfgp_handle_t* out) {
     h->device = device;
     h->stream = nullptr;
     h->nb = 32;
+    h->grad_chunk = 16;
+    if (const char* gc = getenv("MFGP_GRAD_CHUNK")) h->grad_chunk = std::max(1, atoi(gc));
     const char* env = getenv("MFGP_TILE");
     if (env && atoi(env) == 64) h->nb = 64;
     *out = h;
@@ -417,7 +413,7 @@ int mfgp_gpr_workspace_size(mfgp_handle_t h, int n, int p, int d, size_t* bytes)
     CHECK_H(h);
     CHECK_D(d);
     if (n < 1 || p < 1 || !bytes) return MFGP_ERR_ARG;
-    *bytes = gpr_layout(h->nb, n, p, d, nullptr).bytes;
+    *bytes = gpr_layout(h->nb, n, p, d, nullptr, h->grad_chunk).bytes;
     return MFGP_OK;
 }
 
@@ -482,7 +478,7 @@ int mfgp_gpr_predict_workspace_size(mfgp_handle_t h, int n, int p, int d, int ns
     CHECK_H(h);
     CHECK_D(d);
     if (n < 1 || p < 1 || nstar < 0 || !bytes) return MFGP_ERR_ARG;
-    *bytes = pred_layout(h->nb, n, p, d, nstar, nullptr).bytes;
+    *bytes = pred_layout(h->nb, n, p, d, nstar, nullptr, h->grad_chunk).bytes;
     return MFGP_OK;
 }
 

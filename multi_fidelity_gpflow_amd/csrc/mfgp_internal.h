@@ -19,6 +19,8 @@ struct GramArgs {
     double diag_add;                          // extra constant on i==j<n (jitter)
     // fused factor of tile (0,0) (LML layout only)
     double* Dd; long sD; double* ldiag; long sL; int* info;
+    // fused RHS init (LML layout only; R == nullptr: skip): R = [I | Y]
+    double* R; long ldr; long sR; const double* Y; long ldy; long sY; int p, ppad;
 };
 
 struct CholArgs {
@@ -36,6 +38,8 @@ struct AlphaArgs {
     double* alpha; long lda;              // Npad x Ppad
     double* zpart;                        // T*Tp partial sums of Z^2 (valid region)
     int T, Tp, n, p;
+    double* apart;                        // [chunk][Npad x Ppad] partial products
+    int npad;
 };
 
 struct GradArgs {
@@ -45,6 +49,7 @@ struct GradArgs {
     const double* theta;
     double* gpart; int gstride;           // per task partial gradient
     int T, Tp, n, P, D;
+    int chunk;                            // m-tiles per task
 };
 
 struct FinArgs {
@@ -64,6 +69,7 @@ struct FinArgs {
     double lr, b1, b2, eps;
     double* loss_hist;                // loss_hist[step] = -lml (pre-step)
     int noise_index;                  // theta entry using Shift(1e-6) o Softplus
+    double* items;                    // [2 + G] stage-1 reduction results
 };
 
 struct PredAArgs {
@@ -88,7 +94,9 @@ size_t gram_smem_bytes(int nb);
 size_t chol_smem_bytes(int nb);
 size_t grad_smem_bytes(int nb);
 int chol_step_blocks(int T, int Tp, int k);
-int grad_tasks(int T);
+int grad_tasks(int T, int chunk);
+int alpha_tasks(int T, int Tp);
+
 
 template <int NB> void launch_gram(const GramArgs& g, int nblocks, int batch, hipStream_t s);
 template <int NB> void launch_chol_steps(CholArgs c, int batch, hipStream_t s);
@@ -99,6 +107,7 @@ template <int NB> void launch_pred(const PredAArgs& pa, const PredOutArgs& po, i
 __global__ void k_rhs_init(double* R, long ldr, long sR, int npad, int ppad, const double* Y, long ldy, long sY,
                            int n, int p);
 __global__ void k_finalize(FinArgs a);
+__global__ void k_reduce_items(FinArgs a);
 __global__ void k_theta_from_u(const double* u, double* theta, int G, int noise_index);
 __global__ void k_kdiag(const double* X, long ldx, int n, int D, const double* theta, double* out);
 __global__ void k_selftest_mfma(double* out);

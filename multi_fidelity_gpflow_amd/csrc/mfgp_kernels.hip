@@ -18,6 +18,7 @@
 namespace mfgp {
 
 constexpr int MAXD = 32;
+constexpr int ALPHA_CH = 4;   // m-tiles per alpha task
 
 // ============================================================ K1: gram
 
@@ -128,6 +129,22 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
         }
     }
     if (!a.padded) return;
+    if (a.R != nullptr) {
+        // fused RHS init: R tile (ti, tj) of the identity part, and row block ti of Y
+        double* Rb = a.R + b * a.sR;
+        for (int e = threadIdx.x; e < NB * NB; e += NTHREADS) {
+            const int r = e / NB, c = e % NB;
+            Rb[(long)(ti * NB + r) * a.ldr + tj * NB + c] = (ti == tj && r == c) ? 1.0 : 0.0;
+        }
+        if (tj == 0) {
+            const double* Yb = a.Y + b * a.sY;
+            for (int e = threadIdx.x; e < NB * a.ppad; e += NTHREADS) {
+                const int r = e / a.ppad, c = e % a.ppad;
+                const int gr = ti * NB + r;
+                Rb[(long)gr * a.ldr + a.npad + c] = (gr < a.n1 && c < a.p) ? Yb[(long)gr * a.ldy + c] : 0.0;
+            }
+        }
+    }
     __syncthreads();
     tile_store<NB>(out + (long)ti * NB * a.ldo + tj * NB, a.ldo, tile);
     if (a.Dd != nullptr && ti == 0 && tj == 0) {
@@ -136,7 +153,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
         tile_potrf_inv<NB>(tile, rtile, dg, &bad);
         tile_store<NB>(a.Dd + b * a.sD, NB, rtile);
         for (int r = threadIdx.x; r < NB; r += NTHREADS) a.ldiag[b * a.sL + r] = dg[r];
-        if (threadIdx.x == 0 && bad && a.info[b] == 0) a.info[b] = bad;
+        if (threadIdx.x == 0) a.info[b] = bad;   // first writer of info in the sequence: initialises it
     }
 }
 
@@ -286,19 +303,38 @@ __global__ void k_rhs_init(double* R, long ldr, long sR, int npad, int ppad, con
 
 // ============================================================ K3: alpha = L^{-T} Z
 
+__host__ __device__ inline int alpha_row_chunks(int T, int i) { return (T - i + ALPHA_CH - 1) / ALPHA_CH; }
+
+int alpha_tasks(int T, int Tp) {
+    int s = 0;
+    for (int i = 0; i < T; ++i) s += Tp * alpha_row_chunks(T, i);
+    return s;
+}
+
+// alpha_i = sum_{m >= i} Linv_mi^T Z_m, split over m-chunks of ALPHA_CH tiles; each
+// task writes its partial product into slab[ch]; k_alpha_reduce sums the slabs.
 template <int NB>
 __global__ __launch_bounds__(NTHREADS) void k_alpha(AlphaArgs a) {
+    constexpr int S = TileCfg<NB>::S;
     constexpr int E = TileCfg<NB>::ELEMS;
     extern __shared__ __attribute__((aligned(16))) double smem[];
     double* Ls = smem;
     double* Zs = Ls + E;
     double* red = Zs + E;
-    const int i = blockIdx.x / a.Tp, cy = blockIdx.x % a.Tp;
+    int t = blockIdx.x, i = 0;
+    for (;; ++i) {
+        const int cnt = a.Tp * alpha_row_chunks(a.T, i);
+        if (t < cnt) break;
+        t -= cnt;
+    }
+    const int nch = alpha_row_chunks(a.T, i);
+    const int cy = t / nch, ch = t % nch;
+    const int m0 = i + ch * ALPHA_CH, m1 = min(a.T, m0 + ALPHA_CH);
     auto Xt = [&](int r, int c) { return a.Xo + (long)r * NB * a.ldx + (long)c * NB; };
     Acc<NB> acc;
     acc_zero(acc);
     double z2 = 0.0;
-    for (int m = i; m < a.T; ++m) {
+    for (int m = m0; m < m1; ++m) {
         tile_load<NB>(Ls, Xt(m, i), a.ldx);
         tile_load<NB>(Zs, Xt(m, a.T + cy), a.ldx);
         __syncthreads();
@@ -306,7 +342,7 @@ __global__ __launch_bounds__(NTHREADS) void k_alpha(AlphaArgs a) {
             for (int e = threadIdx.x; e < NB * NB; e += NTHREADS) {
                 const int r = e / NB, c = e % NB;
                 if (i * NB + r < a.n && cy * NB + c < a.p) {
-                    const double z = Zs[r * TileCfg<NB>::S + c];
+                    const double z = Zs[r * S + c];
                     z2 += z * z;
                 }
             }
@@ -314,19 +350,31 @@ __global__ __launch_bounds__(NTHREADS) void k_alpha(AlphaArgs a) {
         tile_mma<NB, true, false>(acc, Ls, Zs, 1.0);
         __syncthreads();
     }
-    acc_store(acc, a.alpha + (long)i * NB * a.lda + (long)cy * NB, a.lda);
-    z2 = block_sum(z2, red);
-    if (threadIdx.x == 0) a.zpart[blockIdx.x] = z2;
+    const long slab = (long)a.npad * a.lda;
+    acc_store(acc, a.apart + ch * slab + (long)i * NB * a.lda + (long)cy * NB, a.lda);
+    if (ch == 0) {
+        z2 = block_sum(z2, red);
+        if (threadIdx.x == 0) a.zpart[i * a.Tp + cy] = z2;
+    }
+}
+
+__global__ void k_alpha_reduce(AlphaArgs a, int NB) {
+    const long total = (long)a.npad * a.lda;
+    for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const int r = (int)(e / a.lda);
+        const int nch = alpha_row_chunks(a.T, r / NB);
+        double s = 0.0;
+        for (int ch = 0; ch < nch; ++ch) s += a.apart[ch * total + e];
+        a.alpha[e] = s;
+    }
 }
 
 // ============================================================ K5: gradient
-constexpr int GRAD_CH = 8;   // m-range chunk per task (load balance)
+__host__ __device__ inline int grad_row_chunks(int T, int i, int ch) { return (T - i + ch - 1) / ch; }
 
-__host__ __device__ inline int grad_row_chunks(int T, int i) { return (T - i + GRAD_CH - 1) / GRAD_CH; }
-
-int grad_tasks(int T) {
+int grad_tasks(int T, int ch) {
     int s = 0;
-    for (int i = 0; i < T; ++i) s += (i + 1) * grad_row_chunks(T, i);
+    for (int i = 0; i < T; ++i) s += (i + 1) * grad_row_chunks(T, i, ch);
     return s;
 }
 
@@ -350,14 +398,14 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
     // decode task -> (i, j, m0, m1)
     int t = blockIdx.x, i = 0;
     for (;; ++i) {
-        const int cnt = (i + 1) * grad_row_chunks(a.T, i);
+        const int cnt = (i + 1) * grad_row_chunks(a.T, i, a.chunk);
         if (t < cnt) break;
         t -= cnt;
     }
-    const int nch = grad_row_chunks(a.T, i);
+    const int nch = grad_row_chunks(a.T, i, a.chunk);
     const int j = t / nch, ch = t % nch;
-    const int m0 = i + ch * GRAD_CH;
-    const int m1 = min(a.T, m0 + GRAD_CH);
+    const int m0 = i + ch * a.chunk;
+    const int m1 = min(a.T, m0 + a.chunk);
     auto Xt = [&](int r, int c) { return a.Xo + (long)r * NB * a.ldx + (long)c * NB; };
 
     // stage raw inputs of the two row tiles
@@ -459,7 +507,7 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
         else if (qx <= a.D) { const double l = th.lL(qx - 1); v /= l * l * l; }
         else if (qx == 1 + a.D) v /= th.vD();
         else if (qx <= 1 + 2 * a.D) { const double l = th.lD(qx - 2 - a.D); v /= l * l * l; }
-        a.gpart[(long)blockIdx.x * a.gstride + qx] = v;
+        a.gpart[(long)qx * gridDim.x + blockIdx.x] = v;   // [quantity][task]: coalesced reduction
     }
 }
 
@@ -477,42 +525,52 @@ __device__ __forceinline__ double tf_softplus(double x) {
     return log(exp(x) + 1.0);
 }
 
-__global__ __launch_bounds__(NTHREADS) void k_finalize(FinArgs a) {
+// Stage 1 of the step reduction: workgroup `it` sums item `it` of
+// [sum Z^2, sum log L_ii, grad_0 .. grad_{G-1}] (partials stored [item][task]) with
+// all 256 threads in flight at once; deterministic order.
+__global__ __launch_bounds__(NTHREADS) void k_reduce_items(FinArgs a) {
     __shared__ double red[4];
-    __shared__ double gsh[2 * MAXD + 4];
-    __shared__ double lml_sh;
-    const int G = theta_size(a.D);
-    double z2 = 0.0, ld = 0.0;
-    for (int e = threadIdx.x; e < a.nz; e += NTHREADS) z2 += a.zpart[e];
-    for (int e = threadIdx.x; e < a.n; e += NTHREADS) ld += log(a.ldiag[e]);
-    z2 = block_sum(z2, red);
-    ld = block_sum(ld, red);
-    const double LOG2PI = 1.8378770664093453;
-    double lml = -0.5 * z2 - (double)a.P * ld - 0.5 * (double)a.n * (double)a.P * LOG2PI;
-    if (a.info[0] != 0) lml = NAN;
-    if (a.want_grad) {
-        for (int q = 0; q < G; ++q) {
-            double s = 0.0;
-            for (int e = threadIdx.x; e < a.ng; e += NTHREADS) s += a.gpart[(long)e * a.gstride + q];
-            s = block_sum(s, red);
-            if (threadIdx.x == 0) gsh[q] = s;
+    const int it = blockIdx.x;
+    double s = 0.0;
+    if (it == 0) {
+        for (int e = threadIdx.x; e < a.nz; e += NTHREADS) s += a.zpart[e];
+    } else if (it == 1) {
+        for (int e = threadIdx.x; e < a.n; e += NTHREADS) s += log(a.ldiag[e]);
+    } else {
+        const double* src = a.gpart + (long)(it - 2) * a.ng;
+        double s1 = 0.0, s2 = 0.0, s3 = 0.0;
+        int e = threadIdx.x;
+        for (; e + 3 * NTHREADS < a.ng; e += 4 * NTHREADS) {
+            s += src[e];
+            s1 += src[e + NTHREADS];
+            s2 += src[e + 2 * NTHREADS];
+            s3 += src[e + 3 * NTHREADS];
         }
+        for (; e < a.ng; e += NTHREADS) s += src[e];
+        s = (s + s1) + (s2 + s3);
     }
-    if (threadIdx.x == 0) {
-        lml_sh = lml;
-        a.out[0] = lml;
-    }
-    __syncthreads();
+    s = block_sum(s, red);
+    if (threadIdx.x == 0) a.items[it] = s;
+}
+
+// Stage 2: LML, gradient output and the optional Keras-Adam step (one wave).
+__global__ __launch_bounds__(64) void k_finalize(FinArgs a) {
+    const int G = theta_size(a.D);
+    const double* items = a.items;
+    const double LOG2PI = 1.8378770664093453;
+    double lml = -0.5 * items[0] - (double)a.P * items[1] - 0.5 * (double)a.n * (double)a.P * LOG2PI;
+    if (a.info[0] != 0) lml = NAN;
+    if (threadIdx.x == 0) a.out[0] = lml;
     if (a.want_grad)
-        for (int q = threadIdx.x; q < G; q += NTHREADS) a.out[1 + q] = gsh[q];
+        for (int q = threadIdx.x; q < G; q += 64) a.out[1 + q] = items[2 + q];
     if (!a.adam) return;
-    __syncthreads();
+    const double* gsh = items + 2;
     const int s = *a.step;
-    if (threadIdx.x == 0) a.loss_hist[s] = -lml_sh;
+    if (threadIdx.x == 0) a.loss_hist[s] = -lml;
     if (a.info[0] != 0) return;   // non-PD: leave parameters untouched (host raises)
     const double t = (double)(s + 1);
     const double alpha = a.lr * sqrt(1.0 - pow(a.b2, t)) / (1.0 - pow(a.b1, t));
-    for (int q = threadIdx.x; q < G; q += NTHREADS) {
+    for (int q = threadIdx.x; q < G; q += 64) {
         if (a.trainable[q]) {
             const double uq = a.u[q];
             double gc = gsh[q];
@@ -532,7 +590,6 @@ __global__ __launch_bounds__(NTHREADS) void k_finalize(FinArgs a) {
             a.theta[q] = tf_softplus(un) + (q == a.noise_index ? 1e-6 : 0.0);
         }
     }
-    __syncthreads();
     if (threadIdx.x == 0) *a.step = s + 1;
 }
 
@@ -635,12 +692,14 @@ void launch_chol_steps(CholArgs c, int batch, hipStream_t s) {
 }
 template <int NB>
 void launch_alpha(const AlphaArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_alpha<NB>, dim3(a.T * a.Tp), dim3(NTHREADS), sizeof(double) * (2 * NB * (NB + 2) + 4), s,
-                       a);
+    hipLaunchKernelGGL(k_alpha<NB>, dim3(alpha_tasks(a.T, a.Tp)), dim3(NTHREADS),
+                       sizeof(double) * (2 * NB * (NB + 2) + 4), s, a);
+    const long total = (long)a.npad * a.lda;
+    hipLaunchKernelGGL(k_alpha_reduce, dim3((int)std::min<long>((total + 255) / 256, 1024)), dim3(256), 0, s, a, NB);
 }
 template <int NB>
 void launch_grad(const GradArgs& g, hipStream_t s) {
-    hipLaunchKernelGGL(k_grad<NB>, dim3(grad_tasks(g.T)), dim3(NTHREADS), grad_smem_bytes(NB), s, g);
+    hipLaunchKernelGGL(k_grad<NB>, dim3(grad_tasks(g.T, g.chunk)), dim3(NTHREADS), grad_smem_bytes(NB), s, g);
 }
 template <int NB>
 void launch_pred(const PredAArgs& pa, const PredOutArgs& po, int T, hipStream_t s) {
