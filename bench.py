@@ -38,6 +38,22 @@ sys.path.insert(0, ROOT)
 GOKU = os.path.join(ROOT, "tests", "golden", "data", "matter_power_1128_Box1000_Part750_36_Box1000_Part3000_z0")
 FP64_PEAK_TFLOPS = 78.6   # MI355X dense FP64 (vector = matrix on gfx950), MI355X_MICROARCH.md
 HBM_PEAK_GBS = 8000.0
+# HBM bytes per dispatch from the committed rocprofv3 PMC passes (tools/profile_round.sh ->
+# tools/summarize_profile.py); the bench cannot count PMC on itself.
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01", "pmc_summary.json")
+
+
+def pmc_traffic(kernel_prefix, nb):
+    """(bytes per dispatch, source) of the dominant kernel from the committed PMC summary."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            kern = json.load(f)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None, None
+    for name, v in kern.items():
+        if f"{kernel_prefix}<{nb}>" in name:
+            return v["hbm_bytes"], os.path.relpath(PMC_SUMMARY, ROOT)
+    return None, None
 
 
 def load_goku():
@@ -77,7 +93,7 @@ def roofline(model, n, p, d, reps=10):
     for _ in range(reps):
         acc += np.array(gpr_phase_times(eng, X, Y, theta))
     ms = acc / reps
-    names = ["rhs_init", "gram", "chol_steps", "alpha", "grad", "finalize"]
+    names = ["pre", "gram", "chol_steps", "alpha", "grad", "finalize"]
     nb = eng.tile()
     T = -(-n // nb)
     # algorithmic work per phase (SURVEY §8(d) figures)
@@ -93,14 +109,18 @@ def roofline(model, n, p, d, reps=10):
     per_launch_ms = t_ms / launches[dom]
     per_launch_flop = flops[dom] / launches[dom]
     achieved = per_launch_flop / (per_launch_ms * 1e-3) / 1e12
+    kname = {"chol_steps": "k_chol_step", "gram": "k_gram", "alpha": "k_alpha", "grad": "k_grad"}[dom]
+    traffic, tsrc = pmc_traffic(kname, nb)
     return {
-        "kernel": {"chol_steps": "k_chol_step", "gram": "k_gram", "alpha": "k_alpha", "grad": "k_grad"}[dom],
+        "kernel": kname,
         "bound": "mfma",
         "achieved": round(achieved, 4),
         "peak": FP64_PEAK_TFLOPS,
         "unit": "TFLOP/s",
         "frac": round(achieved / FP64_PEAK_TFLOPS, 5),
-        "traffic": None,
+        "traffic": traffic,
+        "traffic_unit": "bytes per launch (FETCH_SIZE x2 + WRITE_SIZE)",
+        "traffic_source": tsrc,
         "launches_per_step": launches[dom],
         "avg_launch_us": round(per_launch_ms * 1e3, 3),
         "flop_per_launch": per_launch_flop,

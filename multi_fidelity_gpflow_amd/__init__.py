@@ -9,8 +9,9 @@ from .params import Parameter, positive, set_trainable, parameter_dict, multiple
 from .kernels import (SquaredExponential, RBF, LinearMultiFidelityKernel,  # noqa: F401
                       LinearCoregionalization, SeparateIndependent)
 from .models import MultiFidelityGPModel, Gaussian, CholeskyError  # noqa: F401
-from .svgp import LatentMFCoregionalizationSVGP, SingleBinSVGP, initialize_W  # noqa: F401
-from .data import PowerSpecs  # noqa: F401
+from .svgp import LatentMFCoregionalizationSVGP, SingleBinSVGP, initialize_W, initialize_W_pca  # noqa: F401
+from .data import PowerSpecs, map_to_unit_cube, input_normalize  # noqa: F401
+from . import data  # noqa: F401
 from ._lib import MFGPError  # noqa: F401
 
 __version__ = "0.1.0"
