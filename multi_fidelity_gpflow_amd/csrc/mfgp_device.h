@@ -163,6 +163,22 @@ __device__ __forceinline__ double rcp_nr(double a) {
     return fma(r, e, r);
 }
 
+// ---------------------------------------------------------------- pivot check
+// First non-positive / non-finite pivot of an NB = 32 tile (1-based, 0 if none) without a
+// serial scan (a dependent LDS walk costs ~3.8k clocks): thread (row i = t/8, g = t%8 == 0)
+// flags its row, one ballot per wave, lane 0 writes the wave's first row into slot[w].
+// slot[] (4 ints) must be read back after a barrier: pivot_check_result().
+__device__ __forceinline__ void pivot_check_post(double d, int* slot) {
+    const int t = threadIdx.x;
+    const bool fl = ((t & 7) == 0) && !(d > 0.0 && d < INFINITY);
+    const unsigned long long m = __ballot(fl);
+    if ((t & 63) == 0) slot[t >> 6] = m ? 8 * (t >> 6) + (__ffsll((long long)m) - 1) / 8 + 1 : 0;
+}
+__device__ __forceinline__ int pivot_check_result(const int* slot) {
+    const int s0 = slot[0], s1 = slot[1], s2 = slot[2], s3 = slot[3];
+    return s0 ? s0 : s1 ? s1 : s2 ? s2 : s3;
+}
+
 // ---------------------------------------------------------------- diag factor
 // Cholesky of an SPD NB x NB tile A fused with the inverse of its factor.
 // On exit R holds D = L^{-1} (lower, zero above) and dg[i] = L_ii.
@@ -240,19 +256,150 @@ __device__ __forceinline__ void tile_potrf_inv<32>(double* __restrict__ A, doubl
         if (i == k1) *reinterpret_cast<double4*>(rowb + nxt * NB + c0) = double4{r[0], r[1], r[2], r[3]};
         __syncthreads();
     }
-    if (g == 0) dg[i] = dgk;
-    __syncthreads();
     (void)dump;
-    // L_ii = sqrt(a_ii); D = diag(1/L) R
-    const double li = sqrt(dg[i]);
+    // L_ii = sqrt(a_ii); D = diag(1/L) R; the pivot check needs no serial scan
+    pivot_check_post(dgk, bad);
+    const double li = sqrt(dgk);
     const double rli = 1.0 / li;
-    if (t == 0) {
-        int b = 0;
-        for (int k = 0; k < NB && !b; ++k)
-            if (!(dg[k] > 0.0 && dg[k] < INFINITY)) b = k + 1;
-        *bad = b;
+    __syncthreads();
+    if (t == 0) *bad = pivot_check_result(bad);
+    if (g == 0) dg[i] = li;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) R[i * S + c0 + q] = (c0 + q <= i) ? r[q] * rli : 0.0;
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------- 4-pivot blocked diag factor
+// NB = 32 Cholesky + inverse by blocked LDL^T elimination, 4 pivots per barrier round
+// (8 rounds instead of 32: the per-round LDS publish -> barrier -> read latency is the
+// cost, not the arithmetic).  Thread t owns row i = t/8, columns 4g..4g+3 of A and R.
+// Round k (= 4 rd): the 4 current columns C = A[:, k..k+3] (zero above row k) and the 4
+// pivot rows R_P = R[k..k+3, :] are published; every thread factors the pivot block
+// M = C[k..k+3, :] = L_M D_M L_M^T redundantly in registers (rcp only, no sqrt), then
+//   A_i -= w_i C^T,            w_i = C_i M^{-1}                 (rows >= k+4; rows < k
+//                                                               have C_i = 0: no-op)
+//   R_i -= v_i R_P,            v_i = w_i, or -(L_M^{-1})_{p,<p} for pivot row p = i-k.
+// R accumulates L_u^{-1} (unit lower); at the end D = diag(d)^{-1/2} L_u^{-1} = L^{-1}
+// and dg = sqrt(d).  A is left as garbage.  Non-positive pivots report through *bad.
+__device__ __forceinline__ void tile_potrf_inv_k4(double* A, double* R, double* dg, int* bad) {
+    constexpr int NB = 32;
+    constexpr int S = TileCfg<NB>::S;
+    double* colb = R;                 // [2][NB][4]
+    double* rowb = R + 2 * NB * 4;    // [2][4][NB]
+    double* piv = R + 4 * NB * 4;     // [NB]
+    const int t = threadIdx.x;
+    const int i = t >> 3, g = t & 7, c0 = 4 * g;
+    double a[4], r[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        a[q] = A[i * S + c0 + q];
+        r[q] = (i == c0 + q) ? 1.0 : 0.0;
     }
     __syncthreads();
+    if (g == 0) {
+        *reinterpret_cast<double2*>(colb + i * 4) = double2{a[0], a[1]};
+        *reinterpret_cast<double2*>(colb + i * 4 + 2) = double2{a[2], a[3]};
+    }
+    if (i < 4) {
+        *reinterpret_cast<double2*>(rowb + i * NB + c0) = double2{r[0], r[1]};
+        *reinterpret_cast<double2*>(rowb + i * NB + c0 + 2) = double2{r[2], r[3]};
+    }
+    __syncthreads();
+#pragma unroll 2
+    for (int rd = 0; rd < NB / 4; ++rd) {
+        const int k = 4 * rd, cur = rd & 1, nxt = cur ^ 1;
+        const double* C = colb + cur * NB * 4;
+        const double* RP = rowb + cur * 4 * NB;
+        double M[4][4], Ci[4], Cj[4][4], Rp[4][4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const double2 u = *reinterpret_cast<const double2*>(C + (k + p) * 4);
+            const double2 w = *reinterpret_cast<const double2*>(C + (k + p) * 4 + 2);
+            M[p][0] = u.x; M[p][1] = u.y; M[p][2] = w.x; M[p][3] = w.y;
+        }
+        {
+            const double2 u = *reinterpret_cast<const double2*>(C + i * 4);
+            const double2 w = *reinterpret_cast<const double2*>(C + i * 4 + 2);
+            Ci[0] = u.x; Ci[1] = u.y; Ci[2] = w.x; Ci[3] = w.y;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const double2 u = *reinterpret_cast<const double2*>(C + (c0 + q) * 4);
+            const double2 w = *reinterpret_cast<const double2*>(C + (c0 + q) * 4 + 2);
+            Cj[q][0] = u.x; Cj[q][1] = u.y; Cj[q][2] = w.x; Cj[q][3] = w.y;
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const double2 u = *reinterpret_cast<const double2*>(RP + m * NB + c0);
+            const double2 w = *reinterpret_cast<const double2*>(RP + m * NB + c0 + 2);
+            Rp[m][0] = u.x; Rp[m][1] = u.y; Rp[m][2] = w.x; Rp[m][3] = w.y;
+        }
+        // LDL^T of the pivot block (lower entries): u_ab = L_ab d_b = e_ab
+        const double d0 = M[0][0];
+        const double i0 = rcp_nr(d0);
+        const double L10 = M[1][0] * i0, L20 = M[2][0] * i0, L30 = M[3][0] * i0;
+        const double d1 = M[1][1] - L10 * M[1][0];
+        const double i1 = rcp_nr(d1);
+        const double e21 = M[2][1] - L20 * M[1][0];
+        const double e31 = M[3][1] - L30 * M[1][0];
+        const double L21 = e21 * i1, L31 = e31 * i1;
+        const double d2 = M[2][2] - L20 * M[2][0] - L21 * e21;
+        const double i2 = rcp_nr(d2);
+        const double e32 = M[3][2] - L30 * M[2][0] - L31 * e21;
+        const double L32 = e32 * i2;
+        const double d3 = M[3][3] - L30 * M[3][0] - L31 * e31 - L32 * e32;
+        const double i3 = rcp_nr(d3);
+        // w = C_i M^{-1} = ((C_i L^{-T}) D^{-1}) L^{-1}
+        const double y0 = Ci[0];
+        const double y1 = Ci[1] - L10 * y0;
+        const double y2 = Ci[2] - L20 * y0 - L21 * y1;
+        const double y3 = Ci[3] - L30 * y0 - L31 * y1 - L32 * y2;
+        const double w3 = y3 * i3;
+        const double w2 = y2 * i2 - L32 * w3;
+        const double w1 = y1 * i1 - L21 * w2 - L31 * w3;
+        const double w0 = y0 * i0 - L10 * w1 - L20 * w2 - L30 * w3;
+        // pivot rows of R: R_P <- L^{-1} R_P, i.e. v = -(L^{-1})_{p, m<p}
+        const double N10 = -L10;
+        const double N21 = -L21, N20 = -(L20 + L21 * N10);
+        const double N32 = -L32, N31 = -(L31 + L32 * N21), N30 = -(L30 + L31 * N10 + L32 * N20);
+        const int pr = i - k;
+        double v0 = w0, v1 = w1, v2 = w2, v3 = w3;
+        if (pr >= 0 && pr < 4) {
+            v0 = (pr == 1) ? -N10 : (pr == 2) ? -N20 : (pr == 3) ? -N30 : 0.0;
+            v1 = (pr == 2) ? -N21 : (pr == 3) ? -N31 : 0.0;
+            v2 = (pr == 3) ? -N32 : 0.0;
+            v3 = 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            a[q] -= w0 * Cj[q][0] + w1 * Cj[q][1] + w2 * Cj[q][2] + w3 * Cj[q][3];
+            r[q] -= v0 * Rp[0][q] + v1 * Rp[1][q] + v2 * Rp[2][q] + v3 * Rp[3][q];
+        }
+        if (t == 0) {
+            piv[k] = d0; piv[k + 1] = d1; piv[k + 2] = d2; piv[k + 3] = d3;
+        }
+        if (rd + 1 < NB / 4) {
+            const int kn = k + 4;
+            double* Cn = colb + nxt * NB * 4;
+            double* Rn = rowb + nxt * 4 * NB;
+            if (g == rd + 1) {
+                const bool z = i < kn;
+                *reinterpret_cast<double2*>(Cn + i * 4) = double2{z ? 0.0 : a[0], z ? 0.0 : a[1]};
+                *reinterpret_cast<double2*>(Cn + i * 4 + 2) = double2{z ? 0.0 : a[2], z ? 0.0 : a[3]};
+            }
+            if (i >= kn && i < kn + 4) {
+                *reinterpret_cast<double2*>(Rn + (i - kn) * NB + c0) = double2{r[0], r[1]};
+                *reinterpret_cast<double2*>(Rn + (i - kn) * NB + c0 + 2) = double2{r[2], r[3]};
+            }
+        }
+        __syncthreads();
+    }
+    const double di = piv[i];
+    pivot_check_post(di, bad);
+    __syncthreads();
+    if (t == 0) *bad = pivot_check_result(bad);
+    const double li = sqrt(di);
+    const double rli = 1.0 / li;
     if (g == 0) dg[i] = li;
 #pragma unroll
     for (int q = 0; q < 4; ++q) R[i * S + c0 + q] = (c0 + q <= i) ? r[q] * rli : 0.0;

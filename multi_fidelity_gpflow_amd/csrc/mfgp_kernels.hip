@@ -18,6 +18,8 @@
 namespace mfgp {
 
 constexpr int MAXD = 32;
+constexpr int XS = MAXD + 1;   // LDS row stride of staged inputs: odd, so a wave reading one
+                                // dimension of 16-32 different rows hits distinct banks
 constexpr int ALPHA_CH = 4;   // m-tiles per alpha task
 
 // ============================================================ K1: gram
@@ -26,21 +28,21 @@ template <int NB>
 __device__ __forceinline__ void stage_rows(double* aL, double* aD, double* nL, double* nD, double* f,
                                            const double* X, long ldx, int n, int r0, int D,
                                            const MFTheta& th, int rbf_only) {
-    // aL[r*MAXD + d] = X[r][d] / lL[d] ; nL[r] = sum aL^2 (GPflow square_distance)
+    // aL[r*XS + d] = X[r][d] / lL[d] ; nL[r] = sum aL^2 (GPflow square_distance)
     for (int e = threadIdx.x; e < NB * D; e += NTHREADS) {
         const int r = e / D, d = e % D;
         const int gr = r0 + r;
         const double x = (gr < n) ? X[(long)gr * ldx + d] : 0.0;
-        aL[r * MAXD + d] = x / th.lL(d);
-        if (!rbf_only) aD[r * MAXD + d] = x / th.lD(d);
+        aL[r * XS + d] = x / th.lL(d);
+        if (!rbf_only) aD[r * XS + d] = x / th.lD(d);
     }
     __syncthreads();
     for (int r = threadIdx.x; r < NB; r += NTHREADS) {
         double sL = 0.0, sD = 0.0;
         for (int d = 0; d < D; ++d) {
-            const double a = aL[r * MAXD + d];
+            const double a = aL[r * XS + d];
             sL += a * a;
-            if (!rbf_only) { const double b = aD[r * MAXD + d]; sD += b * b; }
+            if (!rbf_only) { const double b = aD[r * XS + d]; sD += b * b; }
         }
         nL[r] = sL;
         nD[r] = sD;
@@ -79,10 +81,10 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
     constexpr int S = TileCfg<NB>::S;
     extern __shared__ __attribute__((aligned(16))) double smem[];
     double* aL1 = smem;
-    double* aD1 = aL1 + NB * MAXD;
-    double* aL2 = aD1 + NB * MAXD;
-    double* aD2 = aL2 + NB * MAXD;
-    double* nL1 = aD2 + NB * MAXD;
+    double* aD1 = aL1 + NB * XS;
+    double* aL2 = aD1 + NB * XS;
+    double* aD2 = aL2 + NB * XS;
+    double* nL1 = aD2 + NB * XS;
     double* nD1 = nL1 + NB;
     double* f1 = nD1 + NB;
     double* nL2 = f1 + NB;
@@ -118,8 +120,8 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
     for (int e = threadIdx.x; e < NB * NB; e += NTHREADS) {
         const int r = e / NB, c = e % NB;
         const int gi = ti * NB + r, gj = tj * NB + c;
-        double v = gram_entry(aL1 + r * MAXD, aD1 + r * MAXD, nL1[r], nD1[r], f1[r],
-                              aL2 + c * MAXD, aD2 + c * MAXD, nL2[c], nD2[c], f2[c], a.D, th, a.rbf_only);
+        double v = gram_entry(aL1 + r * XS, aD1 + r * XS, nL1[r], nD1[r], f1[r],
+                              aL2 + c * XS, aD2 + c * XS, nL2[c], nD2[c], f2[c], a.D, th, a.rbf_only);
         if (a.padded) {
             if (gi == gj) v = (gi < a.n1) ? v + noise + a.diag_add : 1.0;   // identity padding
             tile[r * S + c] = v;
@@ -159,7 +161,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
 
 size_t gram_smem_bytes(int nb) {
     const size_t tile = (size_t)nb * (nb + 2);
-    return sizeof(double) * (4 * (size_t)nb * MAXD + 6 * (size_t)nb + 2 * tile + nb + 2);
+    return sizeof(double) * (4 * (size_t)nb * XS + 6 * (size_t)nb + 2 * tile + nb + 2);
 }
 
 // ============================================================ K2: tile Cholesky step
@@ -387,9 +389,9 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     double* As = smem;
     double* Bs = As + E;
-    double* xi = Bs + E;              // NB x MAXD raw rows of tile i
-    double* xj = xi + NB * MAXD;      // NB x MAXD raw rows of tile j
-    double* fi = xj + NB * MAXD;      // NB
+    double* xi = Bs + E;              // NB x XS raw rows of tile i
+    double* xj = xi + NB * XS;        // NB x XS raw rows of tile j
+    double* fi = xj + NB * XS;      // NB
     double* fj = fi + NB;             // NB
     double* red = fj + NB;            // 4 x (2*MAXD+4)
     const int G = theta_size(a.D);
@@ -414,7 +416,7 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
         const int gi = i * NB + r, gj = j * NB + r;
         const double vi = (gi < a.n) ? a.X[(long)gi * a.ldxx + d] : 0.0;
         const double vj = (gj < a.n) ? a.X[(long)gj * a.ldxx + d] : 0.0;
-        if (d < a.D) { xi[r * MAXD + d] = vi; xj[r * MAXD + d] = vj; }
+        if (d < a.D) { xi[r * XS + d] = vi; xj[r * XS + d] = vj; }
         else { fi[r] = (gi < a.n) ? vi : -1.0; fj[r] = (gj < a.n) ? vj : -1.0; }
     }
 
@@ -458,7 +460,7 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
             if ((L1 || H1) && (L2 || H2)) {
                 double s2 = 0.0, s2d = 0.0;
                 for (int d = 0; d < a.D; ++d) {
-                    const double df = xi[ri * MAXD + d] - xj[cj * MAXD + d];
+                    const double df = xi[ri * XS + d] - xj[cj * XS + d];
                     const double d2 = df * df;
                     const double ql = th.lL(d);
                     s2 += d2 / (ql * ql);
@@ -492,7 +494,7 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int e = q * 4 + r;
-                const double df = xi[acc_row<NB>(q, r) * MAXD + d] - xj[acc_col<NB>(q) * MAXD + d];
+                const double df = xi[acc_row<NB>(q, r) * XS + d] - xj[acc_col<NB>(q) * XS + d];
                 tl += cL[e] * df * df;
                 td += cD[e] * df * df;
             }
@@ -512,7 +514,7 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
 }
 
 size_t grad_smem_bytes(int nb) {
-    return sizeof(double) * (2 * (size_t)nb * (nb + 2) + 2 * (size_t)nb * MAXD + 2 * nb + 4 * (2 * MAXD + 4));
+    return sizeof(double) * (2 * (size_t)nb * (nb + 2) + 2 * (size_t)nb * XS + 2 * nb + 4 * (2 * MAXD + 4));
 }
 
 // ============================================================ K4: finalize (+Adam)
