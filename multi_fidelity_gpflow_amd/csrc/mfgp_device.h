@@ -196,9 +196,9 @@ template <int NB>
 __device__ void tile_potrf_inv(double* __restrict__ A, double* __restrict__ R, double* __restrict__ dg,
                                int* __restrict__ bad);
 
-template <>
-__device__ __forceinline__ void tile_potrf_inv<32>(double* __restrict__ A, double* __restrict__ R,
-                                                   double* __restrict__ dg, int* __restrict__ bad) {
+// One-pivot-per-barrier form (kept as the reference variant for tools/ubench_tile.hip).
+__device__ __forceinline__ void tile_potrf_inv_pivot32(double* __restrict__ A, double* __restrict__ R,
+                                                       double* __restrict__ dg, int* __restrict__ bad) {
     // Branch-free pivot loop (measured ~3x faster than the predicated form on gfx950):
     //  * the pivot column of A is published WHOLE, zero above the pivot, so the
     //    unconditional update a_ic -= s_i a_ck / a_kk is an exact no-op on finalized
@@ -404,6 +404,176 @@ __device__ __forceinline__ void tile_potrf_inv_k4(double* A, double* R, double* 
 #pragma unroll
     for (int q = 0; q < 4; ++q) R[i * S + c0 + q] = (c0 + q <= i) ? r[q] * rli : 0.0;
     __syncthreads();
+}
+
+// ---------------------------------------------------------------- MFMA 4-pivot diag factor
+// NB = 32 Cholesky + inverse, 4 pivots per barrier round with the rank-4 updates on the
+// matrix core.  The tile stays in MFMA accumulator layout for the whole factorization:
+// wave w owns the 16x16 blocks (w>>1, w&1) of A and of R (lane l: rows 16bi + (l>>4) + 4q,
+// column 16bj + (l&15)).  Round k = 4 rd publishes C = A[:, k..k+3] (zero above row k) and
+// R_P = R[k..k+3, :] through LDS; every lane factors the 4x4 pivot block M = C[k..k+3, :] =
+// L_M D_M L_M^T in registers (same elimination order as pivot-by-pivot, no explicit
+// inverse: an explicit M^{-1} lost ill-conditioned Forrester Grams) and feeds the matrix core
+//   A -= (Y D_M^{-1}) Y^T, Y = C L_M^{-T};   R -= V R_P     (one v_mfma_f64_16x16x4 each)
+// with V = C M^{-1} (= Y D_M^{-1} L_M^{-1}, by substitution) for rows >= k+4 and
+// V = I - L_M^{-1} on the pivot rows, so R accumulates L_u^{-1}; pivots d give D = diag(d)^{-1/2}
+// L_u^{-1} = L^{-1} and dg = sqrt(d).  The A tile's LDS doubles as the publish buffer.
+struct M4Buf {
+    double* colb;   // [2][NB][4]
+    double* rowb;   // [2][4][NB]
+    double* piv;    // [NB]
+};
+
+template <int RD>
+__device__ __forceinline__ void m4_round(const M4Buf& B, f64x4& aA, f64x4& aR, int bi, int bj, int lc, int lr) {
+    constexpr int NB = 32;
+    if constexpr (RD < NB / 4) {
+        constexpr int k = 4 * RD, cur = RD & 1, nxt = cur ^ 1;
+        const double* C = B.colb + cur * NB * 4;
+        const double* RP = B.rowb + cur * 4 * NB;
+        const int ia = 16 * bi + lc;   // A-operand row of this lane
+        const int cg = 16 * bj + lc;   // accumulator / B-operand column
+        // ---- reads: pivot block (lower), own operand row, B operands
+        const double2 r0a = *reinterpret_cast<const double2*>(C + (k + 0) * 4);
+        const double2 r1a = *reinterpret_cast<const double2*>(C + (k + 1) * 4);
+        const double2 r2a = *reinterpret_cast<const double2*>(C + (k + 2) * 4);
+        const double2 r2b = *reinterpret_cast<const double2*>(C + (k + 2) * 4 + 2);
+        const double2 r3a = *reinterpret_cast<const double2*>(C + (k + 3) * 4);
+        const double2 r3b = *reinterpret_cast<const double2*>(C + (k + 3) * 4 + 2);
+        const double2 cia = *reinterpret_cast<const double2*>(C + ia * 4);
+        const double2 cib = *reinterpret_cast<const double2*>(C + ia * 4 + 2);
+        const double2 cja = *reinterpret_cast<const double2*>(C + cg * 4);
+        const double2 cjb = *reinterpret_cast<const double2*>(C + cg * 4 + 2);
+        const double bR = RP[lr * NB + cg];
+        const double m00 = r0a.x, m10 = r1a.x, m11 = r1a.y, m20 = r2a.x, m21 = r2a.y, m22 = r2b.x;
+        const double m30 = r3a.x, m31 = r3a.y, m32 = r3b.x, m33 = r3b.y;
+        // ---- LDL^T of the pivot block (the same elimination order as a pivot-by-pivot
+        //      Cholesky; no explicit inverse, so ill-conditioned blocks stay as stable)
+        const double i0 = rcp_nr(m00);
+        const double L10 = m10 * i0, L20 = m20 * i0, L30 = m30 * i0;
+        const double d1 = fma(-L10, m10, m11);
+        const double i1 = rcp_nr(d1);
+        const double e21 = fma(-L20, m10, m21), e31 = fma(-L30, m10, m31);
+        const double L21 = e21 * i1, L31 = e31 * i1;
+        const double d2 = fma(-L21, e21, fma(-L20, m20, m22));
+        const double i2 = rcp_nr(d2);
+        const double e32 = fma(-L31, e21, fma(-L30, m20, m32));
+        const double L32 = e32 * i2;
+        const double d3 = fma(-L32, e32, fma(-L31, e31, fma(-L30, m30, m33)));
+        const double i3 = rcp_nr(d3);
+        // ---- Y = C L_M^{-T} (rows ia and cg), A -= (Y D^{-1}) Y^T
+        const double y0 = cia.x;
+        const double y1 = fma(-L10, y0, cia.y);
+        const double y2 = fma(-L21, y1, fma(-L20, y0, cib.x));
+        const double y3 = fma(-L32, y2, fma(-L31, y1, fma(-L30, y0, cib.y)));
+        const double z0 = y0 * i0, z1 = y1 * i1, z2 = y2 * i2, z3 = y3 * i3;
+        const double u0 = cja.x;
+        const double u1 = fma(-L10, u0, cja.y);
+        const double u2 = fma(-L21, u1, fma(-L20, u0, cjb.x));
+        const double u3 = fma(-L32, u2, fma(-L31, u1, fma(-L30, u0, cjb.y)));
+        const double wl = (lr == 0) ? z0 : (lr == 1) ? z1 : (lr == 2) ? z2 : z3;
+        const double bA = (lr == 0) ? u0 : (lr == 1) ? u1 : (lr == 2) ? u2 : u3;
+        // ---- R multipliers against the original pivot rows: V = Z L_M^{-1} (rows >= k+4;
+        //      rows < k have C = 0), and on pivot row p: -(L_M^{-1})_{p, <p}
+        const double x3 = z3;
+        const double x2 = fma(-L32, x3, z2);
+        const double x1 = fma(-L31, x3, fma(-L21, x2, z1));
+        const double x0 = fma(-L30, x3, fma(-L20, x2, fma(-L10, x1, z0)));
+        double vl = (lr == 0) ? x0 : (lr == 1) ? x1 : (lr == 2) ? x2 : x3;
+        if (bi == (k >> 4)) {   // wave-uniform
+            const int p = lc - (k & 15);
+            if (p >= 0 && p < 4) {
+                const double c20 = fma(-L21, L10, L20);                      // -(N20)
+                const double c31 = fma(-L32, L21, L31);                      // -(N31)
+                const double c30 = fma(-L32, c20, fma(-L31, L10, L30));      // -(N30)
+                const double v1 = (lr == 0) ? L10 : 0.0;
+                const double v2 = (lr == 0) ? c20 : (lr == 1) ? L21 : 0.0;
+                const double v3 = (lr == 0) ? c30 : (lr == 1) ? c31 : (lr == 2) ? L32 : 0.0;
+                vl = (p == 1) ? v1 : (p == 2) ? v2 : (p == 3) ? v3 : 0.0;
+            }
+        }
+        // ---- rank-4 updates on the matrix core
+        aA = __builtin_amdgcn_mfma_f64_16x16x4f64(-wl, bA, aA, 0, 0, 0);
+        aR = __builtin_amdgcn_mfma_f64_16x16x4f64(-vl, bR, aR, 0, 0, 0);
+        if (threadIdx.x == 0) {
+            B.piv[k] = m00;
+            B.piv[k + 1] = d1;
+            B.piv[k + 2] = d2;
+            B.piv[k + 3] = d3;
+        }
+        // ---- publish round RD+1
+        if constexpr (RD + 1 < NB / 4) {
+            constexpr int kn = k + 4;
+            double* Cn = B.colb + nxt * NB * 4;
+            double* Rn = B.rowb + nxt * 4 * NB;
+            if (bj == (kn >> 4)) {
+                const int m = lc - (kn & 15);
+                if (m >= 0 && m < 4) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int rg = 16 * bi + lr + 4 * q;
+                        Cn[rg * 4 + m] = (rg >= kn) ? aA[q] : 0.0;
+                    }
+                }
+            }
+            if (bi == (kn >> 4)) Rn[lr * NB + cg] = aR[((kn & 15) >> 2)];
+        }
+        __syncthreads();
+        m4_round<RD + 1>(B, aA, aR, bi, bj, lc, lr);
+    }
+}
+
+__device__ __forceinline__ void tile_potrf_inv_m4(double* A, double* R, double* dg, int* bad) {
+    constexpr int NB = 32;
+    constexpr int S = TileCfg<NB>::S;
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    const int bi = w >> 1, bj = w & 1, lc = l & 15, lr = l >> 4;
+    const int cg = 16 * bj + lc;
+    f64x4 aA, aR;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int rg = 16 * bi + lr + 4 * q;
+        aA[q] = A[rg * S + cg];
+        aR[q] = (rg == cg) ? 1.0 : 0.0;
+    }
+    __syncthreads();   // A's LDS becomes the publish buffer
+    const M4Buf B{A, A + 2 * NB * 4, A + 4 * NB * 4};
+    if (bj == 0 && lc < 4) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) B.colb[(16 * bi + lr + 4 * q) * 4 + lc] = aA[q];
+    }
+    if (bi == 0) B.rowb[lr * NB + cg] = (lr == cg) ? 1.0 : 0.0;
+    __syncthreads();
+    m4_round<0>(B, aA, aR, bi, bj, lc, lr);
+    // pivots d_i of the LDL^T, dg = sqrt(d),
+    // first bad pivot by one ballot; then D = diag(d)^{-1/2} L_u^{-1} (lower)
+    double* dpiv = B.rowb;   // publish buffers are dead after the last round
+    if (t < 64) {
+        double d = 1.0;
+        if (t < NB) {
+            d = B.piv[t];
+            dg[t] = sqrt(d);
+            dpiv[t] = d;
+        }
+        const unsigned long long m = __ballot(!(d > 0.0 && d < INFINITY));
+        if (t == 0) *bad = m ? __ffsll((long long)m) : 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int rg = 16 * bi + lr + 4 * q;
+        const double sc = 1.0 / dg[rg];
+        R[rg * S + cg] = (cg <= rg) ? aR[q] * sc : 0.0;
+    }
+    __syncthreads();
+}
+
+// NB = 32 uses the MFMA 4-pivot form (12.7k vs 15.5k shader clocks for the pivot form,
+// tools/ubench_tile.hip).
+template <>
+__device__ __forceinline__ void tile_potrf_inv<32>(double* __restrict__ A, double* __restrict__ R,
+                                                   double* __restrict__ dg, int* __restrict__ bad) {
+    tile_potrf_inv_m4(A, R, dg, bad);
 }
 
 // ---------------------------------------------------------------- blocked diag factor

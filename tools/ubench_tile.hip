@@ -198,6 +198,144 @@ __device__ __forceinline__ void k4_abl(double* A, double* R, double* dg, int* ba
 }
 
 
+template <int RD, int ABL>
+__device__ __forceinline__ void m4x_round(const M4Buf& B, f64x4& aA, f64x4& aR, int bi, int bj, int lc, int lr) {
+    constexpr int NB = 32;
+    if constexpr (RD < NB / 4) {
+        constexpr int k = 4 * RD, cur = RD & 1, nxt = cur ^ 1;
+        const double* C = B.colb + cur * NB * 4;
+        const double* RP = B.rowb + cur * 4 * NB;
+        const int ia = 16 * bi + lc;   // A-operand row of this lane
+        const int cg = 16 * bj + lc;   // accumulator / B-operand column
+        // ---- reads: pivot block (lower), own operand row, B operands
+        const double2 r0a = *reinterpret_cast<const double2*>(C + (k + 0) * 4);
+        const double2 r1a = *reinterpret_cast<const double2*>(C + (k + 1) * 4);
+        const double2 r2a = *reinterpret_cast<const double2*>(C + (k + 2) * 4);
+        const double2 r2b = *reinterpret_cast<const double2*>(C + (k + 2) * 4 + 2);
+        const double2 r3a = *reinterpret_cast<const double2*>(C + (k + 3) * 4);
+        const double2 r3b = *reinterpret_cast<const double2*>(C + (k + 3) * 4 + 2);
+        const double2 cia = *reinterpret_cast<const double2*>(C + ia * 4);
+        const double2 cib = *reinterpret_cast<const double2*>(C + ia * 4 + 2);
+        const double bA = C[cg * 4 + lr];
+        const double bR = RP[lr * NB + cg];
+        const double m00 = r0a.x, m10 = r1a.x, m11 = r1a.y, m20 = r2a.x, m21 = r2a.y, m22 = r2b.x;
+        const double m30 = r3a.x, m31 = r3a.y, m32 = r3b.x, m33 = r3b.y;
+        // ---- M^{-1} by 2x2 blocks: P = M[0:2,0:2], Q = M[0:2,2:4], S = M[2:4,2:4]
+        const double detP = fma(m00, m11, -m10 * m10);
+        const double rP = rcp_nr(detP);
+        const double P00 = m11 * rP, P01 = -m10 * rP, P11 = m00 * rP;
+        const double X00 = fma(P00, m20, P01 * m21), X01 = fma(P00, m30, P01 * m31);
+        const double X10 = fma(P01, m20, P11 * m21), X11 = fma(P01, m30, P11 * m31);
+        const double S00 = m22 - fma(m20, X00, m21 * X10);
+        const double S01 = m32 - fma(m20, X01, m21 * X11);
+        const double S11 = m33 - fma(m30, X01, m31 * X11);
+        const double detS = fma(S00, S11, -S01 * S01);
+        const double rS = rcp_nr(detS);
+        const double I00 = S11 * rS, I01 = -S01 * rS, I11 = S00 * rS;
+        const double Y00 = fma(X00, I00, X01 * I01), Y01 = fma(X00, I01, X01 * I11);
+        const double Y10 = fma(X10, I00, X11 * I01), Y11 = fma(X10, I01, X11 * I11);
+        const double T00 = P00 + fma(Y00, X00, Y01 * X01);
+        const double T01 = P01 + fma(Y00, X10, Y01 * X11);
+        const double T11 = P11 + fma(Y10, X10, Y11 * X11);
+        // ---- w = C_ia M^{-1}; this lane feeds w[lr]
+        const double c0 = cia.x, c1 = cia.y, c2 = cib.x, c3 = cib.y;
+        const double w0 = fma(c0, T00, fma(c1, T01, -fma(c2, Y00, c3 * Y01)));
+        const double w1 = fma(c0, T01, fma(c1, T11, -fma(c2, Y10, c3 * Y11)));
+        const double w2 = fma(c2, I00, fma(c3, I01, -fma(c0, Y00, c1 * Y10)));
+        const double w3 = fma(c2, I01, fma(c3, I11, -fma(c0, Y01, c1 * Y11)));
+        const double wl = (lr == 0) ? w0 : (lr == 1) ? w1 : (lr == 2) ? w2 : w3;
+        double vl = wl;
+        // ---- pivot rows of R: v = -(L_M^{-1})_{p, lr} for lr < p (wave-uniform branch)
+        if (ABL != 1 && ABL != 3 && bi == (k >> 4)) {
+            const int p = lc - (k & 15);
+            if (p >= 0 && p < 4) {
+                const double r0 = rcp_nr(m00);
+                const double L10 = m10 * r0, L20 = m20 * r0, L30 = m30 * r0;
+                const double id1 = m00 * rP;
+                const double e21 = m21 - L20 * m10, e31 = m31 - L30 * m10;
+                const double L21 = e21 * id1, L31 = e31 * id1;
+                const double L32 = (m32 - L30 * m20 - L31 * e21) * rcp_nr(S00);
+                const double N10 = -L10, N21 = -L21, N32 = -L32;
+                const double N20 = -(L20 + L21 * N10);
+                const double N31 = -(L31 + L32 * N21);
+                const double N30 = -(L30 + L31 * N10 + L32 * N20);
+                const double row1 = (lr == 0) ? N10 : 0.0;
+                const double row2 = (lr == 0) ? N20 : (lr == 1) ? N21 : 0.0;
+                const double row3 = (lr == 0) ? N30 : (lr == 1) ? N31 : (lr == 2) ? N32 : 0.0;
+                vl = -((p == 1) ? row1 : (p == 2) ? row2 : (p == 3) ? row3 : 0.0);
+            }
+        }
+        // ---- rank-4 updates on the matrix core
+        aA = __builtin_amdgcn_mfma_f64_16x16x4f64(-wl, bA, aA, 0, 0, 0);
+        aR = __builtin_amdgcn_mfma_f64_16x16x4f64(-vl, bR, aR, 0, 0, 0);
+        if ((ABL == 0 || ABL == 1) && threadIdx.x == 0) {
+            B.piv[k] = m00;
+            B.piv[k + 1] = detP / m00;
+            B.piv[k + 2] = S00;
+            B.piv[k + 3] = detS / S00;
+        }
+        // ---- publish round RD+1
+        if constexpr (RD + 1 < NB / 4) {
+            constexpr int kn = k + 4;
+            double* Cn = B.colb + nxt * NB * 4;
+            double* Rn = B.rowb + nxt * 4 * NB;
+            if (bj == (kn >> 4)) {
+                const int m = lc - (kn & 15);
+                if (m >= 0 && m < 4) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int rg = 16 * bi + lr + 4 * q;
+                        Cn[rg * 4 + m] = (rg >= kn) ? aA[q] : 0.0;
+                    }
+                }
+            }
+            if (bi == (kn >> 4)) Rn[lr * NB + cg] = aR[((kn & 15) >> 2)];
+        }
+        __syncthreads();
+        m4x_round<RD + 1, ABL>(B, aA, aR, bi, bj, lc, lr);
+    }
+}
+
+template <int ABL>
+__device__ __forceinline__ void m4x(double* A, double* R, double* dg, int* bad) {
+    constexpr int NB = 32;
+    constexpr int S = TileCfg<NB>::S;
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    const int bi = w >> 1, bj = w & 1, lc = l & 15, lr = l >> 4;
+    const int cg = 16 * bj + lc;
+    f64x4 aA, aR;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int rg = 16 * bi + lr + 4 * q;
+        aA[q] = A[rg * S + cg];
+        aR[q] = (rg == cg) ? 1.0 : 0.0;
+    }
+    __syncthreads();   // A's LDS becomes the publish buffer
+    const M4Buf B{A, A + 2 * NB * 4, A + 4 * NB * 4};
+    if (bj == 0 && lc < 4) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) B.colb[(16 * bi + lr + 4 * q) * 4 + lc] = aA[q];
+    }
+    if (bi == 0) B.rowb[lr * NB + cg] = (lr == cg) ? 1.0 : 0.0;
+    __syncthreads();
+    m4x_round<0, ABL>(B, aA, aR, bi, bj, lc, lr);
+    // D = diag(d)^{-1/2} L_u^{-1} (lower); dg = sqrt(d); first bad pivot by one ballot
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int rg = 16 * bi + lr + 4 * q;
+        const double sc = 1.0 / sqrt(B.piv[rg]);
+        R[rg * S + cg] = (cg <= rg) ? aR[q] * sc : 0.0;
+    }
+    if (t < 64) {
+        const double d = (t < NB) ? B.piv[t] : 1.0;
+        if (t < NB) dg[t] = sqrt(d);
+        const unsigned long long m = __ballot(!(d > 0.0 && d < INFINITY));
+        if (t == 0) *bad = m ? __ffsll((long long)m) : 0;
+    }
+    __syncthreads();
+}
+
+
 template <int NB, int WHAT>
 __global__ __launch_bounds__(256) void k_bench(const double* Ag, double* out, long long* cyc, int reps) {
     constexpr int E = TileCfg<NB>::ELEMS;
@@ -211,13 +349,17 @@ __global__ __launch_bounds__(256) void k_bench(const double* Ag, double* out, lo
         tile_load<NB>(B, Ag, NB);
         __syncthreads();
         if (it == 1) t0 = __builtin_amdgcn_s_memtime();
-        if (WHAT == 0) tile_potrf_inv<NB>(A, R, dg, &bad);
+        if (WHAT == 0) { if constexpr (NB == 32) tile_potrf_inv_pivot32(A, R, dg, &bad); else tile_potrf_inv<NB>(A, R, dg, &bad); }
         if (WHAT == 1) { tile_mma<NB, false, true>(acc, A, B, 1.0); __syncthreads(); }
         if (WHAT == 2) { __syncthreads(); }
         if (WHAT == 3) { for (int k = 0; k < NB; ++k) __syncthreads(); }
         __shared__ long long st[2];
         if (WHAT == 6 && NB == 32) { potrf_probe(A, R, (long long*)(dg + NB + 2)); if (threadIdx.x == 0 && it == reps - 1) for (int q = 0; q < 4; ++q) cyc[4 + q] = ((long long*)(dg + NB + 2))[q]; }
         if (WHAT == 7 && NB == 32) tile_potrf_inv_k4(A, R, dg, &bad);
+        if (WHAT == 12 && NB == 32) tile_potrf_inv_m4(A, R, dg, &bad);
+        if (WHAT == 13 && NB == 32) m4x<1>(A, R, dg, &bad);
+        if (WHAT == 14 && NB == 32) m4x<2>(A, R, dg, &bad);
+        if (WHAT == 15 && NB == 32) m4x<3>(A, R, dg, &bad);
         __shared__ long long stk[14];
         if (WHAT == 8 && NB == 32) k4_abl<1>(A, R, dg, &bad, stk);
         if (WHAT == 9 && NB == 32) k4_abl<2>(A, R, dg, &bad, stk);
@@ -229,7 +371,7 @@ __global__ __launch_bounds__(256) void k_bench(const double* Ag, double* out, lo
     }
     if (threadIdx.x == 0) { cyc[0] = (t1 - t0) / (reps - 2); if (WHAT == 4) { cyc[3] = t1; } }
     if (WHAT == 1) acc_store(acc, out, NB);
-    if (WHAT == 0 || WHAT == 4 || WHAT == 7) tile_store<NB>(out, NB, R);
+    if (WHAT == 0 || WHAT == 4 || WHAT == 7 || WHAT == 12) tile_store<NB>(out, NB, R);
 }
 
 template <int NB, int WHAT>
@@ -250,7 +392,7 @@ void run(const char* name, const double* dA, double* dO, long long* dc) {
         printf("    per-pivot phases (sum over 32 pivots): reads %lld | compute %lld | write %lld | barrier %lld clk\n", cc[4], cc[5], cc[6], cc[7]); }
     if (WHAT == 4) { long long cc[4]; hipMemcpy(cc, dc, sizeof(cc), hipMemcpyDeviceToHost);
         printf("    last iter: factor-phase end -> diag-inv end %lld clk, diag-inv end -> t1 %lld clk\n", cc[2] - cc[1], cc[3] - cc[2]); }
-    if (WHAT == 0 || WHAT == 4 || WHAT == 7) {
+    if (WHAT == 0 || WHAT == 4 || WHAT == 7 || WHAT == 12) {
         static double cur[64 * 64];
         hipMemcpy(cur, dO, sizeof(double) * NB * NB, hipMemcpyDeviceToHost);
         printf("    D[0][0]=%.6f D[1][0]=%.6f D[1][1]=%.6f D[31][0]=%.6e D[0][1]=%.3e D[31][31]=%.6f\n", cur[0], cur[NB], cur[NB+1], cur[31*NB], cur[1], cur[31*NB+31]);
@@ -274,7 +416,7 @@ int main() {
         hipMalloc(&dA, sizeof(double) * nb * nb); hipMalloc(&dO, sizeof(double) * nb * nb); hipMalloc(&dc, 256);
         hipMemcpy(dA, h, sizeof(double) * nb * nb, hipMemcpyHostToDevice);
         if (nb == 32) {
-            run<32, 6>("potrf probe", dA, dO, dc); run<32, 0>("tile_potrf_inv", dA, dO, dc); run<32, 4>("tile_potrf_inv_b8", dA, dO, dc); run<32, 7>("tile_potrf_inv_k4", dA, dO, dc); run<32, 8>("k4: no rcp", dA, dO, dc); run<32, 9>("k4: no publish", dA, dO, dc); run<32, 10>("k4: no update", dA, dO, dc); run<32, 11>("k4: stamps", dA, dO, dc); run<32, 1>("tile_mma (A B^T)", dA, dO, dc);
+            run<32, 6>("potrf probe", dA, dO, dc); run<32, 0>("tile_potrf_inv", dA, dO, dc); run<32, 4>("tile_potrf_inv_b8", dA, dO, dc); run<32, 7>("tile_potrf_inv_k4", dA, dO, dc); run<32, 12>("tile_potrf_inv_m4 (MFMA)", dA, dO, dc); run<32, 13>("m4: no N", dA, dO, dc); run<32, 14>("m4: raw piv", dA, dO, dc); run<32, 15>("m4: no N + raw piv", dA, dO, dc); run<32, 8>("k4: no rcp", dA, dO, dc); run<32, 9>("k4: no publish", dA, dO, dc); run<32, 10>("k4: no update", dA, dO, dc); run<32, 11>("k4: stamps", dA, dO, dc); run<32, 1>("tile_mma (A B^T)", dA, dO, dc);
             run<32, 2>("1 barrier + loads", dA, dO, dc); run<32, 3>("NB barriers", dA, dO, dc);
         } else {
             run<64, 0>("tile_potrf_inv", dA, dO, dc); run<64, 4>("tile_potrf_inv_b8", dA, dO, dc); run<64, 1>("tile_mma (A B^T)", dA, dO, dc);
