@@ -523,21 +523,18 @@ __device__ __forceinline__ void m4_round(const M4Buf& B, f64x4& aA, f64x4& aR, i
     }
 }
 
-__device__ __forceinline__ void tile_potrf_inv_m4(double* A, double* R, double* dg, int* bad) {
+// Entry with the tile already in accumulator layout (the Acc<32> of tile_mma: wave w
+// holds block (w>>1, w&1)); scratch: >= 544 doubles of LDS nobody reads concurrently.
+__device__ __forceinline__ void tile_potrf_inv_m4_acc(f64x4 aA, double* scratch, double* R, double* dg, int* bad) {
     constexpr int NB = 32;
     constexpr int S = TileCfg<NB>::S;
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
     const int bi = w >> 1, bj = w & 1, lc = l & 15, lr = l >> 4;
     const int cg = 16 * bj + lc;
-    f64x4 aA, aR;
+    f64x4 aR;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int rg = 16 * bi + lr + 4 * q;
-        aA[q] = A[rg * S + cg];
-        aR[q] = (rg == cg) ? 1.0 : 0.0;
-    }
-    __syncthreads();   // A's LDS becomes the publish buffer
-    const M4Buf B{A, A + 2 * NB * 4, A + 4 * NB * 4};
+    for (int q = 0; q < 4; ++q) aR[q] = (16 * bi + lr + 4 * q == cg) ? 1.0 : 0.0;
+    const M4Buf B{scratch, scratch + 2 * NB * 4, scratch + 4 * NB * 4};
     if (bj == 0 && lc < 4) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) B.colb[(16 * bi + lr + 4 * q) * 4 + lc] = aA[q];
@@ -562,10 +559,22 @@ __device__ __forceinline__ void tile_potrf_inv_m4(double* A, double* R, double* 
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int rg = 16 * bi + lr + 4 * q;
-        const double sc = 1.0 / dg[rg];
+        const double sc = rcp_nr(dg[rg]);
         R[rg * S + cg] = (cg <= rg) ? aR[q] * sc : 0.0;
     }
     __syncthreads();
+}
+
+// Entry from an LDS tile A (row-major, stride S); A's LDS becomes the publish buffer.
+__device__ __forceinline__ void tile_potrf_inv_m4(double* A, double* R, double* dg, int* bad) {
+    constexpr int S = TileCfg<32>::S;
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    const int bi = w >> 1, bj = w & 1, lc = l & 15, lr = l >> 4;
+    f64x4 aA;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) aA[q] = A[(16 * bi + lr + 4 * q) * S + 16 * bj + lc];
+    __syncthreads();
+    tile_potrf_inv_m4_acc(aA, A, R, dg, bad);
 }
 
 // NB = 32 uses the MFMA 4-pivot form (12.7k vs 15.5k shader clocks for the pivot form,

@@ -210,6 +210,8 @@ __global__ __launch_bounds__(NTHREADS) void k_chol_step(CholArgs a) {
         tri_decode(t, ii, jj);
         const int i = k + 1 + ii, j = k + 1 + jj;
         tile_load<NB>(T0, At(i, k), lda);
+        Acc<NB> cij;                                     // A_ij in flight with the panel loads
+        acc_load(cij, At(i, j), lda);
         __syncthreads();
         Acc<NB> acc;
         acc_zero(acc);
@@ -226,13 +228,17 @@ __global__ __launch_bounds__(NTHREADS) void k_chol_step(CholArgs a) {
             PJ = Pj;
         }
         __syncthreads();
-        acc_load(acc, At(i, j), lda);
+        acc = cij;
         tile_mma<NB, false, true>(acc, Pi, PJ, -1.0);    // A_ij -= P_i P_j^T
         if (i == j && i == k + 1) {
             // next diagonal tile is final: factor it and publish D_{k+1}
-            acc_to_lds(acc, T0);
-            __syncthreads();
-            tile_potrf_inv<NB>(T0, Pj, dg, &bad);
+            if constexpr (NB == 32) {
+                tile_potrf_inv_m4_acc(acc.v[0], T0, Pj, dg, &bad);   // straight from registers
+            } else {
+                acc_to_lds(acc, T0);
+                __syncthreads();
+                tile_potrf_inv<NB>(T0, Pj, dg, &bad);
+            }
             tile_store<NB>(a.Dd + b * a.sD + (long)(k + 1) * NB * NB, NB, Pj);
             for (int r = threadIdx.x; r < NB; r += NTHREADS) a.ldiag[b * a.sL + (k + 1) * NB + r] = dg[r];
             if (threadIdx.x == 0 && bad && a.info[b] == 0) a.info[b] = (k + 1) * NB + bad;
@@ -248,20 +254,21 @@ __global__ __launch_bounds__(NTHREADS) void k_chol_step(CholArgs a) {
         const int cc = t % ncol;
         const int c = (cc <= k) ? cc : T + (cc - k - 1);
         tile_load<NB>(T0, Rt(k, c), ldr);
+        tile_load<NB>(Pi, At(i, k), lda);                // A_ik staged in Pi's buffer
+        Acc<NB> ric;
+        acc_load(ric, Rt(i, c), ldr);
         __syncthreads();
         Acc<NB> acc;
         acc_zero(acc);
         tile_mma<NB, false, false>(acc, Ds, T0, 1.0);    // X_kc
         acc_to_lds(acc, Pj);
         if (i == k + 1) acc_store(acc, Xt(k, c), ldx);
-        __syncthreads();
-        tile_load<NB>(T0, At(i, k), lda);
-        __syncthreads();
         acc_zero(acc);
-        tile_mma<NB, false, true>(acc, T0, Ds, 1.0);     // P_i
+        tile_mma<NB, false, true>(acc, Pi, Ds, 1.0);     // P_i = A_ik D_k^T
+        __syncthreads();                                 // everyone done reading Pi / Pj(X) writes
         acc_to_lds(acc, Pi);
         __syncthreads();
-        acc_load(acc, Rt(i, c), ldr);
+        acc = ric;
         tile_mma<NB, false, false>(acc, Pi, Pj, -1.0);
         acc_store(acc, Rt(i, c), ldr);
         return;
