@@ -336,6 +336,42 @@ __device__ __forceinline__ void m4x(double* A, double* R, double* dg, int* bad) 
 }
 
 
+
+// tile product with the K loop split over two accumulators (breaks the MFMA dependency chain)
+template <int NB, bool TA, bool TB>
+__device__ __forceinline__ void tile_mma2(Acc<NB>& acc, const double* __restrict__ As, const double* __restrict__ Bs, double alpha) {
+    constexpr int S = TileCfg<NB>::S;
+    constexpr int BPW = TileCfg<NB>::BPW;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int li = lane & 15, lk = lane >> 4;
+    const int rb = 16 * BPW * (w >> 1), cb = 16 * BPW * (w & 1);
+    Acc<NB> acc2; acc_zero(acc2);
+#pragma unroll
+    for (int k0 = 0; k0 < NB; k0 += 8) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int k = k0 + 4 * h + lk;
+            double a[BPW], b[BPW];
+#pragma unroll
+            for (int t = 0; t < BPW; ++t) {
+                const int i = rb + 16 * t + li;
+                const int j = cb + 16 * t + li;
+                a[t] = alpha * (TA ? As[k * S + i] : As[i * S + k]);
+                b[t] = TB ? Bs[j * S + k] : Bs[k * S + j];
+            }
+#pragma unroll
+            for (int ti = 0; ti < BPW; ++ti)
+#pragma unroll
+                for (int tj = 0; tj < BPW; ++tj) {
+                    f64x4& c = h ? acc2.v[ti * BPW + tj] : acc.v[ti * BPW + tj];
+                    c = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ti], b[tj], c, 0, 0, 0);
+                }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < TileCfg<NB>::NBLK; ++q) acc.v[q] += acc2.v[q];
+}
+
 template <int NB, int WHAT>
 __global__ __launch_bounds__(256) void k_bench(const double* Ag, double* out, long long* cyc, int reps) {
     constexpr int E = TileCfg<NB>::ELEMS;
@@ -351,6 +387,7 @@ __global__ __launch_bounds__(256) void k_bench(const double* Ag, double* out, lo
         if (it == 1) t0 = __builtin_amdgcn_s_memtime();
         if (WHAT == 0) { if constexpr (NB == 32) tile_potrf_inv_pivot32(A, R, dg, &bad); else tile_potrf_inv<NB>(A, R, dg, &bad); }
         if (WHAT == 1) { tile_mma<NB, false, true>(acc, A, B, 1.0); __syncthreads(); }
+        if (WHAT == 16) { tile_mma2<NB, false, true>(acc, A, B, 1.0); __syncthreads(); }
         if (WHAT == 2) { __syncthreads(); }
         if (WHAT == 3) { for (int k = 0; k < NB; ++k) __syncthreads(); }
         __shared__ long long st[2];
@@ -370,8 +407,8 @@ __global__ __launch_bounds__(256) void k_bench(const double* Ag, double* out, lo
         if (it == reps - 1) t1 = __builtin_amdgcn_s_memtime();
     }
     if (threadIdx.x == 0) { cyc[0] = (t1 - t0) / (reps - 2); if (WHAT == 4) { cyc[3] = t1; } }
-    if (WHAT == 1) acc_store(acc, out, NB);
-    if (WHAT == 0 || WHAT == 4 || WHAT == 7 || WHAT == 12) tile_store<NB>(out, NB, R);
+    if (WHAT == 1 || WHAT == 16) acc_store(acc, out, NB);
+    if (WHAT == 0 || WHAT == 4 || WHAT == 7 || WHAT == 12 || WHAT == 17) tile_store<NB>(out, NB, R);
 }
 
 template <int NB, int WHAT>
@@ -392,7 +429,7 @@ void run(const char* name, const double* dA, double* dO, long long* dc) {
         printf("    per-pivot phases (sum over 32 pivots): reads %lld | compute %lld | write %lld | barrier %lld clk\n", cc[4], cc[5], cc[6], cc[7]); }
     if (WHAT == 4) { long long cc[4]; hipMemcpy(cc, dc, sizeof(cc), hipMemcpyDeviceToHost);
         printf("    last iter: factor-phase end -> diag-inv end %lld clk, diag-inv end -> t1 %lld clk\n", cc[2] - cc[1], cc[3] - cc[2]); }
-    if (WHAT == 0 || WHAT == 4 || WHAT == 7 || WHAT == 12) {
+    if (WHAT == 0 || WHAT == 4 || WHAT == 7 || WHAT == 12 || WHAT == 17) {
         static double cur[64 * 64];
         hipMemcpy(cur, dO, sizeof(double) * NB * NB, hipMemcpyDeviceToHost);
         printf("    D[0][0]=%.6f D[1][0]=%.6f D[1][1]=%.6f D[31][0]=%.6e D[0][1]=%.3e D[31][31]=%.6f\n", cur[0], cur[NB], cur[NB+1], cur[31*NB], cur[1], cur[31*NB+31]);
@@ -416,10 +453,10 @@ int main() {
         hipMalloc(&dA, sizeof(double) * nb * nb); hipMalloc(&dO, sizeof(double) * nb * nb); hipMalloc(&dc, 256);
         hipMemcpy(dA, h, sizeof(double) * nb * nb, hipMemcpyHostToDevice);
         if (nb == 32) {
-            run<32, 6>("potrf probe", dA, dO, dc); run<32, 0>("tile_potrf_inv", dA, dO, dc); run<32, 4>("tile_potrf_inv_b8", dA, dO, dc); run<32, 7>("tile_potrf_inv_k4", dA, dO, dc); run<32, 12>("tile_potrf_inv_m4 (MFMA)", dA, dO, dc); run<32, 13>("m4: no N", dA, dO, dc); run<32, 14>("m4: raw piv", dA, dO, dc); run<32, 15>("m4: no N + raw piv", dA, dO, dc); run<32, 8>("k4: no rcp", dA, dO, dc); run<32, 9>("k4: no publish", dA, dO, dc); run<32, 10>("k4: no update", dA, dO, dc); run<32, 11>("k4: stamps", dA, dO, dc); run<32, 1>("tile_mma (A B^T)", dA, dO, dc);
+            run<32, 6>("potrf probe", dA, dO, dc); run<32, 0>("tile_potrf_inv", dA, dO, dc); run<32, 4>("tile_potrf_inv_b8", dA, dO, dc); run<32, 7>("tile_potrf_inv_k4", dA, dO, dc); run<32, 12>("tile_potrf_inv_m4 (MFMA)", dA, dO, dc); run<32, 13>("m4: no N", dA, dO, dc); run<32, 14>("m4: raw piv", dA, dO, dc); run<32, 15>("m4: no N + raw piv", dA, dO, dc); run<32, 8>("k4: no rcp", dA, dO, dc); run<32, 9>("k4: no publish", dA, dO, dc); run<32, 10>("k4: no update", dA, dO, dc); run<32, 11>("k4: stamps", dA, dO, dc); run<32, 1>("tile_mma (A B^T)", dA, dO, dc); run<32, 16>("tile_mma2 (2 accumulators)", dA, dO, dc);
             run<32, 2>("1 barrier + loads", dA, dO, dc); run<32, 3>("NB barriers", dA, dO, dc);
         } else {
-            run<64, 0>("tile_potrf_inv", dA, dO, dc); run<64, 4>("tile_potrf_inv_b8", dA, dO, dc); run<64, 1>("tile_mma (A B^T)", dA, dO, dc);
+            run<64, 0>("tile_potrf_inv", dA, dO, dc); run<64, 4>("tile_potrf_inv_b8", dA, dO, dc); run<64, 1>("tile_mma (A B^T)", dA, dO, dc); run<64, 16>("tile_mma2 (2 accumulators)", dA, dO, dc);
             run<64, 2>("1 barrier + loads", dA, dO, dc); run<64, 3>("NB barriers", dA, dO, dc);
         }
         hipFree(dA); hipFree(dO); hipFree(dc);
