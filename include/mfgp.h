@@ -128,6 +128,36 @@ int mfgp_svgp_elbo(mfgp_handle_t h, int n, int m, int l, int p, int d, const dou
                    const double* q_sqrt, const double* W, double noise, double scale, double jitter, void* ws,
                    size_t ws_bytes, double* out, double* g_mu, double* g_var, int* info);
 
+/* Gradient of the same objective (the GradientTape of LatentMFCoregionalizationSVGP.optimize,
+ * mfgpflow/linear_svgp.py:181-191, and SingleBinSVGP.optimize, singlebin_svgp.py:81-86)
+ * E = VE * scale - kl_mult * KL (kl_mult = 1: the ELBO) with respect to the CONSTRAINED
+ * parameters: gZ [M][d+1] (fidelity column 0), gtheta [L][2d+4] (noise slot 0),
+ * gq_mu [M][L], gq_sqrt [L][M][M] (lower part), gW [P][L] (unused if W == NULL), gnoise [1].
+ * noise is a DEVICE pointer (so a training step can be graph-captured).  out / g_mu / g_var
+ * as mfgp_svgp_elbo (out[0] is the plain ELBO).  Workspace: mfgp_svgp_grad_workspace_size. */
+int mfgp_svgp_grad_workspace_size(mfgp_handle_t h, int n, int m, int l, int p, int d, size_t* bytes);
+int mfgp_svgp_elbo_grad(mfgp_handle_t h, int n, int m, int l, int p, int d, const double* X, int ldx,
+                        const double* Y, int ldy, const double* Z, int ldz, const double* thetas,
+                        const double* q_mu, const double* q_sqrt, const double* W, const double* noise,
+                        double scale, double kl_mult, double jitter, void* ws, size_t ws_bytes, double* out, double* g_mu,
+                        double* g_var, double* gZ, double* gtheta, double* gq_mu, double* gq_sqrt, double* gW,
+                        double* gnoise, int* info);
+
+/* One Keras-2.10 (legacy) Adam step on a packed parameter vector (the apply_gradients of
+ * the SVGP optimize loops, linear_svgp.py:190 / singlebin_svgp.py:86): u unconstrained,
+ * c constrained with transform[q] = 0 identity, 1 Softplus, 2 Shift(1e-6) o Softplus;
+ * g = d(+objective)/dc (e.g. the mfgp_svgp_elbo_grad outputs laid out in c's packing);
+ * entries with trainable[q] == 0 are left alone; span (may be NULL) ties contiguous entries
+ * to one variable (isotropic lengthscales): span[q] = k > 0 for a variable of k entries
+ * starting at q (gradient summed, value written to all k), 0 for its followers; learning
+ * rate lr_sched[*step] (device array, e.g. the float32 CosineDecay schedule).  Then loss_hist[*step] =
+ * -out[0] + (kl_mult - 1) out[1], kl_hist[*step] = out[1] (either may be NULL) and ++*step. */
+int mfgp_adam_packed(mfgp_handle_t h, int n, double* u, double* c, const double* g, double* m, double* v,
+                     const unsigned char* trainable, const unsigned char* transform, const unsigned char* span,
+                     int* step,
+                     const double* lr_sched, double beta1, double beta2, double eps, const double* out,
+                     double kl_mult, double* loss_hist, double* kl_hist);
+
 /* SVGP.predict_f(Xnew, full_cov=False) of the same models (GPflow posteriors with
  * mix_latent_gp): latent moments g_mu / g_var [L][nstar] and mixed f_mu / f_var
  * [nstar][P].  Workspace: mfgp_svgp_workspace_size(h, nstar, m, l, p, d). */

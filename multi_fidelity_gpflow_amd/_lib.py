@@ -46,6 +46,10 @@ SIGNATURES = {
                        _p, _p, _p],
     "mfgp_svgp_predict": [_p, _i, _i, _i, _i, _i, _p, _i, _p, _i, _p, _p, _p, _p, _d, _p, _sz, _p, _p, _p, _p,
                           _p],
+    "mfgp_svgp_grad_workspace_size": [_p, _i, _i, _i, _i, _i, C.POINTER(_sz)],
+    "mfgp_svgp_elbo_grad": [_p, _i, _i, _i, _i, _i, _p, _i, _p, _i, _p, _i, _p, _p, _p, _p, _p, _d, _d, _d, _p,
+                            _sz, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
+    "mfgp_adam_packed": [_p, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _d, _d, _d, _p, _d, _p, _p],
     "mfgp_selftest_mfma": [_p, _p],
 }
 

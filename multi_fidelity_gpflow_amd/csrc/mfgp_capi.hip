@@ -305,7 +305,17 @@ size_t svgp_workspace_bytes(int nb, int n, int m, int l, int p, int d);
 int svgp_elbo_impl(hipStream_t s, int nb, int n, int m, int l, int p, int d, const double* X, int ldx,
                    const double* Y, int ldy, const double* Z, int ldz, const double* thetas, const double* q_mu,
                    const double* q_sqrt, const double* W, double noise, double scale, double jitter, void* ws,
-                   size_t ws_bytes, double* out, double* g_mu, double* g_var, int* info);
+                   size_t ws_bytes, double* out, double* g_mu, double* g_var, int* info, const double* noise_dev);
+size_t svgp_grad_workspace_bytes(int nb, int n, int m, int l, int p, int d);
+int svgp_grad_impl(hipStream_t s, int nb, int n, int m, int l, int p, int d, const double* X, int ldx, const double* Y,
+                   int ldy, const double* Z, int ldz, const double* thetas, const double* q_mu, const double* q_sqrt,
+                   const double* W, const double* noise_dev, double noise_host, double scale, double kl_mult,
+                   double jitter, void* ws, size_t ws_bytes, double* out, double* g_mu, double* g_var, double* gZ,
+                   double* gtheta, double* gq_mu, double* gq_sqrt, double* gW, double* gnoise, int* info);
+int adam_packed_impl(hipStream_t st, int n, double* u, double* c, const double* g, double* m, double* v,
+                     const unsigned char* trainable, const unsigned char* transform, const unsigned char* span,
+                     int* step, const double* lr_sched, double b1, double b2, double eps, const double* out,
+                     double klm, double* loss_hist, double* kl_hist);
 
 int svgp_predict_impl(hipStream_t s, int nb, int n, int m, int l, int p, int d, const double* Xs, int ldx,
                       const double* Z, int ldz, const double* thetas, const double* q_mu, const double* q_sqrt,
@@ -529,7 +539,45 @@ int mfgp_svgp_elbo(mfgp_handle_t h, int n, int m, int l, int p, int d, const dou
         return MFGP_ERR_ARG;
     if (!W && l != p) return MFGP_ERR_ARG;
     return svgp_elbo_impl(h->stream, h->nb, n, m, l, p, d, X, ldx, Y, ldy, Z, ldz, thetas, q_mu, q_sqrt, W, noise,
-                          scale, jitter, ws, ws_bytes, out, g_mu, g_var, info);
+                          scale, jitter, ws, ws_bytes, out, g_mu, g_var, info, nullptr);
+}
+
+int mfgp_svgp_grad_workspace_size(mfgp_handle_t h, int n, int m, int l, int p, int d, size_t* bytes) {
+    CHECK_H(h);
+    CHECK_D(d);
+    if (bytes == nullptr || n < 1 || m < 1 || l < 1 || p < 1) return MFGP_ERR_ARG;
+    *bytes = svgp_grad_workspace_bytes(h->nb, n, m, l, p, d);
+    return MFGP_OK;
+}
+
+int mfgp_svgp_elbo_grad(mfgp_handle_t h, int n, int m, int l, int p, int d, const double* X, int ldx,
+                        const double* Y, int ldy, const double* Z, int ldz, const double* thetas,
+                        const double* q_mu, const double* q_sqrt, const double* W, const double* noise,
+                        double scale, double kl_mult, double jitter, void* ws, size_t ws_bytes, double* out, double* g_mu,
+                        double* g_var, double* gZ, double* gtheta, double* gq_mu, double* gq_sqrt, double* gW,
+                        double* gnoise, int* info) {
+    CHECK_H(h);
+    CHECK_D(d);
+    if (n < 1 || m < 1 || l < 1 || p < 1 || !X || !Y || !Z || !thetas || !q_mu || !q_sqrt || !noise || !ws ||
+        !out || !g_mu || !g_var || !gZ || !gtheta || !gq_mu || !gq_sqrt || !gnoise || !info)
+        return MFGP_ERR_ARG;
+    if (W == nullptr && l != p) return MFGP_ERR_ARG;
+    if (W != nullptr && gW == nullptr) return MFGP_ERR_ARG;
+    if (ldx < d + 1 || ldz < d + 1 || ldy < p) return MFGP_ERR_ARG;
+    return svgp_grad_impl(h->stream, h->nb, n, m, l, p, d, X, ldx, Y, ldy, Z, ldz, thetas, q_mu, q_sqrt, W, noise, 0.0,
+                          scale, kl_mult, jitter, ws, ws_bytes, out, g_mu, g_var, gZ, gtheta, gq_mu, gq_sqrt, gW,
+                          gnoise, info);
+}
+
+int mfgp_adam_packed(mfgp_handle_t h, int n, double* u, double* c, const double* g, double* m, double* v,
+                     const unsigned char* trainable, const unsigned char* transform, const unsigned char* span,
+                     int* step, const double* lr_sched, double beta1, double beta2, double eps, const double* out,
+                     double kl_mult, double* loss_hist, double* kl_hist) {
+    CHECK_H(h);
+    if (n < 1 || !u || !c || !g || !m || !v || !trainable || !transform || !step || !lr_sched || !out)
+        return MFGP_ERR_ARG;
+    return adam_packed_impl(h->stream, n, u, c, g, m, v, trainable, transform, span, step, lr_sched, beta1, beta2, eps,
+                            out, kl_mult, loss_hist, kl_hist);
 }
 
 int mfgp_svgp_predict(mfgp_handle_t h, int nstar, int m, int l, int p, int d, const double* Xs, int ldxs,

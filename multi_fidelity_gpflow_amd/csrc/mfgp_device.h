@@ -163,6 +163,15 @@ __device__ __forceinline__ double rcp_nr(double a) {
     return fma(r, e, r);
 }
 
+// ---------------------------------------------------------------- parameter transforms
+__device__ __forceinline__ double tf_softplus(double x) {
+    // tensorflow/core/kernels/softplus_op.h
+    const double thr = -34.04365338911715;   // log(DBL_EPSILON) + 2
+    if (x > -thr) return x;
+    if (x < thr) return exp(x);
+    return log(exp(x) + 1.0);
+}
+
 // ---------------------------------------------------------------- pivot check
 // First non-positive / non-finite pivot of an NB = 32 tile (1-based, 0 if none) without a
 // serial scan (a dependent LDS walk costs ~3.8k clocks): thread (row i = t/8, g = t%8 == 0)

@@ -526,13 +526,6 @@ size_t grad_smem_bytes(int nb) {
 
 // ============================================================ K4: finalize (+Adam)
 
-__device__ __forceinline__ double tf_softplus(double x) {
-    // tensorflow/core/kernels/softplus_op.h
-    const double thr = -34.04365338911715;   // log(DBL_EPSILON) + 2
-    if (x > -thr) return x;
-    if (x < thr) return exp(x);
-    return log(exp(x) + 1.0);
-}
 
 // Stage 1 of the step reduction: workgroup `it` sums item `it` of
 // [sum Z^2, sum log L_ii, grad_0 .. grad_{G-1}] (partials stored [item][task]) with

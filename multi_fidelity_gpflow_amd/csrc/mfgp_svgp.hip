@@ -62,6 +62,18 @@ size_t svgp_workspace_bytes(int nb, int n, int m, int l, int p, int d) {
     return svgp_layout(nb, n, m, l, p, d, nullptr).bytes;
 }
 
+// forward intermediates for the gradient pass (mfgp_svgp_grad.hip)
+void svgp_forward_buffers(int nb, int n, int m, int l, int p, int d, void* ws, double** Xo, double** C, double** Kuf,
+                          double** Lq, int* mpad, int* npad) {
+    const SvgpLayout S = svgp_layout(nb, n, m, l, p, d, ws);
+    *Xo = S.Xo;
+    *C = S.C;
+    *Kuf = S.Kuf;
+    *Lq = S.Lq;
+    *mpad = S.mpad;
+    *npad = S.npad;
+}
+
 // tril(q_sqrt_l) into a zero-padded Mpad x Mpad buffer
 __global__ void k_lq_pad(const double* q_sqrt, int m, int mpad, double* Lq) {
     const int l = blockIdx.z;
@@ -204,9 +216,10 @@ __global__ void k_svgp_moments(const double* pa, const double* pb, const double*
 
 // Gaussian variational expectations summed over (n, p); mixing f = g W^T, f_var = g_var (W o W)^T
 __global__ __launch_bounds__(NTHREADS) void k_svgp_ve(const double* g_mu, const double* g_var, const double* W,
-                                                      const double* Y, long ldy, int n, int p, int L, double noise,
-                                                      double* ve_part) {
+                                                      const double* Y, long ldy, int n, int p, int L, double noise_h,
+                                                      const double* noise_dev, double* ve_part) {
     __shared__ double red[4];
+    const double noise = noise_dev ? noise_dev[0] : noise_h;
     const double LOG2PI = 1.8378770664093453;
     const double c0 = -0.5 * LOG2PI - 0.5 * log(noise);
     const double inv = 1.0 / noise;
@@ -293,7 +306,7 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
                     int ldy, const double* Z, int ldz, const double* thetas, const double* q_mu,
                     const double* q_sqrt, const double* W, double noise, double scale, double jitter, void* ws,
                     size_t ws_bytes, double* out, double* g_mu, double* g_var, int* info, double* f_mu = nullptr,
-                    double* f_var = nullptr) {
+                    double* f_var = nullptr, const double* noise_dev = nullptr) {
     const SvgpLayout S = svgp_layout(NB, n, m, L, p, d, ws);
     if (ws_bytes < S.bytes) return -2;
     const long mm = (long)S.mpad * S.mpad;
@@ -345,7 +358,7 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
     }
     const int nve = 512;
     hipLaunchKernelGGL(k_svgp_ve, dim3(nve), dim3(NTHREADS), 0, s, g_mu, g_var, W, Y, (long)ldy, n, p, L, noise,
-                       S.ve_part);
+                       noise_dev, S.ve_part);
     hipLaunchKernelGGL(k_svgp_kl, dim3(L), dim3(NTHREADS), 0, s, q_mu, q_sqrt, m, L, S.kl_part);
     hipLaunchKernelGGL(k_svgp_final, dim3(1), dim3(64), 0, s, S.ve_part, nve, S.kl_part, L, scale, info, out);
     return hipGetLastError() == hipSuccess ? 0 : -3;
@@ -354,12 +367,12 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
 int svgp_elbo_impl(hipStream_t s, int nb, int n, int m, int l, int p, int d, const double* X, int ldx,
                    const double* Y, int ldy, const double* Z, int ldz, const double* thetas, const double* q_mu,
                    const double* q_sqrt, const double* W, double noise, double scale, double jitter, void* ws,
-                   size_t ws_bytes, double* out, double* g_mu, double* g_var, int* info) {
+                   size_t ws_bytes, double* out, double* g_mu, double* g_var, int* info, const double* noise_dev) {
     if (nb == 64)
         return svgp_run<64>(s, n, m, l, p, d, X, ldx, Y, ldy, Z, ldz, thetas, q_mu, q_sqrt, W, noise, scale, jitter,
-                            ws, ws_bytes, out, g_mu, g_var, info);
+                            ws, ws_bytes, out, g_mu, g_var, info, nullptr, nullptr, noise_dev);
     return svgp_run<32>(s, n, m, l, p, d, X, ldx, Y, ldy, Z, ldz, thetas, q_mu, q_sqrt, W, noise, scale, jitter, ws,
-                        ws_bytes, out, g_mu, g_var, info);
+                        ws_bytes, out, g_mu, g_var, info, nullptr, nullptr, noise_dev);
 }
 
 int svgp_predict_impl(hipStream_t s, int nb, int n, int m, int l, int p, int d, const double* Xs, int ldx,

@@ -1,0 +1,669 @@
+// SVGP ELBO gradient (whitened, Gaussian likelihood) on the MI355X engine.
+//
+// Reference: the GradientTape of LatentMFCoregionalizationSVGP.optimize
+// (mfgpflow/linear_svgp.py:181-191) and SingleBinSVGP.optimize (singlebin_svgp.py:81-86):
+// d(-ELBO) w.r.t. q_mu, q_sqrt (FillTriangular), Z (inducing points, fidelity column
+// included), every latent kernel's (vL, lL, vD, lD, rho), W and the Gaussian noise.
+//
+// Per latent (Li = chol(Kuu)^{-1}, A = Li Kuf, B = Lq^T A, C = Lq^T Li, m = q_mu[:, l]),
+// with upstream alpha = dE/dg_mu and beta = dE/dg_var (E = the ELBO):
+//   dE/dm     = Li (Kuf alpha) - m
+//   dE/dLq    = tril(2 Li Q C^T) - Lq + diag(1 / Lq_ii),   Q = Kuf diag(beta) Kuf^T
+//   dE/dKuf   = 2 F Kuf diag(beta) + (Li^T m) alpha^T,     F = C^T C - Li^T Li
+//   dE/dLi    = tril(m u^T + 2 (Lq C - Li) Q),            u = Kuf alpha
+//   dE/dKuu   = -Li^T Psi(tril(dE/dLi) Li^T) Li,  Psi(H) = (tril H + tril H^T - diag H) / 2
+//               (the adjoint of Li = chol(Kuu)^{-1}: dLi = -Phi(Li dKuu Li^T) Li)
+//   dE/dKff   = beta
+// and the kernel / inducing-point gradients are the weighted derivative sums
+//   sum_ab dE/dK_ab dk(a, b)/dtheta  over (Z, Z) and (Z, X), plus the K_diag term.
+// All products are batched over latents and run on v_mfma_f64_16x16x4 tiles (k_bgemm).
+#include <algorithm>
+
+#include "mfgp_device.h"
+#include "mfgp_internal.h"
+
+namespace mfgp {
+
+static inline int cdv(int a, int b) { return (a + b - 1) / b; }
+
+// ---------------------------------------------------------------- batched GEMM
+// D = alpha * op(A) diag(s) op(B) [* diag(colscale)] + beta * Cin + x y^T   (tril: zero j > i)
+struct BgemmArgs {
+    const double* A; long lda; long sA;
+    const double* B; long ldb; long sB;
+    const double* s; long ss;              // k scaling (nullptr: none)
+    const double* colscale; long scs;      // output column scaling (nullptr: none)
+    const double* Cin; long ldc; long sC; double beta;
+    const double* x; long sx; const double* y; long sy;   // rank-1 term (nullptr: none)
+    double* D; long ldd; long sD;
+    double alpha;
+    int Mt, Nt, Kt, tril;
+};
+
+template <int NB, bool TA, bool TB>
+__global__ __launch_bounds__(NTHREADS) void k_bgemm(BgemmArgs a) {
+    constexpr int S = TileCfg<NB>::S;
+    constexpr int E = TileCfg<NB>::ELEMS;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    double* As = smem;
+    double* Bs = As + E;
+    const int b = blockIdx.z;
+    const int ti = blockIdx.x / a.Nt, tj = blockIdx.x % a.Nt;
+    if (a.tril && tj > ti) {   // strictly-upper output tile of a lower-masked product: zeros
+        Acc<NB> z;
+        acc_zero(z);
+        acc_store(z, a.D + b * a.sD + (long)ti * NB * a.ldd + (long)tj * NB, a.ldd);
+        return;
+    }
+    const double* A = a.A + b * a.sA;
+    const double* B = a.B + b * a.sB;
+    const double* s = a.s ? a.s + b * a.ss : nullptr;
+    Acc<NB> acc;
+    acc_zero(acc);
+    for (int kt = 0; kt < a.Kt; ++kt) {
+        tile_load<NB>(As, TA ? A + (long)kt * NB * a.lda + (long)ti * NB : A + (long)ti * NB * a.lda + (long)kt * NB,
+                      a.lda);
+        tile_load<NB>(Bs, TB ? B + (long)tj * NB * a.ldb + (long)kt * NB : B + (long)kt * NB * a.ldb + (long)tj * NB,
+                      a.ldb);
+        if (s) {
+            __syncthreads();
+            for (int e = threadIdx.x; e < NB * NB; e += NTHREADS) {
+                const int r = e / NB, c = e % NB;
+                Bs[r * S + c] *= s[(long)kt * NB + (TB ? c : r)];
+            }
+        }
+        __syncthreads();
+        tile_mma<NB, TA, TB>(acc, As, Bs, a.alpha);
+        __syncthreads();
+    }
+    double* Dt = a.D + b * a.sD;
+#pragma unroll
+    for (int q = 0; q < TileCfg<NB>::NBLK; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = ti * NB + acc_row<NB>(q, r), j = tj * NB + acc_col<NB>(q);
+            double v = acc.v[q][r];
+            if (a.colscale) v *= a.colscale[b * a.scs + j];
+            if (a.Cin) v += a.beta * a.Cin[b * a.sC + (long)i * a.ldc + j];
+            if (a.x) v += a.x[b * a.sx + i] * a.y[b * a.sy + j];
+            if (a.tril && j > i) v = 0.0;
+            Dt[(long)i * a.ldd + j] = v;
+        }
+}
+
+size_t bgemm_smem(int nb) { return 2 * sizeof(double) * (size_t)nb * (nb + 2); }
+
+template <int NB>
+static void bgemm(hipStream_t st, int ta, int tb, const BgemmArgs& a, int batch) {
+    dim3 g(a.Mt * a.Nt, 1, batch);
+    const size_t sm = bgemm_smem(NB);
+    if (!ta && !tb) hipLaunchKernelGGL((k_bgemm<NB, false, false>), g, dim3(NTHREADS), sm, st, a);
+    else if (!ta && tb) hipLaunchKernelGGL((k_bgemm<NB, false, true>), g, dim3(NTHREADS), sm, st, a);
+    else if (ta && !tb) hipLaunchKernelGGL((k_bgemm<NB, true, false>), g, dim3(NTHREADS), sm, st, a);
+    else hipLaunchKernelGGL((k_bgemm<NB, true, true>), g, dim3(NTHREADS), sm, st, a);
+}
+
+// plain square product helper on Mpad x Mpad batched matrices
+template <int NB>
+static void sq(hipStream_t st, int Tm, int L, long mm, long ld, int ta, const double* A, int tb, const double* B,
+               double* D, double alpha = 1.0, const double* Cin = nullptr, double beta = 0.0, int tril = 0,
+               const double* x = nullptr, const double* y = nullptr, long sxy = 0) {
+    BgemmArgs a{};
+    a.A = A; a.lda = ld; a.sA = mm;
+    a.B = B; a.ldb = ld; a.sB = mm;
+    a.Cin = Cin; a.ldc = ld; a.sC = mm; a.beta = beta;
+    a.x = x; a.sx = sxy; a.y = y; a.sy = sxy;
+    a.D = D; a.ldd = ld; a.sD = mm;
+    a.alpha = alpha;
+    a.Mt = Tm; a.Nt = Tm; a.Kt = Tm; a.tril = tril;
+    bgemm<NB>(st, ta, tb, a, L);
+}
+
+// ---------------------------------------------------------------- matvec (batched)
+// y[b][r] = alpha * sum_c op(A)[r][c] x[b][c] + beta * z[b][r]      (one wave per output row)
+__global__ __launch_bounds__(NTHREADS) void k_bmatvec(const double* A, long lda, long sA, int trans,
+                                                      const double* x, long sx, int rows, int cols,
+                                                      double alpha, const double* z, long sz, double beta,
+                                                      double* y, long sy) {
+    const int b = blockIdx.z;
+    const int lane = threadIdx.x & 63;
+    const int r = blockIdx.x * (NTHREADS / 64) + (threadIdx.x >> 6);
+    if (r >= rows) return;
+    const double* Ab = A + b * sA;
+    const double* xb = x + b * sx;
+    double acc = 0.0;
+    for (int c = lane; c < cols; c += 64) acc += (trans ? Ab[(long)c * lda + r] : Ab[(long)r * lda + c]) * xb[c];
+    acc = wave_sum(acc);
+    if (lane == 0) y[b * sy + r] = alpha * acc + (z ? beta * z[b * sz + r] : 0.0);
+}
+
+// ---------------------------------------------------------------- elementwise pieces
+// Psi(H) = (tril H + tril H^T - diag H) / 2 (symmetric), padded square batch
+__global__ void k_psi(const double* H, double* P, int mpad, long mm) {
+    const int b = blockIdx.z;
+    for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < mm; e += (long)gridDim.x * blockDim.x) {
+        const int i = (int)(e / mpad), j = (int)(e % mpad);
+        const double* h = H + b * mm;
+        double v;
+        if (i > j) v = 0.5 * h[e];
+        else if (i < j) v = 0.5 * h[(long)j * mpad + i];
+        else v = 0.5 * h[e];
+        P[b * mm + e] = v;
+    }
+}
+
+// dE/dLq := G - klm (Lq - diag(1/Lq_ii)) on the m x m lower part; zero elsewhere.  Out: [L][m][m]
+__global__ void k_glq_final(const double* G, const double* Lq, int m, int mpad, long mm, double klm, double* out) {
+    const int b = blockIdx.z;
+    const long tot = (long)m * m;
+    for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < tot; e += (long)gridDim.x * blockDim.x) {
+        const int i = (int)(e / m), j = (int)(e % m);
+        double v = 0.0;
+        if (j <= i) {
+            const double lq = Lq[b * mm + (long)i * mpad + j];
+            v = G[b * mm + (long)i * mpad + j] - klm * lq;
+            if (i == j) v += klm / lq;
+        }
+        out[(long)b * tot + e] = v;
+    }
+}
+
+// q_mu [m][L] -> padded per-latent vectors [L][mpad]
+__global__ void k_qmu_pad(const double* q_mu, int m, int L, int mpad, double* qm) {
+    const int l = blockIdx.z;
+    for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < mpad; r += gridDim.x * blockDim.x)
+        qm[(long)l * mpad + r] = (r < m) ? q_mu[(long)r * L + l] : 0.0;
+}
+
+// gq_mu[m][L] from the padded per-latent vectors
+__global__ void k_qmu_unpad(const double* g, int m, int L, int mpad, double* out) {
+    const int l = blockIdx.z;
+    for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < m; r += gridDim.x * blockDim.x)
+        out[(long)r * L + l] = g[(long)l * mpad + r];
+}
+
+// ---------------------------------------------------------------- VE backward
+// r[n][p] = scale (y - f_mu) / s2 ; alpha[l][n] = sum_p r W[p][l] ; beta[l][n] = -scale/(2 s2) sum_p W[p][l]^2
+// (W == nullptr: identity mixing, L == P).  Also dE/dnoise partials (one per block).
+__global__ __launch_bounds__(NTHREADS) void k_ve_bwd(const double* g_mu, const double* g_var, const double* W,
+                                                     const double* Y, long ldy, int n, int p, int L,
+                                                     const double* noise, double scale, int npad, double* r,
+                                                     double* alpha, double* beta, double* gnoise_part) {
+    __shared__ double red[4];
+    const double s2 = noise[0];
+    const double inv = 1.0 / s2;
+    double gs = 0.0;
+    const long tot = (long)n * p;
+    for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < tot; e += (long)gridDim.x * blockDim.x) {
+        const int i = (int)(e / p), c = (int)(e % p);
+        double fm, fv;
+        if (W) {
+            fm = 0.0;
+            fv = 0.0;
+            for (int l = 0; l < L; ++l) {
+                const double w = W[(long)c * L + l];
+                fm += g_mu[(long)l * n + i] * w;
+                fv += g_var[(long)l * n + i] * (w * w);
+            }
+        } else {
+            fm = g_mu[(long)c * n + i];
+            fv = g_var[(long)c * n + i];
+        }
+        const double dy = Y[(long)i * ldy + c] - fm;
+        r[e] = scale * dy * inv;
+        gs += -0.5 * inv + 0.5 * (dy * dy + fv) * inv * inv;
+    }
+    gs = block_sum(gs, red);
+    if (threadIdx.x == 0) gnoise_part[blockIdx.x] = scale * gs;
+    (void)alpha; (void)beta; (void)npad;
+}
+
+// alpha / beta per latent (padded to npad with zeros)
+__global__ void k_ab(const double* r, const double* W, int n, int p, int L, const double* noise, double scale,
+                     int npad, double* alpha, double* beta) {
+    const int l = blockIdx.z;
+    const double inv = 1.0 / noise[0];
+    double wsq = 0.0;
+    if (W)
+        for (int c = 0; c < p; ++c) wsq += W[(long)c * L + l] * W[(long)c * L + l];
+    else
+        wsq = 1.0;
+    const double bconst = -0.5 * scale * inv * wsq;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < npad; i += gridDim.x * blockDim.x) {
+        double a = 0.0;
+        if (i < n) {
+            if (W)
+                for (int c = 0; c < p; ++c) a += r[(long)i * p + c] * W[(long)c * L + l];
+            else
+                a = r[(long)i * p + l];
+        }
+        alpha[(long)l * npad + i] = a;
+        beta[(long)l * npad + i] = (i < n) ? bconst : 0.0;
+    }
+}
+
+// dE/dW[c][l] = sum_n r[n][c] g_mu[l][n] - (scale / s2) W[c][l] sum_n g_var[l][n]   (one wave per entry)
+__global__ __launch_bounds__(NTHREADS) void k_gw(const double* r, const double* g_mu, const double* g_var,
+                                                 const double* W, int n, int p, int L, const double* noise,
+                                                 double scale, double* gW) {
+    const int lane = threadIdx.x & 63;
+    const int e = blockIdx.x * (NTHREADS / 64) + (threadIdx.x >> 6);
+    if (e >= p * L) return;
+    const int c = e / L, l = e % L;
+    double s1 = 0.0, s2 = 0.0;
+    for (int i = lane; i < n; i += 64) {
+        s1 += r[(long)i * p + c] * g_mu[(long)l * n + i];
+        s2 += g_var[(long)l * n + i];
+    }
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    if (lane == 0) gW[e] = s1 - scale / noise[0] * W[e] * s2;
+}
+
+// ---------------------------------------------------------------- kernel derivative sums
+// For pairs (a in P1 = Z rows, b in P2), weight Wt[a][b] (padded row-major):
+//   gth[q] += sum Wt dk/dtheta_q     (q over [vL, lL(D), vD, lD(D), rho])
+//   gz[a][d] += zf * sum_b Wt dk(a, b)/dz_a[d]
+// One workgroup per (a-tile of 32 rows, b-chunk); thread: row a = t % 32, b stride 8.
+constexpr int KG_ROWS = 32, KG_COLS = 256;
+template <int DC>
+__global__ __launch_bounds__(NTHREADS) void k_kgrad(const double* P1, long ld1, int n1, const double* P2, long ld2,
+                                                    int n2, const double* Wt, long ldw, long sW, const double* thetas,
+                                                    int G, int D, double zf, int nbc, double* gth_part,
+                                                    double* gz_part) {
+    __shared__ double red[NTHREADS];
+    __shared__ double zs[KG_ROWS][DC + 1];
+    const int l = blockIdx.z;
+    const int at = blockIdx.x / nbc, bc = blockIdx.x % nbc;
+    const int t = threadIdx.x;
+    const int ar = t % KG_ROWS, bs = t / KG_ROWS;   // 8 column lanes per row
+    const int a = at * KG_ROWS + ar;
+    const MFTheta th{thetas + (long)l * G, D};
+    const double vL = th.vL(), vD = th.vD(), rho = th.rho();
+    double gl[DC], gd[DC], gz[DC];
+    double gvL = 0.0, gvD = 0.0, grho = 0.0;
+#pragma unroll
+    for (int d = 0; d < DC; ++d) { gl[d] = 0.0; gd[d] = 0.0; gz[d] = 0.0; }
+    if (a < n1) {
+        const double fa = P1[(long)a * ld1 + D];
+        const bool La = (fa == 0.0), Ha = (fa == 1.0);
+        if (La || Ha) {
+            double za[DC];
+#pragma unroll
+            for (int d = 0; d < DC; ++d) za[d] = (d < D) ? P1[(long)a * ld1 + d] : 0.0;
+            const int b0 = bc * KG_COLS, b1 = min(n2, b0 + KG_COLS);
+            for (int b = b0 + bs; b < b1; b += NTHREADS / KG_ROWS) {
+                const double w = Wt[l * sW + (long)a * ldw + b];
+                if (w == 0.0) continue;
+                const double fb = P2[(long)b * ld2 + D];
+                const bool Lb = (fb == 0.0), Hb = (fb == 1.0);
+                if (!(Lb || Hb)) continue;
+                double rL = 0.0, rD = 0.0, dl[DC];
+#pragma unroll
+                for (int d = 0; d < DC; ++d) {
+                    dl[d] = (d < D) ? za[d] - P2[(long)b * ld2 + d] : 0.0;
+                    if (d < D) {
+                        const double il = 1.0 / th.lL(d), id = 1.0 / th.lD(d);
+                        rL += dl[d] * dl[d] * il * il;
+                        rD += dl[d] * dl[d] * id * id;
+                    }
+                }
+                const double sa = La ? 1.0 : rho, sb = Lb ? 1.0 : rho;
+                const double kL = vL * exp(-0.5 * rL);
+                const double wl = w * sa * sb * kL;
+                gvL += wl / vL;
+                grho += w * ((Ha ? sb : 0.0) + (Hb ? sa : 0.0)) * kL;
+                const bool hh = Ha && Hb;
+                const double kD = hh ? vD * exp(-0.5 * rD) : 0.0;
+                const double wd = w * kD;
+                if (hh) gvD += wd / vD;
+#pragma unroll
+                for (int d = 0; d < DC; ++d) {
+                    if (d < D) {
+                        const double il = 1.0 / th.lL(d), id = 1.0 / th.lD(d);
+                        const double qL = dl[d] * dl[d] * il * il;
+                        gl[d] += wl * qL * il;
+                        gz[d] -= wl * dl[d] * il * il;
+                        if (hh) {
+                            const double qD = dl[d] * dl[d] * id * id;
+                            gd[d] += wd * qD * id;
+                            gz[d] -= wd * dl[d] * id * id;
+                        }
+                    }
+                }
+            }
+        }
+    }
+    // theta partials: block reduction per entry (G entries in the MFTheta layout)
+    auto reduce_store = [&](double v, int q) {
+        red[t] = v;
+        __syncthreads();
+        for (int o = NTHREADS / 2; o > 0; o >>= 1) {
+            if (t < o) red[t] += red[t + o];
+            __syncthreads();
+        }
+        if (t == 0) gth_part[((long)l * gridDim.x + blockIdx.x) * G + q] = red[0];
+        __syncthreads();
+    };
+    reduce_store(gvL, 0);
+    for (int d = 0; d < D; ++d) reduce_store(gl[d < DC ? d : 0] * (d < DC ? 1.0 : 0.0), 1 + d);
+    reduce_store(gvD, 1 + D);
+    for (int d = 0; d < D; ++d) reduce_store(gd[d < DC ? d : 0] * (d < DC ? 1.0 : 0.0), 2 + D + d);
+    reduce_store(grho, 2 + 2 * D);
+    if (t == 0) gth_part[((long)l * gridDim.x + blockIdx.x) * G + (G - 1)] = 0.0;   // noise slot
+    // z partials: rows of this tile, summed over the 8 column lanes
+    for (int e = t; e < KG_ROWS * (DC + 1); e += NTHREADS) (&zs[0][0])[e] = 0.0;
+    __syncthreads();
+    for (int s8 = 0; s8 < NTHREADS / KG_ROWS; ++s8) {
+        if (bs == s8)
+            for (int d = 0; d < D && d < DC; ++d) zs[ar][d] += gz[d];
+        __syncthreads();
+    }
+    for (int e = t; e < KG_ROWS * D; e += NTHREADS) {
+        const int r = e / D, d = e % D;
+        const int ag = at * KG_ROWS + r;
+        gz_part[(((long)l * gridDim.x + blockIdx.x) * KG_ROWS + r) * D + d] = (ag < n1) ? zf * zs[r][d] : 0.0;
+    }
+}
+
+// K_diag term: dE/dtheta from dE/dKff = beta  (vL: L + rho^2 H ; vD: H ; rho: 2 rho vL H)
+__global__ __launch_bounds__(NTHREADS) void k_kff_grad(const double* X, long ldx, int n, const double* beta,
+                                                       int npad, const double* thetas, int G, int D,
+                                                       double* gth_kff) {
+    __shared__ double red[4];
+    const int l = blockIdx.x;
+    const MFTheta th{thetas + (long)l * G, D};
+    double sL = 0.0, sH = 0.0;
+    for (int i = threadIdx.x; i < n; i += NTHREADS) {
+        const double f = X[(long)i * ldx + D];
+        const double bb = beta[(long)l * npad + i];
+        if (f == 0.0) sL += bb;
+        else if (f == 1.0) sH += bb;
+    }
+    sL = block_sum(sL, red);
+    sH = block_sum(sH, red);
+    if (threadIdx.x == 0) {
+        const double rho = th.rho();
+        double* g = gth_kff + (long)l * G;
+        for (int q = 0; q < G; ++q) g[q] = 0.0;
+        g[0] = sL + rho * rho * sH;
+        g[1 + D] = sH;
+        g[2 + 2 * D] = 2.0 * rho * th.vL() * sH;
+    }
+}
+
+// Final reductions: gtheta[l][q] (kff + Kuu + Kuf partials), gZ[m][D+1] (sum over latents;
+// fidelity column 0), gnoise = sum of partials.
+__global__ void k_grad_reduce(const double* gth_uu, int nb_uu, const double* gth_uf, int nb_uf, const double* gth_kff,
+                              const double* gz_uu, const double* gz_uf, int n_at, int nbc_uu, int nbc_uf, int L,
+                              int G, int D, int m, const double* gnoise_part, int nnoise, double* gtheta, double* gZ,
+                              double* gnoise) {
+    const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const int nth = L * G;
+    if (tid < nth) {
+        const int l = tid / G, q = tid % G;
+        double s = gth_kff[(long)l * G + q];
+        for (int bk = 0; bk < nb_uu; ++bk) s += gth_uu[((long)l * nb_uu + bk) * G + q];
+        for (int bk = 0; bk < nb_uf; ++bk) s += gth_uf[((long)l * nb_uf + bk) * G + q];
+        gtheta[tid] = s;
+    } else if (tid < nth + m * (D + 1)) {
+        const int e = tid - nth;
+        const int a = e / (D + 1), d = e % (D + 1);
+        double s = 0.0;
+        if (d < D) {
+            const int at = a / KG_ROWS, r = a % KG_ROWS;
+            for (int l = 0; l < L; ++l) {
+                for (int bc = 0; bc < nbc_uu; ++bc)
+                    s += gz_uu[(((long)l * nb_uu + at * nbc_uu + bc) * KG_ROWS + r) * D + d];
+                for (int bc = 0; bc < nbc_uf; ++bc)
+                    s += gz_uf[(((long)l * nb_uf + at * nbc_uf + bc) * KG_ROWS + r) * D + d];
+            }
+        }
+        gZ[e] = s;
+    } else if (tid == nth + m * (D + 1)) {
+        double s = 0.0;
+        for (int i = 0; i < nnoise; ++i) s += gnoise_part[i];
+        gnoise[0] = s;
+    }
+    (void)n_at;
+}
+
+// ---------------------------------------------------------------- driver
+struct SvgpGradLayout {
+    double *qm, *alpha, *beta, *u, *Q, *E, *Gb, *H, *P, *Sig, *F, *Kbar, *T1, *gLq, *vli, *gqm, *r, *gnp, *gth_uu,
+        *gth_uf, *gth_kff, *gz_uu, *gz_uf;
+    int nbc_uu, nbc_uf, n_at, nb_uu, nb_uf, nnoise;
+    size_t bytes;
+};
+
+static SvgpGradLayout grad_layout(int nb, int n, int m, int L, int p, int d, size_t base_off, void* ws) {
+    SvgpGradLayout g;
+    const int mpad = cdv(m, nb) * nb, npad = cdv(n, nb) * nb;
+    const size_t mm = (size_t)mpad * mpad;
+    const int G = theta_size(d);
+    g.n_at = cdv(m, KG_ROWS);
+    g.nbc_uu = cdv(m, KG_COLS);
+    g.nbc_uf = cdv(n, KG_COLS);
+    g.nb_uu = g.n_at * g.nbc_uu;
+    g.nb_uf = g.n_at * g.nbc_uf;
+    g.nnoise = 256;
+    size_t off = base_off;
+    char* base = (char*)ws;
+    auto take = [&](size_t count) {
+        off = (off + 255) & ~(size_t)255;
+        double* ptr = base ? reinterpret_cast<double*>(base + off) : nullptr;
+        off += count * sizeof(double);
+        return ptr;
+    };
+    g.qm = take((size_t)L * mpad);
+    g.alpha = take((size_t)L * npad);
+    g.beta = take((size_t)L * npad);
+    g.u = take((size_t)L * mpad);
+    g.vli = take((size_t)L * mpad);
+    g.gqm = take((size_t)L * mpad);
+    g.Q = take(mm * L);
+    g.E = take(mm * L);
+    g.Gb = take(mm * L);
+    g.H = take(mm * L);
+    g.P = take(mm * L);
+    g.Sig = take(mm * L);
+    g.F = take(mm * L);
+    g.T1 = take(mm * L);
+    g.gLq = take(mm * L);
+    g.Kbar = take((size_t)mpad * npad * L);
+    g.r = take((size_t)n * p + 8);
+    g.gnp = take(g.nnoise);
+    g.gth_uu = take((size_t)L * g.nb_uu * G);
+    g.gth_uf = take((size_t)L * g.nb_uf * G);
+    g.gth_kff = take((size_t)L * G);
+    g.gz_uu = take((size_t)L * g.nb_uu * KG_ROWS * d + 8);
+    g.gz_uf = take((size_t)L * g.nb_uf * KG_ROWS * d + 8);
+    g.bytes = off + 256;
+    return g;
+}
+
+size_t svgp_workspace_bytes(int nb, int n, int m, int l, int p, int d);
+
+size_t svgp_grad_workspace_bytes(int nb, int n, int m, int l, int p, int d) {
+    return grad_layout(nb, n, m, l, p, d, svgp_workspace_bytes(nb, n, m, l, p, d), nullptr).bytes;
+}
+
+int svgp_elbo_impl(hipStream_t s, int nb, int n, int m, int l, int p, int d, const double* X, int ldx,
+                   const double* Y, int ldy, const double* Z, int ldz, const double* thetas, const double* q_mu,
+                   const double* q_sqrt, const double* W, double noise, double scale, double jitter, void* ws,
+                   size_t ws_bytes, double* out, double* g_mu, double* g_var, int* info, const double* noise_dev);
+// forward intermediates of svgp_run (mfgp_svgp.hip)
+void svgp_forward_buffers(int nb, int n, int m, int l, int p, int d, void* ws, double** Xo, double** C, double** Kuf,
+                          double** Lq, int* mpad, int* npad);
+
+template <int DC>
+static void launch_kgrad(hipStream_t s, const double* P1, long ld1, int n1, const double* P2, long ld2, int n2,
+                         const double* Wt, long ldw, long sW, const double* thetas, int G, int D, double zf, int nat,
+                         int nbc, int L, double* gth, double* gz) {
+    hipLaunchKernelGGL(k_kgrad<DC>, dim3(nat * nbc, 1, L), dim3(NTHREADS), 0, s, P1, ld1, n1, P2, ld2, n2, Wt, ldw,
+                       sW, thetas, G, D, zf, nbc, gth, gz);
+}
+
+template <int NB>
+static int svgp_grad_run(hipStream_t s, int n, int m, int L, int p, int d, const double* X, int ldx, const double* Y,
+                         int ldy, const double* Z, int ldz, const double* thetas, const double* q_mu,
+                         const double* q_sqrt, const double* W, const double* noise_dev, double scale, double jitter,
+                         void* ws, size_t ws_bytes, double* out, double* g_mu, double* g_var, double* gZ,
+                         double* gtheta, double* gq_mu, double* gq_sqrt, double* gW, double* gnoise, int* info,
+                         double noise_host, double kl_mult) {
+    const size_t base = svgp_workspace_bytes(NB, n, m, L, p, d);
+    const SvgpGradLayout g = grad_layout(NB, n, m, L, p, d, base, ws);
+    if (ws_bytes < g.bytes) return -2;
+    // forward (fills Xo = Li, C = Lq^T Li, Kuf, Lq; g_mu / g_var; out = [elbo, KL, VE])
+    int rc = svgp_elbo_impl(s, NB, n, m, L, p, d, X, ldx, Y, ldy, Z, ldz, thetas, q_mu, q_sqrt, W, noise_host, scale,
+                            jitter, ws, ws_bytes, out, g_mu, g_var, info, noise_dev);
+    if (rc) return rc;
+    double *Li, *C, *Kuf, *Lq;
+    int mpad, npad;
+    svgp_forward_buffers(NB, n, m, L, p, d, ws, &Li, &C, &Kuf, &Lq, &mpad, &npad);
+    const int Tm = mpad / NB, Tn = npad / NB;
+    const long mm = (long)mpad * mpad, mn = (long)mpad * npad;
+    const int G = theta_size(d);
+    // 1. VE backward
+    hipLaunchKernelGGL(k_ve_bwd, dim3(g.nnoise), dim3(NTHREADS), 0, s, g_mu, g_var, W, Y, (long)ldy, n, p, L,
+                       noise_dev, scale, npad, g.r, g.alpha, g.beta, g.gnp);
+    hipLaunchKernelGGL(k_ab, dim3(cdv(npad, 256), 1, L), dim3(256), 0, s, g.r, W, n, p, L, noise_dev, scale, npad,
+                       g.alpha, g.beta);
+    if (W) hipLaunchKernelGGL(k_gw, dim3(cdv(p * L, NTHREADS / 64)), dim3(NTHREADS), 0, s, g.r, g_mu, g_var, W, n, p, L,
+                              noise_dev, scale, gW);
+    hipLaunchKernelGGL(k_qmu_pad, dim3(cdv(mpad, 256), 1, L), dim3(256), 0, s, q_mu, m, L, mpad, g.qm);
+    // 2. u = Kuf alpha ; Q = Kuf diag(beta) Kuf^T
+    hipLaunchKernelGGL(k_bmatvec, dim3(cdv(mpad, NTHREADS / 64), 1, L), dim3(NTHREADS), 0, s, Kuf, (long)npad, mn, 0,
+                       g.alpha, (long)npad, mpad, npad, 1.0, (const double*)nullptr, 0L, 0.0, g.u, (long)mpad);
+    {
+        BgemmArgs a{};
+        a.A = Kuf; a.lda = npad; a.sA = mn;
+        a.B = Kuf; a.ldb = npad; a.sB = mn;
+        a.s = g.beta; a.ss = npad;
+        a.D = g.Q; a.ldd = mpad; a.sD = mm;
+        a.alpha = 1.0;
+        a.Mt = Tm; a.Nt = Tm; a.Kt = Tn;
+        bgemm<NB>(s, 0, 1, a, L);
+    }
+    // 3. dE/dm = Li u - m
+    hipLaunchKernelGGL(k_bmatvec, dim3(cdv(mpad, NTHREADS / 64), 1, L), dim3(NTHREADS), 0, s, Li, (long)mpad, mm, 0,
+                       g.u, (long)mpad, mpad, mpad, 1.0, g.qm, (long)mpad, -kl_mult, g.gqm, (long)mpad);
+    hipLaunchKernelGGL(k_qmu_unpad, dim3(cdv(m, 256), 1, L), dim3(256), 0, s, g.gqm, m, L, mpad, gq_mu);
+    // 4. E = Lq C - Li ; Gb = tril(2 E Q + m u^T)
+    sq<NB>(s, Tm, L, mm, mpad, 0, Lq, 0, C, g.E, 1.0, Li, -1.0);
+    sq<NB>(s, Tm, L, mm, mpad, 0, g.E, 0, g.Q, g.Gb, 2.0, nullptr, 0.0, 1, g.qm, g.u, mpad);
+    // 5. Sigma_bar = -Li^T Psi(Gb Li^T) Li
+    sq<NB>(s, Tm, L, mm, mpad, 0, g.Gb, 1, Li, g.H);
+    hipLaunchKernelGGL(k_psi, dim3(std::min<long>(cdv((int)mm, 256), 1024), 1, L), dim3(256), 0, s, g.H, g.P, mpad, mm);
+    sq<NB>(s, Tm, L, mm, mpad, 0, g.P, 0, Li, g.T1);
+    sq<NB>(s, Tm, L, mm, mpad, 1, Li, 0, g.T1, g.Sig, -1.0);
+    // 6. F = C^T C - Li^T Li ; Kbar = 2 F Kuf diag(beta) + (Li^T m) alpha^T
+    sq<NB>(s, Tm, L, mm, mpad, 1, C, 0, C, g.T1);
+    sq<NB>(s, Tm, L, mm, mpad, 1, Li, 0, Li, g.F, -1.0, g.T1, 1.0);
+    hipLaunchKernelGGL(k_bmatvec, dim3(cdv(mpad, NTHREADS / 64), 1, L), dim3(NTHREADS), 0, s, Li, (long)mpad, mm, 1,
+                       g.qm, (long)mpad, mpad, mpad, 1.0, (const double*)nullptr, 0L, 0.0, g.vli, (long)mpad);
+    {
+        BgemmArgs a{};
+        a.A = g.F; a.lda = mpad; a.sA = mm;
+        a.B = Kuf; a.ldb = npad; a.sB = mn;
+        a.colscale = g.beta; a.scs = npad;
+        a.x = g.vli; a.sx = mpad; a.y = g.alpha; a.sy = npad;
+        a.D = g.Kbar; a.ldd = npad; a.sD = mn;
+        a.alpha = 2.0;
+        a.Mt = Tm; a.Nt = Tn; a.Kt = Tm;
+        bgemm<NB>(s, 0, 0, a, L);
+    }
+    // 7. dE/dLq = tril(2 Li Q C^T) - Lq + diag(1/Lq_ii)
+    sq<NB>(s, Tm, L, mm, mpad, 0, Li, 0, g.Q, g.T1);
+    sq<NB>(s, Tm, L, mm, mpad, 0, g.T1, 1, C, g.gLq, 2.0, nullptr, 0.0, 1);
+    hipLaunchKernelGGL(k_glq_final, dim3(std::min(cdv(m * m, 256), 1024), 1, L), dim3(256), 0, s, g.gLq, Lq, m, mpad,
+                       mm, kl_mult, gq_sqrt);
+    // 8. kernel / inducing-point derivative sums
+    if (d <= 16) {
+        launch_kgrad<16>(s, Z, ldz, m, Z, ldz, m, g.Sig, mpad, mm, thetas, G, d, 2.0, g.n_at, g.nbc_uu, L, g.gth_uu,
+                         g.gz_uu);
+        launch_kgrad<16>(s, Z, ldz, m, X, ldx, n, g.Kbar, npad, mn, thetas, G, d, 1.0, g.n_at, g.nbc_uf, L, g.gth_uf,
+                         g.gz_uf);
+    } else {
+        launch_kgrad<32>(s, Z, ldz, m, Z, ldz, m, g.Sig, mpad, mm, thetas, G, d, 2.0, g.n_at, g.nbc_uu, L, g.gth_uu,
+                         g.gz_uu);
+        launch_kgrad<32>(s, Z, ldz, m, X, ldx, n, g.Kbar, npad, mn, thetas, G, d, 1.0, g.n_at, g.nbc_uf, L, g.gth_uf,
+                         g.gz_uf);
+    }
+    hipLaunchKernelGGL(k_kff_grad, dim3(L), dim3(NTHREADS), 0, s, X, (long)ldx, n, g.beta, npad, thetas, G, d,
+                       g.gth_kff);
+    const int tot = L * G + m * (d + 1) + 1;
+    hipLaunchKernelGGL(k_grad_reduce, dim3(cdv(tot, 256)), dim3(256), 0, s, g.gth_uu, g.nb_uu, g.gth_uf, g.nb_uf,
+                       g.gth_kff, g.gz_uu, g.gz_uf, g.n_at, g.nbc_uu, g.nbc_uf, L, G, d, m, g.gnp, g.nnoise, gtheta,
+                       gZ, gnoise);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+int svgp_grad_impl(hipStream_t s, int nb, int n, int m, int l, int p, int d, const double* X, int ldx, const double* Y,
+                   int ldy, const double* Z, int ldz, const double* thetas, const double* q_mu, const double* q_sqrt,
+                   const double* W, const double* noise_dev, double noise_host, double scale, double kl_mult,
+                   double jitter, void* ws, size_t ws_bytes, double* out, double* g_mu, double* g_var, double* gZ,
+                   double* gtheta, double* gq_mu, double* gq_sqrt, double* gW, double* gnoise, int* info) {
+    if (nb == 64)
+        return svgp_grad_run<64>(s, n, m, l, p, d, X, ldx, Y, ldy, Z, ldz, thetas, q_mu, q_sqrt, W, noise_dev, scale,
+                                 jitter, ws, ws_bytes, out, g_mu, g_var, gZ, gtheta, gq_mu, gq_sqrt, gW, gnoise, info,
+                                 noise_host, kl_mult);
+    return svgp_grad_run<32>(s, n, m, l, p, d, X, ldx, Y, ldy, Z, ldz, thetas, q_mu, q_sqrt, W, noise_dev, scale,
+                             jitter, ws, ws_bytes, out, g_mu, g_var, gZ, gtheta, gq_mu, gq_sqrt, gW, gnoise, info,
+                             noise_host, kl_mult);
+}
+
+// ---------------------------------------------------------------- packed Adam (training step)
+// One Keras-2.10 (legacy) Adam step on a packed parameter vector: u unconstrained,
+// c constrained (c = u, softplus(u) or softplus(u) + 1e-6 by transform[q] = 0 / 1 / 2),
+// g = d(+objective)/dc  (the loss is its negative), learning rate lr_sched[*step].
+// TF's SoftplusGrad division form g / (exp(-u) + 1) carries the gradient to u.
+__global__ void k_adam_packed(int n, double* u, double* c, const double* g, double* m, double* v,
+                              const unsigned char* trainable, const unsigned char* transform,
+                              const unsigned char* span, const int* step, const double* lr_sched, double b1,
+                              double b2, double eps) {
+    const int s = *step;
+    const double t = (double)(s + 1);
+    const double alpha = lr_sched[s] * sqrt(1.0 - pow(b2, t)) / (1.0 - pow(b1, t));
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
+        const int k = span ? span[q] : 1;   // 0: follower of a tied variable (written by its leader)
+        if (!trainable[q] || k == 0) continue;
+        const int tr = transform[q];
+        const double uq = u[q];
+        double gc = 0.0;
+        for (int j = 0; j < k; ++j) gc += g[q + j];
+        const double gl = -gc;   // d loss / d c
+        const double gu = (tr == 0) ? gl : gl / (exp(-uq) + 1.0);
+        const double mq = m[q] + (gu - m[q]) * (1.0 - b1);
+        const double vq = v[q] + (gu * gu - v[q]) * (1.0 - b2);
+        const double un = uq - (mq * alpha) / (sqrt(vq) + eps);
+        const double cn = (tr == 0) ? un : tf_softplus(un) + (tr == 2 ? 1e-6 : 0.0);
+        m[q] = mq;
+        v[q] = vq;
+        for (int j = 0; j < k; ++j) {
+            u[q + j] = un;
+            c[q + j] = cn;
+        }
+    }
+}
+
+// loss_hist[step] = -out[0] + (klm - 1) out[1] (the optimised objective), kl_hist[step] = out[1]; ++step
+__global__ void k_step_record(const double* out, double klm, double* loss_hist, double* kl_hist, int* step) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const int s = *step;
+    if (loss_hist) loss_hist[s] = -out[0] + (klm - 1.0) * out[1];
+    if (kl_hist) kl_hist[s] = out[1];
+    *step = s + 1;
+}
+
+int adam_packed_impl(hipStream_t st, int n, double* u, double* c, const double* g, double* m, double* v,
+                     const unsigned char* trainable, const unsigned char* transform, const unsigned char* span,
+                     int* step, const double* lr_sched, double b1, double b2, double eps, const double* out,
+                     double klm, double* loss_hist, double* kl_hist) {
+    hipLaunchKernelGGL(k_adam_packed, dim3(std::min(cdv(n, 256), 1024)), dim3(256), 0, st, n, u, c, g, m, v, trainable,
+                       transform, span, step, lr_sched, b1, b2, eps);
+    hipLaunchKernelGGL(k_step_record, dim3(1), dim3(64), 0, st, out, klm, loss_hist, kl_hist, step);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+}  // namespace mfgp

@@ -179,6 +179,30 @@ class Engine:
                                       ptr(info)), "mfgp_svgp_elbo")
         return out, g_mu, g_var, info
 
+    def svgp_elbo_grad(self, X, Y, Z, thetas, q_mu, q_sqrt, W, noise, scale, kl_mult, jitter, out, g_mu, g_var,
+                       gZ, gtheta, gq_mu, gq_sqrt, gW, gnoise, info):
+        """Gradient of VE*scale - kl_mult*KL w.r.t. the constrained SVGP parameters (all device
+        tensors, written in place; noise is a device scalar)."""
+        n, dp1 = X.shape
+        d = dp1 - 1
+        p = Y.shape[1]
+        m = Z.shape[0]
+        L = thetas.shape[0]
+        nbytes = self._size(self.lib.mfgp_svgp_grad_workspace_size, n, m, L, p, d)
+        ws = self.workspace("svgp_grad", nbytes)
+        check(self.lib.mfgp_svgp_elbo_grad(self.h, n, m, L, p, d, ptr(X), dp1, ptr(Y), Y.stride(0), ptr(Z), dp1,
+                                           ptr(thetas), ptr(q_mu), ptr(q_sqrt), ptr(W), ptr(noise), float(scale),
+                                           float(kl_mult), float(jitter), ptr(ws), ws.numel(), ptr(out), ptr(g_mu),
+                                           ptr(g_var), ptr(gZ), ptr(gtheta), ptr(gq_mu), ptr(gq_sqrt), ptr(gW),
+                                           ptr(gnoise), ptr(info)), "mfgp_svgp_elbo_grad")
+
+    def adam_packed(self, u, c, g, m, v, trainable, transform, span, step, lr_sched, b1, b2, eps, out, kl_mult,
+                    loss_hist, kl_hist):
+        check(self.lib.mfgp_adam_packed(self.h, u.numel(), ptr(u), ptr(c), ptr(g), ptr(m), ptr(v), ptr(trainable),
+                                        ptr(transform), ptr(span), ptr(step), ptr(lr_sched), float(b1), float(b2),
+                                        float(eps), ptr(out), float(kl_mult), ptr(loss_hist), ptr(kl_hist)),
+              "mfgp_adam_packed")
+
     def svgp_predict(self, Xs, Z, thetas, q_mu, q_sqrt, W, p, jitter=1e-6):
         ns, dp1 = Xs.shape
         d = dp1 - 1

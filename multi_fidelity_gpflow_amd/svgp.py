@@ -8,8 +8,9 @@
 
 ``elbo``, ``prior_kl`` and ``predict_f`` run in libmfgp.so (mfgp_svgp_elbo /
 mfgp_svgp_predict: batched K_uu factor, fused K_uf K_uu^{-1} products, mixing,
-variational expectations, KL).  The ELBO gradient on the device is the next row of
-SURVEY §8(f) (#2); ``optimize`` raises until it lands.
+variational expectations, KL).  ``optimize`` runs the analytic ELBO
+gradient (mfgp_svgp_elbo_grad) and a packed Keras-Adam step (mfgp_adam_packed) per
+iteration, replayed from hipGraphs; all state stays in HBM (_SVGPTrainer).
 """
 from __future__ import annotations
 
@@ -21,8 +22,8 @@ import torch
 
 from .engine import Engine, theta_size, to_dev
 from .kernels import LinearCoregionalization, LinearMultiFidelityKernel, SeparateIndependent
-from .models import CholeskyError, Gaussian
-from .params import Module, Parameter, as_result, parameter_dict, multiple_assign
+from .models import CholeskyError, Gaussian, _StepRunner
+from .params import Module, Parameter, Softplus, as_result, parameter_dict, multiple_assign
 
 DEFAULT_JITTER = 1e-6
 
@@ -127,15 +128,269 @@ class _SVGPBase(Module):
         mean, var = self.predict_f(Xnew, full_cov, full_output_cov)
         return mean, as_result(var + float(self.likelihood.variance.numpy()))
 
-    def optimize(self, *args, **kwargs):
-        raise NotImplementedError(
-            "SVGP training needs the ELBO gradient on the device (SURVEY §8(f) row 2, next round); "
-            "elbo / predict_f run on the MI355X engine now")
+    def elbo_and_grad(self, data, kl_multiplier=1.0):
+        """(ELBO, dict of d(VE*scale - kl_multiplier*KL)/d(constrained parameter)) on the device:
+        keys 'Z', 'theta' [L, 2d+4] (theta_vector layout), 'q_mu', 'q_sqrt' (lower), 'W', 'noise'."""
+        tr = _SVGPTrainer(self, data, max_iters=1, initial_lr=0.0, kl_multiplier=kl_multiplier, graph=False)
+        e = tr.elbo_now()
+        g = {k: v.cpu().numpy().copy() for k, v in tr.grad_views().items()}
+        return e, g
+
+    def _optimize(self, data, max_iters, initial_lr, unfix_noise_after, kl_multiplier, reset_history, graph,
+                  graph_chunk, verbose, every):
+        tr = _SVGPTrainer(self, data, max_iters, initial_lr, kl_multiplier, graph=graph, graph_chunk=graph_chunk)
+        noise_fixed = not self.likelihood.variance.trainable
+        done = 0
+        while done < max_iters:
+            stop = max_iters
+            if noise_fixed and unfix_noise_after is not None and done <= unfix_noise_after < max_iters:
+                stop = unfix_noise_after + 1
+            if verbose:
+                stop = min(stop, done + every)
+            tr.run(stop - done)
+            done = stop
+            if noise_fixed and unfix_noise_after is not None and done == unfix_noise_after + 1:
+                tr.set_trainable("noise", True)
+                noise_fixed = False
+            if verbose:
+                print(f"Iteration {done - 1}: loss = {tr.loss_at(done - 1)}", flush=True)
+        tr.finish(reset_history)
+        return tr
 
     def save_model(self, filename):
         """parameter_dict pickled (linear_svgp.py:206-212) — our own file format."""
         with open(filename, "wb") as f:
             pickle.dump(parameter_dict(self), f)
+
+
+
+def cosine_decay_schedule(initial_lr, decay_steps, n):
+    """tf.keras.optimizers.schedules.CosineDecay (TF 2.10, alpha = 0) for steps 0..n-1,
+    evaluated in float32 like TF (the python-float initial lr is a float32 tensor)."""
+    out = np.empty(max(int(n), 1), dtype=np.float64)
+    lr0 = np.float32(initial_lr)
+    ds = np.float32(max(int(decay_steps), 1))
+    for t in range(out.size):
+        frac = np.float32(min(t, decay_steps)) / ds
+        cosd = np.float32(0.5) * (np.float32(1.0) + np.cos(np.float32(np.pi) * frac, dtype=np.float32))
+        out[t] = float(np.float32(lr0 * cosd))
+    return out
+
+
+def _transform_code(p: Parameter) -> int:
+    t = p.transform
+    if t is None:
+        return 0
+    if isinstance(t, Softplus) and float(t.lower or 0.0) == 0.0:
+        return 1
+    if isinstance(t, Softplus) and float(t.lower or 0.0) == 1e-6:
+        return 2
+    raise NotImplementedError(f"transform {t!r} is not supported by the device Adam step")
+
+
+class _SVGPTrainer:
+    """Device state of one SVGP optimize() call.
+
+    Every trainable quantity lives in ONE packed fp64 buffer of constrained values
+    ``c`` (the model's Z / thetas / q_mu / q_sqrt / W / noise are views into it), with
+    the unconstrained ``u``, Adam moments, per-entry trainable / transform / tie-span
+    bytes, a packed gradient buffer of the same layout (written in place by
+    mfgp_svgp_elbo_grad), the float32 CosineDecay schedule and the step counter.  One
+    iteration = one gradient call + one mfgp_adam_packed call; iterations are replayed
+    from hipGraphs on a dedicated stream."""
+
+    def __init__(self, model, data, max_iters, initial_lr, kl_multiplier=1.0, graph=True, graph_chunk=50):
+        self.model = model
+        self.eng = eng = Engine.get()
+        dev = eng.device
+        X, Y = data
+        Xh = np.ascontiguousarray(np.asarray(X.cpu() if isinstance(X, torch.Tensor) else X, dtype=np.float64))
+        Yh = np.ascontiguousarray(np.asarray(Y.cpu() if isinstance(Y, torch.Tensor) else Y, dtype=np.float64))
+        if Yh.ndim == 1:
+            Yh = Yh[:, None]
+        self.klm = float(kl_multiplier)
+        self.max_iters = max(int(max_iters), 1)
+        Zp = model.inducing_variable
+        m, dp1 = Zp.shape
+        d = dp1 - 1
+        self.d, self.m = d, m
+        kernels = model.kernel.kernels
+        L = len(kernels)
+        G = theta_size(d)
+        p = Yh.shape[1]
+        self.L, self.G, self.p = L, G, p
+        Wp = model.kernel.W if isinstance(model.kernel, LinearCoregionalization) else None
+        # ---- packed layout: (name, shape, c, u, trainable, transform, span)
+        segs = []
+        segs.append(("Z", (m, dp1), Zp.numpy(), Zp.unconstrained_variable, np.full((m, dp1), Zp.trainable), 0, None))
+        self._theta_refs = []
+        tc = np.zeros((L, G)); tu = np.zeros((L, G)); tt = np.zeros((L, G), bool)
+        tf = np.zeros((L, G), np.uint8); ts = np.ones((L, G), np.uint8)
+        for l, k in enumerate(kernels):
+            refs = [(k.kernel_L.variance, None)]
+            refs += [(k.kernel_L.lengthscales, None if k.kernel_L.lengthscales.shape == () else (i,)) for i in range(d)]
+            refs += [(k.kernel_delta.variance, None)]
+            refs += [(k.kernel_delta.lengthscales, None if k.kernel_delta.lengthscales.shape == () else (i,))
+                     for i in range(d)]
+            refs += [(k.rho, (0, 0))]
+            seen = {}
+            for q, (prm, idx) in enumerate(refs):
+                cv, uv = prm.numpy(), prm.unconstrained_variable
+                tc[l, q] = float(cv if idx is None else cv[idx])
+                tu[l, q] = float(uv if idx is None else uv[idx])
+                tt[l, q] = prm.trainable
+                tf[l, q] = _transform_code(prm)
+                key = (id(prm), idx)
+                if key in seen:   # tied entry (isotropic lengthscale): follower of the first
+                    ts[l, q] = 0
+                    ts[l, seen[key]] += 1
+                else:
+                    seen[key] = q
+            tt[l, G - 1] = False   # noise slot of the theta layout is unused here
+            self._theta_refs.append(refs)
+        segs.append(("theta", (L, G), tc, tu, tt, tf, ts))
+        qm = model.q_mu
+        segs.append(("q_mu", (m, L), qm.numpy(), qm.unconstrained_variable, np.full((m, L), qm.trainable), 0, None))
+        qs = model.q_sqrt
+        low = np.tril(np.ones((m, m), bool))[None].repeat(L, axis=0)
+        segs.append(("q_sqrt", (L, m, m), np.tril(qs.numpy()), np.tril(qs.unconstrained_variable),
+                     low & qs.trainable, 0, None))
+        if Wp is not None:
+            segs.append(("W", (p, L), Wp.numpy(), Wp.unconstrained_variable, np.full((p, L), Wp.trainable), 0, None))
+        nv = model.likelihood.variance
+        segs.append(("noise", (1,), np.reshape(nv.numpy(), (1,)), np.reshape(nv.unconstrained_variable, (1,)),
+                     np.full((1,), nv.trainable), _transform_code(nv), None))
+        self.layout = {}
+        off = 0
+        cs, us, trs, tfs, sps = [], [], [], [], []
+        for name, shape, cv, uv, tv, trf, spn in segs:
+            size = int(np.prod(shape))
+            self.layout[name] = (off, shape)
+            off += size
+            cs.append(np.asarray(cv, np.float64).reshape(-1))
+            us.append(np.asarray(uv, np.float64).reshape(-1))
+            trs.append(np.asarray(tv, bool).reshape(-1))
+            tfs.append(np.asarray(trf if isinstance(trf, np.ndarray) else np.full(size, trf), np.uint8).reshape(-1))
+            sps.append(np.asarray(spn if spn is not None else np.ones(size), np.uint8).reshape(-1))
+        self.n = off
+        self.stream = torch.cuda.Stream(dev)
+        f64 = dict(dtype=torch.float64, device=dev)
+        with torch.cuda.stream(self.stream):
+            self.X = torch.tensor(Xh, **f64)
+            self.Y = torch.tensor(Yh, **f64)
+            self.c = torch.tensor(np.concatenate(cs), **f64)
+            self.u = torch.tensor(np.concatenate(us), **f64)
+            self.g = torch.zeros(self.n, **f64)
+            self.mo = torch.zeros(self.n, **f64)
+            self.vo = torch.zeros(self.n, **f64)
+            self.trainable = torch.tensor(np.concatenate(trs).astype(np.uint8), device=dev)
+            self.transform = torch.tensor(np.concatenate(tfs), device=dev)
+            self.span = torch.tensor(np.concatenate(sps), device=dev)
+            self.step_t = torch.zeros((1,), dtype=torch.int32, device=dev)
+            self.lr = torch.tensor(cosine_decay_schedule(initial_lr, max_iters, self.max_iters), **f64)
+            self.loss_hist = torch.zeros((self.max_iters,), **f64)
+            self.kl_hist = torch.zeros((self.max_iters,), **f64)
+            self.out = torch.zeros((3,), **f64)
+            n = Xh.shape[0]
+            self.g_mu = torch.empty((L, n), **f64)
+            self.g_var = torch.empty((L, n), **f64)
+            self.info = torch.zeros((L,), dtype=torch.int32, device=dev)
+        self.scale = (model.num_data / n) if model.num_data else 1.0
+        self.b1, self.b2 = float(np.float32(0.9)), float(np.float32(0.999))
+        self.done = 0
+        self.runner = _StepRunner(self._step, graph_chunk if graph else 0)
+        if graph:   # size the workspace outside capture
+            self.grad()
+
+    def view(self, buf, name):
+        off, shape = self.layout[name]
+        return buf[off:off + int(np.prod(shape))].view(*shape)
+
+    def grad_views(self):
+        return {k: self.view(self.g, k) for k in self.layout}
+
+    def grad(self):
+        """One gradient evaluation at the current parameters, ordered on the trainer's stream."""
+        with torch.cuda.stream(self.stream):
+            self._grad()
+
+    def _grad(self):
+        c, g = self.c, self.g
+        W = self.view(c, "W") if "W" in self.layout else None
+        gW = self.view(g, "W") if "W" in self.layout else None
+        self.eng.svgp_elbo_grad(self.X, self.Y, self.view(c, "Z"), self.view(c, "theta"), self.view(c, "q_mu"),
+                                self.view(c, "q_sqrt"), W, self.view(c, "noise"), self.scale, self.klm,
+                                DEFAULT_JITTER, self.out, self.g_mu, self.g_var, self.view(g, "Z"),
+                                self.view(g, "theta"), self.view(g, "q_mu"), self.view(g, "q_sqrt"), gW,
+                                self.view(g, "noise"), self.info)
+
+    def _step(self):
+        self._grad()
+        self.eng.adam_packed(self.u, self.c, self.g, self.mo, self.vo, self.trainable, self.transform, self.span,
+                             self.step_t, self.lr, self.b1, self.b2, 1e-7, self.out, self.klm, self.loss_hist,
+                             self.kl_hist)
+
+    def run(self, n):
+        if self.done + n > self.max_iters:
+            raise ValueError("SVGP optimize: more iterations than max_iters")
+        with torch.cuda.stream(self.stream):
+            self.runner.run(n)
+        self.done += n
+
+    def set_trainable(self, name, flag):
+        off, shape = self.layout[name]
+        with torch.cuda.stream(self.stream):
+            self.trainable[off:off + int(np.prod(shape))] = int(bool(flag))
+        if name == "noise":
+            self.model.likelihood.variance.trainable = bool(flag)
+
+    def sync(self):
+        self.stream.synchronize()
+
+    def elbo_now(self):
+        """ELBO at the current parameters (one gradient evaluation, synchronised)."""
+        self.grad()
+        self.sync()
+        return float(self.out[0].item())
+
+    def loss_at(self, i):
+        self.sync()
+        return float(self.loss_hist[i].item())
+
+    def finish(self, reset_history=True):
+        self.sync()
+        model = self.model
+        u = self.u.cpu().numpy()
+
+        def seg(name):
+            off, shape = self.layout[name]
+            return u[off:off + int(np.prod(shape))].reshape(shape)
+
+        model.inducing_variable.unconstrained_variable = seg("Z")
+        model.q_mu.unconstrained_variable = seg("q_mu")
+        qs = model.q_sqrt.unconstrained_variable
+        model.q_sqrt.unconstrained_variable = np.where(np.tril(np.ones(qs.shape[-2:], bool)), seg("q_sqrt"), qs)
+        if "W" in self.layout:
+            model.kernel.W.unconstrained_variable = seg("W")
+        model.likelihood.variance.unconstrained_variable = np.reshape(seg("noise"), model.likelihood.variance.shape)
+        th = seg("theta")
+        for l, refs in enumerate(self._theta_refs):
+            for q, (prm, idx) in enumerate(refs):
+                if idx is None:
+                    prm.unconstrained_variable = np.full(prm.shape, th[l, q])
+                else:
+                    arr = prm.unconstrained_variable.copy()
+                    arr[idx] = th[l, q]
+                    prm.unconstrained_variable = arr
+        h = self.loss_hist[:self.done].cpu().numpy()
+        k = self.kl_hist[:self.done].cpu().numpy()
+        if reset_history:
+            model.loss_history = []
+        model.loss_history.extend(np.float64(v) for v in h)
+        if hasattr(model, "kl_history"):
+            model.kl_history.extend(np.float64(v) for v in k)
+        if int(self.info.max().item()) != 0 or not np.all(np.isfinite(h)):
+            raise CholeskyError("SVGP optimize: Cholesky of K_uu failed")
 
 
 class LatentMFCoregionalizationSVGP(_SVGPBase):
@@ -168,6 +423,14 @@ class LatentMFCoregionalizationSVGP(_SVGPBase):
     def _W(self):
         return self.kernel.W.numpy()
 
+    def optimize(self, data, max_iters=10000, initial_lr=0.005, unfix_noise_after=5000, kl_multiplier=1.0,
+                 verbose=False, graph=True, graph_chunk=50):
+        """linear_svgp.py:153-203: Adam + CosineDecay(initial_lr, max_iters) on
+        -ELBO + (kl_multiplier - 1) KL; loss_history / kl_history are appended.  (The
+        reference's noise-unfix branch compares loss_type with 'gausssian' and never
+        fires: the noise keeps the trainable flag it has.)"""
+        self._optimize(data, max_iters, initial_lr, None, kl_multiplier, False, graph, graph_chunk, verbose, 100)
+
 
 class SingleBinSVGP(_SVGPBase):
     """mfgpflow/singlebin_svgp.py:20-62 constructor semantics (Z values are ignored;
@@ -182,6 +445,12 @@ class SingleBinSVGP(_SVGPBase):
         M = Zi.shape[0]
         self._setup(Zi, np.zeros((M, num_outputs)), np.repeat(np.eye(M)[None], num_outputs, axis=0) * 0.1,
                     Gaussian(), None)
+
+    def optimize(self, data, max_iters=10000, initial_lr=0.01, unfix_noise_after=5000, verbose=False, graph=True,
+                 graph_chunk=50):
+        """singlebin_svgp.py:64-97: Adam + CosineDecay(initial_lr, max_iters) on -ELBO;
+        loss_history restarts; the noise becomes trainable after iteration unfix_noise_after."""
+        self._optimize(data, max_iters, initial_lr, unfix_noise_after, 1.0, True, graph, graph_chunk, verbose, 10)
 
     @staticmethod
     def load_model(filename, X, Y, kernel_L, kernel_delta, num_outputs, Z):

@@ -152,3 +152,50 @@ class SingleBinTrainer:
                 self.v[k] += (g * g - self.v[k]) * (1.0 - self.b2)
                 var -= (self.m[k] * alpha) / (torch.sqrt(self.v[k]) + self.eps)
         return float(loss.detach())
+
+
+def initialize_W_ref(output_dim, num_latents, window_fraction=0.3, scale=0.5):
+    """mfgpflow/linear_svgp.py:17-48 (structured diagonal W, P x L)."""
+    W = np.zeros((output_dim, num_latents))
+    window = max(int(output_dim * window_fraction), 2)
+    stride = max(output_dim // (num_latents - 1), 1) if num_latents > 1 else 1
+    for j in range(num_latents):
+        center = min(int(j * stride), output_dim - 1)
+        for i in range(output_dim):
+            if abs(i - center) < window / 2:
+                W[i, j] = np.exp(-0.1 * abs(i - center))
+    return W * scale
+
+
+class LatentTrainer(SingleBinTrainer):
+    """LatentMFCoregionalizationSVGP.optimize (linear_svgp.py:153-203) restated with torch
+    autograd: W trainable (w_type='diagonal'), q_sqrt = I per latent, noise 1.0,
+    num_data = N, loss = -ELBO + (kl_multiplier - 1) KL recorded before each update."""
+
+    def __init__(self, X, Y, kw, lr=0.005, max_iters=10000, kl_multiplier=1.0):
+        from sklearn.cluster import KMeans
+        Z = KMeans(n_clusters=kw["num_inducing"], random_state=42).fit(X).cluster_centers_
+        L, P = kw["num_latents"], kw["num_outputs"]
+        super().__init__(X, Y, Z, lr=lr, max_iters=max_iters)
+        M, D = Z.shape[0], Z.shape[1] - 1
+        u1 = float(softplus_inverse(1.0))
+        self.P = L   # per-latent parameter blocks below are sized by L
+        self.vars.update({
+            "q_mu": torch.zeros((M, L), dtype=torch.float64, requires_grad=True),
+            "q_sqrt_tri": torch.tensor(np.tile(np.eye(M)[np.tril_indices(M)], (L, 1)), requires_grad=True),
+            "vL": torch.full((L,), u1, dtype=torch.float64, requires_grad=True),
+            "lL": torch.full((L, D), u1, dtype=torch.float64, requires_grad=True),
+            "vD": torch.full((L,), u1, dtype=torch.float64, requires_grad=True),
+            "lD": torch.full((L, D), u1, dtype=torch.float64, requires_grad=True),
+            "rho": torch.full((L,), u1, dtype=torch.float64, requires_grad=True),
+            "W": torch.tensor(initialize_W_ref(P, L, kw.get("window_fraction", 0.4), kw.get("scale", 0.2)),
+                              requires_grad=True),
+        })
+        self.m = {k: torch.zeros_like(v) for k, v in self.vars.items()}
+        self.v = {k: torch.zeros_like(v) for k, v in self.vars.items()}
+        self.klm = kl_multiplier
+
+    def neg_elbo(self):
+        Z, kps, q_mu, q_sqrt, noise = self.constrained()
+        e, kl, _ = elbo_t(self.X, self.Y, Z, kps, q_mu, q_sqrt, self.vars["W"], noise, num_data=self.X.shape[0])
+        return -e + (self.klm - 1.0) * kl

@@ -110,3 +110,97 @@ def test_singlebin_elbo_kat(hbs, kats):
             k.rho.assign(np.full((1, 1), float(kp["rho"])))
         v = -float(m.elbo((X, Y)))
         assert abs(v - ref[str(i)]) < 1e-8 * abs(ref[str(i)]), (i, v, ref[str(i)])
+
+
+# ---------------------------------------------------------------- gradients
+def _autograd_grads(model, X, Y, W=None, num_data=None, kl_mult=1.0):
+    """d(VE*scale - kl_mult*KL)/d(constrained params) by torch autograd through the oracle."""
+    D = model.inducing_variable.shape[1] - 1
+    Z, kps, q_mu, q_sqrt, Wt, noise = _oracle_state(model, W)
+    leaves = [Z, q_mu, q_sqrt, noise] + ([Wt] if Wt is not None else [])
+    for kp in kps:
+        leaves += list(kp.values())
+    for t in leaves:
+        t.requires_grad_(True)
+    e, kl, ve = S.elbo_t(torch.tensor(X), torch.tensor(Y), Z, kps, q_mu, q_sqrt, Wt, noise, num_data=num_data)
+    obj = e - (kl_mult - 1.0) * kl
+    obj.backward()
+    th = np.zeros((len(kps), 2 * D + 4))
+    for l, kp in enumerate(kps):
+        th[l, 0] = kp["vL"].grad
+        th[l, 1:1 + D] = kp["lL"].grad.numpy()
+        th[l, 1 + D] = kp["vD"].grad
+        th[l, 2 + D:2 + 2 * D] = kp["lD"].grad.numpy()
+        th[l, 2 + 2 * D] = kp["rho"].grad
+    g = dict(Z=Z.grad.numpy(), q_mu=q_mu.grad.numpy(), q_sqrt=np.tril(q_sqrt.grad.numpy()), noise=noise.grad.numpy(),
+             theta=th)
+    if Wt is not None:
+        g["W"] = Wt.grad.numpy()
+    return float(e), g
+
+
+def _check_grads(gd, ga, tol):
+    for k, ref in ga.items():
+        got = np.asarray(gd[k]).reshape(np.shape(ref))
+        scale = max(np.abs(ref).max(), 1e-30)
+        err = np.abs(got - ref).max() / scale
+        assert err < tol, (k, err)
+
+
+@pytest.mark.parametrize("randomize", [False, True])
+def test_singlebin_elbo_grad_vs_autograd(hbs, randomize):
+    X, Y = hbs["X"], hbs["Y"][:, :7]
+    m = M.SingleBinSVGP(X, Y, M.SquaredExponential(lengthscales=np.ones(5)),
+                        M.SquaredExponential(lengthscales=np.ones(5)), 7, Z=np.zeros((20, 6)))
+    if randomize:
+        _randomize(m, 21)
+    e, gd = m.elbo_and_grad((X, Y))
+    eo, ga = _autograd_grads(m, X, Y)
+    assert abs(e - eo) < 1e-7 * abs(eo)   # value-path tolerance (module docstring)
+    _check_grads(gd, ga, 1e-6)
+
+
+@pytest.mark.parametrize("kl_mult", [1.0, 0.3])
+def test_latent_elbo_grad_vs_autograd(hbs, kl_mult):
+    X, Y = hbs["X"], hbs["Y"]
+    D, P = X.shape[1] - 1, Y.shape[1]
+    m = M.LatentMFCoregionalizationSVGP(X, Y, M.SquaredExponential(lengthscales=np.ones(D)),
+                                        M.SquaredExponential(lengthscales=np.ones(D)), num_latents=4,
+                                        num_inducing=24, num_outputs=P, w_type='diagonal')
+    _randomize(m, 22)
+    e, gd = m.elbo_and_grad((X, Y), kl_multiplier=kl_mult)
+    eo, ga = _autograd_grads(m, X, Y, m.kernel.W.numpy(), num_data=X.shape[0], kl_mult=kl_mult)
+    assert abs(e - eo) < 1e-7 * abs(eo)   # value-path tolerance (module docstring)
+    _check_grads(gd, ga, 1e-6)
+
+
+def test_singlebin_training_kat(hbs, kats):
+    """notebooks/demo matter power single bin.ipynb:156-159: -ELBO after Adam steps 0/10/20/30
+    (M=50, initial_lr=0.1, 2000-step CosineDecay), run as the reference's optimize loop."""
+    X, Y = hbs["X"], hbs["Y"]
+    ref = kats["hbs_singlebin_svgp_neg_elbo"]["values"]
+    m = M.SingleBinSVGP(X, Y, M.SquaredExponential(lengthscales=np.ones(5)),
+                        M.SquaredExponential(lengthscales=np.ones(5)), 49, Z=np.zeros((50, 6)))
+    tr = M.svgp._SVGPTrainer(m, (X, Y), max_iters=2000, initial_lr=0.1, graph=True, graph_chunk=10)
+    for i in range(31):
+        tr.run(1)
+        if str(i) in ref:
+            got = -tr.elbo_now()
+            assert abs(got - ref[str(i)]) < 2e-6 * abs(ref[str(i)]), (i, got, ref[str(i)])
+
+
+def test_latent_training_matches_oracle(hbs):
+    """20 optimize() steps of the latent model vs. the same Adam/CosineDecay loop on the
+    torch-CPU oracle (autograd gradients)."""
+    X, Y = hbs["X"], hbs["Y"]
+    D, P = X.shape[1] - 1, Y.shape[1]
+    kw = dict(num_latents=3, num_inducing=16, num_outputs=P, w_type='diagonal')
+    m = M.LatentMFCoregionalizationSVGP(X, Y, M.SquaredExponential(lengthscales=np.ones(D)),
+                                        M.SquaredExponential(lengthscales=np.ones(D)), **kw)
+    m.optimize((X, Y), max_iters=20, initial_lr=0.05)
+    hist = np.array(m.loss_history)
+    assert hist.shape == (20,) and np.all(np.isfinite(hist)) and hist[-1] < hist[0]
+    # oracle: same loop on the autograd gradients
+    ref = S.LatentTrainer(X, Y, kw, lr=0.05, max_iters=20)
+    oh = [ref.step() for _ in range(20)]
+    np.testing.assert_allclose(hist, oh, rtol=1e-6)
