@@ -280,10 +280,14 @@ __global__ __launch_bounds__(NTHREADS) void k_kgrad(const double* P1, long ld1, 
     const int a = at * KG_ROWS + ar;
     const MFTheta th{thetas + (long)l * G, D};
     const double vL = th.vL(), vD = th.vD(), rho = th.rho();
-    double gl[DC], gd[DC], gz[DC];
+    double gl[DC], gd[DC], gz[DC], il[DC], id[DC];
     double gvL = 0.0, gvD = 0.0, grho = 0.0;
 #pragma unroll
-    for (int d = 0; d < DC; ++d) { gl[d] = 0.0; gd[d] = 0.0; gz[d] = 0.0; }
+    for (int d = 0; d < DC; ++d) {
+        gl[d] = 0.0; gd[d] = 0.0; gz[d] = 0.0;
+        il[d] = (d < D) ? 1.0 / th.lL(d) : 0.0;   // inverse lengthscales hoisted out of the pair loop
+        id[d] = (d < D) ? 1.0 / th.lD(d) : 0.0;
+    }
     if (a < n1) {
         const double fa = P1[(long)a * ld1 + D];
         const bool La = (fa == 0.0), Ha = (fa == 1.0);
@@ -302,11 +306,9 @@ __global__ __launch_bounds__(NTHREADS) void k_kgrad(const double* P1, long ld1, 
 #pragma unroll
                 for (int d = 0; d < DC; ++d) {
                     dl[d] = (d < D) ? za[d] - P2[(long)b * ld2 + d] : 0.0;
-                    if (d < D) {
-                        const double il = 1.0 / th.lL(d), id = 1.0 / th.lD(d);
-                        rL += dl[d] * dl[d] * il * il;
-                        rD += dl[d] * dl[d] * id * id;
-                    }
+                    const double xl = dl[d] * il[d], xd = dl[d] * id[d];
+                    rL += xl * xl;
+                    rD += xd * xd;
                 }
                 const double sa = La ? 1.0 : rho, sb = Lb ? 1.0 : rho;
                 const double kL = vL * exp(-0.5 * rL);
@@ -319,16 +321,13 @@ __global__ __launch_bounds__(NTHREADS) void k_kgrad(const double* P1, long ld1, 
                 if (hh) gvD += wd / vD;
 #pragma unroll
                 for (int d = 0; d < DC; ++d) {
-                    if (d < D) {
-                        const double il = 1.0 / th.lL(d), id = 1.0 / th.lD(d);
-                        const double qL = dl[d] * dl[d] * il * il;
-                        gl[d] += wl * qL * il;
-                        gz[d] -= wl * dl[d] * il * il;
-                        if (hh) {
-                            const double qD = dl[d] * dl[d] * id * id;
-                            gd[d] += wd * qD * id;
-                            gz[d] -= wd * dl[d] * id * id;
-                        }
+                    const double tl = dl[d] * il[d] * il[d];   // (x_a - x_b) / l^2
+                    gl[d] += wl * tl * dl[d] * il[d];          // dk/dl = k (x_a - x_b)^2 / l^3
+                    gz[d] -= wl * tl;
+                    if (hh) {
+                        const double td = dl[d] * id[d] * id[d];
+                        gd[d] += wd * td * dl[d] * id[d];
+                        gz[d] -= wd * td;
                     }
                 }
             }
