@@ -86,7 +86,7 @@ def step_flops(n, p, d):
     return gram + n ** 3 / 3 + n * n * p + 2 * n ** 3 / 3 + 2 * n * n * p + n * (n + 1) / 2 * (4 * d + 10)
 
 
-def roofline(model, n, p, d, reps=10):
+def roofline(model, n, p, d, reps=10, pmc=True):
     """Dominant kernel family from live hipEvent phase times (launch stream)."""
     from multi_fidelity_gpflow_amd.engine import gpr_phase_times
     eng, X, Y = model._device_data()
@@ -113,7 +113,7 @@ def roofline(model, n, p, d, reps=10):
     per_launch_flop = flops[dom] / launches[dom]
     achieved = per_launch_flop / (per_launch_ms * 1e-3) / 1e12
     kname = {"chol_steps": "k_chol_step", "gram": "k_gram", "alpha": "k_alpha", "grad": "k_grad"}[dom]
-    traffic, tsrc = pmc_traffic(kname, nb)
+    traffic, tsrc = pmc_traffic(kname, nb) if pmc else (None, None)
     return {
         "kernel": kname,
         "bound": "mfma",
@@ -160,7 +160,12 @@ def main():
     ap.add_argument("--tile", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-train-predict", action="store_true")
+    ap.add_argument("--config", choices=["goku", "synth"], default="goku",
+                    help="goku: the BASELINE metric; synth: SURVEY §8(d) scale-up (N=18432, P=512, fp64)")
     args = ap.parse_args()
+    if args.config == "synth":
+        args.no_cpu_baseline = True
+        args.no_train_predict = True
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -175,7 +180,11 @@ def main():
     if args.tile:
         eng.set_tile(args.tile)
 
-    X, Y, Xt, Yt = broadcast_inputs(rank, world, device)
+    if args.config == "synth":
+        from multi_fidelity_gpflow_amd.data import synthetic_multifidelity
+        X, Y, Xt, Yt = synthetic_multifidelity()   # deterministic: every rank builds the same set
+    else:
+        X, Y, Xt, Yt = broadcast_inputs(rank, world, device)
     n, d, P = X.shape[0], X.shape[1] - 1, Y.shape[1]
     from multi_fidelity_gpflow_amd.distributed import bin_block
     b0, b1 = bin_block(P, rank, world)
@@ -183,7 +192,7 @@ def main():
 
     model = make_model(X, Yr)
     K, W = args.steps, args.warmup
-    sess = model.adam_session(0.1, K + W, graph=True, graph_chunk=50)
+    sess = model.adam_session(0.1, K + W, graph=True, graph_chunk=50 if args.config == "goku" else 2)
     sess.run(W)
     sess.sync()
     if world > 1:
@@ -218,15 +227,17 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             tp = float(t.item())
 
-    roof = roofline(model, n, Yr.shape[1], d)
+    roof = roofline(model, n, Yr.shape[1], d, pmc=args.config == "goku")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(X, Y)
 
     if rank == 0:
         value = world * K / dt
+        synth = args.config == "synth"
         line = {
-            "metric": "LML evals/sec (Goku 1128LF/36HF multi-bin, value+grad+Adam step)",
+            "metric": ("LML evals/sec (synthetic 16384LF/2048HF D=10 P=512, value+grad+Adam step)" if synth else
+                       "LML evals/sec (Goku 1128LF/36HF multi-bin, value+grad+Adam step)"),
             "value": round(value, 3),
             "unit": "evals/s",
             "n_gpus": world,
@@ -237,8 +248,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "Goku z=0 P(k) (reference data files, tests/golden/data), RCCL-broadcast from rank 0",
-            "config": {"workload": "goku_multibin_adam_step", "n_lf": 1128, "n_hf": 36, "d": d, "p": P,
+            "data": ("synthetic (SURVEY §8(d) recipe, seed 20251015), built on every rank" if synth else
+                     "Goku z=0 P(k) (reference data files, tests/golden/data), RCCL-broadcast from rank 0"),
+            "config": {"workload": "synth_multibin_adam_step" if synth else "goku_multibin_adam_step",
+                       "n_lf": int((X[:, -1] == 0).sum()), "n_hf": int((X[:, -1] == 1).sum()), "d": d, "p": P,
                        "bins_per_rank": Yr.shape[1], "tile": eng.tile(),
                        "parallelism": f"bins{world}" if world > 1 else "single"},
             "bin_throughput": round(P * K / dt, 2),
@@ -246,8 +259,8 @@ def main():
             "step_tflops": round(step_flops(n, P, d) * value / 1e12, 4),
             "roofline": roof,
             "cpu_baseline": cpu,
-            "published_m1_cpu": {"train_1000_adam_s": 142.36, "evals_per_s": 7.02,
-                                 "source": "notebooks/demo: goku power spectra.ipynb:120"},
+            "published_m1_cpu": None if synth else {"train_1000_adam_s": 142.36, "evals_per_s": 7.02,
+                                                    "source": "notebooks/demo: goku power spectra.ipynb:120"},
         }
         print(json.dumps(line))
     if world > 1:

@@ -73,3 +73,25 @@ def multifidelity_training_set(data: PowerSpecs):
     Y = np.vstack([Y_LF, Y_HF])
     Xt = data.X_test_norm[0]
     return X, Y, np.hstack([Xt, np.ones((len(Xt), 1))]), data.Y_test[0]
+
+
+def synthetic_multifidelity(n_lf=16384, n_hf=2048, d=10, p=512, n_test=2048, seed=20251015):
+    """The synthetic scale-up configuration of SURVEY §8(d) (the reference has none):
+    X ~ U[0,1]^d, Y_L[:, p] = f_p(x) + 0.01 eps, Y_H = 1.2 f_p(x) + 0.1 g_p(x) + 0.005 eps,
+    f_p, g_p = (1/sqrt(d)) sum_k sin(2 pi k_pk x_k + phi_pk), k ~ U[0.5, 1.5], phi ~ U[0, 2 pi].
+    Returns (X [n_lf+n_hf, d+1] with the fidelity column, Y, X_test [n_test, d+1] HF, Y_test)."""
+    rng = np.random.default_rng(seed)
+    kf, pf = rng.uniform(0.5, 1.5, (p, d)), rng.uniform(0, 2 * np.pi, (p, d))
+    kg, pg = rng.uniform(0.5, 1.5, (p, d)), rng.uniform(0, 2 * np.pi, (p, d))
+
+    def f(x, k, ph):
+        return np.sin(2 * np.pi * x[:, None, :] * k[None] + ph[None]).sum(-1) / np.sqrt(d)
+
+    XL = rng.uniform(0, 1, (n_lf, d))
+    XH = rng.uniform(0, 1, (n_hf, d))
+    Xt = rng.uniform(0, 1, (n_test, d))
+    YL = f(XL, kf, pf) + 0.01 * rng.standard_normal((n_lf, p))
+    YH = 1.2 * f(XH, kf, pf) + 0.1 * f(XH, kg, pg) + 0.005 * rng.standard_normal((n_hf, p))
+    Yt = 1.2 * f(Xt, kf, pf) + 0.1 * f(Xt, kg, pg)
+    X = np.vstack([np.hstack([XL, np.zeros((n_lf, 1))]), np.hstack([XH, np.ones((n_hf, 1))])])
+    return X, np.vstack([YL, YH]), np.hstack([Xt, np.ones((n_test, 1))]), Yt

@@ -239,3 +239,33 @@ def test_large_synthetic_properties(eng):
         parts += float(_model(X, Y[:, i:i + 2], q).log_marginal_likelihood())
     assert abs(full - parts) < 1e-9 * abs(full)
     assert abs(full - O.gpr_lml(X, Y, _oracle_params(m))) < 1e-9 * abs(full)
+
+
+@pytest.mark.parametrize("n_lf,n_hf,p", [(3584, 512, 64)])
+def test_synthetic_scaleup_lml_vs_torch(n_lf, n_hf, p):
+    """Synthetic scale-up recipe at N = 4096: LML and gradient-free LML
+    of the HIP path vs. torch.linalg (fp64, on the GPU) on the same Gram built in torch
+    (property check at a size the CPU oracle would take minutes on)."""
+    from multi_fidelity_gpflow_amd.data import synthetic_multifidelity
+    X, Y, _, _ = synthetic_multifidelity(n_lf, n_hf, 10, p, 16, seed=7)
+    m = M.MultiFidelityGPModel(X, Y, M.SquaredExponential(lengthscales=np.full(10, 0.7)),
+                               M.SquaredExponential(lengthscales=np.full(10, 0.9), variance=0.3))
+    m.likelihood.variance.assign(1e-2)
+    lml = float(m.log_marginal_likelihood())
+    dev = torch.device("cuda")
+    Xd, Yd = torch.tensor(X, device=dev), torch.tensor(Y, device=dev)
+
+    def rbf(A, B, v, l):
+        a, b = A / l, B / l
+        return v * torch.exp(-0.5 * (-2 * a @ b.T + (a * a).sum(1)[:, None] + (b * b).sum(1)[None]))
+    f = Xd[:, -1]
+    s = (f == 0).double() + (f == 1).double()   # rho = 1
+    h = (f == 1).double()
+    K = (s[:, None] * s[None]) * rbf(Xd[:, :-1], Xd[:, :-1], 1.0, 0.7) \
+        + (h[:, None] * h[None]) * rbf(Xd[:, :-1], Xd[:, :-1], 0.3, 0.9)
+    K += 1e-2 * torch.eye(K.shape[0], device=dev, dtype=torch.float64)
+    L = torch.linalg.cholesky(K)
+    Z = torch.linalg.solve_triangular(L, Yd, upper=False)
+    ref = float(-0.5 * (Z * Z).sum() - Yd.shape[1] * torch.log(torch.diagonal(L)).sum()
+                - 0.5 * Yd.numel() * np.log(2 * np.pi))
+    assert abs(lml - ref) < 1e-9 * abs(ref), (lml, ref)
