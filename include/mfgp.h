@@ -108,6 +108,28 @@ int mfgp_gpr_predict(mfgp_handle_t h, int n, int p, int d, int nstar, const doub
                      int ldy, const double* Xs, int ldxs, const double* theta, void* ws, size_t ws_bytes,
                      double* mean, int ldm, double* var, int* info);
 
+/* GraphMultiFidelityKernel / GraphMultiFidelityGPModel (mfgpflow/graph.py:7-188) with
+ * nlf = m LF sources (fidelity flags 0..m-1 LF, m HF; 1 <= m <= 4).  theta layout
+ * (graph_theta_size = (m+1)(d+1) + m + m^2 + 1 entries):
+ *   [v_0, l_0(d), .., v_{m-1}, l_{m-1}(d), v_delta, l_delta(d), rho_0..rho_{m-1},
+ *    rhoLF[m][m] (row-major; diagonal unused, 1.0), noise]
+ * K's LF-LF block (i, j) is rhoLF[i][j] k_i (the ROW source's kernel, graph.py:61-63), so K
+ * is not symmetric for rhoLF[i][j] != rhoLF[j][i]; like TF, the factorization reads the
+ * lower triangle.  The LML adds the kernel's 1e-6 jitter (graph.py:96) and the noise;
+ * mfgp_gmf_gram adds diag_add (pass 1e-6 to mirror K(X)).  The gradient (want_grad) is
+ * d LML / d theta over every entry of K, as TF differentiates it. */
+int mfgp_gmf_gram(mfgp_handle_t h, int nlf, int n1, int n2, int d, const double* X1, int ldx1, const double* X2,
+                  int ldx2, const double* theta, double diag_add, double* K, int ldk);
+int mfgp_gmf_kdiag(mfgp_handle_t h, int nlf, int n, int d, const double* X, int ldx, const double* theta,
+                   double* out);
+int mfgp_gmf_gpr_workspace_size(mfgp_handle_t h, int nlf, int n, int p, int d, size_t* bytes);
+int mfgp_gmf_gpr_lml(mfgp_handle_t h, int nlf, int n, int p, int d, const double* X, int ldx, const double* Y,
+                     int ldy, const double* theta, int want_grad, void* ws, size_t ws_bytes, double* out, int* info);
+int mfgp_gmf_gpr_predict_workspace_size(mfgp_handle_t h, int nlf, int n, int p, int d, int nstar, size_t* bytes);
+int mfgp_gmf_gpr_predict(mfgp_handle_t h, int nlf, int n, int p, int d, int nstar, const double* X, int ldx,
+                         const double* Y, int ldy, const double* Xs, int ldxs, const double* theta, void* ws,
+                         size_t ws_bytes, double* mean, int ldm, double* var, int* info);
+
 /* Batched Cholesky factor inverse of SPD matrices (tf.linalg.cholesky +
  * triangular_solve(L, I) as used by GPflow's conditionals): Linv = chol(A)^{-1},
  * ldiag = diag(chol(A)).  A, Linv: [batch][n][n] with strides sA / sL elements. */
@@ -145,7 +167,7 @@ int mfgp_svgp_elbo_grad(mfgp_handle_t h, int n, int m, int l, int p, int d, cons
 
 /* One Keras-2.10 (legacy) Adam step on a packed parameter vector (the apply_gradients of
  * the SVGP optimize loops, linear_svgp.py:190 / singlebin_svgp.py:86): u unconstrained,
- * c constrained with transform[q] = 0 identity, 1 Softplus, 2 Shift(1e-6) o Softplus;
+ * c constrained with transform[q] = 0 identity, 1 Softplus, 2 Shift(1e-6) o Softplus, 3 Sigmoid;
  * g = d(+objective)/dc (e.g. the mfgp_svgp_elbo_grad outputs laid out in c's packing);
  * entries with trainable[q] == 0 are left alone; span (may be NULL) ties contiguous entries
  * to one variable (isotropic lengthscales): span[q] = k > 0 for a variable of k entries

@@ -10,6 +10,8 @@ from .kernels import (SquaredExponential, RBF, LinearMultiFidelityKernel,  # noq
                       LinearCoregionalization, SeparateIndependent)
 from .models import MultiFidelityGPModel, Gaussian, CholeskyError  # noqa: F401
 from .svgp import LatentMFCoregionalizationSVGP, SingleBinSVGP, initialize_W, initialize_W_pca  # noqa: F401
+from .kernels import GraphMultiFidelityKernel  # noqa: F401
+from .graph import GraphMultiFidelityGPModel  # noqa: F401
 from .data import PowerSpecs, map_to_unit_cube, input_normalize  # noqa: F401
 from . import data  # noqa: F401
 from ._lib import MFGPError  # noqa: F401

@@ -50,6 +50,12 @@ SIGNATURES = {
     "mfgp_svgp_elbo_grad": [_p, _i, _i, _i, _i, _i, _p, _i, _p, _i, _p, _i, _p, _p, _p, _p, _p, _d, _d, _d, _p,
                             _sz, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
     "mfgp_adam_packed": [_p, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _d, _d, _d, _p, _d, _p, _p],
+    "mfgp_gmf_gram": [_p, _i, _i, _i, _i, _p, _i, _p, _i, _p, _d, _p, _i],
+    "mfgp_gmf_kdiag": [_p, _i, _i, _i, _p, _i, _p, _p],
+    "mfgp_gmf_gpr_workspace_size": [_p, _i, _i, _i, _i, C.POINTER(_sz)],
+    "mfgp_gmf_gpr_lml": [_p, _i, _i, _i, _i, _p, _i, _p, _i, _p, _i, _p, _sz, _p, _p],
+    "mfgp_gmf_gpr_predict_workspace_size": [_p, _i, _i, _i, _i, _i, C.POINTER(_sz)],
+    "mfgp_gmf_gpr_predict": [_p, _i, _i, _i, _i, _i, _p, _i, _p, _i, _p, _i, _p, _p, _sz, _p, _i, _p, _p],
     "mfgp_selftest_mfma": [_p, _p],
 }
 

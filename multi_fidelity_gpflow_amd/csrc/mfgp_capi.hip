@@ -23,6 +23,8 @@ namespace mfgp {
 
 static inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 
+constexpr double GRAPH_JITTER = 1e-6;   // graph.py:96: K_full += 1e-6 I
+
 struct Carve {
     char* base;
     size_t off = 0;
@@ -42,14 +44,14 @@ struct GprLayout {
     size_t bytes;
 };
 
-static GprLayout gpr_layout(int nb, int n, int p, int d, void* ws, int grad_chunk) {
+static GprLayout gpr_layout(int nb, int n, int p, int d, void* ws, int grad_chunk, int nlf = 0) {
     GprLayout L;
     L.nb = nb;
     L.T = ceil_div(n, nb);
     L.npad = L.T * nb;
     L.Tp = ceil_div(p > 0 ? p : 1, nb);
     L.ppad = L.Tp * nb;
-    L.G = theta_size(d);
+    L.G = kernel_theta_size(nlf, d);
     L.gstride = (L.G + 3) & ~3;
     L.ng = grad_tasks(L.T, grad_chunk);
     Carve c(ws);
@@ -72,7 +74,7 @@ static inline hipError_t last() { return hipGetLastError(); }
 
 template <int NB>
 static void gram_lml_and_factor(hipStream_t s, const GprLayout& L, int n, int p, int d, const double* X, int ldx,
-                                const double* Y, int ldy, const double* theta, int* info) {
+                                const double* Y, int ldy, const double* theta, int* info, int nlf = 0) {
     const long ldr = L.npad + L.ppad;
     GramArgs g{};
     g.R = L.R; g.ldr = ldr; g.sR = 0; g.Y = Y; g.ldy = ldy; g.sY = 0; g.p = p; g.ppad = L.ppad;
@@ -80,8 +82,8 @@ static void gram_lml_and_factor(hipStream_t s, const GprLayout& L, int n, int p,
     g.X2 = X; g.ldx2 = ldx; g.sx2 = 0; g.n2 = n;
     g.theta = theta; g.stheta = 0; g.D = d; g.rbf_only = 0;
     g.out = L.A; g.ldo = L.npad; g.so = 0;
-    g.padded = 1; g.npad = L.npad; g.tiles_c = L.T; g.add_noise = 1; g.diag_add = 0.0;
-    g.Dd = L.Dd; g.sD = 0; g.ldiag = L.ldiag; g.sL = 0; g.info = info;
+    g.padded = 1; g.npad = L.npad; g.tiles_c = L.T; g.add_noise = 1; g.diag_add = nlf ? GRAPH_JITTER : 0.0;
+    g.Dd = L.Dd; g.sD = 0; g.ldiag = L.ldiag; g.sL = 0; g.info = info; g.nlf = nlf;
     launch_gram<NB>(g, L.T * (L.T + 1) / 2, 1, s);
     CholArgs c{};
     c.A = L.A; c.lda = L.npad; c.sA = 0;
@@ -102,8 +104,8 @@ struct PhaseMarks {
 template <int NB>
 static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X, int ldx, const double* Y, int ldy,
                           double* theta, int want_grad, void* ws, size_t ws_bytes, double* out, int* info,
-                          const FinArgs* adam, PhaseMarks* pm = nullptr) {
-    const GprLayout L = gpr_layout(NB, n, p, d, ws, h->grad_chunk);
+                          const FinArgs* adam, PhaseMarks* pm = nullptr, int nlf = 0) {
+    const GprLayout L = gpr_layout(NB, n, p, d, ws, h->grad_chunk, nlf);
     if (ws_bytes < L.bytes) return MFGP_ERR_WORKSPACE;
     hipStream_t s = h->stream;
     const long ldr = L.npad + L.ppad;
@@ -116,8 +118,8 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
         g.X2 = X; g.ldx2 = ldx; g.sx2 = 0; g.n2 = n;
         g.theta = theta; g.stheta = 0; g.D = d; g.rbf_only = 0;
         g.out = L.A; g.ldo = L.npad; g.so = 0;
-        g.padded = 1; g.npad = L.npad; g.tiles_c = L.T; g.add_noise = 1; g.diag_add = 0.0;
-        g.Dd = L.Dd; g.sD = 0; g.ldiag = L.ldiag; g.sL = 0; g.info = info;
+        g.padded = 1; g.npad = L.npad; g.tiles_c = L.T; g.add_noise = 1; g.diag_add = nlf ? GRAPH_JITTER : 0.0;
+        g.Dd = L.Dd; g.sD = 0; g.ldiag = L.ldiag; g.sL = 0; g.info = info; g.nlf = nlf;
         launch_gram<NB>(g, L.T * (L.T + 1) / 2, 1, s);
     }
     if (pm) pm->mark(s);
@@ -136,7 +138,7 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
     if (pm) pm->mark(s);
     if (want_grad) {
         GradArgs ga{L.Xo, ldr, L.alpha, (long)L.ppad, X, (long)ldx, theta, L.gpart, L.gstride, L.T, L.Tp, n, p, d,
-                    h->grad_chunk};
+                    h->grad_chunk, nlf};
         launch_grad<NB>(ga, s);
     }
     if (pm) pm->mark(s);
@@ -149,6 +151,7 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
     f.out = out;
     f.adam = adam != nullptr;
     f.items = L.items;
+    f.G = L.G;
     hipLaunchKernelGGL(k_reduce_items, dim3(2 + (want_grad ? L.G : 0)), dim3(NTHREADS), 0, s, f);
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, f);
     if (pm) pm->mark(s);
@@ -262,9 +265,9 @@ struct PredLayout {
     size_t bytes;
 };
 
-static PredLayout pred_layout(int nb, int n, int p, int d, int nstar, void* ws, int grad_chunk) {
+static PredLayout pred_layout(int nb, int n, int p, int d, int nstar, void* ws, int grad_chunk, int nlf = 0) {
     PredLayout P;
-    P.g = gpr_layout(nb, n, p, d, ws, grad_chunk);
+    P.g = gpr_layout(nb, n, p, d, ws, grad_chunk, nlf);
     P.Ts = ceil_div(nstar > 0 ? nstar : 1, nb);
     P.nspad = P.Ts * nb;
     Carve c(ws);
@@ -279,21 +282,21 @@ static PredLayout pred_layout(int nb, int n, int p, int d, int nstar, void* ws, 
 template <int NB>
 static int predict_impl(mfgp_handle_t h, int n, int p, int d, int nstar, const double* X, int ldx, const double* Y,
                         int ldy, const double* Xs, int ldxs, const double* theta, void* ws, size_t ws_bytes,
-                        double* mean, int ldm, double* var, int* info) {
-    const PredLayout P = pred_layout(NB, n, p, d, nstar, ws, h->grad_chunk);
+                        double* mean, int ldm, double* var, int* info, int nlf = 0) {
+    const PredLayout P = pred_layout(NB, n, p, d, nstar, ws, h->grad_chunk, nlf);
     if (ws_bytes < P.bytes) return MFGP_ERR_WORKSPACE;
     hipStream_t s = h->stream;
     const GprLayout& L = P.g;
-    gram_lml_and_factor<NB>(s, L, n, p, d, X, ldx, Y, ldy, theta, info);
+    gram_lml_and_factor<NB>(s, L, n, p, d, X, ldx, Y, ldy, theta, info, nlf);
     (void)hipMemsetAsync(P.Kmn, 0, sizeof(double) * (size_t)L.npad * P.nspad, s);
     GramArgs g{};
     g.X1 = X; g.ldx1 = ldx; g.n1 = n;
     g.X2 = Xs; g.ldx2 = ldxs; g.n2 = nstar;
     g.theta = theta; g.D = d; g.rbf_only = 0;
-    g.out = P.Kmn; g.ldo = P.nspad; g.padded = 0; g.tiles_c = P.Ts; g.diag_add = 0.0;
+    g.out = P.Kmn; g.ldo = P.nspad; g.padded = 0; g.tiles_c = P.Ts; g.diag_add = 0.0; g.nlf = nlf;
     launch_gram<NB>(g, L.T * P.Ts, 1, s);
     hipLaunchKernelGGL(k_kdiag, dim3(ceil_div(nstar, 256)), dim3(256), 0, s, Xs, (long)ldxs, nstar, d, theta,
-                       P.kdiag);
+                       P.kdiag, nlf);
     const long ldr = L.npad + L.ppad;
     PredAArgs pa{L.Xo, ldr, P.Kmn, (long)P.nspad, P.Am, (long)P.nspad, P.Ts};
     PredOutArgs po{P.Am, (long)P.nspad, L.Xo, ldr, P.kdiag, mean, (long)ldm, var, L.T, L.Tp, nstar, p};
@@ -382,7 +385,7 @@ int mfgp_set_tile(mfgp_handle_t h, int nb) {
 int mfgp_get_tile(mfgp_handle_t h) { return h ? h->nb : MFGP_ERR_ARG; }
 
 static int gram_common(mfgp_handle_t h, int n1, int n2, int d, const double* X1, int ldx1, const double* X2,
-                       int ldx2, const double* params, double diag_add, double* K, int ldk, int rbf) {
+                       int ldx2, const double* params, double diag_add, double* K, int ldk, int rbf, int nlf = 0) {
     CHECK_H(h);
     CHECK_D(d);
     if (n1 < 0 || n2 < 0 || !X1 || !X2 || !params || !K) return MFGP_ERR_ARG;
@@ -391,7 +394,7 @@ static int gram_common(mfgp_handle_t h, int n1, int n2, int d, const double* X1,
     g.X1 = X1; g.ldx1 = ldx1; g.n1 = n1;
     g.X2 = X2; g.ldx2 = ldx2; g.n2 = n2;
     g.theta = params; g.D = d; g.rbf_only = rbf;
-    g.out = K; g.ldo = ldk; g.padded = 0; g.diag_add = diag_add;
+    g.out = K; g.ldo = ldk; g.padded = 0; g.diag_add = diag_add; g.nlf = nlf;
     const int nb = h->nb;
     g.tiles_c = ceil_div(n2, nb);
     const int blocks = ceil_div(n1, nb) * g.tiles_c;
@@ -415,8 +418,77 @@ int mfgp_mf_kdiag(mfgp_handle_t h, int n, int d, const double* X, int ldx, const
     CHECK_D(d);
     if (n < 0 || !X || !theta || !out) return MFGP_ERR_ARG;
     if (n == 0) return MFGP_OK;
-    hipLaunchKernelGGL(k_kdiag, dim3(ceil_div(n, 256)), dim3(256), 0, h->stream, X, (long)ldx, n, d, theta, out);
+    hipLaunchKernelGGL(k_kdiag, dim3(ceil_div(n, 256)), dim3(256), 0, h->stream, X, (long)ldx, n, d, theta, out, 0);
     return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;
+}
+
+// ---------------------------------------------------------------- graph kernel (graph.py)
+#define CHECK_LF(m) \
+    if ((m) < 1 || (m) > MFGP_MAX_LF) return MFGP_ERR_ARG
+
+int mfgp_gmf_gram(mfgp_handle_t h, int nlf, int n1, int n2, int d, const double* X1, int ldx1, const double* X2,
+                  int ldx2, const double* theta, double diag_add, double* K, int ldk) {
+    CHECK_LF(nlf);
+    return gram_common(h, n1, n2, d, X1, ldx1, X2, ldx2, theta, diag_add, K, ldk, 0, nlf);
+}
+
+int mfgp_gmf_kdiag(mfgp_handle_t h, int nlf, int n, int d, const double* X, int ldx, const double* theta,
+                   double* out) {
+    CHECK_H(h);
+    CHECK_D(d);
+    CHECK_LF(nlf);
+    if (n < 0 || !X || !theta || !out) return MFGP_ERR_ARG;
+    if (n == 0) return MFGP_OK;
+    hipLaunchKernelGGL(k_kdiag, dim3(ceil_div(n, 256)), dim3(256), 0, h->stream, X, (long)ldx, n, d, theta, out,
+                       nlf);
+    return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;
+}
+
+int mfgp_gmf_gpr_workspace_size(mfgp_handle_t h, int nlf, int n, int p, int d, size_t* bytes) {
+    CHECK_H(h);
+    CHECK_D(d);
+    CHECK_LF(nlf);
+    if (n < 1 || p < 1 || !bytes) return MFGP_ERR_ARG;
+    *bytes = gpr_layout(h->nb, n, p, d, nullptr, h->grad_chunk, nlf).bytes;
+    return MFGP_OK;
+}
+
+int mfgp_gmf_gpr_lml(mfgp_handle_t h, int nlf, int n, int p, int d, const double* X, int ldx, const double* Y,
+                     int ldy, const double* theta, int want_grad, void* ws, size_t ws_bytes, double* out, int* info) {
+    CHECK_H(h);
+    CHECK_D(d);
+    CHECK_LF(nlf);
+    if (n < 1 || p < 1 || !X || !Y || !theta || !ws || !out || !info) return MFGP_ERR_ARG;
+    if (h->nb == 64)
+        return gpr_value_grad<64>(h, n, p, d, X, ldx, Y, ldy, (double*)theta, want_grad, ws, ws_bytes, out, info,
+                                  nullptr, nullptr, nlf);
+    return gpr_value_grad<32>(h, n, p, d, X, ldx, Y, ldy, (double*)theta, want_grad, ws, ws_bytes, out, info,
+                              nullptr, nullptr, nlf);
+}
+
+int mfgp_gmf_gpr_predict_workspace_size(mfgp_handle_t h, int nlf, int n, int p, int d, int nstar, size_t* bytes) {
+    CHECK_H(h);
+    CHECK_D(d);
+    CHECK_LF(nlf);
+    if (n < 1 || p < 1 || nstar < 0 || !bytes) return MFGP_ERR_ARG;
+    *bytes = pred_layout(h->nb, n, p, d, nstar, nullptr, h->grad_chunk, nlf).bytes;
+    return MFGP_OK;
+}
+
+int mfgp_gmf_gpr_predict(mfgp_handle_t h, int nlf, int n, int p, int d, int nstar, const double* X, int ldx,
+                         const double* Y, int ldy, const double* Xs, int ldxs, const double* theta, void* ws,
+                         size_t ws_bytes, double* mean, int ldm, double* var, int* info) {
+    CHECK_H(h);
+    CHECK_D(d);
+    CHECK_LF(nlf);
+    if (n < 1 || p < 1 || nstar < 0 || !X || !Y || !theta || !ws || !info) return MFGP_ERR_ARG;
+    if (nstar == 0) return MFGP_OK;
+    if (!Xs || !mean || !var) return MFGP_ERR_ARG;
+    if (h->nb == 64)
+        return predict_impl<64>(h, n, p, d, nstar, X, ldx, Y, ldy, Xs, ldxs, theta, ws, ws_bytes, mean, ldm, var,
+                                info, nlf);
+    return predict_impl<32>(h, n, p, d, nstar, X, ldx, Y, ldy, Xs, ldxs, theta, ws, ws_bytes, mean, ldm, var, info,
+                            nlf);
 }
 
 int mfgp_gpr_workspace_size(mfgp_handle_t h, int n, int p, int d, size_t* bytes) {

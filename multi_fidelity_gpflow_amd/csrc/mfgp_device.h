@@ -796,4 +796,50 @@ struct MFTheta {
 
 __host__ __device__ constexpr int theta_size(int D) { return 2 * D + 4; }
 
+// GraphMultiFidelityKernel (mfgpflow/graph.py:7-115) with m LF sources: theta layout
+//   [v_0, l_0(D), .., v_{m-1}, l_{m-1}(D), v_delta, l_delta(D), rho_0..rho_{m-1},
+//    rhoLF (m x m, row-major; diagonal unused), noise]
+constexpr int MFGP_MAX_LF = 4;
+struct GraphTheta {
+    const double* t;
+    int D, m;
+    __device__ double v(int s) const { return t[s * (1 + D)]; }            // s = m: delta
+    __device__ double l(int s, int d) const { return t[s * (1 + D) + 1 + d]; }
+    __device__ double rho(int i) const { return t[(m + 1) * (1 + D) + i]; }
+    __device__ double rhoLF(int i, int j) const { return t[(m + 1) * (1 + D) + m + i * m + j]; }
+};
+__host__ __device__ constexpr int graph_theta_size(int m, int D) { return (m + 1) * (1 + D) + m + m * m + 1; }
+__host__ __device__ constexpr int kernel_theta_size(int nlf, int D) {
+    return nlf ? graph_theta_size(nlf, D) : theta_size(D);
+}
+// fidelity flag -> source index (0..m-1 LF, m HF), -1 for anything else (graph.py:47-50 masks)
+__device__ __forceinline__ int graph_source(double f, int m) {
+    for (int i = 0; i <= m; ++i)
+        if (f == (double)i) return i;
+    return -1;
+}
+// one RBF term of source s between raw rows xa, xb
+__device__ __forceinline__ double graph_k(const double* xa, const double* xb, int s, const GraphTheta& th) {
+    double r2 = 0.0;
+    for (int d = 0; d < th.D; ++d) {
+        const double q = (xa[d] - xb[d]) / th.l(s, d);
+        r2 += q * q;
+    }
+    return th.v(s) * exp(-0.5 * r2);
+}
+// K(a, b) of graph.py:55-97 (row a with source sa, column b with source sb).  The LF-LF
+// block uses the ROW source's kernel (graph.py:61-63), so K is not symmetric for
+// rhoLF[i][j] != rhoLF[j][i]; the Cholesky reads the lower triangle like TF's.
+__device__ __forceinline__ double graph_entry(const double* xa, const double* xb, int sa, int sb,
+                                              const GraphTheta& th) {
+    if (sa < 0 || sb < 0) return 0.0;
+    const int m = th.m;
+    if (sa < m && sb < m) return (sa == sb ? 1.0 : th.rhoLF(sa, sb)) * graph_k(xa, xb, sa, th);
+    if (sa < m) return graph_k(xa, xb, sa, th) * th.rho(sa);
+    if (sb < m) return graph_k(xa, xb, sb, th) * th.rho(sb);
+    double s = 0.0;
+    for (int i = 0; i < m; ++i) s += graph_k(xa, xb, i, th) * (th.rho(i) * th.rho(i));
+    return s + graph_k(xa, xb, m, th);
+}
+
 }  // namespace mfgp

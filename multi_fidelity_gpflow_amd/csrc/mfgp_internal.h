@@ -21,6 +21,7 @@ struct GramArgs {
     double* Dd; long sD; double* ldiag; long sL; int* info;
     // fused RHS init (LML layout only; R == nullptr: skip): R = [I | Y]
     double* R; long ldr; long sR; const double* Y; long ldy; long sY; int p, ppad;
+    int nlf;                                  // 0: LinearMultiFidelityKernel; m >= 1: graph kernel, m LF sources
 };
 
 struct CholArgs {
@@ -50,6 +51,7 @@ struct GradArgs {
     double* gpart; int gstride;           // per task partial gradient
     int T, Tp, n, P, D;
     int chunk;                            // m-tiles per task
+    int nlf;                              // kernel family (GramArgs::nlf)
 };
 
 struct FinArgs {
@@ -70,6 +72,7 @@ struct FinArgs {
     double* loss_hist;                // loss_hist[step] = -lml (pre-step)
     int noise_index;                  // theta entry using Shift(1e-6) o Softplus
     double* items;                    // [2 + G] stage-1 reduction results
+    int G;                            // theta entries (kernel_theta_size)
 };
 
 struct PredAArgs {
@@ -109,7 +112,7 @@ __global__ void k_rhs_init(double* R, long ldr, long sR, int npad, int ppad, con
 __global__ void k_finalize(FinArgs a);
 __global__ void k_reduce_items(FinArgs a);
 __global__ void k_theta_from_u(const double* u, double* theta, int G, int noise_index);
-__global__ void k_kdiag(const double* X, long ldx, int n, int D, const double* theta, double* out);
+__global__ void k_kdiag(const double* X, long ldx, int n, int D, const double* theta, double* out, int nlf);
 __global__ void k_selftest_mfma(double* out);
 
 }  // namespace mfgp

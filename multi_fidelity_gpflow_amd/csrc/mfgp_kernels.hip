@@ -18,7 +18,8 @@
 namespace mfgp {
 
 constexpr int MAXD = 32;
-constexpr int XS = MAXD + 1;   // LDS row stride of staged inputs: odd, so a wave reading one
+constexpr int XS = MAXD + 1;
+constexpr int RSTRIDE = 192;   // per-wave gradient slots (>= kernel_theta_size for MAXD, MFGP_MAX_LF)   // LDS row stride of staged inputs: odd, so a wave reading one
                                 // dimension of 16-32 different rows hits distinct banks
 constexpr int ALPHA_CH = 4;   // m-tiles per alpha task
 
@@ -109,19 +110,35 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
         tj = blockIdx.x % a.tiles_c;
     }
     const MFTheta th{a.theta + b * a.stheta, a.D};
+    const GraphTheta gth{a.theta + b * a.stheta, a.D, a.nlf};
     const double* X1 = a.X1 + b * a.sx1;
     const double* X2 = a.X2 + b * a.sx2;
-    stage_rows<NB>(aL1, aD1, nL1, nD1, f1, X1, a.ldx1, a.n1, ti * NB, a.D, th, a.rbf_only);
-    stage_rows<NB>(aL2, aD2, nL2, nD2, f2, X2, a.ldx2, a.n2, tj * NB, a.D, th, a.rbf_only);
+    if (a.nlf) {   // graph kernel: raw rows + source index (f1/f2 hold the source as a double)
+        for (int e = threadIdx.x; e < NB * (a.D + 1); e += NTHREADS) {
+            const int r = e / (a.D + 1), d = e % (a.D + 1);
+            const int g1 = ti * NB + r, g2 = tj * NB + r;
+            const double v1 = (g1 < a.n1) ? X1[(long)g1 * a.ldx1 + d] : 0.0;
+            const double v2 = (g2 < a.n2) ? X2[(long)g2 * a.ldx2 + d] : 0.0;
+            if (d < a.D) { aL1[r * XS + d] = v1; aL2[r * XS + d] = v2; }
+            else {
+                f1[r] = (g1 < a.n1) ? (double)graph_source(v1, a.nlf) : -1.0;
+                f2[r] = (g2 < a.n2) ? (double)graph_source(v2, a.nlf) : -1.0;
+            }
+        }
+    } else {
+        stage_rows<NB>(aL1, aD1, nL1, nD1, f1, X1, a.ldx1, a.n1, ti * NB, a.D, th, a.rbf_only);
+        stage_rows<NB>(aL2, aD2, nL2, nD2, f2, X2, a.ldx2, a.n2, tj * NB, a.D, th, a.rbf_only);
+    }
     __syncthreads();
 
-    const double noise = a.add_noise ? th.noise() : 0.0;
+    const double noise = a.add_noise ? a.theta[b * a.stheta + kernel_theta_size(a.nlf, a.D) - 1] : 0.0;
     double* out = a.out + b * a.so;
     for (int e = threadIdx.x; e < NB * NB; e += NTHREADS) {
         const int r = e / NB, c = e % NB;
         const int gi = ti * NB + r, gj = tj * NB + c;
-        double v = gram_entry(aL1 + r * XS, aD1 + r * XS, nL1[r], nD1[r], f1[r],
-                              aL2 + c * XS, aD2 + c * XS, nL2[c], nD2[c], f2[c], a.D, th, a.rbf_only);
+        double v = a.nlf ? graph_entry(aL1 + r * XS, aL2 + c * XS, (int)f1[r], (int)f2[c], gth)
+                         : gram_entry(aL1 + r * XS, aD1 + r * XS, nL1[r], nD1[r], f1[r],
+                                      aL2 + c * XS, aD2 + c * XS, nL2[c], nD2[c], f2[c], a.D, th, a.rbf_only);
         if (a.padded) {
             if (gi == gj) v = (gi < a.n1) ? v + noise + a.diag_add : 1.0;   // identity padding
             tile[r * S + c] = v;
@@ -388,7 +405,7 @@ int grad_tasks(int T, int ch) {
 }
 
 
-template <int NB>
+template <int NB, bool GRAPH>
 __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
     constexpr int S = TileCfg<NB>::S;
     constexpr int E = TileCfg<NB>::ELEMS;
@@ -400,8 +417,8 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
     double* xj = xi + NB * XS;        // NB x XS raw rows of tile j
     double* fi = xj + NB * XS;      // NB
     double* fj = fi + NB;             // NB
-    double* red = fj + NB;            // 4 x (2*MAXD+4)
-    const int G = theta_size(a.D);
+    double* red = fj + NB;            // 4 x RSTRIDE
+    const int G = kernel_theta_size(a.nlf, a.D);
     const MFTheta th{a.theta, a.D};
 
     // decode task -> (i, j, m0, m1)
@@ -424,7 +441,10 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
         const double vi = (gi < a.n) ? a.X[(long)gi * a.ldxx + d] : 0.0;
         const double vj = (gj < a.n) ? a.X[(long)gj * a.ldxx + d] : 0.0;
         if (d < a.D) { xi[r * XS + d] = vi; xj[r * XS + d] = vj; }
-        else { fi[r] = (gi < a.n) ? vi : -1.0; fj[r] = (gj < a.n) ? vj : -1.0; }
+        else if (a.nlf) {   // graph kernel: source index
+            fi[r] = (gi < a.n) ? (double)graph_source(vi, a.nlf) : -1.0;
+            fj[r] = (gj < a.n) ? (double)graph_source(vj, a.nlf) : -1.0;
+        } else { fi[r] = (gi < a.n) ? vi : -1.0; fj[r] = (gj < a.n) ? vj : -1.0; }
     }
 
     // W_ij (tile) = [alpha_i alpha_j^T] - P * sum_m Linv_mi^T Linv_mj
@@ -449,6 +469,94 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
     }
     __syncthreads();
 
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    auto put = [&](int qidx, double v) {
+        v = wave_sum(v);
+        if (lane == 0) red[wv * RSTRIDE + qidx] = v;
+    };
+    if constexpr (GRAPH) {
+        // graph kernel (graph.py:55-97): 1/2 W_ab dK_ab/dtheta over all (a, b); a lower tile
+        // (i > j) also carries the mirrored entry K_ba, which differs in the LF-LF block.
+        const GraphTheta gt{a.theta, a.D, a.nlf};
+        const int m = a.nlf;
+        double co[MFGP_MAX_LF + 1][NE];       // per element: 1/2 W * dK/dk_s * k_s
+        double grho[MFGP_MAX_LF], grl[MFGP_MAX_LF * MFGP_MAX_LF];
+        double gn = 0.0;
+#pragma unroll
+        for (int s2 = 0; s2 < MFGP_MAX_LF; ++s2) grho[s2] = 0.0;
+#pragma unroll
+        for (int s2 = 0; s2 < MFGP_MAX_LF * MFGP_MAX_LF; ++s2) grl[s2] = 0.0;
+#pragma unroll
+        for (int q = 0; q < TileCfg<NB>::NBLK; ++q)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int e = q * 4 + r;
+                const int ri = acc_row<NB>(q, r), cj = acc_col<NB>(q);
+                const int sa = (int)fi[ri], sb = (int)fj[cj];
+                const double w = 0.5 * acc.v[q][r];
+#pragma unroll
+                for (int s2 = 0; s2 <= MFGP_MAX_LF; ++s2) co[s2][e] = 0.0;
+                if (sa >= 0 && sb >= 0) {
+                    double ks[MFGP_MAX_LF + 1];
+                    for (int s2 = 0; s2 <= m; ++s2) ks[s2] = graph_k(xi + ri * XS, xj + cj * XS, s2, gt);
+                    auto accum = [&](int s1, int t1) {   // entry with row source s1, column source t1
+                        if (s1 < m && t1 < m) {
+                            if (s1 == t1) co[s1][e] += w * ks[s1];
+                            else {
+                                co[s1][e] += w * gt.rhoLF(s1, t1) * ks[s1];
+                                grl[s1 * m + t1] += w * ks[s1];
+                            }
+                        } else if (s1 < m || t1 < m) {
+                            const int u = (s1 < m) ? s1 : t1;
+                            co[u][e] += w * gt.rho(u) * ks[u];
+                            grho[u] += w * ks[u];
+                        } else {
+                            for (int k2 = 0; k2 < m; ++k2) {
+                                const double rr = gt.rho(k2);
+                                co[k2][e] += w * rr * rr * ks[k2];
+                                grho[k2] += w * 2.0 * rr * ks[k2];
+                            }
+                            co[m][e] += w * ks[m];
+                        }
+                    };
+                    accum(sa, sb);
+                    if (i != j) accum(sb, sa);
+                }
+                if (i == j && ri == cj && i * NB + ri < a.n) gn += w;
+            }
+        for (int s2 = 0; s2 <= m; ++s2) {
+            double vs = 0.0;
+#pragma unroll
+            for (int e = 0; e < NE; ++e) vs += co[s2][e];
+            put(s2 * (1 + a.D), vs);
+            for (int d = 0; d < a.D; ++d) {
+                double tl = 0.0;
+#pragma unroll
+                for (int q = 0; q < TileCfg<NB>::NBLK; ++q)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const double df = xi[acc_row<NB>(q, r) * XS + d] - xj[acc_col<NB>(q) * XS + d];
+                        tl += co[s2][q * 4 + r] * df * df;
+                    }
+                put(s2 * (1 + a.D) + 1 + d, tl);
+            }
+        }
+        const int ro = (m + 1) * (1 + a.D);
+        for (int k2 = 0; k2 < m; ++k2) put(ro + k2, grho[k2]);
+        for (int k2 = 0; k2 < m * m; ++k2) put(ro + m + k2, grl[k2]);
+        put(G - 1, gn);
+        __syncthreads();
+        for (int qx = threadIdx.x; qx < G; qx += NTHREADS) {
+            double v = (red[qx] + red[RSTRIDE + qx]) + (red[2 * RSTRIDE + qx] + red[3 * RSTRIDE + qx]);
+            if (qx < ro) {
+                const int s2 = qx / (1 + a.D), d = qx % (1 + a.D);
+                if (d == 0) v /= gt.v(s2);
+                else { const double l = gt.l(s2, d - 1); v /= l * l * l; }
+            }
+            a.gpart[(long)qx * gridDim.x + blockIdx.x] = v;
+        }
+        return;
+    }
     // epilogue: contract with dK/dtheta recomputed from the inputs
     const double wscale = (i == j) ? 0.5 : 1.0;   // 1/2 * (2 for the mirrored tile)
     const double rho = th.rho();
@@ -485,11 +593,6 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
             grho += w * (hi * sj + si * hj) * kL;
             if (i == j && ri == cj && i * NB + ri < a.n) gnoise += w;
         }
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    auto put = [&](int qidx, double v) {
-        v = wave_sum(v);
-        if (lane == 0) red[wv * (2 * MAXD + 4) + qidx] = v;
-    };
     put(0, gvL);
     put(1 + a.D, gvD);
     put(2 + 2 * a.D, grho);
@@ -510,7 +613,7 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
     }
     __syncthreads();
     for (int qx = threadIdx.x; qx < G; qx += NTHREADS) {
-        const int st = 2 * MAXD + 4;
+        const int st = RSTRIDE;
         double v = (red[qx] + red[st + qx]) + (red[2 * st + qx] + red[3 * st + qx]);
         if (qx == 0) v /= th.vL();
         else if (qx <= a.D) { const double l = th.lL(qx - 1); v /= l * l * l; }
@@ -521,7 +624,7 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
 }
 
 size_t grad_smem_bytes(int nb) {
-    return sizeof(double) * (2 * (size_t)nb * (nb + 2) + 2 * (size_t)nb * XS + 2 * nb + 4 * (2 * MAXD + 4));
+    return sizeof(double) * (2 * (size_t)nb * (nb + 2) + 2 * (size_t)nb * XS + 2 * nb + 4 * RSTRIDE);
 }
 
 // ============================================================ K4: finalize (+Adam)
@@ -557,7 +660,7 @@ __global__ __launch_bounds__(NTHREADS) void k_reduce_items(FinArgs a) {
 
 // Stage 2: LML, gradient output and the optional Keras-Adam step (one wave).
 __global__ __launch_bounds__(64) void k_finalize(FinArgs a) {
-    const int G = theta_size(a.D);
+    const int G = a.G ? a.G : theta_size(a.D);
     const double* items = a.items;
     const double LOG2PI = 1.8378770664093453;
     double lml = -0.5 * items[0] - (double)a.P * items[1] - 0.5 * (double)a.n * (double)a.P * LOG2PI;
@@ -658,11 +761,23 @@ __global__ __launch_bounds__(NTHREADS) void k_pred_out(PredOutArgs a) {
 }
 
 // K_diag (linear.py:106-136)
-__global__ void k_kdiag(const double* X, long ldx, int n, int D, const double* theta, double* out) {
+__global__ void k_kdiag(const double* X, long ldx, int n, int D, const double* theta, double* out, int nlf) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const MFTheta th{theta, D};
     const double f = X[(long)i * ldx + D];
+    if (nlf) {   // graph.py:101-115 (no jitter on the diagonal here)
+        const GraphTheta th{theta, D, nlf};
+        const int s = graph_source(f, nlf);
+        double v = 0.0;
+        if (s >= 0 && s < nlf) v = th.v(s);
+        else if (s == nlf) {
+            for (int k = 0; k < nlf; ++k) v += th.v(k) * (th.rho(k) * th.rho(k));
+            v += th.v(nlf);
+        }
+        out[i] = v;
+        return;
+    }
+    const MFTheta th{theta, D};
     const double rho = th.rho();
     out[i] = (f == 0.0) ? th.vL() : ((f == 1.0) ? th.vL() * (rho * rho) + th.vD() : 0.0);
 }
@@ -701,7 +816,12 @@ void launch_alpha(const AlphaArgs& a, hipStream_t s) {
 }
 template <int NB>
 void launch_grad(const GradArgs& g, hipStream_t s) {
-    hipLaunchKernelGGL(k_grad<NB>, dim3(grad_tasks(g.T, g.chunk)), dim3(NTHREADS), grad_smem_bytes(NB), s, g);
+    if (g.nlf)
+        hipLaunchKernelGGL((k_grad<NB, true>), dim3(grad_tasks(g.T, g.chunk)), dim3(NTHREADS), grad_smem_bytes(NB), s,
+                           g);
+    else
+        hipLaunchKernelGGL((k_grad<NB, false>), dim3(grad_tasks(g.T, g.chunk)), dim3(NTHREADS), grad_smem_bytes(NB),
+                           s, g);
 }
 template <int NB>
 void launch_pred(const PredAArgs& pa, const PredOutArgs& po, int T, hipStream_t s) {

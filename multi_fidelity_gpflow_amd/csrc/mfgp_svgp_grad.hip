@@ -632,11 +632,16 @@ __global__ void k_adam_packed(int n, double* u, double* c, const double* g, doub
         double gc = 0.0;
         for (int j = 0; j < k; ++j) gc += g[q + j];
         const double gl = -gc;   // d loss / d c
-        const double gu = (tr == 0) ? gl : gl / (exp(-uq) + 1.0);
+        double gu;
+        if (tr == 0) gu = gl;
+        else if (tr == 3) {   // tfp Sigmoid: SigmoidGrad dy * y * (1 - y)
+            const double y = 1.0 / (1.0 + exp(-uq));
+            gu = gl * y * (1.0 - y);
+        } else gu = gl / (exp(-uq) + 1.0);   // Softplus: TF SoftplusGrad form
         const double mq = m[q] + (gu - m[q]) * (1.0 - b1);
         const double vq = v[q] + (gu * gu - v[q]) * (1.0 - b2);
         const double un = uq - (mq * alpha) / (sqrt(vq) + eps);
-        const double cn = (tr == 0) ? un : tf_softplus(un) + (tr == 2 ? 1e-6 : 0.0);
+        const double cn = (tr == 0) ? un : (tr == 3) ? 1.0 / (1.0 + exp(-un)) : tf_softplus(un) + (tr == 2 ? 1e-6 : 0.0);
         m[q] = mq;
         v[q] = vq;
         for (int j = 0; j < k; ++j) {

@@ -144,6 +144,50 @@ class Engine:
               "mfgp_gpr_predict")
         return mean, var, info
 
+    # ---- GraphMultiFidelityKernel (graph.py) with nlf LF sources
+    def gmf_gram(self, nlf, X1, X2, theta, diag_add=0.0):
+        n1, dp1 = X1.shape
+        n2 = X2.shape[0]
+        K = torch.empty((n1, n2), dtype=torch.float64, device=self.device)
+        check(self.lib.mfgp_gmf_gram(self.h, nlf, n1, n2, dp1 - 1, ptr(X1), dp1, ptr(X2), X2.shape[1], ptr(theta),
+                                     float(diag_add), ptr(K), n2), "mfgp_gmf_gram")
+        return K
+
+    def gmf_kdiag(self, nlf, X, theta):
+        n, dp1 = X.shape
+        out = torch.empty((n,), dtype=torch.float64, device=self.device)
+        check(self.lib.mfgp_gmf_kdiag(self.h, nlf, n, dp1 - 1, ptr(X), dp1, ptr(theta), ptr(out)), "mfgp_gmf_kdiag")
+        return out
+
+    def gmf_lml(self, nlf, X, Y, theta, want_grad=False, out=None, info=None):
+        n, dp1 = X.shape
+        p = Y.shape[1]
+        d = dp1 - 1
+        nbytes = self._size(self.lib.mfgp_gmf_gpr_workspace_size, nlf, n, p, d)
+        ws = self.workspace("gmf", nbytes)
+        if out is None:
+            out = torch.empty((1 + theta.numel(),), dtype=torch.float64, device=self.device)
+        if info is None:
+            info = torch.empty((1,), dtype=torch.int32, device=self.device)
+        check(self.lib.mfgp_gmf_gpr_lml(self.h, nlf, n, p, d, ptr(X), dp1, ptr(Y), p, ptr(theta), int(want_grad),
+                                        ptr(ws), ws.numel(), ptr(out), ptr(info)), "mfgp_gmf_gpr_lml")
+        return out, info
+
+    def gmf_predict(self, nlf, X, Y, Xs, theta):
+        n, dp1 = X.shape
+        p = Y.shape[1]
+        d = dp1 - 1
+        ns = Xs.shape[0]
+        nbytes = self._size(self.lib.mfgp_gmf_gpr_predict_workspace_size, nlf, n, p, d, ns)
+        ws = self.workspace("gmf_pred", nbytes)
+        mean = torch.empty((ns, p), dtype=torch.float64, device=self.device)
+        var = torch.empty((ns,), dtype=torch.float64, device=self.device)
+        info = torch.empty((1,), dtype=torch.int32, device=self.device)
+        check(self.lib.mfgp_gmf_gpr_predict(self.h, nlf, n, p, d, ns, ptr(X), dp1, ptr(Y), p, ptr(Xs), Xs.shape[1],
+                                            ptr(theta), ptr(ws), ws.numel(), ptr(mean), p, ptr(var), ptr(info)),
+              "mfgp_gmf_gpr_predict")
+        return mean, var, info
+
     def potrf_inv(self, A: torch.Tensor):
         """A: [n, n] or [b, n, n] SPD -> (Linv, diag(L), info[b])."""
         batched = A.dim() == 3

@@ -104,6 +104,63 @@ class LinearMultiFidelityKernel(Kernel):
         return as_result(eng.mf_kdiag(X1, self.theta(d, eng.device, ith_output_dim)))
 
 
+class GraphMultiFidelityKernel(Kernel):
+    """Graph-structured multi-fidelity kernel (mfgpflow/graph.py:7-115): m LF sources
+    (fidelity flags 0..m-1) and HF (flag m), f_H = sum_i rho_i f_Li + delta.
+
+    LF-LF block (i, j) = rho_LF[i, j] k_i (i != j; 1 on the diagonal) — the row source's
+    kernel, so K is not symmetric unless rho_LF is; LF-HF = rho_i k_i; HF-HF =
+    sum_i rho_i^2 k_i + k_delta; K(X, X2) carries the reference's 1e-6 I jitter
+    (graph.py:96), K_diag does not.  Only rho[:, 0] is used (ith_output_dim = 0).
+    """
+
+    JITTER = 1e-6
+
+    def __init__(self, kernel_Ls, kernel_delta, num_LF, num_output_dims):
+        from .params import Sigmoid
+        self.num_LF = int(num_LF)
+        self.kernel_Ls = list(kernel_Ls)
+        self.kernel_delta = kernel_delta
+        self.rho = Parameter(np.ones((self.num_LF, num_output_dims)), transform=positive())
+        self.rho_LF = Parameter(0.5 * np.ones((self.num_LF, self.num_LF)), transform=Sigmoid())
+
+    def theta_entries(self, d: int):
+        """(Parameter, index) for every theta entry of the include/mfgp.h graph layout (noise excluded)."""
+        ents = []
+        for k in self.kernel_Ls + [self.kernel_delta]:
+            ents.append((k.variance, None))
+            ents += [(k.lengthscales, None if k.lengthscales.shape == () else (i,)) for i in range(d)]
+        ents += [(self.rho, (i, 0)) for i in range(self.num_LF)]
+        ents += [(self.rho_LF, (i, j)) for i in range(self.num_LF) for j in range(self.num_LF)]
+        return ents
+
+    def theta_vector(self, d: int, noise: float = 0.0) -> np.ndarray:
+        vals = []
+        for prm, idx in self.theta_entries(d):
+            v = prm.numpy()
+            vals.append(float(v if idx is None else v[idx]))
+        return np.array(vals + [noise])
+
+    def K(self, X, X2=None, ith_output_dim=0):
+        eng = Engine.get()
+        X1 = to_dev(X, eng.device)
+        X2d = X1 if X2 is None else to_dev(X2, eng.device)
+        if X1.shape[0] != X2d.shape[0]:
+            # graph.py:96 adds tf.eye(n1) to an [n1, n2] matrix: the reference raises here
+            raise ValueError("GraphMultiFidelityKernel.K(X, X2) with len(X) != len(X2): the reference adds "
+                             "tf.eye(len(X)) to K and fails the same way")
+        d = X1.shape[1] - 1
+        th = torch.tensor(self.theta_vector(d), dtype=torch.float64, device=eng.device)
+        return as_result(eng.gmf_gram(self.num_LF, X1, X2d, th, diag_add=self.JITTER))
+
+    def K_diag(self, X, ith_output_dim=0):
+        eng = Engine.get()
+        X1 = to_dev(X, eng.device)
+        d = X1.shape[1] - 1
+        th = torch.tensor(self.theta_vector(d), dtype=torch.float64, device=eng.device)
+        return as_result(eng.gmf_kdiag(self.num_LF, X1, th))
+
+
 class Combination(Kernel):
     def __init__(self, kernels):
         self.kernels = list(kernels)

@@ -35,6 +35,23 @@ def tf_softplus_inverse(y):
     return np.where(small, np.log(np.where(small, y, 1.0)), np.where(large, y, val))
 
 
+class Sigmoid:
+    """tfp.bijectors.Sigmoid (graph.py:36 rho_LF): forward 1/(1+exp(-u)), inverse log(y) - log1p(-y)."""
+
+    lower = None
+
+    def forward(self, u):
+        return 1.0 / (1.0 + np.exp(-np.asarray(u, dtype=np.float64)))
+
+    def inverse(self, v):
+        v = np.asarray(v, dtype=np.float64)
+        return np.log(v) - np.log1p(-v)
+
+    def dforward(self, u):
+        y = self.forward(u)
+        return y * (1.0 - y)
+
+
 class Softplus:
     """tfp.bijectors.Softplus, optionally chained with Shift(lower)."""
 
@@ -48,6 +65,10 @@ class Softplus:
     def inverse(self, v):
         v = np.asarray(v, dtype=np.float64)
         return tf_softplus_inverse(v - self.lower if self.lower else v)
+
+    def dforward(self, u):
+        """TF SoftplusGrad form 1 / (exp(-u) + 1)."""
+        return 1.0 / (np.exp(-np.asarray(u, dtype=np.float64)) + 1.0)
 
     def forward_grad(self, u):
         return 1.0 / (np.exp(-np.asarray(u, dtype=np.float64)) + 1.0)
