@@ -160,6 +160,9 @@ def main():
     ap.add_argument("--tile", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-train-predict", action="store_true")
+    ap.add_argument("--mode", choices=["shard", "shared"], default="shard",
+                    help="shard: per-shard-theta bin blocks (no inner-loop collective); shared: one model, "
+                         "one all-reduce of 1+G doubles per step (reference-parity mode, SURVEY 8(e))")
     ap.add_argument("--config", choices=["goku", "synth"], default="goku",
                     help="goku: the BASELINE metric; synth: SURVEY §8(d) scale-up (N=18432, P=512, fp64)")
     args = ap.parse_args()
@@ -192,7 +195,12 @@ def main():
 
     model = make_model(X, Yr)
     K, W = args.steps, args.warmup
-    sess = model.adam_session(0.1, K + W, graph=True, graph_chunk=50 if args.config == "goku" else 2)
+    if args.mode == "shared":
+        from multi_fidelity_gpflow_amd.distributed import SharedThetaTrainer
+        sess = SharedThetaTrainer(model, 0.1, K + W)
+        sess.sync = torch.cuda.synchronize
+    else:
+        sess = model.adam_session(0.1, K + W, graph=True, graph_chunk=50 if args.config == "goku" else 2)
     sess.run(W)
     sess.sync()
     if world > 1:
@@ -233,7 +241,8 @@ def main():
         cpu = cpu_baseline(X, Y)
 
     if rank == 0:
-        value = world * K / dt
+        shared = args.mode == "shared"
+        value = (K if shared else world * K) / dt
         synth = args.config == "synth"
         line = {
             "metric": ("LML evals/sec (synthetic 16384LF/2048HF D=10 P=512, value+grad+Adam step)" if synth else
@@ -245,7 +254,7 @@ def main():
             "warmup": W,
             "ms_per_step": round(dt / K * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if shared else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": ("synthetic (SURVEY §8(d) recipe, seed 20251015), built on every rank" if synth else
@@ -253,7 +262,8 @@ def main():
             "config": {"workload": "synth_multibin_adam_step" if synth else "goku_multibin_adam_step",
                        "n_lf": int((X[:, -1] == 0).sum()), "n_hf": int((X[:, -1] == 1).sum()), "d": d, "p": P,
                        "bins_per_rank": Yr.shape[1], "tile": eng.tile(),
-                       "parallelism": f"bins{world}" if world > 1 else "single"},
+                       "parallelism": (f"bins{world}-shared-theta" if shared else f"bins{world}") if world > 1
+                       else "single", "mode": args.mode},
             "bin_throughput": round(P * K / dt, 2),
             "train_predict_s": None if tp is None else round(tp, 4),
             "step_tflops": round(step_flops(n, P, d) * value / 1e12, 4),

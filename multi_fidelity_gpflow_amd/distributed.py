@@ -1,11 +1,14 @@
 """Multi-GPU sharding of the multi-bin emulator over output k-bins.
 
 One process per GPU.  The P output bins are split into contiguous blocks, one per
-rank; every rank trains an independent multi-bin model (its own theta) on its
-block — the reference's shared Gram makes a bin only an extra right-hand side, so
-this is the "embarrassing" per-shard-theta mode.  Collectives happen only at the
-edges: ONE broadcast of the packed inputs from rank 0 before training and one
-gather of the posterior blocks after it; nothing inside the training loop.
+rank.  Two modes:
+  * per-shard theta (default, bench.py): every rank trains an independent multi-bin
+    model on its block — the reference's shared Gram makes a bin only an extra
+    right-hand side, so this is the "embarrassing" mode.  Collectives happen only at
+    the edges: ONE broadcast of the packed inputs from rank 0 before training and one
+    gather of the posterior blocks after it; nothing inside the training loop.
+  * shared theta (SharedThetaTrainer): one model, the reference's trajectory; one
+    all-reduce of 1 + G doubles per iteration.
 Backend "nccl" is RCCL over xGMI on ROCm; "gloo" is used for CPU tests.
 """
 from __future__ import annotations
@@ -72,3 +75,95 @@ def gather_bin_blocks(block: torch.Tensor, p: int, rank: int, world: int) -> tor
     parts = [torch.empty_like(padded) for _ in range(world)]
     dist.all_gather(parts, padded)
     return torch.cat([parts[r][:, :widths[r]] for r in range(world)], dim=1)
+
+
+class SharedThetaTrainer:
+    """Reference-parity multi-GPU training of ONE multi-bin model (SURVEY §8(e) shared-theta
+    mode).  Every rank holds the full X and its contiguous bin block of Y; per Adam
+    iteration it evaluates the block's LML and dLML/dtheta (the shared Gram / Cholesky is
+    replicated, the bins' solves are split), ONE all-reduce sums the 1 + G values over
+    ranks (the multi-bin LML is additive over output columns), and every rank applies the
+    same Keras-Adam step, so theta stays identical everywhere and the trajectory is the
+    single-model one of MultiFidelityGPModel.optimize(use_adam=True) (linear.py:200-214).
+
+    Device path: mfgp_gpr_lml(want_grad) -> dist.all_reduce (RCCL over xGMI) ->
+    mfgp_adam_packed.  The three hooks can be replaced (CPU rehearsal with gloo)."""
+
+    def __init__(self, model, lr, max_iters, lml_grad=None, allreduce=None, adam=None):
+        from .engine import Engine
+        self.model = model
+        self.max_iters = max(int(max_iters), 1)
+        tm = model._theta_map()
+        self.tm = tm
+        G = len(tm.entries)
+        u = tm.u()
+        trainable = tm.trainable().astype(np.uint8)
+        transform = np.ones(G, np.uint8)
+        transform[tm.noise_index] = 2
+        tie = tm.tie()
+        span = np.ones(G, np.uint8)
+        for q in range(G):
+            lead = int(np.argmax(tie == tie[q]))
+            if lead != q:
+                span[q] = 0
+                span[lead] += 1
+        self.done = 0
+        self.hist = []
+        if lml_grad is None:   # MI355X path
+            eng, X, Y = model._device_data()
+            dev = eng.device
+            f64 = dict(dtype=torch.float64, device=dev)
+            self.eng, self.X, self.Y = eng, X, Y
+            self.theta = torch.tensor(tm.theta(), **f64)
+            self.u = torch.tensor(u, **f64)
+            self.m = torch.zeros(G, **f64)
+            self.v = torch.zeros(G, **f64)
+            self.trainable = torch.tensor(trainable, device=dev)
+            self.transform = torch.tensor(transform, device=dev)
+            self.span = torch.tensor(span, device=dev)
+            self.step_t = torch.zeros((1,), dtype=torch.int32, device=dev)
+            self.lr = torch.full((self.max_iters,), float(np.float32(lr)), **f64)
+            self.hist_t = torch.zeros((self.max_iters,), **f64)
+            self.out = torch.zeros((1 + G,), **f64)
+            self.info = torch.zeros((1,), dtype=torch.int32, device=dev)
+            self.b1, self.b2 = float(np.float32(0.9)), float(np.float32(0.999))
+
+            def _lml_grad():
+                out, info = eng.gpr_lml(self.X, self.Y, self.theta, want_grad=True)
+                self.out.copy_(out)
+                self.info.copy_(info)
+                return self.out
+
+            def _adam(out):
+                eng.adam_packed(self.u, self.theta, out[1:], self.m, self.v, self.trainable, self.transform,
+                                self.span, self.step_t, self.lr, self.b1, self.b2, 1e-7, out, 1.0, self.hist_t,
+                                None)
+            self.lml_grad, self.adam = _lml_grad, _adam
+        else:
+            self.lml_grad, self.adam = lml_grad, adam
+        self.allreduce = allreduce or (lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM)
+                                       if dist.is_available() and dist.is_initialized() else None)
+
+    def step(self):
+        out = self.lml_grad()
+        self.allreduce(out)
+        self.adam(out)
+        self.done += 1
+
+    def run(self, n):
+        if self.done + n > self.max_iters:
+            raise ValueError("SharedThetaTrainer: more iterations than max_iters")
+        for _ in range(n):
+            self.step()
+
+    def finish(self):
+        """Write theta back into the model (device path) and its loss_history."""
+        from .models import CholeskyError
+        if not hasattr(self, "u"):
+            return
+        torch.cuda.synchronize()
+        self.tm.set_u(self.u.cpu().numpy())
+        h = self.hist_t[:self.done].cpu().numpy()
+        self.model.loss_history = [np.float64(v) for v in h]
+        if int(self.info.item()) != 0 or not np.all(np.isfinite(h)):
+            raise CholeskyError("shared-theta optimize: Cholesky failed")

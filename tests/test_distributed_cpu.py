@@ -60,3 +60,80 @@ def test_two_rank_bin_sharding(tmp_path, hbs):
     assert abs(r["lml"].sum() - full) < 1e-9 * abs(full)
     mean_full, _ = O.gpr_predict_f(hbs["X"], hbs["Y"], hbs["Xtest"], O.MFParams.initial(5, 49))
     np.testing.assert_allclose(r["mean"], mean_full, rtol=0, atol=1e-10)
+
+
+def _theta_flat(lml, g):
+    return np.concatenate([[lml, g["vL"]], g["lL"], [g["vD"]], g["lD"], [g["rho0"], g["noise"]]])
+
+
+def _shared_worker(rank, world, port, out_path, steps):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from multi_fidelity_gpflow_amd.distributed import SharedThetaTrainer, bin_block
+    from oracle import mfgp_oracle as O
+    d = O.load_powerspecs(HBS_DIR)
+    X, Y = d["X"], d["Y"]
+    D = X.shape[1] - 1
+    b0, b1 = bin_block(Y.shape[1], rank, world)
+    p0 = O.MFParams.initial(D, Y.shape[1])
+    st = {"u": O.pack_unconstrained(p0), "opt": O.AdamTF210(lr=0.1), "hist": []}
+
+    def lml_grad():   # the block's LML and dLML/dtheta at the shared theta (oracle compute)
+        lml, g = O.gpr_lml_and_grad(X, Y[:, b0:b1], O.unpack_unconstrained(st["u"], p0))
+        return torch.tensor(_theta_flat(lml, g), dtype=torch.float64)
+
+    def adam(out):    # identical on every rank: Keras Adam on the summed gradient
+        o = out.numpy()
+        st["hist"].append(-o[0])
+        g = {"vL": -o[1], "lL": -o[2:2 + D], "vD": -o[2 + D], "lD": -o[3 + D:3 + 2 * D], "rho0": -o[3 + 2 * D]}
+        st["u"] = st["opt"].step(st["u"], O.grad_unconstrained(st["u"], g))
+
+    class _TM:   # theta map stub (the device state is not used with injected hooks)
+        entries = list(range(2 * D + 4))
+        noise_index = 2 * D + 3
+
+        def u(self):
+            return np.zeros(2 * D + 4)
+
+        def trainable(self):
+            return np.ones(2 * D + 4, bool)
+
+        def tie(self):
+            return np.arange(2 * D + 4)
+
+    class _Model:
+        def _theta_map(self):
+            return _TM()
+
+    tr = SharedThetaTrainer(_Model(), 0.1, steps, lml_grad=lml_grad, adam=adam)
+    tr.run(steps)
+    if rank == 0:
+        np.save(out_path, np.array(st["hist"]))
+    dist.destroy_process_group()
+
+
+def _single_model_hist(d, steps):
+    from oracle import mfgp_oracle as O
+    p0 = O.MFParams.initial(5, 49)
+    u = O.pack_unconstrained(p0)
+    opt = O.AdamTF210(lr=0.1)
+    hist = []
+    for _ in range(steps):
+        lml, g = O.gpr_lml_and_grad(d["X"], d["Y"], O.unpack_unconstrained(u, p0))
+        hist.append(-lml)
+        u = opt.step(u, O.grad_unconstrained(u, {k: -np.asarray(v) for k, v in g.items()}))
+    return np.array(hist)
+
+
+def test_two_rank_shared_theta_matches_single_model(tmp_path):
+    """Shared-theta mode (SharedThetaTrainer): 2 ranks x half of the 49 HBS bins, one
+    all-reduce per iteration, reproduce the single-model Adam trajectory (oracle compute)."""
+    from oracle import mfgp_oracle as O
+    steps = 3
+    out = str(tmp_path / "h.npy")
+    mp.spawn(_shared_worker, args=(2, _free_port(), out, steps), nprocs=2, join=True)
+    hist = np.load(out)
+    np.testing.assert_allclose(hist, _single_model_hist(O.load_powerspecs(HBS_DIR), steps), rtol=1e-10)

@@ -269,3 +269,20 @@ def test_synthetic_scaleup_lml_vs_torch(n_lf, n_hf, p):
     ref = float(-0.5 * (Z * Z).sum() - Yd.shape[1] * torch.log(torch.diagonal(L)).sum()
                 - 0.5 * Yd.numel() * np.log(2 * np.pi))
     assert abs(lml - ref) < 1e-9 * abs(ref), (lml, ref)
+
+
+def test_shared_theta_trainer_matches_adam_session(hbs):
+    """distributed.SharedThetaTrainer's device path (LML+grad, all-reduce, packed Adam) on one
+    rank reproduces MultiFidelityGPModel.optimize(use_adam=True)'s trajectory."""
+    from multi_fidelity_gpflow_amd.distributed import SharedThetaTrainer
+    X, Y = hbs["X"], hbs["Y"]
+    mk = lambda: M.MultiFidelityGPModel(X, Y, M.SquaredExponential(lengthscales=np.ones(5)),
+                                        M.SquaredExponential(lengthscales=np.ones(5)))
+    a = mk()
+    a.optimize(max_iters=30, learning_rate=0.1, use_adam=True, verbose=False)
+    b = mk()
+    tr = SharedThetaTrainer(b, 0.1, 30)
+    tr.run(30)
+    tr.finish()
+    np.testing.assert_allclose(b.loss_history, a.loss_history, rtol=1e-11)
+    np.testing.assert_allclose(b.kernel.rho.numpy()[0], a.kernel.rho.numpy()[0], rtol=1e-11)
