@@ -92,27 +92,27 @@ def roofline(model, n, p, d, reps=10, pmc=True):
     eng, X, Y = model._device_data()
     theta = torch.tensor(model._theta_map().theta(), dtype=torch.float64, device=eng.device)
     gpr_phase_times(eng, X, Y, theta)   # warm
-    acc = np.zeros(6)
+    acc = np.zeros(5)
     for _ in range(reps):
         acc += np.array(gpr_phase_times(eng, X, Y, theta))
     ms = acc / reps
-    names = ["pre", "gram", "chol_steps", "alpha", "grad", "finalize"]
+    names = ["pre", "gram", "chol_steps", "grad", "finalize"]
     nb = eng.tile()
     T = -(-n // nb)
     # algorithmic work per phase (SURVEY §8(d) figures)
     flops = {
         "gram": (n * (n + 1) / 2) * (3 * d + 6),
-        "chol_steps": n ** 3 / 3 + n ** 3 / 3 + n * n * p,   # potrf + L^{-1} (trtri) + Z = L^{-1} Y
-        "alpha": n * n * p,
+        # potrf + L^{-1} (trtri) + Z = L^{-1} Y + alpha = L^{-T} Z (fused into the steps)
+        "chol_steps": n ** 3 / 3 + n ** 3 / 3 + n * n * p + n * n * p,
         "grad": n ** 3 / 3 + n * n * p + n * (n + 1) / 2 * (4 * d + 10),
     }
-    launches = {"gram": 1, "chol_steps": T, "alpha": 1, "grad": 1}
+    launches = {"gram": 1, "chol_steps": T, "grad": 1}
     dom = max(flops, key=lambda k: ms[names.index(k)])
     t_ms = ms[names.index(dom)]
     per_launch_ms = t_ms / launches[dom]
     per_launch_flop = flops[dom] / launches[dom]
     achieved = per_launch_flop / (per_launch_ms * 1e-3) / 1e12
-    kname = {"chol_steps": "k_chol_step", "gram": "k_gram", "alpha": "k_alpha", "grad": "k_grad"}[dom]
+    kname = {"chol_steps": "k_chol_step", "gram": "k_gram", "grad": "k_grad"}[dom]
     traffic, tsrc = pmc_traffic(kname, nb) if pmc else (None, None)
     return {
         "kernel": kname,

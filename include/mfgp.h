@@ -91,8 +91,8 @@ int mfgp_gpr_adam_step(mfgp_handle_t h, int n, int p, int d, const double* X, in
 
 /* Diagnostic: the mfgp_gpr_lml(want_grad=1) sequence with hipEvents recorded on
  * the handle's stream between its phases; synchronises and writes the elapsed
- * milliseconds of [pre (empty), gram+R init+first factor, tile Cholesky steps, alpha,
- * gradient, finalize] into the HOST array ms[6]. */
+ * milliseconds of [pre (empty), gram+R init+first factor, tile Cholesky steps (with
+ * alpha = L^{-T} Z fused in), gradient, reductions+finalize] into the HOST array ms[5]. */
 int mfgp_gpr_lml_phase_times(mfgp_handle_t h, int n, int p, int d, const double* X, int ldx, const double* Y,
                              int ldy, const double* theta, void* ws, size_t ws_bytes, double* out, int* info,
                              float* ms);

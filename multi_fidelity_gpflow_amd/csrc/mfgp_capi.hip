@@ -40,7 +40,9 @@ struct Carve {
 
 struct GprLayout {
     int nb, npad, T, ppad, Tp, G, gstride, ng;
-    double *A, *R, *Xo, *Dd, *ldiag, *alpha, *zpart, *gpart, *apart, *items;
+    double *A, *R, *Xo, *Dd, *ldiag, *alpha, *zpart, *gpart, *items;
+    int* cnt;   // reduce-arrival counter, zeroed by k_gram each call
+    int ncnt;
     size_t bytes;
 };
 
@@ -64,8 +66,9 @@ static GprLayout gpr_layout(int nb, int n, int p, int d, void* ws, int grad_chun
     L.alpha = c.take<double>((size_t)L.npad * L.ppad);
     L.zpart = c.take<double>((size_t)L.T * L.Tp);
     L.gpart = c.take<double>((size_t)L.ng * L.gstride);
-    L.apart = c.take<double>((size_t)((L.T + 3) / 4) * L.npad * L.ppad);
     L.items = c.take<double>((size_t)L.G + 8);
+    L.ncnt = 1;
+    L.cnt = c.take<int>((size_t)L.ncnt);
     L.bytes = c.off + 256;
     return L;
 }
@@ -120,6 +123,7 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
         g.out = L.A; g.ldo = L.npad; g.so = 0;
         g.padded = 1; g.npad = L.npad; g.tiles_c = L.T; g.add_noise = 1; g.diag_add = nlf ? GRAPH_JITTER : 0.0;
         g.Dd = L.Dd; g.sD = 0; g.ldiag = L.ldiag; g.sL = 0; g.info = info; g.nlf = nlf;
+        g.cnt = L.cnt; g.ncnt = L.ncnt;
         launch_gram<NB>(g, L.T * (L.T + 1) / 2, 1, s);
     }
     if (pm) pm->mark(s);
@@ -130,11 +134,9 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
         c.Xo = L.Xo; c.ldx = ldr; c.sX = 0;
         c.Dd = L.Dd; c.sD = 0; c.ldiag = L.ldiag; c.sL = 0; c.info = info;
         c.T = L.T; c.Tp = L.Tp; c.k = 0;
+        c.alpha = L.alpha; c.ldal = L.ppad; c.zpart = L.zpart; c.n = n; c.p = p;
         launch_chol_steps<NB>(c, 1, s);
     }
-    if (pm) pm->mark(s);
-    AlphaArgs aa{L.Xo, ldr, L.alpha, (long)L.ppad, L.zpart, L.T, L.Tp, n, p, L.apart, L.npad};
-    launch_alpha<NB>(aa, s);
     if (pm) pm->mark(s);
     if (want_grad) {
         GradArgs ga{L.Xo, ldr, L.alpha, (long)L.ppad, X, (long)ldx, theta, L.gpart, L.gstride, L.T, L.Tp, n, p, d,
@@ -152,8 +154,8 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
     f.adam = adam != nullptr;
     f.items = L.items;
     f.G = L.G;
+    f.cnt = L.cnt;
     hipLaunchKernelGGL(k_reduce_items, dim3(2 + (want_grad ? L.G : 0)), dim3(NTHREADS), 0, s, f);
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, f);
     if (pm) pm->mark(s);
     return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;
 }
@@ -535,7 +537,7 @@ int mfgp_gpr_lml_phase_times(mfgp_handle_t h, int n, int p, int d, const double*
     CHECK_D(d);
     if (n < 1 || p < 1 || !X || !Y || !theta || !ws || !out || !info || !ms) return MFGP_ERR_ARG;
     PhaseMarks pm;
-    for (int i = 0; i < 7; ++i) (void)hipEventCreate(&pm.ev[i]);
+    for (int i = 0; i < 6; ++i) (void)hipEventCreate(&pm.ev[i]);
     int rc = (h->nb == 64)
                  ? gpr_value_grad<64>(h, n, p, d, X, ldx, Y, ldy, (double*)theta, 1, ws, ws_bytes, out, info,
                                       nullptr, &pm)
@@ -545,7 +547,7 @@ int mfgp_gpr_lml_phase_times(mfgp_handle_t h, int n, int p, int d, const double*
         (void)hipEventSynchronize(pm.ev[pm.count - 1]);
         for (int i = 0; i + 1 < pm.count; ++i) (void)hipEventElapsedTime(&ms[i], pm.ev[i], pm.ev[i + 1]);
     }
-    for (int i = 0; i < 7; ++i) (void)hipEventDestroy(pm.ev[i]);
+    for (int i = 0; i < 6; ++i) (void)hipEventDestroy(pm.ev[i]);
     return rc;
 }
 

@@ -71,6 +71,30 @@ __device__ __forceinline__ void acc_store(const Acc<NB>& a, double* __restrict__
 #pragma unroll
         for (int r = 0; r < 4; ++r) g[(long)acc_row<NB>(q, r) * ld + acc_col<NB>(q)] = a.v[q][r];
 }
+// ---- cross-workgroup hand-off without L2 flushes.  gfx950 has one L2 per XCD, so an
+// agent-scope fence (__threadfence) writes back / invalidates the whole L2
+// (buffer_wbl2 / buffer_inv sc1, microseconds).  Data that another workgroup reads in
+// the same launch is instead stored and loaded as agent-scope relaxed atomics
+// (global_store / global_load ... sc1: coherent at the device level); a producer drains
+// its stores (s_waitcnt 0) before the workgroup barrier and the counter atomic.
+__device__ __forceinline__ void st_coherent(double* p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_coherent(const double* p) {
+    return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void drain_stores() { __builtin_amdgcn_s_waitcnt(0); }
+// Call after drain_stores() + __syncthreads(); thread 0 only.  Returns the old count.
+__device__ __forceinline__ int arrive(int* c) {
+    return __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <int NB>
+__device__ __forceinline__ void acc_store_coherent(const Acc<NB>& a, double* __restrict__ g, long ld) {
+#pragma unroll
+    for (int q = 0; q < TileCfg<NB>::NBLK; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) st_coherent(g + (long)acc_row<NB>(q, r) * ld + acc_col<NB>(q), a.v[q][r]);
+}
 template <int NB>
 __device__ __forceinline__ void acc_to_lds(const Acc<NB>& a, double* __restrict__ s) {
     constexpr int S = TileCfg<NB>::S;

@@ -22,6 +22,7 @@ struct GramArgs {
     // fused RHS init (LML layout only; R == nullptr: skip): R = [I | Y]
     double* R; long ldr; long sR; const double* Y; long ldy; long sY; int p, ppad;
     int nlf;                                  // 0: LinearMultiFidelityKernel; m >= 1: graph kernel, m LF sources
+    int* cnt; int ncnt;                       // arrival counters zeroed by workgroup 0 (alpha / reduce merge)
 };
 
 struct CholArgs {
@@ -32,16 +33,13 @@ struct CholArgs {
     double* ldiag; long sL;              // diag(L)
     int* info;
     int T, Tp, k;
+    // Optional (batch 1, LML path): alpha = L^{-T} Z accumulated row by row as rows of
+    // [L^{-1} | Z] become final, and the sum Z^2 partials.  nullptr: skipped.
+    double* alpha; long ldal;            // Npad x Ppad
+    double* zpart;                       // [T*Tp]
+    int n, p;
 };
 
-struct AlphaArgs {
-    const double* Xo; long ldx;           // [L^{-1} | Z]
-    double* alpha; long lda;              // Npad x Ppad
-    double* zpart;                        // T*Tp partial sums of Z^2 (valid region)
-    int T, Tp, n, p;
-    double* apart;                        // [chunk][Npad x Ppad] partial products
-    int npad;
-};
 
 struct GradArgs {
     const double* Xo; long ldx;           // [L^{-1} | Z]
@@ -73,6 +71,7 @@ struct FinArgs {
     int noise_index;                  // theta entry using Shift(1e-6) o Softplus
     double* items;                    // [2 + G] stage-1 reduction results
     int G;                            // theta entries (kernel_theta_size)
+    int* cnt;                         // arrival counter (zero on entry): last item workgroup finalizes
 };
 
 struct PredAArgs {
@@ -96,20 +95,17 @@ constexpr int MAXD_HOST = 32;
 size_t gram_smem_bytes(int nb);
 size_t chol_smem_bytes(int nb);
 size_t grad_smem_bytes(int nb);
-int chol_step_blocks(int T, int Tp, int k);
+int chol_step_blocks(int T, int Tp, int k, bool alpha = false);
 int grad_tasks(int T, int chunk);
-int alpha_tasks(int T, int Tp);
 
 
 template <int NB> void launch_gram(const GramArgs& g, int nblocks, int batch, hipStream_t s);
 template <int NB> void launch_chol_steps(CholArgs c, int batch, hipStream_t s);
-template <int NB> void launch_alpha(const AlphaArgs& a, hipStream_t s);
 template <int NB> void launch_grad(const GradArgs& g, hipStream_t s);
 template <int NB> void launch_pred(const PredAArgs& pa, const PredOutArgs& po, int T, hipStream_t s);
 
 __global__ void k_rhs_init(double* R, long ldr, long sR, int npad, int ppad, const double* Y, long ldy, long sY,
                            int n, int p);
-__global__ void k_finalize(FinArgs a);
 __global__ void k_reduce_items(FinArgs a);
 __global__ void k_theta_from_u(const double* u, double* theta, int G, int noise_index);
 __global__ void k_kdiag(const double* X, long ldx, int n, int D, const double* theta, double* out, int nlf);

@@ -3,11 +3,11 @@
 //   K1  k_gram            per-fidelity RBF distance + rho-scaled block assembly
 //                         (mfgpflow/linear.py:55-104, GPflow SquaredExponential.K)
 //   K2  k_chol_step       right-looking tile Cholesky fused with the inverse
-//                         factor L^{-1} and the forward solve Z = L^{-1} Y
-//   K3  k_alpha           alpha = L^{-T} Z  (+ sum Z^2 partials for the LML)
+//                         factor L^{-1}, the forward solve Z = L^{-1} Y and, as rows
+//                         become final, alpha = L^{-T} Z and the sum Z^2 partials
 //   K5  k_grad            W = alpha alpha^T - P K^{-1} contracted with dK/dtheta,
 //                         K^{-1} = L^{-T} L^{-1} formed tile-by-tile, never stored
-//   K4  k_finalize        LML reduction, gradient reduction, optional Adam step
+//   K4  k_reduce_items    LML / gradient reductions; the last workgroup finalizes (+Adam)
 //   K6  k_pred_a / k_pred_out   posterior mean / variance (GPflow base_conditional)
 //
 // Every kernel runs 256-thread workgroups on NB x NB fp64 tiles; tile products
@@ -21,7 +21,6 @@ constexpr int MAXD = 32;
 constexpr int XS = MAXD + 1;
 constexpr int RSTRIDE = 192;   // per-wave gradient slots (>= kernel_theta_size for MAXD, MFGP_MAX_LF)   // LDS row stride of staged inputs: odd, so a wave reading one
                                 // dimension of 16-32 different rows hits distinct banks
-constexpr int ALPHA_CH = 4;   // m-tiles per alpha task
 
 // ============================================================ K1: gram
 
@@ -98,6 +97,8 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
                                                    // would shift the dynamic base off 16 B (G17)
 
     const int b = blockIdx.z;
+    if (a.cnt && blockIdx.x == 0 && b == 0)
+        for (int e = threadIdx.x; e < a.ncnt; e += NTHREADS) a.cnt[e] = 0;
     int ti, tj;
     if (a.padded) {   // lower tiles: t -> (ti, tj), ti >= tj
         const int t = blockIdx.x;
@@ -189,6 +190,23 @@ __device__ __forceinline__ void tri_decode(int t, int& i, int& j) {
     while (r * (r + 1) / 2 > t) --r;
     i = r;
     j = t - r * (r + 1) / 2;
+}
+
+// zpart[k*Tp + cy] = sum of Z_k^2 over the valid (n x p) region of Y tile cy; Xs holds
+// Z_k tile cy in LDS, visible to the whole workgroup.  red: >= 4 doubles of LDS.
+template <int NB>
+__device__ void chol_zpart(const CholArgs& a, int k, int cy, const double* Xs, double* red) {
+    constexpr int S = TileCfg<NB>::S;
+    double z2 = 0.0;
+    for (int e = threadIdx.x; e < NB * NB; e += NTHREADS) {
+        const int r = e / NB, col = e % NB;
+        if (k * NB + r < a.n && cy * NB + col < a.p) {
+            const double z = Xs[r * S + col];
+            z2 += z * z;
+        }
+    }
+    z2 = block_sum(z2, red);
+    if (threadIdx.x == 0) a.zpart[k * a.Tp + cy] = z2;
 }
 
 template <int NB>
@@ -288,9 +306,39 @@ __global__ __launch_bounds__(NTHREADS) void k_chol_step(CholArgs a) {
         acc = ric;
         tile_mma<NB, false, false>(acc, Pi, Pj, -1.0);
         acc_store(acc, Rt(i, c), ldr);
+        if (a.alpha && i == k + 1 && c >= T) chol_zpart<NB>(a, k, c - T, Pj, dg);
         return;
     }
     t -= nR;
+    if (a.alpha) {
+        // ---- alpha_c (+)= X_kc^T Z_k for c <= k: row k of [L^{-1} | Z] is final in this
+        // launch (X = D_k R_k).  alpha_c is first written at k == c, then accumulated in
+        // launch order -- replaces a separate alpha = L^{-T} Z pass.
+        const int nAl = (k + 1) * Tp;
+        if (t < nAl) {
+            const int c = t / Tp, cy = t % Tp;
+            double* al = a.alpha + (long)c * NB * a.ldal + (long)cy * NB;
+            tile_load<NB>(T0, Rt(k, c), ldr);
+            tile_load<NB>(Pi, Rt(k, T + cy), ldr);
+            Acc<NB> acc;
+            if (c == k) acc_zero(acc);
+            else acc_load(acc, al, a.ldal);
+            __syncthreads();
+            Acc<NB> x, z;
+            acc_zero(x);
+            tile_mma<NB, false, false>(x, Ds, T0, 1.0);   // X_kc
+            acc_zero(z);
+            tile_mma<NB, false, false>(z, Ds, Pi, 1.0);   // Z_k (tile cy)
+            __syncthreads();
+            acc_to_lds(x, Pj);
+            acc_to_lds(z, T0);
+            __syncthreads();
+            tile_mma<NB, true, false>(acc, Pj, T0, 1.0);
+            acc_store(acc, al, a.ldal);
+            return;
+        }
+        t -= nAl;
+    }
     // ---- last step writers: X_{T-1,c} = D_{T-1} R_{T-1,c}
     {
         const int c = t;   // 0..T-1 identity tiles, T..T+Tp-1 Y tiles
@@ -300,12 +348,17 @@ __global__ __launch_bounds__(NTHREADS) void k_chol_step(CholArgs a) {
         acc_zero(acc);
         tile_mma<NB, false, false>(acc, Ds, T0, 1.0);
         acc_store(acc, Xt(k, c), ldx);
+        if (a.alpha && c >= T) {
+            acc_to_lds(acc, Pj);
+            __syncthreads();
+            chol_zpart<NB>(a, k, c - T, Pj, dg);
+        }
     }
 }
 
-int chol_step_blocks(int T, int Tp, int k) {
+int chol_step_blocks(int T, int Tp, int k, bool alpha) {
     const int rem = T - k - 1;
-    return rem * (rem + 1) / 2 + rem * (k + 1 + Tp) + ((k == T - 1) ? (T + Tp) : 0);
+    return rem * (rem + 1) / 2 + rem * (k + 1 + Tp) + (alpha ? (k + 1) * Tp : 0) + ((k == T - 1) ? (T + Tp) : 0);
 }
 
 size_t chol_smem_bytes(int nb) { return sizeof(double) * (4 * (size_t)nb * (nb + 2) + nb + 2); }
@@ -324,74 +377,6 @@ __global__ void k_rhs_init(double* R, long ldr, long sR, int npad, int ppad, con
             v = (Y != nullptr && r < n && pc < p) ? Y[b * sY + (long)r * ldy + pc] : 0.0;
         }
         R[b * sR + (long)r * ldr + c] = v;
-    }
-}
-
-// ============================================================ K3: alpha = L^{-T} Z
-
-__host__ __device__ inline int alpha_row_chunks(int T, int i) { return (T - i + ALPHA_CH - 1) / ALPHA_CH; }
-
-int alpha_tasks(int T, int Tp) {
-    int s = 0;
-    for (int i = 0; i < T; ++i) s += Tp * alpha_row_chunks(T, i);
-    return s;
-}
-
-// alpha_i = sum_{m >= i} Linv_mi^T Z_m, split over m-chunks of ALPHA_CH tiles; each
-// task writes its partial product into slab[ch]; k_alpha_reduce sums the slabs.
-template <int NB>
-__global__ __launch_bounds__(NTHREADS) void k_alpha(AlphaArgs a) {
-    constexpr int S = TileCfg<NB>::S;
-    constexpr int E = TileCfg<NB>::ELEMS;
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    double* Ls = smem;
-    double* Zs = Ls + E;
-    double* red = Zs + E;
-    int t = blockIdx.x, i = 0;
-    for (;; ++i) {
-        const int cnt = a.Tp * alpha_row_chunks(a.T, i);
-        if (t < cnt) break;
-        t -= cnt;
-    }
-    const int nch = alpha_row_chunks(a.T, i);
-    const int cy = t / nch, ch = t % nch;
-    const int m0 = i + ch * ALPHA_CH, m1 = min(a.T, m0 + ALPHA_CH);
-    auto Xt = [&](int r, int c) { return a.Xo + (long)r * NB * a.ldx + (long)c * NB; };
-    Acc<NB> acc;
-    acc_zero(acc);
-    double z2 = 0.0;
-    for (int m = m0; m < m1; ++m) {
-        tile_load<NB>(Ls, Xt(m, i), a.ldx);
-        tile_load<NB>(Zs, Xt(m, a.T + cy), a.ldx);
-        __syncthreads();
-        if (m == i) {   // sum of squares of Z_i (rows < n, cols < p)
-            for (int e = threadIdx.x; e < NB * NB; e += NTHREADS) {
-                const int r = e / NB, c = e % NB;
-                if (i * NB + r < a.n && cy * NB + c < a.p) {
-                    const double z = Zs[r * S + c];
-                    z2 += z * z;
-                }
-            }
-        }
-        tile_mma<NB, true, false>(acc, Ls, Zs, 1.0);
-        __syncthreads();
-    }
-    const long slab = (long)a.npad * a.lda;
-    acc_store(acc, a.apart + ch * slab + (long)i * NB * a.lda + (long)cy * NB, a.lda);
-    if (ch == 0) {
-        z2 = block_sum(z2, red);
-        if (threadIdx.x == 0) a.zpart[i * a.Tp + cy] = z2;
-    }
-}
-
-__global__ void k_alpha_reduce(AlphaArgs a, int NB) {
-    const long total = (long)a.npad * a.lda;
-    for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-        const int r = (int)(e / a.lda);
-        const int nch = alpha_row_chunks(a.T, r / NB);
-        double s = 0.0;
-        for (int ch = 0; ch < nch; ++ch) s += a.apart[ch * total + e];
-        a.alpha[e] = s;
     }
 }
 
@@ -630,6 +615,48 @@ size_t grad_smem_bytes(int nb) {
 // ============================================================ K4: finalize (+Adam)
 
 
+// Stage 2: LML, gradient output and the optional Keras-Adam step; run by the last
+// item workgroup of k_reduce_items to arrive.
+__device__ void finalize_body(const FinArgs& a) {
+    const int G = a.G ? a.G : theta_size(a.D);
+    const double* items = a.items;
+    const double LOG2PI = 1.8378770664093453;
+    double lml = -0.5 * ld_coherent(items) - (double)a.P * ld_coherent(items + 1) - 0.5 * (double)a.n * (double)a.P * LOG2PI;
+    if (a.info[0] != 0) lml = NAN;
+    if (threadIdx.x == 0) a.out[0] = lml;
+    if (a.want_grad)
+        for (int q = threadIdx.x; q < G; q += NTHREADS) a.out[1 + q] = ld_coherent(items + 2 + q);
+    if (!a.adam) return;
+    const double* gsh = items + 2;
+    const int s = *a.step;
+    if (threadIdx.x == 0) a.loss_hist[s] = -lml;
+    if (a.info[0] != 0) return;   // non-PD: leave parameters untouched (host raises)
+    const double t = (double)(s + 1);
+    const double alpha = a.lr * sqrt(1.0 - pow(a.b2, t)) / (1.0 - pow(a.b1, t));
+    for (int q = threadIdx.x; q < G; q += NTHREADS) {
+        if (a.trainable[q]) {
+            const double uq = a.u[q];
+            double gc = ld_coherent(gsh + q);
+            if (a.tie) {   // a variable shared by several theta entries gets the summed gradient
+                gc = 0.0;
+                for (int r = 0; r < G; ++r)
+                    if (a.tie[r] == a.tie[q]) gc += ld_coherent(gsh + r);
+            }
+            const double g = (-gc) / (exp(-uq) + 1.0);   // loss = -lml; TF SoftplusGrad form
+            double mq = a.m[q], vq = a.v[q];
+            mq += (g - mq) * (1.0 - a.b1);
+            vq += (g * g - vq) * (1.0 - a.b2);
+            const double un = uq - (mq * alpha) / (sqrt(vq) + a.eps);
+            a.m[q] = mq;
+            a.v[q] = vq;
+            a.u[q] = un;
+            a.theta[q] = tf_softplus(un) + (q == a.noise_index ? 1e-6 : 0.0);
+        }
+    }
+    __syncthreads();   // every wave has read *a.step
+    if (threadIdx.x == 0) *a.step = s + 1;
+}
+
 // Stage 1 of the step reduction: workgroup `it` sums item `it` of
 // [sum Z^2, sum log L_ii, grad_0 .. grad_{G-1}] (partials stored [item][task]) with
 // all 256 threads in flight at once; deterministic order.
@@ -655,48 +682,17 @@ __global__ __launch_bounds__(NTHREADS) void k_reduce_items(FinArgs a) {
         s = (s + s1) + (s2 + s3);
     }
     s = block_sum(s, red);
-    if (threadIdx.x == 0) a.items[it] = s;
+    __shared__ int last;
+    if (threadIdx.x == 0) {
+        st_coherent(a.items + it, s);
+        drain_stores();
+        last = arrive(a.cnt) == (int)gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    finalize_body(a);
 }
 
-// Stage 2: LML, gradient output and the optional Keras-Adam step (one wave).
-__global__ __launch_bounds__(64) void k_finalize(FinArgs a) {
-    const int G = a.G ? a.G : theta_size(a.D);
-    const double* items = a.items;
-    const double LOG2PI = 1.8378770664093453;
-    double lml = -0.5 * items[0] - (double)a.P * items[1] - 0.5 * (double)a.n * (double)a.P * LOG2PI;
-    if (a.info[0] != 0) lml = NAN;
-    if (threadIdx.x == 0) a.out[0] = lml;
-    if (a.want_grad)
-        for (int q = threadIdx.x; q < G; q += 64) a.out[1 + q] = items[2 + q];
-    if (!a.adam) return;
-    const double* gsh = items + 2;
-    const int s = *a.step;
-    if (threadIdx.x == 0) a.loss_hist[s] = -lml;
-    if (a.info[0] != 0) return;   // non-PD: leave parameters untouched (host raises)
-    const double t = (double)(s + 1);
-    const double alpha = a.lr * sqrt(1.0 - pow(a.b2, t)) / (1.0 - pow(a.b1, t));
-    for (int q = threadIdx.x; q < G; q += 64) {
-        if (a.trainable[q]) {
-            const double uq = a.u[q];
-            double gc = gsh[q];
-            if (a.tie) {   // a variable shared by several theta entries gets the summed gradient
-                gc = 0.0;
-                for (int r = 0; r < G; ++r)
-                    if (a.tie[r] == a.tie[q]) gc += gsh[r];
-            }
-            const double g = (-gc) / (exp(-uq) + 1.0);   // loss = -lml; TF SoftplusGrad form
-            double mq = a.m[q], vq = a.v[q];
-            mq += (g - mq) * (1.0 - a.b1);
-            vq += (g * g - vq) * (1.0 - a.b2);
-            const double un = uq - (mq * alpha) / (sqrt(vq) + a.eps);
-            a.m[q] = mq;
-            a.v[q] = vq;
-            a.u[q] = un;
-            a.theta[q] = tf_softplus(un) + (q == a.noise_index ? 1e-6 : 0.0);
-        }
-    }
-    if (threadIdx.x == 0) *a.step = s + 1;
-}
 
 __global__ void k_theta_from_u(const double* u, double* theta, int G, int noise_index) {
     const int q = threadIdx.x;
@@ -800,19 +796,13 @@ void launch_gram(const GramArgs& g, int nblocks, int batch, hipStream_t s) {
 }
 template <int NB>
 void launch_chol_steps(CholArgs c, int batch, hipStream_t s) {
+    if (batch != 1) c.alpha = nullptr;   // fused alpha: single system only
     for (int k = 0; k < c.T; ++k) {
         c.k = k;
-        const int nb = chol_step_blocks(c.T, c.Tp, k);
+        const int nb = chol_step_blocks(c.T, c.Tp, k, c.alpha != nullptr);
         if (nb > 0)
             hipLaunchKernelGGL(k_chol_step<NB>, dim3(nb, 1, batch), dim3(NTHREADS), chol_smem_bytes(NB), s, c);
     }
-}
-template <int NB>
-void launch_alpha(const AlphaArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_alpha<NB>, dim3(alpha_tasks(a.T, a.Tp)), dim3(NTHREADS),
-                       sizeof(double) * (2 * NB * (NB + 2) + 4), s, a);
-    const long total = (long)a.npad * a.lda;
-    hipLaunchKernelGGL(k_alpha_reduce, dim3((int)std::min<long>((total + 255) / 256, 1024)), dim3(256), 0, s, a, NB);
 }
 template <int NB>
 void launch_grad(const GradArgs& g, hipStream_t s) {
@@ -834,8 +824,6 @@ template void launch_gram<32>(const GramArgs&, int, int, hipStream_t);
 template void launch_gram<64>(const GramArgs&, int, int, hipStream_t);
 template void launch_chol_steps<32>(CholArgs, int, hipStream_t);
 template void launch_chol_steps<64>(CholArgs, int, hipStream_t);
-template void launch_alpha<32>(const AlphaArgs&, hipStream_t);
-template void launch_alpha<64>(const AlphaArgs&, hipStream_t);
 template void launch_grad<32>(const GradArgs&, hipStream_t);
 template void launch_grad<64>(const GradArgs&, hipStream_t);
 template void launch_pred<32>(const PredAArgs&, const PredOutArgs&, int, hipStream_t);

@@ -289,7 +289,7 @@ class AdamState:
 
 def gpr_phase_times(eng: Engine, X, Y, theta):
     """Per-phase device times (ms) of one value+grad evaluation, measured with
-    hipEvents on the launch stream: [rhs_init, gram, chol_steps, alpha, grad, finalize]."""
+    hipEvents on the launch stream: [pre, gram, chol_steps (+alpha), grad, finalize]."""
     n, dp1 = X.shape
     p = Y.shape[1]
     d = dp1 - 1
@@ -297,7 +297,7 @@ def gpr_phase_times(eng: Engine, X, Y, theta):
     ws = eng.workspace("gpr", nbytes)
     out = torch.empty((1 + theta_size(d),), dtype=torch.float64, device=eng.device)
     info = torch.empty((1,), dtype=torch.int32, device=eng.device)
-    ms = (C.c_float * 6)()
+    ms = (C.c_float * 5)()
     check(eng.lib.mfgp_gpr_lml_phase_times(eng.h, n, p, d, ptr(X), dp1, ptr(Y), p, ptr(theta), ptr(ws), ws.numel(),
                                            ptr(out), ptr(info), ms), "mfgp_gpr_lml_phase_times")
     return [float(v) for v in ms]
