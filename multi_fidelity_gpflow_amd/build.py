@@ -27,14 +27,14 @@ def needs_rebuild() -> bool:
     return any(os.path.getmtime(p) > t for p in deps if os.path.exists(p))
 
 
-def build_lib(force: bool = False, extra_flags=None, out: str = OUT) -> str:
+def build_lib(force: bool = False, extra_flags=None, out: str = OUT, csrc: str = CSRC) -> str:
     if not force and out == OUT and not needs_rebuild():
         return out
     cmd = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-I" + os.path.join(ROOT, "include"), "-Wno-unused-result"]
     cmd += list(extra_flags or [])
-    cmd += [os.path.join(CSRC, s) for s in SOURCES] + ["-o", out]
-    r = subprocess.run(cmd, cwd=CSRC, capture_output=True, text=True)
+    cmd += [os.path.join(csrc, s) for s in SOURCES] + ["-o", out]
+    r = subprocess.run(cmd, cwd=csrc, capture_output=True, text=True)
     if r.returncode != 0:
         sys.stderr.write(r.stdout + r.stderr)
         raise RuntimeError("hipcc build of libmfgp.so failed")

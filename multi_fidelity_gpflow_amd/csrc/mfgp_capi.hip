@@ -60,7 +60,7 @@ static GprLayout gpr_layout(int nb, int n, int p, int d, void* ws, int grad_chun
     const size_t ldr = (size_t)L.npad + L.ppad;
     L.A = c.take<double>((size_t)L.npad * L.npad);
     L.R = c.take<double>((size_t)L.npad * ldr);
-    L.Xo = c.take<double>((size_t)L.npad * ldr);
+    L.Xo = c.take<double>((size_t)(L.npad + 2 * L.ppad) * ldr);   // + alpha^T rows (k_grad)
     L.Dd = c.take<double>((size_t)L.T * nb * nb);
     L.ldiag = c.take<double>(L.npad);
     L.alpha = c.take<double>((size_t)L.npad * L.ppad);
@@ -139,7 +139,7 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
     }
     if (pm) pm->mark(s);
     if (want_grad) {
-        GradArgs ga{L.Xo, ldr, L.alpha, (long)L.ppad, X, (long)ldx, theta, L.gpart, L.gstride, L.T, L.Tp, n, p, d,
+        GradArgs ga{L.Xo, ldr, X, (long)ldx, theta, L.gpart, L.gstride, L.T, L.Tp, n, p, d,
                     h->grad_chunk, nlf};
         launch_grad<NB>(ga, s);
     }

@@ -117,6 +117,34 @@ __device__ __forceinline__ void tile_load(double* __restrict__ s, const double* 
         *reinterpret_cast<double2*>(s + r * S + c) = v;
     }
 }
+// Split tile_load for software pipelining: fetch (global -> registers, returns at
+// once) and put (registers -> LDS, waits for the fetch).
+// (native <2 x double>: HIP's double2 struct is not promoted to registers when it is
+// carried around a loop, it lands in scratch)
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+template <int NB>
+struct TileRegs {
+    f64x2 v[NB * NB / 2 / NTHREADS];
+};
+template <int NB>
+__device__ __forceinline__ void tile_fetch(TileRegs<NB>& r, const double* __restrict__ g, long ld) {
+#pragma unroll
+    for (int q = 0; q < NB * NB / 2 / NTHREADS; ++q) {
+        const int p = threadIdx.x + q * NTHREADS;
+        const int row = p / (NB / 2), c = 2 * (p % (NB / 2));
+        r.v[q] = *reinterpret_cast<const f64x2*>(g + (long)row * ld + c);
+    }
+}
+template <int NB>
+__device__ __forceinline__ void tile_put(double* __restrict__ s, const TileRegs<NB>& r) {
+    constexpr int S = TileCfg<NB>::S;
+#pragma unroll
+    for (int q = 0; q < NB * NB / 2 / NTHREADS; ++q) {
+        const int p = threadIdx.x + q * NTHREADS;
+        const int row = p / (NB / 2), c = 2 * (p % (NB / 2));
+        *reinterpret_cast<f64x2*>(s + row * S + c) = r.v[q];
+    }
+}
 template <int NB>
 __device__ __forceinline__ void tile_store(double* __restrict__ g, long ld, const double* __restrict__ s) {
     constexpr int S = TileCfg<NB>::S;
@@ -793,6 +821,20 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
+// Sum over each quad of lanes (xor 1, xor 2) with quad_perm DPP moves: no LDS crossbar
+// traffic, a few cycles per step (a __shfl_xor of a double is two ds_bpermute).
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov_f64(double v) {
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double quad_sum(double v) {
+    v += dpp_mov_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += dpp_mov_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+    return v;
+}
+
 // Sum v over the 256-thread workgroup; result valid in every thread.
 // scratch: >= 4 doubles of LDS.  Contains two barriers.
 __device__ __forceinline__ double block_sum(double v, double* scratch) {
@@ -843,6 +885,16 @@ __device__ __forceinline__ int graph_source(double f, int m) {
     return -1;
 }
 // one RBF term of source s between raw rows xa, xb
+// graph_k with the source's inverse squared lengthscales il2[0..D) precomputed
+__device__ __forceinline__ double graph_k_il2(const double* xa, const double* xb, int s, const GraphTheta& th,
+                                              const double* il2) {
+    double r2 = 0.0;
+    for (int d = 0; d < th.D; ++d) {
+        const double q = xa[d] - xb[d];
+        r2 += q * q * il2[d];
+    }
+    return th.v(s) * exp(-0.5 * r2);
+}
 __device__ __forceinline__ double graph_k(const double* xa, const double* xb, int s, const GraphTheta& th) {
     double r2 = 0.0;
     for (int d = 0; d < th.D; ++d) {

@@ -42,8 +42,7 @@ struct CholArgs {
 
 
 struct GradArgs {
-    const double* Xo; long ldx;           // [L^{-1} | Z]
-    const double* alpha; long lda;        // Npad x Ppad
+    const double* Xo; long ldx;           // [L^{-1} | Z], then rows [-alpha^T / P ; alpha^T] (Ppad each)
     const double* X; long ldxx;           // inputs [n, D+1]
     const double* theta;
     double* gpart; int gstride;           // per task partial gradient
@@ -94,7 +93,7 @@ constexpr int MAXD_HOST = 32;
 
 size_t gram_smem_bytes(int nb);
 size_t chol_smem_bytes(int nb);
-size_t grad_smem_bytes(int nb);
+size_t grad_smem_bytes(int nb, int G, int nil2);
 int chol_step_blocks(int T, int Tp, int k, bool alpha = false);
 int grad_tasks(int T, int chunk);
 

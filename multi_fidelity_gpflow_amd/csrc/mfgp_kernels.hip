@@ -18,8 +18,7 @@
 namespace mfgp {
 
 constexpr int MAXD = 32;
-constexpr int XS = MAXD + 1;
-constexpr int RSTRIDE = 192;   // per-wave gradient slots (>= kernel_theta_size for MAXD, MFGP_MAX_LF)   // LDS row stride of staged inputs: odd, so a wave reading one
+constexpr int XS = MAXD + 1;   // LDS row stride of staged inputs: odd, so a wave reading one
                                 // dimension of 16-32 different rows hits distinct banks
 
 // ============================================================ K1: gram
@@ -335,6 +334,22 @@ __global__ __launch_bounds__(NTHREADS) void k_chol_step(CholArgs a) {
             __syncthreads();
             tile_mma<NB, true, false>(acc, Pj, T0, 1.0);
             acc_store(acc, al, a.ldal);
+            if (k == T - 1) {
+                // alpha_c is final: also store alpha^T under [L^{-1} | Z] for k_grad, whose
+                // items are then all TN products: row block T + cy holds -alpha^T / P (A side),
+                // row block T + Tp + cy holds alpha^T (B side).
+                const double sA = -1.0 / (double)a.p;
+                double* xa = Xo + (long)(T + cy) * NB * ldx + (long)c * NB;
+                double* xb = Xo + (long)(T + Tp + cy) * NB * ldx + (long)c * NB;
+#pragma unroll
+                for (int q = 0; q < TileCfg<NB>::NBLK; ++q)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const long o = (long)acc_col<NB>(q) * ldx + acc_row<NB>(q, r);
+                        xa[o] = sA * acc.v[q][r];
+                        xb[o] = acc.v[q][r];
+                    }
+            }
             return;
         }
         t -= nAl;
@@ -381,6 +396,19 @@ __global__ void k_rhs_init(double* R, long ldr, long sR, int npad, int ppad, con
 }
 
 // ============================================================ K5: gradient
+#ifndef MFGP_GRAD_NBUF1
+#define MFGP_GRAD_NBUF1 0
+#endif
+// k_grad LDS: NBUF operand buffers (2: double-buffered m-loop, one barrier per item;
+// NB = 64 tiles are 33 KB each, so one).  MFGP_GRAD_NBUF1 forces one at NB = 32.
+// After the loop the region is reused: raw rows xi, xj, flags fi, fj, then the
+// per-quad gradient partials R [G][GRAD_RLD] and the inverse squared lengthscales.
+template <int NB>
+constexpr int GRAD_NBUF = (NB == 32 && !MFGP_GRAD_NBUF1) ? 2 : 1;
+constexpr int GRAD_RLD = 65;   // 64 quad partials per gradient entry, +1 against bank conflicts
+template <int NB>
+constexpr int GRAD_RED_OFF = (2 * NB * XS + 2 * NB + 1) & ~1;
+
 __host__ __device__ inline int grad_row_chunks(int T, int i, int ch) { return (T - i + ch - 1) / ch; }
 
 int grad_tasks(int T, int ch) {
@@ -396,14 +424,20 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
     constexpr int E = TileCfg<NB>::ELEMS;
     constexpr int NE = TileCfg<NB>::NBLK * 4;
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    double* As = smem;
-    double* Bs = As + E;
-    double* xi = Bs + E;              // NB x XS raw rows of tile i
-    double* xj = xi + NB * XS;        // NB x XS raw rows of tile j
-    double* fi = xj + NB * XS;      // NB
-    double* fj = fi + NB;             // NB
-    double* red = fj + NB;            // 4 x RSTRIDE
+    // LDS: the m-loop operand buffers; after the loop the same region holds the raw
+    // input rows and source flags of the two row tiles, and red follows them.
+    constexpr int NBUF = GRAD_NBUF<NB>;
+    double* As = smem;                // NBUF x E (m-loop operands)
+    double* Bs = As + NBUF * E;       // NBUF x E
+    double* xi = smem;                // NB x XS raw rows of tile i   (epilogue)
+    double* xj = xi + NB * XS;        // NB x XS raw rows of tile j   (epilogue)
+    double* fi = xj + NB * XS;        // NB                           (epilogue)
+    double* fj = fi + NB;             // NB                           (epilogue)
+    static_assert(2 * NB * XS + 2 * NB <= 2 * NBUF * E, "raw rows must fit in the operand region");
     const int G = kernel_theta_size(a.nlf, a.D);
+    double* R = smem + GRAD_RED_OFF<NB>;     // G x GRAD_RLD quad partials   (epilogue)
+    double* il2 = R + G * GRAD_RLD;          // nsrc x D  1 / l^2            (epilogue)
+    const int nsrc = a.nlf ? a.nlf + 1 : 2;
     const MFTheta th{a.theta, a.D};
 
     // decode task -> (i, j, m0, m1)
@@ -419,7 +453,77 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
     const int m1 = min(a.T, m0 + a.chunk);
     auto Xt = [&](int r, int c) { return a.Xo + (long)r * NB * a.ldx + (long)c * NB; };
 
-    // stage raw inputs of the two row tiles
+    // W_ij (tile) = [alpha_i alpha_j^T] - P * sum_m Linv_mi^T Linv_mj  (= -P * acc below)
+    Acc<NB> acc;
+    acc_zero(acc);
+    const double negP = -(double)a.P;
+    {   // Software-pipelined operand stream of TN items acc += A^T B (all unscaled):
+        //   q < nm : A = Linv_{m,i}, B = Linv_{m,j}, m = m0 + q
+        //   q >= nm (chunk 0): A = -alpha^T_{cy,i} / P, B = alpha^T_{cy,j}  (rows T + cy, T+Tp+cy)
+        // so acc = S = sum_m Linv_mi^T Linv_mj - alpha_i alpha_j^T / P and W = -P S (the -P is
+        // folded into the epilogue weight).
+        const int nm = m1 - m0;
+        const int nq = nm + ((ch == 0) ? a.Tp : 0);
+        const long rs = (long)NB * a.ldx;
+        const double* const XA = a.Xo + (long)i * NB;
+        const double* const XB = a.Xo + (long)j * NB;
+#define MFGP_GRAD_FETCH(ra, rb, q)                                                          \
+    do {                                                                                    \
+        const int ra_ = (q) < nm ? m0 + (q) : a.T + (q) - nm;                               \
+        const int rb_ = (q) < nm ? ra_ : ra_ + a.Tp;                                        \
+        tile_fetch<NB>(ra, XA + ra_ * rs, a.ldx);                                           \
+        tile_fetch<NB>(rb, XB + rb_ * rs, a.ldx);                                           \
+    } while (0)
+        if constexpr (NBUF == 2) {
+            // Two LDS buffers + two register sets: item q is fetched two items before it is
+            // put into LDS (three before its product); unrolled by two so the register set
+            // of each item is a compile-time choice.  Invariant at even q: buffer 0 holds
+            // item q, set 1 item q+1, set 0 item q+2.
+            TileRegs<NB> ra0, rb0, ra1, rb1;
+            double* A0 = As;
+            double* B0 = Bs;
+            double* A1 = As + E;
+            double* B1 = Bs + E;
+            MFGP_GRAD_FETCH(ra0, rb0, 0);
+            tile_put<NB>(A0, ra0);
+            tile_put<NB>(B0, rb0);
+            if (nq > 1) MFGP_GRAD_FETCH(ra1, rb1, 1);
+            if (nq > 2) MFGP_GRAD_FETCH(ra0, rb0, 2);
+            __syncthreads();
+            for (int q = 0; q < nq; q += 2) {
+                tile_mma<NB, true, false>(acc, A0, B0, 1.0);
+                if (q + 1 < nq) {
+                    tile_put<NB>(A1, ra1);
+                    tile_put<NB>(B1, rb1);
+                    if (q + 3 < nq) MFGP_GRAD_FETCH(ra1, rb1, q + 3);
+                }
+                __syncthreads();
+                if (q + 1 < nq) {
+                    tile_mma<NB, true, false>(acc, A1, B1, 1.0);
+                    if (q + 2 < nq) {
+                        tile_put<NB>(A0, ra0);
+                        tile_put<NB>(B0, rb0);
+                        if (q + 4 < nq) MFGP_GRAD_FETCH(ra0, rb0, q + 4);
+                    }
+                    __syncthreads();
+                }
+            }
+        } else {                              // single LDS buffer (NB = 64), register prefetch
+            TileRegs<NB> ra, rb;
+            MFGP_GRAD_FETCH(ra, rb, 0);
+            for (int q = 0; q < nq; ++q) {
+                tile_put<NB>(As, ra);
+                tile_put<NB>(Bs, rb);
+                if (q + 1 < nq) MFGP_GRAD_FETCH(ra, rb, q + 1);
+                __syncthreads();
+                tile_mma<NB, true, false>(acc, As, Bs, 1.0);
+                __syncthreads();
+            }
+        }
+#undef MFGP_GRAD_FETCH
+    }
+
+    // stage the raw inputs of the two row tiles (operand buffers are free now)
     for (int e = threadIdx.x; e < NB * (a.D + 1); e += NTHREADS) {
         const int r = e / (a.D + 1), d = e % (a.D + 1);
         const int gi = i * NB + r, gj = j * NB + r;
@@ -431,33 +535,32 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
             fj[r] = (gj < a.n) ? (double)graph_source(vj, a.nlf) : -1.0;
         } else { fi[r] = (gi < a.n) ? vi : -1.0; fj[r] = (gj < a.n) ? vj : -1.0; }
     }
-
-    // W_ij (tile) = [alpha_i alpha_j^T] - P * sum_m Linv_mi^T Linv_mj
-    Acc<NB> acc;
-    acc_zero(acc);
-    const double negP = -(double)a.P;
-    for (int m = m0; m < m1; ++m) {
-        __syncthreads();
-        tile_load<NB>(As, Xt(m, i), a.ldx);
-        tile_load<NB>(Bs, Xt(m, j), a.ldx);
-        __syncthreads();
-        tile_mma<NB, true, false>(acc, As, Bs, negP);
-    }
-    if (ch == 0) {
-        for (int cy = 0; cy < a.Tp; ++cy) {
-            __syncthreads();
-            tile_load<NB>(As, a.alpha + (long)i * NB * a.lda + cy * NB, a.lda);
-            tile_load<NB>(Bs, a.alpha + (long)j * NB * a.lda + cy * NB, a.lda);
-            __syncthreads();
-            tile_mma<NB, false, true>(acc, As, Bs, 1.0);
-        }
+    for (int e = threadIdx.x; e < nsrc * a.D; e += NTHREADS) {
+        const int src = e / a.D, d = e % a.D;
+        const double l = a.nlf ? a.theta[src * (1 + a.D) + 1 + d] : (src == 0 ? th.lL(d) : th.lD(d));
+        il2[e] = 1.0 / (l * l);
     }
     __syncthreads();
 
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // gradient entry qidx: quad-sum in registers, one LDS slot per quad (64 per entry)
     auto put = [&](int qidx, double v) {
-        v = wave_sum(v);
-        if (lane == 0) red[wv * RSTRIDE + qidx] = v;
+        v = quad_sum(v);
+        if ((lane & 3) == 0) R[qidx * GRAD_RLD + wv * 16 + (lane >> 2)] = v;
+    };
+    // after a barrier: entry qidx = sum of its 64 partials, 8 lanes per entry
+    auto reduce_entries = [&](auto&& finish) {
+        for (int g0 = 0; g0 < G; g0 += NTHREADS / 8) {
+            const int qx = g0 + (threadIdx.x >> 3), sub = threadIdx.x & 7;
+            double v = 0.0;
+            if (qx < G) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v += R[qx * GRAD_RLD + sub * 8 + u];
+            }
+            v = quad_sum(v);
+            v += __shfl_xor(v, 4, 64);
+            if (sub == 0 && qx < G) a.gpart[(long)qx * gridDim.x + blockIdx.x] = finish(qx, v);
+        }
     };
     if constexpr (GRAPH) {
         // graph kernel (graph.py:55-97): 1/2 W_ab dK_ab/dtheta over all (a, b); a lower tile
@@ -478,12 +581,13 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
                 const int e = q * 4 + r;
                 const int ri = acc_row<NB>(q, r), cj = acc_col<NB>(q);
                 const int sa = (int)fi[ri], sb = (int)fj[cj];
-                const double w = 0.5 * acc.v[q][r];
+                const double w = (0.5 * negP) * acc.v[q][r];
 #pragma unroll
                 for (int s2 = 0; s2 <= MFGP_MAX_LF; ++s2) co[s2][e] = 0.0;
                 if (sa >= 0 && sb >= 0) {
                     double ks[MFGP_MAX_LF + 1];
-                    for (int s2 = 0; s2 <= m; ++s2) ks[s2] = graph_k(xi + ri * XS, xj + cj * XS, s2, gt);
+                    for (int s2 = 0; s2 <= m; ++s2)
+                        ks[s2] = graph_k_il2(xi + ri * XS, xj + cj * XS, s2, gt, il2 + s2 * a.D);
                     auto accum = [&](int s1, int t1) {   // entry with row source s1, column source t1
                         if (s1 < m && t1 < m) {
                             if (s1 == t1) co[s1][e] += w * ks[s1];
@@ -531,19 +635,18 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
         for (int k2 = 0; k2 < m * m; ++k2) put(ro + m + k2, grl[k2]);
         put(G - 1, gn);
         __syncthreads();
-        for (int qx = threadIdx.x; qx < G; qx += NTHREADS) {
-            double v = (red[qx] + red[RSTRIDE + qx]) + (red[2 * RSTRIDE + qx] + red[3 * RSTRIDE + qx]);
+        reduce_entries([&](int qx, double v) {
             if (qx < ro) {
                 const int s2 = qx / (1 + a.D), d = qx % (1 + a.D);
                 if (d == 0) v /= gt.v(s2);
                 else { const double l = gt.l(s2, d - 1); v /= l * l * l; }
             }
-            a.gpart[(long)qx * gridDim.x + blockIdx.x] = v;
-        }
+            return v;
+        });
         return;
     }
     // epilogue: contract with dK/dtheta recomputed from the inputs
-    const double wscale = (i == j) ? 0.5 : 1.0;   // 1/2 * (2 for the mirrored tile)
+    const double wscale = ((i == j) ? 0.5 : 1.0) * negP;   // -P (W = -P acc), 1/2, x2 mirrored
     const double rho = th.rho();
     double cL[NE], cD[NE];
     double gvL = 0.0, gvD = 0.0, grho = 0.0, gnoise = 0.0;
@@ -562,9 +665,8 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
                 for (int d = 0; d < a.D; ++d) {
                     const double df = xi[ri * XS + d] - xj[cj * XS + d];
                     const double d2 = df * df;
-                    const double ql = th.lL(d);
-                    s2 += d2 / (ql * ql);
-                    if (H1 && H2) { const double qd = th.lD(d); s2d += d2 / (qd * qd); }
+                    s2 += d2 * il2[d];
+                    if (H1 && H2) s2d += d2 * il2[a.D + d];
                 }
                 kL = th.vL() * exp(-0.5 * s2);
                 if (H1 && H2) kD = th.vD() * exp(-0.5 * s2d);
@@ -597,19 +699,19 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
         put(2 + a.D + d, td);
     }
     __syncthreads();
-    for (int qx = threadIdx.x; qx < G; qx += NTHREADS) {
-        const int st = RSTRIDE;
-        double v = (red[qx] + red[st + qx]) + (red[2 * st + qx] + red[3 * st + qx]);
+    reduce_entries([&](int qx, double v) {   // gpart [quantity][task]: coalesced reduction
         if (qx == 0) v /= th.vL();
         else if (qx <= a.D) { const double l = th.lL(qx - 1); v /= l * l * l; }
         else if (qx == 1 + a.D) v /= th.vD();
         else if (qx <= 1 + 2 * a.D) { const double l = th.lD(qx - 2 - a.D); v /= l * l * l; }
-        a.gpart[(long)qx * gridDim.x + blockIdx.x] = v;   // [quantity][task]: coalesced reduction
-    }
+        return v;
+    });
 }
 
-size_t grad_smem_bytes(int nb) {
-    return sizeof(double) * (2 * (size_t)nb * (nb + 2) + 2 * (size_t)nb * XS + 2 * nb + 4 * RSTRIDE);
+size_t grad_smem_bytes(int nb, int G, int nil2) {
+    const size_t region = 2 * (size_t)(nb == 32 ? GRAD_NBUF<32> : GRAD_NBUF<64>) * nb * (nb + 2);
+    const size_t epi = (size_t)(nb == 32 ? GRAD_RED_OFF<32> : GRAD_RED_OFF<64>) + (size_t)G * GRAD_RLD + nil2;
+    return sizeof(double) * std::max(region, epi);
 }
 
 // ============================================================ K4: finalize (+Adam)
@@ -806,12 +908,11 @@ void launch_chol_steps(CholArgs c, int batch, hipStream_t s) {
 }
 template <int NB>
 void launch_grad(const GradArgs& g, hipStream_t s) {
+    const size_t lds = grad_smem_bytes(NB, kernel_theta_size(g.nlf, g.D), (g.nlf ? g.nlf + 1 : 2) * g.D);
     if (g.nlf)
-        hipLaunchKernelGGL((k_grad<NB, true>), dim3(grad_tasks(g.T, g.chunk)), dim3(NTHREADS), grad_smem_bytes(NB), s,
-                           g);
+        hipLaunchKernelGGL((k_grad<NB, true>), dim3(grad_tasks(g.T, g.chunk)), dim3(NTHREADS), lds, s, g);
     else
-        hipLaunchKernelGGL((k_grad<NB, false>), dim3(grad_tasks(g.T, g.chunk)), dim3(NTHREADS), grad_smem_bytes(NB),
-                           s, g);
+        hipLaunchKernelGGL((k_grad<NB, false>), dim3(grad_tasks(g.T, g.chunk)), dim3(NTHREADS), lds, s, g);
 }
 template <int NB>
 void launch_pred(const PredAArgs& pa, const PredOutArgs& po, int T, hipStream_t s) {
