@@ -41,6 +41,7 @@ struct Carve {
 struct GprLayout {
     int nb, npad, T, ppad, Tp, G, gstride, ng;
     double *A, *R, *Xo, *Dd, *ldiag, *alpha, *zpart, *gpart, *items;
+    int* gorder;   // k_grad workgroup -> task table, built by k_gram each call
     int* cnt;   // reduce-arrival counter, zeroed by k_gram each call
     int ncnt;
     size_t bytes;
@@ -69,6 +70,7 @@ static GprLayout gpr_layout(int nb, int n, int p, int d, void* ws, int grad_chun
     L.items = c.take<double>((size_t)L.G + 8);
     L.ncnt = 1;
     L.cnt = c.take<int>((size_t)L.ncnt);
+    L.gorder = c.take<int>((size_t)L.ng);
     L.bytes = c.off + 256;
     return L;
 }
@@ -124,7 +126,9 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
         g.padded = 1; g.npad = L.npad; g.tiles_c = L.T; g.add_noise = 1; g.diag_add = nlf ? GRAPH_JITTER : 0.0;
         g.Dd = L.Dd; g.sD = 0; g.ldiag = L.ldiag; g.sL = 0; g.info = info; g.nlf = nlf;
         g.cnt = L.cnt; g.ncnt = L.ncnt;
-        launch_gram<NB>(g, L.T * (L.T + 1) / 2, 1, s);
+        const bool order = want_grad && h->grad_chunk + L.Tp < 2048;   // gram LDS holds the histogram
+        if (order) { g.gorder = L.gorder; g.gT = L.T; g.gchunk = h->grad_chunk; g.gTp = L.Tp; }
+        launch_gram<NB>(g, L.T * (L.T + 1) / 2 + (order ? 1 : 0), 1, s);
     }
     if (pm) pm->mark(s);
     {
@@ -140,7 +144,7 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
     if (pm) pm->mark(s);
     if (want_grad) {
         GradArgs ga{L.Xo, ldr, X, (long)ldx, theta, L.gpart, L.gstride, L.T, L.Tp, n, p, d,
-                    h->grad_chunk, nlf};
+                    h->grad_chunk, nlf, h->grad_chunk + L.Tp < 2048 ? L.gorder : nullptr};
         launch_grad<NB>(ga, s);
     }
     if (pm) pm->mark(s);
@@ -358,7 +362,7 @@ int mfgp_create(int device, mfgp_handle_t* out) {
     h->device = device;
     h->stream = nullptr;
     h->nb = 32;
-    h->grad_chunk = 16;
+    h->grad_chunk = 24;   // k_grad m-tiles per task (sweep at Goku T = 37: 16 -> 33.8 us, 24 -> 31.9, 40 -> 36.7)
     if (const char* gc = getenv("MFGP_GRAD_CHUNK")) h->grad_chunk = std::max(1, atoi(gc));
     const char* env = getenv("MFGP_TILE");
     if (env && atoi(env) == 64) h->nb = 64;

@@ -22,7 +22,9 @@ struct GramArgs {
     // fused RHS init (LML layout only; R == nullptr: skip): R = [I | Y]
     double* R; long ldr; long sR; const double* Y; long ldy; long sY; int p, ppad;
     int nlf;                                  // 0: LinearMultiFidelityKernel; m >= 1: graph kernel, m LF sources
-    int* cnt; int ncnt;                       // arrival counters zeroed by workgroup 0 (alpha / reduce merge)
+    int* cnt; int ncnt;                       // arrival counters zeroed by workgroup 0 (reduce merge)
+    // k_grad task order (nullptr: none): one extra LAST workgroup builds it (grad_order)
+    int* gorder; int gT, gchunk, gTp;
 };
 
 struct CholArgs {
@@ -49,6 +51,7 @@ struct GradArgs {
     int T, Tp, n, P, D;
     int chunk;                            // m-tiles per task
     int nlf;                              // kernel family (GramArgs::nlf)
+    const int* order;                     // workgroup -> task (nullptr: identity), see grad_order
 };
 
 struct FinArgs {
@@ -95,7 +98,7 @@ size_t gram_smem_bytes(int nb);
 size_t chol_smem_bytes(int nb);
 size_t grad_smem_bytes(int nb, int G, int nil2);
 int chol_step_blocks(int T, int Tp, int k, bool alpha = false);
-int grad_tasks(int T, int chunk);
+__host__ __device__ int grad_tasks(int T, int chunk);
 
 
 template <int NB> void launch_gram(const GramArgs& g, int nblocks, int batch, hipStream_t s);

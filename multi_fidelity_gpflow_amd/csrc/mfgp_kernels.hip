@@ -23,6 +23,8 @@ constexpr int XS = MAXD + 1;   // LDS row stride of staged inputs: odd, so a wav
 
 // ============================================================ K1: gram
 
+__device__ void build_grad_order(int T, int chunk, int Tp, int* order, int* hist);
+
 template <int NB>
 __device__ __forceinline__ void stage_rows(double* aL, double* aD, double* nL, double* nD, double* f,
                                            const double* X, long ldx, int n, int r0, int D,
@@ -96,6 +98,10 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
                                                    // would shift the dynamic base off 16 B (G17)
 
     const int b = blockIdx.z;
+    if (a.gorder && blockIdx.x == gridDim.x - 1) {   // extra workgroup: k_grad task order
+        if (b == 0) build_grad_order(a.gT, a.gchunk, a.gTp, a.gorder, reinterpret_cast<int*>(smem));
+        return;
+    }
     if (a.cnt && blockIdx.x == 0 && b == 0)
         for (int e = threadIdx.x; e < a.ncnt; e += NTHREADS) a.cnt[e] = 0;
     int ti, tj;
@@ -411,10 +417,57 @@ constexpr int GRAD_RED_OFF = (2 * NB * XS + 2 * NB + 1) & ~1;
 
 __host__ __device__ inline int grad_row_chunks(int T, int i, int ch) { return (T - i + ch - 1) / ch; }
 
-int grad_tasks(int T, int ch) {
+__host__ __device__ int grad_tasks(int T, int ch) {
     int s = 0;
     for (int i = 0; i < T; ++i) s += (i + 1) * grad_row_chunks(T, i, ch);
     return s;
+}
+
+// k_grad task -> (row i, column j, chunk ch) in the natural order (rows, then columns,
+// then m-chunks); returns the task's item count (m tiles + the alpha items of chunk 0).
+__device__ __forceinline__ int grad_decode(int t, int T, int chunk, int Tp, int& i, int& j, int& ch) {
+    for (i = 0;; ++i) {
+        const int cnt = (i + 1) * grad_row_chunks(T, i, chunk);
+        if (t < cnt) break;
+        t -= cnt;
+    }
+    const int nch = grad_row_chunks(T, i, chunk);
+    j = t / nch;
+    ch = t % nch;
+    const int m0 = i + ch * chunk;
+    return min(T, m0 + chunk) - m0 + (ch == 0 ? Tp : 0);
+}
+
+// Workgroup -> task table for k_grad.  All k_grad workgroups are resident at once and
+// are dealt to CUs in launch order (about blockIdx mod 256), so the natural order piles
+// the long early-row chains onto the same CUs.  Tasks are counting-sorted by item count
+// (longest first) and dealt in a snake over 256 slots, which evens out the MFMA work per
+// CU.  Placement only sets speed: any permutation gives the same result, because k_grad
+// indexes its partial sums by task, not by workgroup.  One workgroup; hist: LDS ints.
+__device__ void build_grad_order(int T, int chunk, int Tp, int* order, int* hist) {
+    const int ntask = grad_tasks(T, chunk);
+    const int lmax = chunk + Tp;
+    for (int l = threadIdx.x; l <= lmax; l += NTHREADS) hist[l] = 0;
+    __syncthreads();
+    int i, j, ch;
+    for (int t = threadIdx.x; t < ntask; t += NTHREADS) atomicAdd(&hist[grad_decode(t, T, chunk, Tp, i, j, ch)], 1);
+    __syncthreads();
+    if (threadIdx.x == 0) {   // exclusive offsets, longest first
+        int o = 0;
+        for (int l = lmax; l >= 0; --l) {
+            const int c = hist[l];
+            hist[l] = o;
+            o += c;
+        }
+    }
+    __syncthreads();
+    constexpr int SLOTS = 256;
+    for (int t = threadIdx.x; t < ntask; t += NTHREADS) {
+        const int p = atomicAdd(&hist[grad_decode(t, T, chunk, Tp, i, j, ch)], 1);
+        const int r = p / SLOTS, k = p % SLOTS;
+        const int width = min(SLOTS, ntask - r * SLOTS);
+        order[r * SLOTS + ((r & 1) ? width - 1 - k : k)] = t;
+    }
 }
 
 
@@ -441,14 +494,9 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
     const MFTheta th{a.theta, a.D};
 
     // decode task -> (i, j, m0, m1)
-    int t = blockIdx.x, i = 0;
-    for (;; ++i) {
-        const int cnt = (i + 1) * grad_row_chunks(a.T, i, a.chunk);
-        if (t < cnt) break;
-        t -= cnt;
-    }
-    const int nch = grad_row_chunks(a.T, i, a.chunk);
-    const int j = t / nch, ch = t % nch;
+    const int task = a.order ? a.order[blockIdx.x] : (int)blockIdx.x;
+    int i, j, ch;
+    grad_decode(task, a.T, a.chunk, a.Tp, i, j, ch);
     const int m0 = i + ch * a.chunk;
     const int m1 = min(a.T, m0 + a.chunk);
     auto Xt = [&](int r, int c) { return a.Xo + (long)r * NB * a.ldx + (long)c * NB; };
@@ -559,7 +607,7 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
             }
             v = quad_sum(v);
             v += __shfl_xor(v, 4, 64);
-            if (sub == 0 && qx < G) a.gpart[(long)qx * gridDim.x + blockIdx.x] = finish(qx, v);
+            if (sub == 0 && qx < G) a.gpart[(long)qx * gridDim.x + task] = finish(qx, v);
         }
     };
     if constexpr (GRAPH) {
@@ -645,9 +693,37 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
         });
         return;
     }
-    // epilogue: contract with dK/dtheta recomputed from the inputs
+    // epilogue: contract with dK/dtheta recomputed from the inputs.  Loops run over d
+    // outermost so the lane's elements share each LDS read of their column inputs.
     const double wscale = ((i == j) ? 0.5 : 1.0) * negP;   // -P (W = -P acc), 1/2, x2 mirrored
     const double rho = th.rho();
+    int ri[NE], cj[NE];
+    bool L1[NE], H1[NE], L2[NE], H2[NE];
+    double s2[NE], s2d[NE];
+    bool anyHH = false;
+#pragma unroll
+    for (int q = 0; q < TileCfg<NB>::NBLK; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int e = q * 4 + r;
+            ri[e] = acc_row<NB>(q, r);
+            cj[e] = acc_col<NB>(q);
+            const double f1 = fi[ri[e]], f2 = fj[cj[e]];
+            L1[e] = f1 == 0.0; H1[e] = f1 == 1.0; L2[e] = f2 == 0.0; H2[e] = f2 == 1.0;
+            anyHH |= H1[e] && H2[e];
+            s2[e] = 0.0;
+            s2d[e] = 0.0;
+        }
+    for (int d = 0; d < a.D; ++d) {
+        const double il = il2[d], ild = il2[a.D + d];
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            const double df = xi[ri[e] * XS + d] - xj[cj[e] * XS + d];
+            const double d2 = df * df;
+            s2[e] += d2 * il;
+            s2d[e] += d2 * ild;
+        }
+    }
     double cL[NE], cD[NE];
     double gvL = 0.0, gvD = 0.0, grho = 0.0, gnoise = 0.0;
 #pragma unroll
@@ -655,30 +731,19 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int e = q * 4 + r;
-            const int ri = acc_row<NB>(q, r), cj = acc_col<NB>(q);
-            const double f1 = fi[ri], f2 = fj[cj];
-            const bool L1 = f1 == 0.0, H1 = f1 == 1.0, L2 = f2 == 0.0, H2 = f2 == 1.0;
             const double w = acc.v[q][r] * wscale;
-            double kL = 0.0, kD = 0.0;
-            if ((L1 || H1) && (L2 || H2)) {
-                double s2 = 0.0, s2d = 0.0;
-                for (int d = 0; d < a.D; ++d) {
-                    const double df = xi[ri * XS + d] - xj[cj * XS + d];
-                    const double d2 = df * df;
-                    s2 += d2 * il2[d];
-                    if (H1 && H2) s2d += d2 * il2[a.D + d];
-                }
-                kL = th.vL() * exp(-0.5 * s2);
-                if (H1 && H2) kD = th.vD() * exp(-0.5 * s2d);
-            }
-            const double si = L1 ? 1.0 : (H1 ? rho : 0.0), sj = L2 ? 1.0 : (H2 ? rho : 0.0);
-            const double hi = H1 ? 1.0 : 0.0, hj = H2 ? 1.0 : 0.0;
+            const bool live = (L1[e] || H1[e]) && (L2[e] || H2[e]);
+            const double kL = live ? th.vL() * exp(-0.5 * s2[e]) : 0.0;
+            double kD = 0.0;
+            if (anyHH && H1[e] && H2[e]) kD = th.vD() * exp(-0.5 * s2d[e]);
+            const double si = L1[e] ? 1.0 : (H1[e] ? rho : 0.0), sj = L2[e] ? 1.0 : (H2[e] ? rho : 0.0);
+            const double hi = H1[e] ? 1.0 : 0.0, hj = H2[e] ? 1.0 : 0.0;
             cL[e] = w * si * sj * kL;
             cD[e] = w * hi * hj * kD;
             gvL += cL[e];
             gvD += cD[e];
             grho += w * (hi * sj + si * hj) * kL;
-            if (i == j && ri == cj && i * NB + ri < a.n) gnoise += w;
+            if (i == j && ri[e] == cj[e] && i * NB + ri[e] < a.n) gnoise += w;
         }
     put(0, gvL);
     put(1 + a.D, gvD);
@@ -687,14 +752,11 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
     for (int d = 0; d < a.D; ++d) {
         double tl = 0.0, td = 0.0;
 #pragma unroll
-        for (int q = 0; q < TileCfg<NB>::NBLK; ++q)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int e = q * 4 + r;
-                const double df = xi[acc_row<NB>(q, r) * XS + d] - xj[acc_col<NB>(q) * XS + d];
-                tl += cL[e] * df * df;
-                td += cD[e] * df * df;
-            }
+        for (int e = 0; e < NE; ++e) {
+            const double df = xi[ri[e] * XS + d] - xj[cj[e] * XS + d];
+            tl += cL[e] * df * df;
+            td += cD[e] * df * df;
+        }
         put(1 + d, tl);
         put(2 + a.D + d, td);
     }
