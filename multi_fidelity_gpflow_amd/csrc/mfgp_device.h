@@ -638,12 +638,481 @@ __device__ __forceinline__ void tile_potrf_inv_m4(double* A, double* R, double* 
     tile_potrf_inv_m4_acc(aA, A, R, dg, bad);
 }
 
-// NB = 32 uses the MFMA 4-pivot form (12.7k vs 15.5k shader clocks for the pivot form,
-// tools/ubench_tile.hip).
+// ---------------------------------------------------------------- single-wave diag factor
+// NB = 32 Cholesky + inverse by ONE wavefront, no workgroup barrier on the pivot chain
+// (a 4-wave publish -> barrier -> read round trip costs ~160 clocks, an in-wave LDS round trip
+// ~120 and an f64 MFMA accumulator hop 64: tools/ubench_lat2.hip).  Wave 0 holds the whole
+// symmetric tile as three 16x16 MFMA accumulator blocks A00, A01 (= A10^T), A11 and the inverse
+// as R00, R10, R11 (lane l: rows 16bi + (l>>4) + 4q, column 16bj + (l&15)).  Round K = 0..7
+// eliminates pivots P = 4K..4K+3 (block LDL^T, un-normalised pivot rows):
+//   * lanes publish the pivot rows A[P, :] (= the pivot columns) into an LDS panel, then every
+//     lane reads the 4x4 pivot block M = L_M D_M L_M^T (factored redundantly in registers, the
+//     m4 elimination order) and its own rows C_i = A[i, P];
+//   * row i below P: W_i = C_i M^{-1} = ((C_i L_M^{-T}) D_M^{-1}) L_M^{-1} by substitution;
+//     pivot row p: W_R = I - T with T = D_M^{-1/2} L_M^{-1} (row p of L_M^{-1} by the same
+//     back substitution on e_p); rows above P: 0;
+//   * A -= W A[P, :] and R -= W_R R[P, :]: one v_mfma_f64_16x16x4 per block, with the pivot
+//     rows of A and R as the B operand exactly as they sit in the accumulator (register K&3),
+//     and W in A-operand layout straight from the lane's own substitution.
+// R then holds L^{-1} = blockdiag(T) L_u^{-1}.  Input: a symmetric tile whose lower triangle is
+// valid, in LDS (X, stride ldx); the upper triangle is never read.  Pn: 128 doubles of LDS that
+// may alias X (wave 0 has read X before it first writes Pn).  All waves must call; waves 1..3
+// only meet the closing barrier.
+// The panel is published and read back by the same wave: its DS operations are processed in
+// issue order, so only the compiler has to be kept from reordering them (no lgkmcnt wait).
+#ifndef W1_PUBLISH_WAIT
+#define W1_PUBLISH_WAIT() asm volatile("" ::: "memory")
+#endif
+// 4-way select on the low two bits of s as two levels of v_cndmask (an equality chain
+// compiles to exec-mask branches, which break the scheduling region of the pivot chain)
+__device__ __forceinline__ double sel4(int s, double v0, double v1, double v2, double v3) {
+    const bool b0 = (s & 1) != 0, b1 = (s & 2) != 0;
+    const double lo = b0 ? v1 : v0, hi = b0 ? v3 : v2;
+    return b1 ? hi : lo;
+}
+
+// R work of round K, deferred into round K+1 (after its LDS reads are issued) so that the
+// in-order issue of the A chain is never held behind it: X = V L_M^{-1}, W_R, R -= W_R R[P, :].
+struct W1Pending {
+    double L10, L20, L30, L21, L31, L32;
+    double v[2][4];   // rows h = 0, 1: Z (rows below) or e_p (pivot rows)
+};
+
+template <int K>
+__device__ __forceinline__ void w1_rwork(const W1Pending& pd, f64x4& r00, f64x4& r10, f64x4& r11, int l) {
+    constexpr int bk = K >> 2, kq = K & 3;
+    const int lc = l & 15, kk = l >> 4, p = lc & 3;
+    double wR[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if (h < bk) { wR[h] = 0.0; continue; }
+        const int row = 16 * h + lc;
+        const bool piv = (row >> 2) == K;
+        const bool below = row > 4 * K + 3;
+        const double x3 = pd.v[h][3];
+        const double x2 = fma(-pd.L32, x3, pd.v[h][2]);
+        const double x1 = fma(-pd.L31, x3, fma(-pd.L21, x2, pd.v[h][1]));
+        const double x0 = fma(-pd.L30, x3, fma(-pd.L20, x2, fma(-pd.L10, x1, pd.v[h][0])));
+        const double xk = sel4(kk, x0, x1, x2, x3);
+        wR[h] = below ? xk : piv ? ((p == kk ? 1.0 : 0.0) - xk) : 0.0;
+    }
+    if constexpr (bk == 0) {
+        const double pR0 = r00[kq];
+        r00 = __builtin_amdgcn_mfma_f64_16x16x4f64(-wR[0], pR0, r00, 0, 0, 0);
+        r10 = __builtin_amdgcn_mfma_f64_16x16x4f64(-wR[1], pR0, r10, 0, 0, 0);
+    } else {
+        const double pR0 = r10[kq], pR1 = r11[kq];
+        r10 = __builtin_amdgcn_mfma_f64_16x16x4f64(-wR[1], pR0, r10, 0, 0, 0);
+        r11 = __builtin_amdgcn_mfma_f64_16x16x4f64(-wR[1], pR1, r11, 0, 0, 0);
+    }
+}
+
+#ifndef W1_ABL
+#define W1_ABL 0
+#endif
+#ifndef W1_STAMP
+#define W1_STAMP(i) ((void)0)
+#endif
+#ifndef W2_STAMP
+#define W2_STAMP(i) ((void)0)
+#endif
+#ifndef W1_SCHED_BARRIER
+#define W1_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)
+#endif
+
+template <int K>
+__device__ __forceinline__ void w1_round(double* __restrict__ Pn, double* __restrict__ dpv, f64x4& a00, f64x4& a01,
+                                         f64x4& a11, f64x4& r00, f64x4& r10, f64x4& r11, W1Pending& pd, int l) {
+    if constexpr (K < 8) {
+        constexpr int bk = K >> 2, kq = K & 3;
+        const int lc = l & 15, kk = l >> 4;
+        W1_STAMP(3 * K);
+        // ---- publish A[4K + kk][col] at Pn[col * 4 + kk]
+        if constexpr (bk == 0) Pn[lc * 4 + kk] = a00[kq];
+        Pn[(16 + lc) * 4 + kk] = (bk == 0) ? a01[kq] : a11[kq];
+        W1_PUBLISH_WAIT();
+        // ---- pivot block (column j of M at Pn[(4K + j) * 4 .. + 3])
+        const f64x2* Pm = reinterpret_cast<const f64x2*>(Pn + 16 * K);
+        const f64x2 c0a = Pm[0], c0b = Pm[1], c1a = Pm[2], c1b = Pm[3], c2b = Pm[5], c3b = Pm[7];
+        // ---- own rows C_i, i = 16h + lc (h = 1 always, h = 0 while bk == 0)
+        const f64x2* Pr = reinterpret_cast<const f64x2*>(Pn);
+        f64x2 u0a = {0.0, 0.0}, u0b = {0.0, 0.0};
+        if constexpr (bk == 0) { u0a = Pr[2 * lc]; u0b = Pr[2 * lc + 1]; }
+        const f64x2 u1a = Pr[2 * (16 + lc)], u1b = Pr[2 * (16 + lc) + 1];
+        W1_SCHED_BARRIER();
+        if constexpr (K > 0) w1_rwork<K - 1>(pd, r00, r10, r11, l);
+        W1_SCHED_BARRIER();
+        W1_STAMP(3 * K + 1);
+        const double m00 = c0a.x, m10 = c0a.y, m20 = c0b.x, m30 = c0b.y;
+        const double m11 = c1a.y, m21 = c1b.x, m31 = c1b.y, m22 = c2b.x, m32 = c2b.y, m33 = c3b.y;
+        // ---- LDL^T of M
+#if W1_ABL & 1
+#define W1RCP(x) __builtin_amdgcn_rcp(x)
+#else
+#define W1RCP(x) rcp_nr(x)
+#endif
+        const double i0 = W1RCP(m00);
+        const double L10 = m10 * i0, L20 = m20 * i0, L30 = m30 * i0;
+        const double d1 = fma(-L10, m10, m11);
+        const double i1 = W1RCP(d1);
+        const double e21 = fma(-L20, m10, m21), e31 = fma(-L30, m10, m31);
+        const double L21 = e21 * i1, L31 = e31 * i1;
+        const double d2 = fma(-L21, e21, fma(-L20, m20, m22));
+        const double i2 = W1RCP(d2);
+        const double e32 = fma(-L31, e21, fma(-L30, m20, m32));
+        const double L32 = e32 * i2;
+        const double d3 = fma(-L32, e32, fma(-L31, e31, fma(-L30, m30, m33)));
+        const double i3 = W1RCP(d3);
+#undef W1RCP
+        // ---- per row: Y = C L_M^{-T}, Z = Y D_M^{-1}; A -= Z Y^T (symmetric form)
+        double zA[2], yB[2], zs[2][4] = {};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (h < bk) { zA[h] = 0.0; yB[h] = 0.0; continue; }
+            const f64x2 ua = h ? u1a : u0a, ub = h ? u1b : u0b;
+            const int row = 16 * h + lc;
+            const bool piv = (row >> 2) == K;
+            const bool below = row > 4 * K + 3;
+            const int p = lc & 3;
+            const double y0 = ua.x;
+            const double y1 = fma(-L10, y0, ua.y);
+            const double y2 = fma(-L21, y1, fma(-L20, y0, ub.x));
+            const double y3 = fma(-L32, y2, fma(-L31, y1, fma(-L30, y0, ub.y)));
+            const double z0 = y0 * i0, z1 = y1 * i1, z2 = y2 * i2, z3 = y3 * i3;
+            zA[h] = below ? sel4(kk, z0, z1, z2, z3) : 0.0;
+            yB[h] = sel4(kk, y0, y1, y2, y3);
+            zs[h][0] = z0; zs[h][1] = z1; zs[h][2] = z2; zs[h][3] = z3;
+        }
+        // ---- rank-4 update of A on the matrix core
+        if constexpr (bk == 0) {
+            a00 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[0], yB[0], a00, 0, 0, 0);
+            a01 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[0], yB[1], a01, 0, 0, 0);
+            a11 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[1], yB[1], a11, 0, 0, 0);
+        } else {
+            a11 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[1], yB[1], a11, 0, 0, 0);
+        }
+        W1_SCHED_BARRIER();
+        W1_STAMP(3 * K + 2);
+        // ---- off the A chain (issued under the MFMA latency): pivots to LDS, R-work inputs
+        dpv[l < 4 ? 4 * K + l : 40 + l] = sel4(l & 3, m00, d1, d2, d3);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const bool piv = ((16 * h + lc) >> 2) == K;
+            const int p = lc & 3;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) pd.v[h][c] = piv ? (p == c ? 1.0 : 0.0) : zs[h][c];
+        }
+        pd.L10 = L10; pd.L20 = L20; pd.L30 = L30; pd.L21 = L21; pd.L31 = L31; pd.L32 = L32;
+        W1_SCHED_BARRIER();
+        w1_round<K + 1>(Pn, dpv, a00, a01, a11, r00, r10, r11, pd, l);
+    } else {
+        w1_rwork<7>(pd, r00, r10, r11, l);
+    }
+}
+
+__device__ __forceinline__ void tile_potrf_inv_w1_core(const double* __restrict__ X, int ldx, double* __restrict__ Pn,
+                                                       double* __restrict__ R, double* __restrict__ dg,
+                                                       int* __restrict__ bad) {
+    constexpr int S = TileCfg<32>::S;
+    if (threadIdx.x < 64) {
+        const int l = threadIdx.x, lc = l & 15, lr = l >> 4;
+        f64x4 a00, a01, a11, r00, r10 = {0.0, 0.0, 0.0, 0.0}, r11;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int r = lr + 4 * q;
+            const int hi = r > lc ? r : lc, lo = r > lc ? lc : r;
+            a00[q] = X[hi * ldx + lo];
+            a11[q] = X[(16 + hi) * ldx + 16 + lo];
+            a01[q] = X[(16 + lc) * ldx + r];
+            r00[q] = (r == lc) ? 1.0 : 0.0;
+            r11[q] = r00[q];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // X fully read before Pn (may alias) is written
+        double* dpv = Pn + 128;                                // [32] pivots + dump slots
+        W1Pending pd;
+        w1_round<0>(Pn, dpv, a00, a01, a11, r00, r10, r11, pd, l);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        // L^{-1} = diag(d)^{-1/2} L_u^{-1}; L_ii = sqrt(d_i); first bad pivot by one ballot
+        double s0[4], s1[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            s0[q] = rcp_nr(sqrt(dpv[lr + 4 * q]));
+            s1[q] = rcp_nr(sqrt(dpv[16 + lr + 4 * q]));
+        }
+        const double dl = dpv[l & 31];
+        const unsigned long long m = __ballot(l < 32 && !(dl > 0.0 && dl < INFINITY));
+        if (l < 32) dg[l] = sqrt(dl);
+        if (l == 0) *bad = m ? __ffsll((long long)m) : 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int r = lr + 4 * q;
+            R[r * S + lc] = (lc <= r) ? r00[q] * s0[q] : 0.0;
+            R[r * S + 16 + lc] = 0.0;
+            R[(16 + r) * S + lc] = r10[q] * s1[q];
+            R[(16 + r) * S + 16 + lc] = (lc <= r) ? r11[q] * s1[q] : 0.0;
+        }
+    }
+    __syncthreads();
+}
+
+// Entry from an LDS tile A (row-major, stride S, lower triangle valid); A doubles as the panel.
+__device__ __forceinline__ void tile_potrf_inv_w1(double* A, double* R, double* dg, int* bad) {
+    tile_potrf_inv_w1_core(A, TileCfg<32>::S, A, R, dg, bad);
+}
+
+// Entry with the tile in accumulator layout (the Acc<32> of tile_mma: wave w holds block
+// (w>>1, w&1)); scratch: >= 32 * 33 doubles of LDS nobody reads concurrently.
+__device__ __forceinline__ void tile_potrf_inv_w1_acc(f64x4 aA, double* scratch, double* R, double* dg, int* bad) {
+    constexpr int LX = 33;
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    const int bi = w >> 1, bj = w & 1;
+    if (bj <= bi) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) scratch[(16 * bi + (l >> 4) + 4 * q) * LX + 16 * bj + (l & 15)] = aA[q];
+    }
+    __syncthreads();
+    tile_potrf_inv_w1_core(scratch, LX, scratch, R, dg, bad);
+}
+
+// ---------------------------------------------------------------- two-wave diag factor
+// The single-wave factor is issue-bound (one wave issues every instruction of the round in
+// order): the R chain (X = C M^{-1} by substitution, W_R, two MFMAs) costs ~280 of its ~1.1k
+// clocks per round.  Here wave 0 runs the A chain only and hands each round's record -- the
+// 4x4 factor (L_M, pivots d) and its rows' Z = C L_M^{-T} D_M^{-1} -- to wave 1 through LDS;
+// wave 1 follows one round behind, runs the R chain and finishes R.  Hand-off inside the
+// workgroup: a wave's DS operations are processed in issue order, so a record written before
+// the round flag is complete when another wave reads the flag; Z slots are a 4-deep ring
+// released by wave 1's ack counter.  Waves 2 and 3 only meet the closing barrier.
+// ws: >= W2_WS doubles of LDS, not aliasing R or dg; the layout below.
+constexpr int W2_ZB = 128;                  // Z ring: 4 slots x [2 rows][64 lanes][4]
+constexpr int W2_REC = W2_ZB + 4 * 512;     // records: 8 rounds x 12 doubles (L10..L32, d0..d3)
+constexpr int W2_FLAG = W2_REC + 8 * 12;    // two ints: round flag (wave 0), ack (wave 1)
+constexpr int W2_WS = W2_FLAG + 2;
+
+// Workgroup-scope relaxed atomics (not volatile: a volatile access is never rewritten from
+// flat to ds_* by address-space inference, and the flat form costs a system-coherent round trip).
+__device__ __forceinline__ int lds_ld_volatile(const int* p) {
+    return __hip_atomic_load(const_cast<int*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st_flag(int* p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// Bounded spin on an LDS counter written by another wave of the workgroup (the bound only
+// guards against a hang; the partner wave always reaches the value within the round).
+__device__ __forceinline__ void w2_wait(const int* p, int v) {
+    for (int it = 0; it < (1 << 20) && lds_ld_volatile(p) < v; ++it) {}
+}
+
+template <int K>
+__device__ __forceinline__ void w2_round_a(double* __restrict__ ws, f64x4& a00, f64x4& a01, f64x4& a11, int l) {
+    if constexpr (K < 8) {
+        constexpr int bk = K >> 2, kq = K & 3;
+        const int lc = l & 15, kk = l >> 4;
+        double* Pn = ws;
+        W2_STAMP(K);
+        if constexpr (bk == 0) Pn[lc * 4 + kk] = a00[kq];
+        Pn[(16 + lc) * 4 + kk] = (bk == 0) ? a01[kq] : a11[kq];
+        asm volatile("" ::: "memory");   // DS order: the reads below see the panel
+        const f64x2* Pm = reinterpret_cast<const f64x2*>(Pn + 16 * K);
+        const f64x2 c0a = Pm[0], c0b = Pm[1], c1a = Pm[2], c1b = Pm[3], c2b = Pm[5], c3b = Pm[7];
+        const f64x2* Pr = reinterpret_cast<const f64x2*>(Pn);
+        f64x2 u0a = {0.0, 0.0}, u0b = {0.0, 0.0};
+        if constexpr (bk == 0) { u0a = Pr[2 * lc]; u0b = Pr[2 * lc + 1]; }
+        const f64x2 u1a = Pr[2 * (16 + lc)], u1b = Pr[2 * (16 + lc) + 1];
+        __builtin_amdgcn_sched_barrier(0);   // all panel reads in flight before the chain
+        const double m00 = c0a.x, m10 = c0a.y, m20 = c0b.x, m30 = c0b.y;
+        const double m11 = c1a.y, m21 = c1b.x, m31 = c1b.y, m22 = c2b.x, m32 = c2b.y, m33 = c3b.y;
+        const double i0 = rcp_nr(m00);
+        const double L10 = m10 * i0, L20 = m20 * i0, L30 = m30 * i0;
+        const double d1 = fma(-L10, m10, m11);
+        const double i1 = rcp_nr(d1);
+        const double e21 = fma(-L20, m10, m21), e31 = fma(-L30, m10, m31);
+        const double L21 = e21 * i1, L31 = e31 * i1;
+        const double d2 = fma(-L21, e21, fma(-L20, m20, m22));
+        const double i2 = rcp_nr(d2);
+        const double e32 = fma(-L31, e21, fma(-L30, m20, m32));
+        const double L32 = e32 * i2;
+        const double d3 = fma(-L32, e32, fma(-L31, e31, fma(-L30, m30, m33)));
+        const double i3 = rcp_nr(d3);
+        double zA[2], yB[2];
+        f64x2 zlo[2], zhi[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (h < bk) { zA[h] = 0.0; yB[h] = 0.0; zlo[h] = f64x2{0.0, 0.0}; zhi[h] = zlo[h]; continue; }
+            const f64x2 ua = h ? u1a : u0a, ub = h ? u1b : u0b;
+            const bool below = 16 * h + lc > 4 * K + 3;
+            const double y0 = ua.x;
+            const double y1 = fma(-L10, y0, ua.y);
+            const double y2 = fma(-L21, y1, fma(-L20, y0, ub.x));
+            const double y3 = fma(-L32, y2, fma(-L31, y1, fma(-L30, y0, ub.y)));
+            const double z0 = y0 * i0, z1 = y1 * i1, z2 = y2 * i2, z3 = y3 * i3;
+            zA[h] = below ? sel4(kk, z0, z1, z2, z3) : 0.0;
+            yB[h] = sel4(kk, y0, y1, y2, y3);
+            zlo[h] = f64x2{z0, z1};
+            zhi[h] = f64x2{z2, z3};
+        }
+        if constexpr (bk == 0) {
+            a00 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[0], yB[0], a00, 0, 0, 0);
+            a01 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[0], yB[1], a01, 0, 0, 0);
+            a11 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[1], yB[1], a11, 0, 0, 0);
+        } else {
+            a11 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[1], yB[1], a11, 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- hand the round to wave 1 (issued under the MFMA latency)
+        const int* flag = reinterpret_cast<const int*>(ws + W2_FLAG);
+        if constexpr (K >= 4) {
+            w2_wait(flag + 1, K - 3);   // slot K & 3 released by wave 1
+            asm volatile("" ::: "memory");
+        }
+        f64x2* zs = reinterpret_cast<f64x2*>(ws + W2_ZB + (K & 3) * 512);
+#pragma unroll
+        for (int h = bk; h < 2; ++h) {
+            zs[(h * 64 + l) * 2] = zlo[h];
+            zs[(h * 64 + l) * 2 + 1] = zhi[h];
+        }
+        asm volatile("" ::: "memory");
+        if (l == 0) {
+            f64x2* rc = reinterpret_cast<f64x2*>(ws + W2_REC + 12 * K);
+            rc[0] = f64x2{L10, L20};
+            rc[1] = f64x2{L30, L21};
+            rc[2] = f64x2{L31, L32};
+            rc[3] = f64x2{m00, d1};
+            rc[4] = f64x2{d2, d3};
+            asm volatile("" ::: "memory");
+            lds_st_flag(reinterpret_cast<int*>(ws + W2_FLAG), K + 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        w2_round_a<K + 1>(ws, a00, a01, a11, l);
+    }
+}
+
+template <int K>
+__device__ __forceinline__ void w2_round_r(double* __restrict__ ws, f64x4& r00, f64x4& r10, f64x4& r11, int l) {
+    if constexpr (K < 8) {
+        constexpr int bk = K >> 2, kq = K & 3;
+        const int lc = l & 15, kk = l >> 4, p = lc & 3;
+        const int* flag = reinterpret_cast<const int*>(ws + W2_FLAG);
+        w2_wait(flag, K + 1);
+        asm volatile("" ::: "memory");
+        W2_STAMP(8 + K);
+        const f64x2* rc = reinterpret_cast<const f64x2*>(ws + W2_REC + 12 * K);
+        const f64x2 q0 = rc[0], q1 = rc[1], q2 = rc[2];
+        const double L10 = q0.x, L20 = q0.y, L30 = q1.x, L21 = q1.y, L31 = q2.x, L32 = q2.y;
+        const f64x2* zs = reinterpret_cast<const f64x2*>(ws + W2_ZB + (K & 3) * 512);
+        f64x2 zlo[2] = {f64x2{0.0, 0.0}, f64x2{0.0, 0.0}}, zhi[2] = {f64x2{0.0, 0.0}, f64x2{0.0, 0.0}};
+#pragma unroll
+        for (int h = bk; h < 2; ++h) {
+            zlo[h] = zs[(h * 64 + l) * 2];
+            zhi[h] = zs[(h * 64 + l) * 2 + 1];
+        }
+        asm volatile("" ::: "memory");   // DS order: the ack is processed after the reads
+        if (l == 0) lds_st_flag(reinterpret_cast<int*>(ws + W2_FLAG) + 1, K + 1);
+        double wR[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (h < bk) { wR[h] = 0.0; continue; }
+            const int row = 16 * h + lc;
+            const bool piv = (row >> 2) == K;
+            const bool below = row > 4 * K + 3;
+            const double v0 = piv ? (p == 0 ? 1.0 : 0.0) : zlo[h].x;
+            const double v1 = piv ? (p == 1 ? 1.0 : 0.0) : zlo[h].y;
+            const double v2 = piv ? (p == 2 ? 1.0 : 0.0) : zhi[h].x;
+            const double v3 = piv ? (p == 3 ? 1.0 : 0.0) : zhi[h].y;
+            const double x3 = v3;
+            const double x2 = fma(-L32, x3, v2);
+            const double x1 = fma(-L31, x3, fma(-L21, x2, v1));
+            const double x0 = fma(-L30, x3, fma(-L20, x2, fma(-L10, x1, v0)));
+            const double xk = sel4(kk, x0, x1, x2, x3);
+            wR[h] = below ? xk : piv ? ((p == kk ? 1.0 : 0.0) - xk) : 0.0;
+        }
+        if constexpr (bk == 0) {
+            const double pR0 = r00[kq];
+            r00 = __builtin_amdgcn_mfma_f64_16x16x4f64(-wR[0], pR0, r00, 0, 0, 0);
+            r10 = __builtin_amdgcn_mfma_f64_16x16x4f64(-wR[1], pR0, r10, 0, 0, 0);
+        } else {
+            const double pR0 = r10[kq], pR1 = r11[kq];
+            r10 = __builtin_amdgcn_mfma_f64_16x16x4f64(-wR[1], pR0, r10, 0, 0, 0);
+            r11 = __builtin_amdgcn_mfma_f64_16x16x4f64(-wR[1], pR1, r11, 0, 0, 0);
+        }
+        w2_round_r<K + 1>(ws, r00, r10, r11, l);
+    }
+}
+
+// Entry with the tile in accumulator layout (wave w holds block (w>>1, w&1) of a symmetric
+// tile whose lower triangle is valid).  ws: W2_WS doubles of LDS, not aliasing R / dg; the
+// caller's reads of ws before the call are fenced here by a barrier.
+__device__ __forceinline__ void tile_potrf_inv_w2_acc(f64x4 aA, double* __restrict__ ws, double* __restrict__ R,
+                                                      double* __restrict__ dg, int* __restrict__ bad) {
+    constexpr int LX = 33;
+    constexpr int S = TileCfg<32>::S;
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    const int bi = w >> 1, bj = w & 1, lc = l & 15, lr = l >> 4;
+    __syncthreads();   // ws may alias tiles the caller's waves were still reading
+    if (bj <= bi) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ws[(16 * bi + lr + 4 * q) * LX + 16 * bj + lc] = aA[q];
+    }
+    if (t == 0) {
+        int* flag = reinterpret_cast<int*>(ws + W2_FLAG);
+        flag[0] = 0;
+        flag[1] = 0;
+    }
+    __syncthreads();
+    if (w == 0) {
+        f64x4 a00, a01, a11;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int r = lr + 4 * q;
+            const int hi = r > lc ? r : lc, lo = r > lc ? lc : r;
+            a00[q] = ws[hi * LX + lo];
+            a11[q] = ws[(16 + hi) * LX + 16 + lo];
+            a01[q] = ws[(16 + lc) * LX + r];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // X read before the panel / ring overwrite it
+        w2_round_a<0>(ws, a00, a01, a11, l);
+        W2_STAMP(16);
+    } else if (w == 1) {
+        f64x4 r00, r10 = {0.0, 0.0, 0.0, 0.0}, r11;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            r00[q] = (lr + 4 * q == lc) ? 1.0 : 0.0;
+            r11[q] = r00[q];
+        }
+        w2_round_r<0>(ws, r00, r10, r11, l);
+        W2_STAMP(17);
+        // L^{-1} = diag(d)^{-1/2} L_u^{-1}; L_ii = sqrt(d_i); first bad pivot by one ballot
+        const double* rec = ws + W2_REC;
+        double s0[4], s1[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int r0 = lr + 4 * q, r1 = 16 + r0;
+            s0[q] = rcp_nr(sqrt(rec[12 * (r0 >> 2) + 6 + (r0 & 3)]));
+            s1[q] = rcp_nr(sqrt(rec[12 * (r1 >> 2) + 6 + (r1 & 3)]));
+        }
+        const int li = l & 31;
+        const double dl = rec[12 * (li >> 2) + 6 + (li & 3)];
+        const unsigned long long m = __ballot(l < 32 && !(dl > 0.0 && dl < INFINITY));
+        if (l < 32) dg[l] = sqrt(dl);
+        if (l == 0) *bad = m ? __ffsll((long long)m) : 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int r = lr + 4 * q;
+            R[r * S + lc] = (lc <= r) ? r00[q] * s0[q] : 0.0;
+            R[r * S + 16 + lc] = 0.0;
+            R[(16 + r) * S + lc] = r10[q] * s1[q];
+            R[(16 + r) * S + 16 + lc] = (lc <= r) ? r11[q] * s1[q] : 0.0;
+        }
+    }
+    __syncthreads();
+}
+
+// NB = 32 uses the single-wave form (9.1k shader clocks vs 12.7k for the 4-wave MFMA 4-pivot
+// form and 15.5k for the pivot form: tools/ubench_w1.hip, tools/ubench_tile.hip).
 template <>
 __device__ __forceinline__ void tile_potrf_inv<32>(double* __restrict__ A, double* __restrict__ R,
                                                    double* __restrict__ dg, int* __restrict__ bad) {
-    tile_potrf_inv_m4(A, R, dg, bad);
+    tile_potrf_inv_w1(A, R, dg, bad);
 }
 
 // ---------------------------------------------------------------- blocked diag factor

@@ -273,7 +273,7 @@ __global__ __launch_bounds__(NTHREADS) void k_chol_step(CholArgs a) {
         if (i == j && i == k + 1) {
             // next diagonal tile is final: factor it and publish D_{k+1}
             if constexpr (NB == 32) {
-                tile_potrf_inv_m4_acc(acc.v[0], T0, Pj, dg, &bad);   // straight from registers
+                tile_potrf_inv_w1_acc(acc.v[0], T0, Pj, dg, &bad);   // straight from registers
             } else {
                 acc_to_lds(acc, T0);
                 __syncthreads();
