@@ -215,6 +215,23 @@ __device__ __forceinline__ double rcp_nr(double a) {
     return fma(r, e, r);
 }
 
+// 1/a by v_rcp_f64 + ONE Newton step (v_rcp_f64 is 4.6e-8 relative, one step 2.2e-15:
+// tools/ubench_rcp.hip); for the pivot chain of the diagonal factor.
+__device__ __forceinline__ double rcp_nr1(double a) {
+    const double r = __builtin_amdgcn_rcp(a);
+    return fma(r, fma(-a, r, 1.0), r);
+}
+// 1/sqrt(a) by v_rsq_f64 + two Newton steps y <- y (1 + (1 - a y^2) / 2).
+__device__ __forceinline__ double rsq_nr(double a) {
+    double y = __builtin_amdgcn_rsq(a);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+        const double e = fma(-a * y, y, 1.0);
+        y = fma(0.5 * y, e, y);
+    }
+    return y;
+}
+
 // ---------------------------------------------------------------- parameter transforms
 __device__ __forceinline__ double tf_softplus(double x) {
     // tensorflow/core/kernels/softplus_op.h
@@ -748,8 +765,10 @@ __device__ __forceinline__ void w1_round(double* __restrict__ Pn, double* __rest
         // ---- LDL^T of M
 #if W1_ABL & 1
 #define W1RCP(x) __builtin_amdgcn_rcp(x)
-#else
+#elif W1_ABL & 2
 #define W1RCP(x) rcp_nr(x)
+#else
+#define W1RCP(x) rcp_nr1(x)
 #endif
         const double i0 = W1RCP(m00);
         const double L10 = m10 * i0, L20 = m20 * i0, L30 = m30 * i0;
@@ -783,10 +802,13 @@ __device__ __forceinline__ void w1_round(double* __restrict__ Pn, double* __rest
             yB[h] = sel4(kk, y0, y1, y2, y3);
             zs[h][0] = z0; zs[h][1] = z1; zs[h][2] = z2; zs[h][3] = z3;
         }
-        // ---- rank-4 update of A on the matrix core
+        // ---- rank-4 update of A on the matrix core (an f64 MFMA holds the SIMD for 64 clocks,
+        //      f64 VALU included: after round 3 rows 0..15 are final, so A00 / A01 are skipped)
         if constexpr (bk == 0) {
-            a00 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[0], yB[0], a00, 0, 0, 0);
-            a01 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[0], yB[1], a01, 0, 0, 0);
+            if constexpr (K < 3) {
+                a00 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[0], yB[0], a00, 0, 0, 0);
+                a01 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[0], yB[1], a01, 0, 0, 0);
+            }
             a11 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[1], yB[1], a11, 0, 0, 0);
         } else {
             a11 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[1], yB[1], a11, 0, 0, 0);
@@ -836,12 +858,12 @@ __device__ __forceinline__ void tile_potrf_inv_w1_core(const double* __restrict_
         double s0[4], s1[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            s0[q] = rcp_nr(sqrt(dpv[lr + 4 * q]));
-            s1[q] = rcp_nr(sqrt(dpv[16 + lr + 4 * q]));
+            s0[q] = rsq_nr(dpv[lr + 4 * q]);
+            s1[q] = rsq_nr(dpv[16 + lr + 4 * q]);
         }
         const double dl = dpv[l & 31];
         const unsigned long long m = __ballot(l < 32 && !(dl > 0.0 && dl < INFINITY));
-        if (l < 32) dg[l] = sqrt(dl);
+        if (l < 32) dg[l] = dl * rsq_nr(dl);
         if (l == 0) *bad = m ? __ffsll((long long)m) : 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
