@@ -44,6 +44,8 @@ typedef struct mfgp_handle_s* mfgp_handle_t;
 #define MFGP_ERR_LAUNCH (-3)
 #define MFGP_ERR_DIM (-4)
 #define MFGP_MAX_D 32
+/* info value written when the persistent Cholesky launch gave up waiting (bounded spin) */
+#define MFGP_FLOW_TIMEOUT (-100)
 
 int mfgp_version(void);
 const char* mfgp_error_string(int code);
@@ -55,6 +57,17 @@ int mfgp_destroy(mfgp_handle_t h);
 int mfgp_set_stream(mfgp_handle_t h, void* hip_stream);
 int mfgp_set_tile(mfgp_handle_t h, int nb);
 int mfgp_get_tile(mfgp_handle_t h);
+/* Cholesky schedule of the LML path (tile 32): 1 = one persistent dataflow launch
+ * (k_chol_flow, default when the device reports its CU count), 0 = one launch per tile step.
+ * Results agree to rounding; a workspace must be sized under the setting it is used with. */
+int mfgp_set_flow(mfgp_handle_t h, int enable);   /* 2: flow + diagnostic timeline */
+int mfgp_get_flow(mfgp_handle_t h);
+/* Where the flow timeline sits inside an mfgp_gpr_* workspace (diagnostic): `count` int64
+ * ticks of the 100 MHz device clock from byte `offset`: per step k the diag workgroup's step
+ * start [k], A' ready [T+k], factor start [2T+k], D_k published [3T+k], owner hand-offs of
+ * A(k,k-2) [4T+k], A(k,k-1) [5T+k], A(k,k) [6T+k] seen, L(k,k-2) formed [7T+k]; then per
+ * worker wave w: first item [8T+3w], done [8T+3w+1], ticks spent waiting [8T+3w+2]. */
+int mfgp_gpr_flow_trace(mfgp_handle_t h, int n, int p, int d, size_t* offset, int* count);
 
 /* gpflow.kernels.SquaredExponential.K(X1, X2) (GPflow 2.9 stationaries.py via
  * utilities/ops.py:square_distance).  params = [variance, lengthscales[d]]. */

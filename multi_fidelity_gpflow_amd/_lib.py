@@ -28,6 +28,9 @@ SIGNATURES = {
     "mfgp_set_stream": [_p, _p],
     "mfgp_set_tile": [_p, _i],
     "mfgp_get_tile": [_p],
+    "mfgp_set_flow": [_p, _i],
+    "mfgp_get_flow": [_p],
+    "mfgp_gpr_flow_trace": [_p, _i, _i, _i, C.POINTER(C.c_size_t), C.POINTER(_i)],
     "mfgp_rbf_gram": [_p, _i, _i, _i, _p, _i, _p, _i, _p, _p, _i],
     "mfgp_mf_gram": [_p, _i, _i, _i, _p, _i, _p, _i, _p, _d, _p, _i],
     "mfgp_mf_kdiag": [_p, _i, _i, _p, _i, _p, _p],
@@ -68,9 +71,11 @@ class MFGPError(RuntimeError):
     pass
 
 
-def load(path: str = LIB_PATH):
-    """Load libmfgp.so (no compute; safe without a GPU)."""
+def load(path: str = None):
+    """Load libmfgp.so (no compute; safe without a GPU).  MFGP_LIB_PATH points at an
+    alternative in-tree build (diagnostic A/B of compile-time variants)."""
     global _lib
+    path = path or os.environ.get("MFGP_LIB_PATH") or LIB_PATH
     with _lock:
         if _lib is None:
             if not os.path.exists(path):

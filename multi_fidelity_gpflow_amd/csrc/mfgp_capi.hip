@@ -11,12 +11,16 @@
 #include "../../include/mfgp.h"
 #include "mfgp_device.h"
 #include "mfgp_internal.h"
+#include "mfgp_flow.h"
 
 struct mfgp_handle_s {
     int device;
     hipStream_t stream;
     int nb;
     int grad_chunk;
+    int flow_wgs;   // k_chol_flow grid (one workgroup per CU); 0: launch-per-step Cholesky
+    int ncu;        // compute units of the device
+    int flow_trace; // k_chol_flow writes its diagnostic timeline into the workspace
 };
 
 namespace mfgp {
@@ -44,10 +48,25 @@ struct GprLayout {
     int* gorder;   // k_grad workgroup -> task table, built by k_gram each call
     int* cnt;   // reduce-arrival counter, zeroed by k_gram each call
     int ncnt;
+    // k_chol_flow (flow_wgs > 0): flags + owner table, both rebuilt by k_gram each call
+    int flow_wgs, nflags;
+    int *flags, *own;
+    double* pub;        // publication area (sentinel-filled by k_gram)
+    long npub;
+    long long* trace;   // k_chol_flow timeline (diagnostic; written only when enabled)
+    int ntrace;
     size_t bytes;
 };
 
-static GprLayout gpr_layout(int nb, int n, int p, int d, void* ws, int grad_chunk, int nlf = 0) {
+// The persistent Cholesky needs every workgroup resident (one per CU) and the owner table
+// to hold every tile; otherwise the launch-per-step sequence runs.
+static int flow_grid(int nb, int T, int Tp, int flow_wgs) {
+    if (nb != 32 || flow_wgs < 2 || T > 255) return 0;
+    if (flow_ntiles(T, Tp) > FLOW_WAVES * (flow_wgs - 1) * FLOW_MAXOWN) return 0;
+    return flow_wgs;
+}
+
+static GprLayout gpr_layout(int nb, int n, int p, int d, void* ws, int grad_chunk, int nlf = 0, int flow_wgs = 0) {
     GprLayout L;
     L.nb = nb;
     L.T = ceil_div(n, nb);
@@ -71,6 +90,14 @@ static GprLayout gpr_layout(int nb, int n, int p, int d, void* ws, int grad_chun
     L.ncnt = 1;
     L.cnt = c.take<int>((size_t)L.ncnt);
     L.gorder = c.take<int>((size_t)L.ng);
+    L.flow_wgs = flow_grid(nb, L.T, L.Tp, flow_wgs);
+    L.nflags = L.flow_wgs ? flow_nflags(L.T, L.Tp) : 0;
+    L.flags = c.take<int>((size_t)L.nflags * FLOW_FSTRIDE);
+    L.npub = L.flow_wgs ? flow_npub(L.T, L.Tp) : 0;
+    L.pub = c.take<double>((size_t)L.npub);
+    L.own = c.take<int>(L.flow_wgs ? (size_t)FLOW_WAVES * (L.flow_wgs - 1) * FLOW_MAXOWN : 0);
+    L.ntrace = L.flow_wgs ? flow_trace_count(L.T, L.flow_wgs) : 0;
+    L.trace = c.take<long long>((size_t)L.ntrace);
     L.bytes = c.off + 256;
     return L;
 }
@@ -110,7 +137,7 @@ template <int NB>
 static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X, int ldx, const double* Y, int ldy,
                           double* theta, int want_grad, void* ws, size_t ws_bytes, double* out, int* info,
                           const FinArgs* adam, PhaseMarks* pm = nullptr, int nlf = 0) {
-    const GprLayout L = gpr_layout(NB, n, p, d, ws, h->grad_chunk, nlf);
+    const GprLayout L = gpr_layout(NB, n, p, d, ws, h->grad_chunk, nlf, h->flow_wgs);
     if (ws_bytes < L.bytes) return MFGP_ERR_WORKSPACE;
     hipStream_t s = h->stream;
     const long ldr = L.npad + L.ppad;
@@ -128,10 +155,23 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
         g.cnt = L.cnt; g.ncnt = L.ncnt;
         const bool order = want_grad && h->grad_chunk + L.Tp < 2048;   // gram LDS holds the histogram
         if (order) { g.gorder = L.gorder; g.gT = L.T; g.gchunk = h->grad_chunk; g.gTp = L.Tp; }
-        launch_gram<NB>(g, L.T * (L.T + 1) / 2 + (order ? 1 : 0), 1, s);
+        if (L.flow_wgs) { g.fown = L.own; g.fW = FLOW_WAVES * (L.flow_wgs - 1); g.fflags = L.flags; g.nfflags = L.nflags; g.fpub = L.pub; g.npub = L.npub; }
+        launch_gram<NB>(g, L.T * (L.T + 1) / 2 + (order ? 1 : 0) + (L.flow_wgs ? 1 : 0), 1, s);
     }
     if (pm) pm->mark(s);
-    {
+    if (L.flow_wgs) {
+        FlowArgs fa{};
+        fa.A = L.A; fa.lda = L.npad;
+        fa.R = L.R; fa.ldr = ldr;
+        fa.Xo = L.Xo; fa.ldx = ldr;
+        fa.Dd = L.Dd; fa.ldiag = L.ldiag; fa.info = info;
+        fa.alpha = L.alpha; fa.ldal = L.ppad; fa.zpart = L.zpart;
+        fa.flags = L.flags; fa.own = L.own; fa.pub = L.pub;
+        fa.T = L.T; fa.Tp = L.Tp; fa.n = n; fa.p = p;
+        fa.trace = h->flow_trace ? L.trace : nullptr;
+        fa.nwaves = FLOW_WAVES * (L.flow_wgs - 1);
+        launch_chol_flow(fa, L.flow_wgs, s);
+    } else {
         CholArgs c{};
         c.A = L.A; c.lda = L.npad; c.sA = 0;
         c.R = L.R; c.ldr = ldr; c.sR = 0;
@@ -363,6 +403,11 @@ int mfgp_create(int device, mfgp_handle_t* out) {
     h->stream = nullptr;
     h->nb = 32;
     h->grad_chunk = 24;   // k_grad m-tiles per task (sweep at Goku T = 37: 16 -> 33.8 us, 24 -> 31.9, 40 -> 36.7)
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 0;
+    h->ncu = ncu;
+    h->flow_wgs = ncu;
+    if (const char* fl = getenv("MFGP_FLOW")) if (atoi(fl) == 0) h->flow_wgs = 0;
     if (const char* gc = getenv("MFGP_GRAD_CHUNK")) h->grad_chunk = std::max(1, atoi(gc));
     const char* env = getenv("MFGP_TILE");
     if (env && atoi(env) == 64) h->nb = 64;
@@ -389,6 +434,27 @@ int mfgp_set_tile(mfgp_handle_t h, int nb) {
 }
 
 int mfgp_get_tile(mfgp_handle_t h) { return h ? h->nb : MFGP_ERR_ARG; }
+
+int mfgp_set_flow(mfgp_handle_t h, int enable) {
+    CHECK_H(h);
+    if (enable < 0 || enable > 2) return MFGP_ERR_ARG;
+    h->flow_wgs = enable ? h->ncu : 0;
+    h->flow_trace = enable == 2;
+    return MFGP_OK;
+}
+
+int mfgp_gpr_flow_trace(mfgp_handle_t h, int n, int p, int d, size_t* offset, int* count) {
+    CHECK_H(h);
+    CHECK_D(d);
+    if (n < 1 || p < 1 || !offset || !count) return MFGP_ERR_ARG;
+    char* const base = reinterpret_cast<char*>((uintptr_t)1 << 20);   // any 256-B aligned stand-in
+    const GprLayout L = gpr_layout(h->nb, n, p, d, base, h->grad_chunk, 0, h->flow_wgs);
+    *offset = (size_t)(reinterpret_cast<char*>(L.trace) - base);
+    *count = L.ntrace;
+    return MFGP_OK;
+}
+
+int mfgp_get_flow(mfgp_handle_t h) { return h ? (h->flow_wgs > 0 ? 1 : 0) : MFGP_ERR_ARG; }
 
 static int gram_common(mfgp_handle_t h, int n1, int n2, int d, const double* X1, int ldx1, const double* X2,
                        int ldx2, const double* params, double diag_add, double* K, int ldk, int rbf, int nlf = 0) {
@@ -455,7 +521,7 @@ int mfgp_gmf_gpr_workspace_size(mfgp_handle_t h, int nlf, int n, int p, int d, s
     CHECK_D(d);
     CHECK_LF(nlf);
     if (n < 1 || p < 1 || !bytes) return MFGP_ERR_ARG;
-    *bytes = gpr_layout(h->nb, n, p, d, nullptr, h->grad_chunk, nlf).bytes;
+    *bytes = gpr_layout(h->nb, n, p, d, nullptr, h->grad_chunk, nlf, h->flow_wgs).bytes;
     return MFGP_OK;
 }
 
@@ -501,7 +567,7 @@ int mfgp_gpr_workspace_size(mfgp_handle_t h, int n, int p, int d, size_t* bytes)
     CHECK_H(h);
     CHECK_D(d);
     if (n < 1 || p < 1 || !bytes) return MFGP_ERR_ARG;
-    *bytes = gpr_layout(h->nb, n, p, d, nullptr, h->grad_chunk).bytes;
+    *bytes = gpr_layout(h->nb, n, p, d, nullptr, h->grad_chunk, 0, h->flow_wgs).bytes;
     return MFGP_OK;
 }
 

@@ -832,12 +832,13 @@ __device__ __forceinline__ void w1_round(double* __restrict__ Pn, double* __rest
     }
 }
 
-__device__ __forceinline__ void tile_potrf_inv_w1_core(const double* __restrict__ X, int ldx, double* __restrict__ Pn,
+// Body run by ONE wave (any wave of the workgroup; no workgroup barrier inside).
+__device__ __forceinline__ void tile_potrf_inv_w1_wave(const double* __restrict__ X, int ldx, double* __restrict__ Pn,
                                                        double* __restrict__ R, double* __restrict__ dg,
                                                        int* __restrict__ bad) {
     constexpr int S = TileCfg<32>::S;
-    if (threadIdx.x < 64) {
-        const int l = threadIdx.x, lc = l & 15, lr = l >> 4;
+    {
+        const int l = threadIdx.x & 63, lc = l & 15, lr = l >> 4;
         f64x4 a00, a01, a11, r00, r10 = {0.0, 0.0, 0.0, 0.0}, r11;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -874,6 +875,12 @@ __device__ __forceinline__ void tile_potrf_inv_w1_core(const double* __restrict_
             R[(16 + r) * S + 16 + lc] = (lc <= r) ? r11[q] * s1[q] : 0.0;
         }
     }
+}
+
+__device__ __forceinline__ void tile_potrf_inv_w1_core(const double* __restrict__ X, int ldx, double* __restrict__ Pn,
+                                                       double* __restrict__ R, double* __restrict__ dg,
+                                                       int* __restrict__ bad) {
+    if (threadIdx.x < 64) tile_potrf_inv_w1_wave(X, ldx, Pn, R, dg, bad);
     __syncthreads();
 }
 

@@ -1,0 +1,102 @@
+// Tile catalogue and owner table of the persistent dataflow Cholesky (k_chol_flow,
+// mfgp_flow.hip).  Header-only: k_gram's extra workgroup builds the owner table.
+#pragma once
+#include "mfgp_device.h"
+#include "mfgp_internal.h"
+
+namespace mfgp {
+
+// ---------------------------------------------------------------- tile catalogue
+// code = type << 20 | i << 10 | j ; R tiles use j = column tile c in [0, T + Tp)
+enum : int { FT_A = 0, FT_R = 1, FT_AL = 2 };
+__host__ __device__ inline int flow_code(int type, int i, int j) { return (type << 20) | (i << 10) | j; }
+
+__host__ __device__ inline void flow_tri(int t, int& i, int& j) {   // row-major lower triangle
+    int r = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+    while ((r + 1) * (r + 2) / 2 <= t) ++r;
+    while (r * (r + 1) / 2 > t) --r;
+    i = r;
+    j = t - r * (r + 1) / 2;
+}
+
+// Owned A tiles: every lower tile except (0,0) (k_gram) and (1,0) .. (2,2) (the diag
+// workgroup works on their initial values).
+__host__ __device__ inline int flow_nA(int T) { return T >= 3 ? T * (T + 1) / 2 - 6 : 0; }
+__host__ __device__ inline int flow_ntiles(int T, int Tp) {
+    return flow_nA(T) + T * (T - 1) / 2 + 2 * T * Tp;
+}
+
+__device__ inline int flow_decode(int g, int T, int Tp) {
+    const int nA = flow_nA(T);
+    int i, j;
+    if (g < nA) { flow_tri(g + 6, i, j); return flow_code(FT_A, i, j); }
+    g -= nA;
+    const int nR = T * (T - 1) / 2;
+    if (g < nR) { flow_tri(g, i, j); return flow_code(FT_R, i + 1, j); }
+    g -= nR;
+    if (g < T * Tp) return flow_code(FT_R, g / Tp, T + g % Tp);
+    g -= T * Tp;
+    return flow_code(FT_AL, g / Tp, g % Tp);
+}
+
+// items of a tile: updates at levels [lo, hi] (hi < lo: none), finalize at level fin (-1: none),
+// pub: the last update hands the tile to the diag workgroup
+struct FlowTile {
+    int type, i, j, lo, hi, fin, pub;
+};
+__host__ __device__ inline FlowTile flow_tile(int code, int T) {
+    FlowTile t;
+    t.type = code >> 20;
+    t.i = (code >> 10) & 1023;
+    t.j = code & 1023;
+    t.pub = 0;
+    if (t.type == FT_A) {
+        t.lo = 0;
+        // (k,k), (k,k-1): panels < k-2;  (k,k-2): all its panels (< k-2), finalized by diag
+        if (t.i <= t.j + 2) { t.hi = t.i - 3; t.fin = -1; t.pub = 1; }
+        else { t.hi = t.j - 1; t.fin = t.j; }
+    } else if (t.type == FT_R) {
+        t.lo = (t.j < T) ? t.j : 0;
+        t.hi = t.i - 1;
+        t.fin = t.i;
+    } else {
+        t.lo = t.i;
+        t.hi = T - 1;
+        t.fin = -1;
+    }
+    return t;
+}
+__host__ __device__ inline int flow_items(int code, int T) {
+    const FlowTile t = flow_tile(code, T);
+    return (t.hi >= t.lo ? t.hi - t.lo + 1 : 0) + (t.fin >= 0 ? 1 : 0);
+}
+
+// Owner table: tiles by descending item count, dealt in snake order over the W worker waves
+// (slot r of wave w).  Run by ONE workgroup (k_gram's extra workgroup) before the flow launch;
+// it also zeroes the flags.  sh: >= 256 ints of LDS.
+__device__ inline void build_flow_owner(int T, int Tp, int W, int* own, int* flags, int nflags, int* sh) {
+    int* hist = sh;          // [128] count per item count, then the start of its rank range
+    int* cur = sh + 128;     // [128]
+    for (int e = threadIdx.x; e < 128; e += NTHREADS) { hist[e] = 0; cur[e] = 0; }
+    for (int e = threadIdx.x; e < W * FLOW_MAXOWN; e += NTHREADS) own[e] = -1;
+    for (int e = threadIdx.x; e < nflags; e += NTHREADS) flags[e * FLOW_FSTRIDE] = 0;
+    __syncthreads();
+    const int n = flow_ntiles(T, Tp);
+    for (int g = threadIdx.x; g < n; g += blockDim.x) atomicAdd(&hist[flow_items(flow_decode(g, T, Tp), T)], 1);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int s = 0;
+        for (int L = 127; L >= 0; --L) { const int c = hist[L]; hist[L] = s; s += c; }
+    }
+    __syncthreads();
+    for (int g = threadIdx.x; g < n; g += blockDim.x) {
+        const int code = flow_decode(g, T, Tp);
+        const int L = flow_items(code, T);
+        const int p = hist[L] + atomicAdd(&cur[L], 1);
+        const int r = p / W, q = p % W;
+        const int w = (r & 1) ? W - 1 - q : q;
+        if (r < FLOW_MAXOWN) own[w * FLOW_MAXOWN + r] = code;
+    }
+}
+
+}  // namespace mfgp

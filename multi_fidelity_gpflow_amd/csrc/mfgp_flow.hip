@@ -1,0 +1,751 @@
+// K2f k_chol_flow: the LML-path tile Cholesky, its inverse factor L^{-1}, the forward solve
+// Z = L^{-1} Y and alpha = L^{-T} Z as ONE persistent dataflow launch (gfx950, NB = 32).
+//
+// Same arithmetic as the launch-per-step k_chol_step sequence (mfgpflow/linear.py:138-153 ->
+// GPflow GPR.log_marginal_likelihood: L = chol(K + s2 I), then the triangular solves), without
+// the T step boundaries: at Goku (T = 37) each step launch costs ~9.4 us although the dependent
+// chain inside it (the next diagonal tile's update and its factor) is ~4 us.
+//
+// Roles.  One workgroup per CU (the dynamic LDS is sized so that two never share one), so every
+// workgroup of the grid is resident and a wait never depends on an unscheduled workgroup.
+//   * workgroup 0 ("diag", 8 waves) runs the chain, see diag_chain below;
+//   * every wave of workgroups 1.. ("workers") owns up to FLOW_MAXOWN output tiles (table built
+//     by k_gram's extra workgroup: tiles sorted by item count, snake-dealt over the waves) and
+//     runs their items level by level -- at level l first the finalize items (need D_l), then
+//     the update items (need panel l):
+//       A(i,j)  : A -= L(i,l) L(j,l)^T for l < j, then L(i,j) = A D_j^T at level j; the tiles
+//                 (k,k), (k,k-1), (k,k-2) stop after level k-3 and hand A' to diag;
+//       R(i,c)  : R -= L(i,l) X(l,c) for c <= l < i, then X(i,c) = D_i R at level i
+//                 (c < T: rows of L^{-1};  c >= T: Y column tiles, X = Z);
+//       al(c,y) : alpha(c,y) += X(l,c)^T Z(l,y) for l >= c.
+//   A wave keeps its running tile in the global array it lives in (only it touches it).
+//
+// Hand-offs: the data is the flag.  Every tile another wave reads is published ONCE per launch
+// into its own slot of the publication area (FlowPub), which k_gram fills with a signalling-NaN
+// sentinel before this launch.  A producer stores the tile with agent-scope relaxed atomics
+// (8-B global_store ... sc1: untorn, write-through) and moves on -- no drain, no flag; a
+// consumer loads it with sc1 loads until no element is the sentinel (wave ballot).  Computed
+// NaNs are quiet, so the signalling pattern never occurs as data.  One memory round trip per
+// hop instead of three (flag poll, payload, producer drain); cdna_hip_programming.md
+// Guideline 16, R2 (data-tagged granules).
+// Published X tiles are stored transposed (X^T) so that every MFMA operand is a row-major read
+// along the contraction index: lane (li, lq) loads 8 consecutive doubles of row 16b + li,
+// contraction indices 8 lq .. 8 lq + 7 (the k order inside an MFMA sum is free).
+// Every wait is bounded (FLOW_TIMEOUT_TICKS of the 100 MHz realtime clock): on expiry the wave
+// raises the abort word, writes info = MFGP_FLOW_TIMEOUT and runs on, so the grid drains.
+#include "../../include/mfgp.h"
+#include "mfgp_device.h"
+#include "mfgp_internal.h"
+#include "mfgp_flow.h"
+
+namespace mfgp {
+
+constexpr long long FLOW_TIMEOUT_TICKS = 5000000;   // 50 ms (s_memrealtime is 100 MHz)
+#ifndef FLOW_SLEEP
+#define FLOW_SLEEP 1
+#endif
+constexpr int WLD = 33;                              // per-wave LDS tile stride (doubles)
+
+__device__ __forceinline__ long long flow_clock() { return __builtin_amdgcn_s_memrealtime(); }
+
+// ---------------------------------------------------------------- single-wave 32x32 tiles
+// Accumulator: c[bi][bj][r] = C[16 bi + lq + 4 r][16 bj + li]   (li = lane & 15, lq = lane >> 4)
+struct WTile {
+    f64x4 v[2][2];
+};
+// MFMA operand: o[b][s] = M[16 b + li][8 lq + s]  (row-major M read along the contraction index)
+struct WOp {
+    double v[2][8];
+};
+
+__device__ __forceinline__ void wt_zero(WTile& t) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) t.v[a][b] = f64x4{0.0, 0.0, 0.0, 0.0};
+}
+template <bool SC1>
+__device__ __forceinline__ void wt_load(WTile& t, const double* P, long ld) {
+    const int li = threadIdx.x & 15, lq = (threadIdx.x >> 4) & 3;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double* q = P + (long)(16 * a + lq + 4 * r) * ld + 16 * b + li;
+                t.v[a][b][r] = SC1 ? ld_coherent(q) : *q;
+            }
+}
+template <bool SC1>
+__device__ __forceinline__ void wt_store(const WTile& t, double* P, long ld) {
+    const int li = threadIdx.x & 15, lq = (threadIdx.x >> 4) & 3;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                double* q = P + (long)(16 * a + lq + 4 * r) * ld + 16 * b + li;
+                if (SC1) st_coherent(q, t.v[a][b][r]);
+                else *q = t.v[a][b][r];
+            }
+}
+// P[col][row] = C[row][col], sc1
+__device__ __forceinline__ void wt_store_t_sc1(const WTile& t, double* P, long ld) {
+    const int li = threadIdx.x & 15, lq = (threadIdx.x >> 4) & 3;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) st_coherent(P + (long)(16 * b + li) * ld + 16 * a + lq + 4 * r, t.v[a][b][r]);
+}
+template <bool SC1>
+__device__ __forceinline__ void op_load(WOp& o, const double* P, long ld) {
+    const int li = threadIdx.x & 15, lq = (threadIdx.x >> 4) & 3;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        const double* q = P + (long)(16 * b + li) * ld + 8 * lq;
+        if (SC1) {
+#pragma unroll
+            for (int s = 0; s < 8; ++s) o.v[b][s] = ld_coherent(q + s);
+        } else {
+#pragma unroll
+            for (int s = 0; s < 8; s += 2) {
+                const f64x2 x = *reinterpret_cast<const f64x2*>(q + s);
+                o.v[b][s] = x.x;
+                o.v[b][s + 1] = x.y;
+            }
+        }
+    }
+}
+// C (+)= sgn * A B with A[i][k] = a(i,k), B[k][j] = b(j,k) in operand form
+template <bool NEG>
+__device__ __forceinline__ void wt_mma(WTile& c, const WOp& a, const WOp& b) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int bj = 0; bj < 2; ++bj)
+                c.v[bi][bj] = __builtin_amdgcn_mfma_f64_16x16x4f64(NEG ? -a.v[bi][s] : a.v[bi][s], b.v[bj][s],
+                                                                   c.v[bi][bj], 0, 0, 0);
+}
+// accumulator -> per-wave LDS tile (row-major, stride WLD)
+__device__ __forceinline__ void wt_to_lds(const WTile& t, double* S) {
+    const int li = threadIdx.x & 15, lq = (threadIdx.x >> 4) & 3;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) S[(16 * a + lq + 4 * r) * WLD + 16 * b + li] = t.v[a][b][r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+}
+// operand o[b][s] = M[16 b + li][8 lq + s] from the LDS tile M  (M as the A side)
+__device__ __forceinline__ void op_rows_lds(WOp& o, const double* S) {
+    const int li = threadIdx.x & 15, lq = (threadIdx.x >> 4) & 3;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int s = 0; s < 8; ++s) o.v[b][s] = S[(16 * b + li) * WLD + 8 * lq + s];
+}
+// operand o[b][s] = M[8 lq + s][16 b + li] from the LDS tile M  (M as the B side, untransposed)
+__device__ __forceinline__ void op_cols_lds(WOp& o, const double* S) {
+    const int li = threadIdx.x & 15, lq = (threadIdx.x >> 4) & 3;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int s = 0; s < 8; ++s) o.v[b][s] = S[(8 * lq + s) * WLD + 16 * b + li];
+}
+__device__ __forceinline__ double wave_sum64(double v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+
+// ---------------------------------------------------------------- publication area
+// Tiles (32 x 32 row-major) in one sentinel-filled region: L(i,j) i > j | D_k | X^T(i,c)
+// (c <= i < T, then the T x Tp Y column tiles) | hand-offs A'(k,k-1), A'(k,k), A'(k,k-2).
+struct FlowPub {
+    double* base;
+    int T, Tp;
+    __device__ double* tile(long idx) const { return base + idx * 1024; }
+    __device__ int nL() const { return T * (T - 1) / 2; }
+    __device__ int nX() const { return T * (T + 1) / 2 + T * Tp; }
+    __device__ double* L(int i, int j) const { return tile(i * (i - 1) / 2 + j); }
+    __device__ double* D(int k) const { return tile(nL() + k); }
+    __device__ double* X(int i, int c) const {
+        return tile(nL() + T + (c < T ? i * (i + 1) / 2 + c : T * (T + 1) / 2 + i * Tp + (c - T)));
+    }
+    __device__ double* H(int kind, int k) const { return tile(nL() + T + nX() + 3 * k + kind); }   // 0: (k,k-1) 1: (k,k) 2: (k,k-2)
+};
+
+struct FlowCtx {
+    FlowArgs a;
+    FlowPub P;
+    long long t0;
+    long long waited;   // worker: ticks spent re-polling (trace only)
+    __device__ double* At(int i, int j) const { return a.A + (long)i * 32 * a.lda + (long)j * 32; }
+    __device__ double* Rt(int i, int c) const { return a.R + (long)i * 32 * a.ldr + (long)c * 32; }
+    __device__ double* Xt(int i, int c) const { return a.Xo + (long)i * 32 * a.ldx + (long)c * 32; }
+};
+
+__device__ __forceinline__ bool is_sent(double v) {
+    return (unsigned long long)__double_as_longlong(v) == FLOW_SENTINEL;
+}
+// Give-up path of every poll: abort word + info after FLOW_TIMEOUT_TICKS (or someone else's abort).
+__device__ __noinline__ bool flow_give_up(int* abortw, int* info, long long t0) {
+    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(abortw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
+        return true;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > FLOW_TIMEOUT_TICKS) {
+        if ((threadIdx.x & 63) == 0) {
+            __hip_atomic_store(abortw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(info, MFGP_FLOW_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return true;
+    }
+    return false;
+}
+// Wait for a published tile (row-major, ld 32): probe 64 of its elements (one 8-B sc1 load
+// per lane) until none is the sentinel, then the caller's full load re-checks every element.
+__device__ __forceinline__ bool pub_probe_ok(const double* P) {
+    const int l = threadIdx.x & 63;
+    return __ballot(is_sent(ld_coherent(P + 16 * l + (l & 15)))) == 0;
+}
+__device__ __noinline__ void pub_wait(const double* P, int* abortw, int* info, long long t0) {
+    for (int spin = 0;; ++spin) {
+        if (pub_probe_ok(P)) return;
+        if ((spin & 7) == 7 && flow_give_up(abortw, info, t0)) return;
+        __builtin_amdgcn_s_sleep(FLOW_SLEEP);
+    }
+}
+// 16-B sc1 loads of an operand from a published tile (buffer_load_dwordx4 ... sc1)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ double bits_d(unsigned lo, unsigned hi) {
+    return __builtin_bit_cast(double, (unsigned long long)lo | ((unsigned long long)hi << 32));
+}
+__device__ __forceinline__ void op_load_pub(WOp& o, const double* P) {
+    const int li = threadIdx.x & 15, lq = (threadIdx.x >> 4) & 3;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(P), (short)0, 8192, 0x00020000);
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, ((16 * b + li) * 32 + 8 * lq + 2 * q) * 8, 0, 16);
+            o.v[b][2 * q] = bits_d(v.x, v.y);
+            o.v[b][2 * q + 1] = bits_d(v.z, v.w);
+        }
+}
+__device__ __forceinline__ bool op_missing(const WOp& o) {
+    bool miss = false;
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int s = 0; s < 8; ++s) miss |= is_sent(o.v[b][s]);
+    return __ballot(miss) != 0;
+}
+// operand of a published tile, re-read until complete
+__device__ __forceinline__ void pub_retry(WOp& o, const double* P, FlowCtx& C) {
+    const long long tw = flow_clock();
+    for (;;) {
+        if (flow_give_up(C.a.flags, C.a.info, C.t0)) break;
+        pub_wait(P, C.a.flags, C.a.info, C.t0);
+        op_load_pub(o, P);
+        if (!op_missing(o)) break;
+    }
+    C.waited += flow_clock() - tw;
+}
+__device__ __forceinline__ void pub_op(WOp& o, const double* P, FlowCtx& C) {
+    op_load_pub(o, P);
+    if (op_missing(o)) pub_retry(o, P, C);
+}
+// two operands in one round trip
+__device__ __forceinline__ void pub_op2(WOp& x, const double* Px, WOp& y, const double* Py, FlowCtx& C) {
+    op_load_pub(x, Px);
+    op_load_pub(y, Py);
+    if (op_missing(x)) pub_retry(x, Px, C);
+    if (op_missing(y)) pub_retry(y, Py, C);
+}
+// the same in accumulator layout
+__device__ __forceinline__ void pub_wt(WTile& t, const double* P, FlowCtx& C) {
+    long long tw = 0;
+    for (int spin = 0;; ++spin) {
+        wt_load<true>(t, P, 32);
+        bool miss = false;
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) miss |= is_sent(t.v[a][b][r]);
+        if (__ballot(miss) == 0) break;
+        if (spin == 0) tw = flow_clock();
+        if (flow_give_up(C.a.flags, C.a.info, C.t0)) break;
+        pub_wait(P, C.a.flags, C.a.info, C.t0);
+    }
+    if (tw) C.waited += flow_clock() - tw;
+}
+
+// ---- worker items (one wave)
+// Finalize from the accumulator in registers; dop: D_j (A tiles) / D_i (R tiles) in operand form.
+//   A(i,j): L(i,j) = A'(i,j) D_j^T;   R(i,c): X(i,c) = D_i R(i,c) (row block i of [L^{-1} | Z])
+__device__ __forceinline__ void flow_finalize_acc(FlowCtx& C, const FlowTile& t, const WTile& acc, const WOp& dop,
+                                                  double* S) {
+    const FlowArgs& a = C.a;
+    const int T = a.T;
+    WTile out;
+    WOp x;
+    wt_to_lds(acc, S);
+    wt_zero(out);
+    if (t.type == FT_A) {
+        op_rows_lds(x, S);
+        wt_mma<false>(out, x, dop);                      // B[k][j'] = D_j[j'][k]
+        wt_store<true>(out, C.P.L(t.i, t.j), 32);
+        return;
+    }
+    op_cols_lds(x, S);                                   // B[k][j] = R[k][j]
+    wt_mma<false>(out, dop, x);                          // A[i'][k] = D_i[i'][k]
+    wt_store_t_sc1(out, C.P.X(t.i, t.j), 32);            // X^T (published first: it feeds others)
+    wt_store<false>(out, C.Xt(t.i, t.j), a.ldx);
+    if (t.j >= T) {
+        // sum of Z^2 over the valid (n x p) part of this tile
+        const int cy = t.j - T;
+        const int li = threadIdx.x & 15, lq = (threadIdx.x >> 4) & 3;
+        double z2 = 0.0;
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = t.i * 32 + 16 * bi + lq + 4 * r, col = cy * 32 + 16 * bj + li;
+                    const double z = out.v[bi][bj][r];
+                    if (row < a.n && col < a.p) z2 += z * z;
+                }
+        z2 = wave_sum64(z2);
+        if ((threadIdx.x & 63) == 0) a.zpart[t.i * a.Tp + cy] = z2;
+    }
+}
+
+// A finalize with no update before it (tiles (i,0), Y tiles of row 0)
+__device__ __forceinline__ void flow_finalize(FlowCtx& C, const FlowTile& t, double* S) {
+    WTile acc;
+    WOp d;
+    if (t.type == FT_A) wt_load<false>(acc, C.At(t.i, t.j), C.a.lda);
+    else wt_load<false>(acc, C.Rt(t.i, t.j), C.a.ldr);
+    pub_op(d, C.P.D(t.fin), C);
+    flow_finalize_acc(C, t, acc, d, S);
+}
+
+// Update at level l; a tile's last update runs straight into its finalize (same registers,
+// D prefetched with the panel operands), so a row of L advances one hop per level.
+__device__ __forceinline__ void flow_update(FlowCtx& C, const FlowTile& t, int l, double* S) {
+    const FlowArgs& a = C.a;
+    const int T = a.T;
+    WTile acc;
+    WOp x, y, d;
+    const bool fin = (l == t.hi) && (t.fin == l + 1);
+    if (t.type == FT_A) {
+        double* dst = C.At(t.i, t.j);
+        wt_load<false>(acc, dst, a.lda);
+        if (fin) {
+            op_load_pub(x, C.P.L(t.i, l));
+            op_load_pub(y, C.P.L(t.j, l));
+            op_load_pub(d, C.P.D(t.fin));
+            if (op_missing(x)) pub_retry(x, C.P.L(t.i, l), C);
+            if (op_missing(y)) pub_retry(y, C.P.L(t.j, l), C);
+        } else if (t.j != t.i) {
+            pub_op2(x, C.P.L(t.i, l), y, C.P.L(t.j, l), C);
+        } else {
+            pub_op(x, C.P.L(t.i, l), C);
+            y = x;
+        }
+        wt_mma<true>(acc, x, y);                         // A(i,j) -= L(i,l) L(j,l)^T
+        if (fin) {
+            if (op_missing(d)) pub_retry(d, C.P.D(t.fin), C);
+            flow_finalize_acc(C, t, acc, d, S);
+        } else if (t.pub && l == t.hi) {
+            wt_store<true>(acc, C.P.H(t.i == t.j ? 1 : t.i == t.j + 1 ? 0 : 2, t.i), 32);
+        } else {
+            wt_store<false>(acc, dst, a.lda);
+        }
+    } else if (t.type == FT_R) {
+        double* dst = C.Rt(t.i, t.j);
+        wt_load<false>(acc, dst, a.ldr);
+        if (fin) {
+            op_load_pub(x, C.P.L(t.i, l));
+            op_load_pub(y, C.P.X(l, t.j));
+            op_load_pub(d, C.P.D(t.fin));
+            if (op_missing(x)) pub_retry(x, C.P.L(t.i, l), C);
+            if (op_missing(y)) pub_retry(y, C.P.X(l, t.j), C);
+        } else {
+            pub_op2(x, C.P.L(t.i, l), y, C.P.X(l, t.j), C);   // L(i,l), X(l,c)^T (B[k][j] = X(l,c)[k][j])
+        }
+        wt_mma<true>(acc, x, y);                         // R(i,c) -= L(i,l) X(l,c)
+        if (fin) {
+            if (op_missing(d)) pub_retry(d, C.P.D(t.fin), C);
+            flow_finalize_acc(C, t, acc, d, S);
+        } else {
+            wt_store<false>(acc, dst, a.ldr);
+        }
+    } else {
+        const int c = t.i, cy = t.j;
+        double* al = a.alpha + (long)c * 32 * a.ldal + (long)cy * 32;
+        if (l == c) wt_zero(acc);
+        else wt_load<false>(acc, al, a.ldal);
+        pub_op2(x, C.P.X(l, c), y, C.P.X(l, T + cy), C); // A[i][k] = X(l,c)[k][i], B[k][j] = Z(l,cy)[k][j]
+        wt_mma<false>(acc, x, y);                        // alpha(c) += X(l,c)^T Z(l)
+        wt_store<false>(acc, al, a.ldal);
+        if (l == T - 1) {
+            // alpha^T rows under [L^{-1} | Z] for k_grad: -alpha^T / P (A side), alpha^T (B side)
+            const double sA = -1.0 / (double)a.p;
+            double* xa = a.Xo + (long)(T + cy) * 32 * a.ldx + (long)c * 32;
+            double* xb = a.Xo + (long)(T + a.Tp + cy) * 32 * a.ldx + (long)c * 32;
+            const int li = threadIdx.x & 15, lq = (threadIdx.x >> 4) & 3;
+#pragma unroll
+            for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+                for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const long o = (long)(16 * bj + li) * a.ldx + 16 * bi + lq + 4 * r;
+                        xa[o] = sA * acc.v[bi][bj][r];
+                        xb[o] = acc.v[bi][bj][r];
+                    }
+        }
+    }
+}
+
+// item log (diagnostic): per worker wave FLOW_LOG items x {code << 8 | level, begin, ready, end}
+constexpr int FLOW_LOG = 40;
+__device__ __forceinline__ void flow_item_log(const FlowCtx& C, int wid, int n, int code, int l, long long i0,
+                                              long long w0) {
+    if (!C.a.trace || n >= FLOW_LOG || (threadIdx.x & 63) != 0) return;
+    long long* e = C.a.trace + 8 * C.a.T + 3 * C.a.nwaves + ((long)wid * FLOW_LOG + n) * 4;
+    const long long t1 = flow_clock();
+    e[0] = ((long long)code << 8) | l;
+    e[1] = i0 - C.t0;
+    e[2] = i0 + (C.waited - w0) - C.t0;
+    e[3] = t1 - C.t0;
+}
+
+// Slot order of a worker wave: A tiles first (they feed the chain), nearest the diagonal
+// first; then the R / Y tiles, then alpha.  Items run level by level in this order.
+__device__ __forceinline__ int flow_prio(int code) {
+    if (code < 0) return 1 << 30;
+    const FlowTile t = flow_tile(code, 1024);
+    return (t.type << 16) | (t.i << 8) | t.j;
+}
+
+__device__ __forceinline__ void flow_worker(FlowCtx& C, int wid, double* S) {
+    const int T = C.a.T;
+    const int* own = C.a.own + wid * FLOW_MAXOWN;
+    int code[FLOW_MAXOWN];
+#pragma unroll
+    for (int s = 0; s < FLOW_MAXOWN; ++s) code[s] = __builtin_amdgcn_readfirstlane(own[s]);
+#pragma unroll
+    for (int a = 0; a < FLOW_MAXOWN; ++a)       // tiny sorting network on the priority key
+#pragma unroll
+        for (int b = 0; b + 1 < FLOW_MAXOWN - a; ++b)
+            if (flow_prio(code[b]) > flow_prio(code[b + 1])) { const int x = code[b]; code[b] = code[b + 1]; code[b + 1] = x; }
+    int last = -1;
+#pragma unroll
+    for (int s = 0; s < FLOW_MAXOWN; ++s) {
+        if (code[s] < 0) continue;
+        const FlowTile t = flow_tile(code[s], T);
+        last = max(last, max(t.hi, t.fin));
+    }
+    const long long tb = flow_clock();
+    C.waited = 0;
+    int nitem = 0;
+    static_assert(FLOW_MAXOWN == 4, "slot select below");
+    auto pick = [&](int s) { return s == 0 ? code[0] : s == 1 ? code[1] : s == 2 ? code[2] : code[3]; };
+    for (int l = 0; l <= last; ++l) {
+#pragma unroll 1
+        for (int s = 0; s < FLOW_MAXOWN; ++s) {
+            const int cs = pick(s);
+            if (cs < 0) continue;
+            const FlowTile t = flow_tile(cs, T);
+            if (t.fin == l && t.hi < t.lo) {
+                const long long i0 = flow_clock(), w0 = C.waited;
+                flow_finalize(C, t, S);
+                flow_item_log(C, wid, nitem++, cs, l, i0, w0);
+            }
+        }
+#pragma unroll 1
+        for (int s = 0; s < FLOW_MAXOWN; ++s) {
+            const int cs = pick(s);
+            if (cs < 0) continue;
+            const FlowTile t = flow_tile(cs, T);
+            if (t.lo <= l && l <= t.hi) {
+                const long long i0 = flow_clock(), w0 = C.waited;
+                flow_update(C, t, l, S);
+                flow_item_log(C, wid, nitem++, cs, l, i0, w0);
+            }
+        }
+    }
+    if (C.a.trace && (threadIdx.x & 63) == 0) {
+        long long* tr = C.a.trace + 8 * T + 3 * wid;
+        tr[0] = tb - C.t0;
+        tr[1] = flow_clock() - C.t0;
+        tr[2] = C.waited;
+    }
+}
+
+// ---- the chain (workgroup 0, 8 waves)
+// Waves 0-3 ("chain") run step k: L(k,k-1) = A''(k,k-1) D_{k-1}^T, A''(k,k) -= L L^T, then
+// wave 0 factors D_k.  Everything around the chain is taken off it by the other waves, which
+// talk to the chain through LDS progress words (a wave's DS operations complete in issue
+// order, so data written before a word's store is visible to whoever reads the word):
+//   wave 4: publishes L(k,k-1), then D_k, X^T(k,k) = D_k^T, Xo(k,k), diag(L), info;
+//   wave 5: L(j,j-2) = A'(j,j-2) D_{j-2}^T as soon as D_{j-2} is in LDS (the owner applied
+//     every panel < j-2), into LDS for waves 6 / 7, then published;
+//   waves 6, 7: prefetch step j while the chain factors step j-1: the owners' A'(j,j-1),
+//     A'(j,j) (panels < j-2 applied) minus panel j-2:
+//     A''(j,j-1) = A'(j,j-1) - L(j,j-2) L(j-1,j-2)^T,  A''(j,j) = A'(j,j) - L(j,j-2) L(j,j-2)^T.
+// Buffers are double-buffered by step parity.
+struct DiagLds {
+    // LDS carve (doubles): Db[2] | Ls[2] | Ap[2] | Cp[2] | L2[2] (NB x S each) | fsc (32 x 33) | dg[2][32]
+    // | bad[2] | words.  Parity-indexed buffers are computed, not held in pointer arrays (a
+    // dynamically indexed pointer array lands in scratch).
+    double* base;
+    static constexpr int E = TileCfg<32>::ELEMS;
+    __device__ double* Db(int q) const { return base + q * E; }        // D_k (stride S)
+    __device__ double* Ls(int q) const { return base + (2 + q) * E; }  // L(k,k-1)
+    __device__ double* Ap(int q) const { return base + (4 + q) * E; }  // A''(k,k-1)
+    __device__ double* Cp(int q) const { return base + (6 + q) * E; }  // A''(k,k)
+    __device__ double* L2(int q) const { return base + (8 + q) * E; }  // L(k,k-2)
+    __device__ double* fsc() const { return base + 10 * E; }           // factor input (32 x 33)
+    __device__ double* dg(int q) const { return base + 10 * E + 32 * 33 + 32 * q; }
+    __device__ int* bad() const { return reinterpret_cast<int*>(base + 10 * E + 32 * 33 + 64); }
+    __device__ int* w() const { return bad() + 2; }
+};
+enum { DW_LS = 0, DW_D, DW_LPUB, DW_DPUB, DW_PRE6, DW_PRE7, DW_BAR, DW_L2, DW_N };
+
+__device__ __forceinline__ int lds_get(const int* p) {
+    return __hip_atomic_load(const_cast<int*>(p), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_put(int* p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_wait_ge(const int* p, int v) {
+    while (__builtin_amdgcn_readfirstlane(lds_get(p)) < v) __builtin_amdgcn_s_sleep(1);
+}
+// barrier of waves 0-3 only (monotonic LDS counter)
+__device__ __forceinline__ void chain_bar(int* cnt, int& epoch) {
+    epoch += 4;
+    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    lds_wait_ge(cnt, epoch);
+}
+
+// wave-level tile (accumulator layout) <-> LDS tile of stride ld
+__device__ __forceinline__ void wt_to_lds_ld(const WTile& t, double* S, int ld) {
+    const int li = threadIdx.x & 15, lq = (threadIdx.x >> 4) & 3;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) S[(16 * a + lq + 4 * r) * ld + 16 * b + li] = t.v[a][b][r];
+}
+__device__ __forceinline__ void op_rows_lds_ld(WOp& o, const double* S, int ld) {
+    const int li = threadIdx.x & 15, lq = (threadIdx.x >> 4) & 3;
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int s = 0; s < 8; ++s) o.v[b][s] = S[(16 * b + li) * ld + 8 * lq + s];
+}
+
+__device__ __forceinline__ void diag_chain(FlowCtx& C, const DiagLds& B) {
+    constexpr int S = TileCfg<32>::S;
+    const FlowArgs& a = C.a;
+    const int T = a.T;
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    int epoch = 0;
+    for (int k = 1; k < T; ++k) {
+        const int pk = k & 1;
+        if (a.trace && threadIdx.x == 0) a.trace[k] = flow_clock() - C.t0;
+        lds_wait_ge(&B.w()[DW_PRE6], k);
+        lds_wait_ge(&B.w()[DW_PRE7], k);
+        lds_wait_ge(&B.w()[DW_D], k - 1);        // D_{k-1} in Db[pk ^ 1]
+        lds_wait_ge(&B.w()[DW_LPUB], k - 2);     // wave 4 is done with Ls[pk] (L(k-2,k-3))
+        if (a.trace && threadIdx.x == 0) a.trace[T + k] = flow_clock() - C.t0;
+        Acc<32> pl;
+        acc_zero(pl);
+        tile_mma<32, false, true>(pl, B.Ap(pk), B.Db(pk ^ 1), 1.0);   // L(k,k-1) = A'' D_{k-1}^T
+        acc_to_lds(pl, B.Ls(pk));
+        Acc<32> cij;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cij.v[0][r] = B.Cp(pk)[acc_row<32>(0, r) * S + acc_col<32>(0)];
+        chain_bar(&B.w()[DW_BAR], epoch);
+        if (threadIdx.x == 0) lds_put(&B.w()[DW_LS], k);
+        tile_mma<32, false, true>(cij, B.Ls(pk), B.Ls(pk), -1.0);   // A''(k,k) -= L L^T
+        {
+            const int bi = w >> 1, bj = w & 1;
+            if (bj <= bi) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) B.fsc()[(16 * bi + (l >> 4) + 4 * q) * 33 + 16 * bj + (l & 15)] = cij.v[0][q];
+            }
+        }
+        chain_bar(&B.w()[DW_BAR], epoch);
+        if (w == 0) {
+            lds_wait_ge(&B.w()[DW_DPUB], k - 2);    // wave 4 is done with Db[pk] (D_{k-2})
+            if (a.trace && threadIdx.x == 0) a.trace[2 * T + k] = flow_clock() - C.t0;
+            tile_potrf_inv_w1_wave(B.fsc(), 33, B.fsc(), B.Db(pk), B.dg(pk), &B.bad()[pk]);
+            if (l == 0) lds_put(&B.w()[DW_D], k);
+        }
+    }
+}
+
+
+__device__ __forceinline__ void diag_publisher(FlowCtx& C, const DiagLds& B) {
+    constexpr int S = TileCfg<32>::S;
+    const FlowArgs& a = C.a;
+    const int T = a.T;
+    const int l = threadIdx.x & 63;
+    for (int k = 0; k < T; ++k) {
+        const int pk = k & 1;
+        if (k > 0) {
+            lds_wait_ge(&B.w()[DW_LS], k);
+            double* dst = C.P.L(k, k - 1);
+            const double* src = B.Ls(pk);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int e = l + 64 * q;
+                st_coherent(dst + e, src[(e >> 5) * S + (e & 31)]);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (l == 0) lds_put(&B.w()[DW_LPUB], k);
+            lds_wait_ge(&B.w()[DW_D], k);
+        }
+        const double* D = B.Db(pk);
+        double* dp = C.P.D(k);
+        double* xt = C.P.X(k, k);
+        double* xo = C.Xt(k, k);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int e = l + 64 * q;
+            st_coherent(dp + e, D[(e >> 5) * S + (e & 31)]);
+        }
+        if (a.trace && l == 0) a.trace[3 * T + k] = flow_clock() - C.t0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int e = l + 64 * q;
+            const int r = e >> 5, c = e & 31;
+            const double v = D[r * S + c];
+            st_coherent(xt + c * 32 + r, v);             // X^T(k,k) = D_k^T
+            xo[(long)r * a.ldx + c] = v;
+        }
+        if (k > 0) {
+            if (l < 32) a.ldiag[k * 32 + l] = B.dg(pk)[l];
+            if (l == 0 && B.bad()[pk] && a.info[0] == 0) a.info[0] = k * 32 + B.bad()[pk];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (l == 0) lds_put(&B.w()[DW_DPUB], k);
+    }
+}
+
+__device__ __forceinline__ void diag_second(FlowCtx& C, const DiagLds& B) {
+    constexpr int S = TileCfg<32>::S;
+    const FlowArgs& a = C.a;
+    const int T = a.T;
+    for (int j = 2; j < T; ++j) {
+        WTile acc;
+        if (j >= 3) pub_wt(acc, C.P.H(2, j), C);
+        else wt_load<true>(acc, C.At(j, j - 2), a.lda);  // A(2,0): k_gram's value
+        if (a.trace && (threadIdx.x & 63) == 0) a.trace[4 * T + j] = flow_clock() - C.t0;
+        lds_wait_ge(&B.w()[DW_D], j - 2);
+        lds_wait_ge(&B.w()[DW_PRE6], j - 2);              // waves 6 / 7 are done with L2[j & 1]
+        lds_wait_ge(&B.w()[DW_PRE7], j - 2);
+        WOp x, y;
+        wt_to_lds_ld(acc, B.L2(j & 1), S);               // staging: A'(j,j-2) as the A operand
+        asm volatile("" ::: "memory");
+        op_rows_lds_ld(x, B.L2(j & 1), S);
+        op_rows_lds_ld(y, B.Db((j - 2) & 1), S);         // B[k][c] = D_{j-2}[c][k]
+        wt_zero(acc);
+        wt_mma<false>(acc, x, y);
+        asm volatile("" ::: "memory");
+        wt_to_lds_ld(acc, B.L2(j & 1), S);
+        if ((threadIdx.x & 63) == 0) lds_put(&B.w()[DW_L2], j);
+        if (a.trace && (threadIdx.x & 63) == 0) a.trace[7 * T + j] = flow_clock() - C.t0;
+        wt_store<true>(acc, C.P.L(j, j - 2), 32);
+    }
+}
+
+__device__ __forceinline__ void diag_prefetch(FlowCtx& C, const DiagLds& B, bool sub) {
+    constexpr int S = TileCfg<32>::S;
+    const FlowArgs& a = C.a;
+    const int T = a.T;
+    int* done = &B.w()[sub ? DW_PRE6 : DW_PRE7];
+    for (int j = 1; j < T; ++j) {
+        const int pj = j & 1;
+        double* dst = sub ? B.Ap(pj) : B.Cp(pj);
+        WTile acc;
+        if (j >= 3) pub_wt(acc, C.P.H(sub ? 0 : 1, j), C);
+        else wt_load<true>(acc, sub ? C.At(j, j - 1) : C.At(j, j), a.lda);   // k_gram's values
+        if (a.trace && (threadIdx.x & 63) == 0) a.trace[(sub ? 5 : 6) * T + j] = flow_clock() - C.t0;
+        if (j >= 2) {
+            WOp x, y;
+            lds_wait_ge(&B.w()[DW_L2], j);
+            op_rows_lds_ld(x, B.L2(pj), S);
+            lds_wait_ge(&B.w()[DW_LS], j - 1);
+            if (sub) op_rows_lds_ld(y, B.Ls(pj ^ 1), S);
+            else y = x;
+            wt_mma<true>(acc, x, y);
+        }
+        wt_to_lds_ld(acc, dst, S);
+        if ((threadIdx.x & 63) == 0) lds_put(done, j);
+    }
+}
+
+__device__ __forceinline__ void flow_diag(FlowCtx& C, double* smem) {
+    DiagLds B;
+    B.base = smem;
+    if (threadIdx.x < DW_N) B.w()[threadIdx.x] = (threadIdx.x == DW_LPUB || threadIdx.x == DW_DPUB) ? -1 : 0;
+    if (threadIdx.x < 2) B.bad()[threadIdx.x] = 0;
+    tile_load<32>(B.Db(0), C.a.Dd, 32);   // D_0: k_gram's fused factor (previous launch)
+    __syncthreads();
+    const int w = threadIdx.x >> 6;
+    if (w < 4) diag_chain(C, B);
+    else if (w == 4) diag_publisher(C, B);
+    else if (w == 5) diag_second(C, B);
+    else diag_prefetch(C, B, w == 6);
+}
+
+__global__ __launch_bounds__(FLOW_THREADS) void k_chol_flow(FlowArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    FlowCtx C;
+    C.a = a;
+    C.P.base = a.pub;
+    C.P.T = a.T;
+    C.P.Tp = a.Tp;
+    C.t0 = flow_clock();
+    if (blockIdx.x == 0) {
+        flow_diag(C, smem);
+        return;
+    }
+    const int w = threadIdx.x >> 6;
+    flow_worker(C, (blockIdx.x - 1) * FLOW_WAVES + w, smem + w * 32 * WLD);
+}
+
+long flow_npub(int T, int Tp) { return 1024L * (T * (T - 1) / 2 + T + T * (T + 1) / 2 + T * Tp + 3 * T); }
+int flow_nflags(int T, int Tp) { (void)T; (void)Tp; return 1; }   // the abort word
+int flow_trace_count(int T, int nwg) { return 8 * T + (3 + 4 * FLOW_LOG) * FLOW_WAVES * (nwg - 1); }
+
+void launch_chol_flow(const FlowArgs& a, int nwg, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_chol_flow),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)FLOW_LDS_BYTES);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_chol_flow, dim3(nwg), dim3(FLOW_THREADS), FLOW_LDS_BYTES, s, a);
+}
+
+}  // namespace mfgp

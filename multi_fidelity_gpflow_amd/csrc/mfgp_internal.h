@@ -25,7 +25,38 @@ struct GramArgs {
     int* cnt; int ncnt;                       // arrival counters zeroed by workgroup 0 (reduce merge)
     // k_grad task order (nullptr: none): one extra LAST workgroup builds it (grad_order)
     int* gorder; int gT, gchunk, gTp;
+    // k_chol_flow owner table (nullptr: none): one more extra workgroup builds it and zeroes
+    // the flow flags (build_flow_owner); every workgroup fills its share of the publication
+    // area with the sentinel
+    int* fown; int fW; int* fflags; int nfflags;
+    double* fpub; long npub;
 };
+
+// k_chol_flow (mfgp_flow.hip): persistent dataflow Cholesky + L^{-1} + Z + alpha, NB = 32, batch 1
+constexpr int FLOW_MAXOWN = 4;                      // tiles per worker wave
+constexpr int FLOW_WAVES = 8;                       // waves per workgroup (two per SIMD)
+constexpr int FLOW_THREADS = 64 * FLOW_WAVES;
+constexpr int FLOW_FSTRIDE = 32;                    // ints per flag: one 128-B line each (polled lines
+                                                    // are not shared, no hot line under 2k pollers)
+constexpr size_t FLOW_LDS_BYTES = 96 * 1024;        // > 80 KB: one workgroup per CU
+constexpr unsigned long long FLOW_SENTINEL = 0x7FF4DEAD7FF4DEADull;   // signalling NaN: "not yet published"
+struct FlowArgs {
+    double* A; long lda;          // K + s2 I lower tiles -> L tiles (in place)
+    double* R; long ldr;          // [I | Y] accumulators -> X^T tiles (in place)
+    double* Xo; long ldx;         // [L^{-1} | Z] (+ alpha^T rows for k_grad)
+    double* Dd;                   // T diagonal inverses D_k (NB x NB)
+    double* ldiag;
+    int* info;
+    double* alpha; long ldal;
+    double* zpart;
+    int* flags;                   // abort word (zeroed by build_flow_owner)
+    double* pub;                  // publication area, flow_npub(T, Tp) doubles of FLOW_SENTINEL
+    const int* own;               // [W * FLOW_MAXOWN] tile codes (-1: none)
+    int T, Tp, n, p;
+    long long* trace;             // diagnostic timeline (nullptr: off), flow_trace_count entries
+    int nwaves;                   // worker waves (trace layout)
+};
+int flow_trace_count(int T, int nwg);
 
 struct CholArgs {
     double* A; long lda; long sA;        // SPD matrix, lower tiles, updated in place
@@ -100,6 +131,10 @@ size_t grad_smem_bytes(int nb, int G, int nil2);
 int chol_step_blocks(int T, int Tp, int k, bool alpha = false);
 __host__ __device__ int grad_tasks(int T, int chunk);
 
+
+int flow_nflags(int T, int Tp);
+long flow_npub(int T, int Tp);
+void launch_chol_flow(const FlowArgs& a, int nwg, hipStream_t s);
 
 template <int NB> void launch_gram(const GramArgs& g, int nblocks, int batch, hipStream_t s);
 template <int NB> void launch_chol_steps(CholArgs c, int batch, hipStream_t s);

@@ -14,6 +14,7 @@
 // go through v_mfma_f64_16x16x4_f64 (mfgp_device.h).
 #include "mfgp_device.h"
 #include "mfgp_internal.h"
+#include "mfgp_flow.h"
 
 namespace mfgp {
 
@@ -98,8 +99,21 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
                                                    // would shift the dynamic base off 16 B (G17)
 
     const int b = blockIdx.z;
+    if (a.fpub && b == 0) {
+        // sentinel fill of the k_chol_flow publication area, spread over the grid.  sc1 (write-
+        // through, line dropped from this XCD's L2): a plain store would leave a clean copy of
+        // the sentinel in this XCD's L2 that the flow's sc1 polls could be served from.
+        unsigned long long* dst = reinterpret_cast<unsigned long long*>(a.fpub);
+        for (long e = blockIdx.x * (long)NTHREADS + threadIdx.x; e < a.npub; e += (long)gridDim.x * NTHREADS)
+            __hip_atomic_store(dst + e, FLOW_SENTINEL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (a.gorder && blockIdx.x == gridDim.x - 1) {   // extra workgroup: k_grad task order
         if (b == 0) build_grad_order(a.gT, a.gchunk, a.gTp, a.gorder, reinterpret_cast<int*>(smem));
+        return;
+    }
+    if (a.fown && blockIdx.x == gridDim.x - 1 - (a.gorder ? 1 : 0)) {   // extra: flow owner table
+        if (b == 0) build_flow_owner(a.npad / NB, a.ppad / NB, a.fW, a.fown, a.fflags, a.nfflags,
+                                     reinterpret_cast<int*>(smem));
         return;
     }
     if (a.cnt && blockIdx.x == 0 && b == 0)

@@ -80,6 +80,13 @@ class Engine:
     def set_tile(self, nb: int):
         check(self.lib.mfgp_set_tile(self.h, nb), "mfgp_set_tile")
 
+    def flow(self) -> bool:
+        return self.lib.mfgp_get_flow(self.h) == 1
+
+    def set_flow(self, enable: bool):
+        """Cholesky schedule of the LML path: persistent dataflow launch (True) or one launch per step."""
+        check(self.lib.mfgp_set_flow(self.h, 1 if enable else 0), "mfgp_set_flow")
+
     # ------------------------------------------------------------ kernels
     def rbf_gram(self, X1: torch.Tensor, X2: torch.Tensor, params: torch.Tensor) -> torch.Tensor:
         n1, d = X1.shape

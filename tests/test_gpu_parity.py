@@ -24,11 +24,16 @@ def eng():
     e.set_tile(32)
 
 
-@pytest.fixture(params=[32, 64], ids=["nb32", "nb64"])
+@pytest.fixture(params=[(32, True), (32, False), (64, False)], ids=["nb32-flow", "nb32-steps", "nb64"])
 def tile(request, eng):
-    eng.set_tile(request.param)
-    yield request.param
+    """Tile size and Cholesky schedule: the persistent dataflow launch (k_chol_flow, NB = 32) or
+    the launch-per-step sequence (k_chol_step)."""
+    nb, flow = request.param
+    eng.set_tile(nb)
+    eng.set_flow(flow)
+    yield nb
     eng.set_tile(32)
+    eng.set_flow(True)
 
 
 def _params(D, P, seed=0, scale=1.0):
@@ -165,6 +170,29 @@ def test_predict_f(which, tile, hbs, goku):
         assert mean.shape == mo.shape and var.shape == vo.shape
         np.testing.assert_allclose(mean.numpy(), mo, rtol=0, atol=1e-9 * max(1, np.abs(mo).max()))
         np.testing.assert_allclose(var.numpy(), vo, rtol=0, atol=1e-9)
+
+
+@pytest.mark.parametrize("n_lf,n_hf,p", [(20, 5, 1), (60, 20, 3), (1128, 36, 64), (1400, 100, 40)])
+def test_flow_matches_step_schedule(n_lf, n_hf, p, eng):
+    """k_chol_flow (one persistent launch) and the launch-per-step k_chol_step sequence compute
+    the same LML and gradient (different MFMA summation orders: rounding-level agreement),
+    T = 1, 3, 37 and 47 tiles; also checks the flow really is the default schedule."""
+    rng = np.random.default_rng(n_lf + p)
+    D = 4
+    X = np.vstack([np.hstack([rng.random((n_lf, D)), np.zeros((n_lf, 1))]),
+                   np.hstack([rng.random((n_hf, D)), np.ones((n_hf, 1))])])
+    Y = np.sin(X[:, :D] @ rng.standard_normal((D, p)) * 3.0)
+    m = _model(X, Y, _params(D, p, seed=3))
+    assert eng.flow() or torch.cuda.get_device_properties(0).multi_processor_count < 2
+    vals = []
+    for flow in (True, False):
+        eng.set_flow(flow)
+        vals.append(m.log_marginal_likelihood_and_grad())
+    eng.set_flow(True)
+    assert abs(vals[0][0] - vals[1][0]) < 1e-11 * abs(vals[1][0])
+    np.testing.assert_allclose(vals[0][1], vals[1][1], rtol=0, atol=1e-9 * np.abs(vals[1][1]).max())
+    lo, go = O.gpr_lml_and_grad(X, Y, _oracle_params(m))
+    assert abs(vals[0][0] - lo) < 1e-10 * abs(lo)
 
 
 def test_tile_size_invariance(eng, goku):
