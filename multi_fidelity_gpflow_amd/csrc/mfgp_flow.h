@@ -19,9 +19,9 @@ __host__ __device__ inline void flow_tri(int t, int& i, int& j) {   // row-major
     j = t - r * (r + 1) / 2;
 }
 
-// Owned A tiles: every lower tile except (0,0) (k_gram) and (1,0) .. (2,2) (the diag
-// workgroup works on their initial values).
-__host__ __device__ inline int flow_nA(int T) { return T >= 3 ? T * (T + 1) / 2 - 6 : 0; }
+// Owned A tiles: every lower tile except (0,0) (k_gram) and the band tiles (k,k-2), (k,k-1),
+// (k,k) of rows k <= 3, which the diag workgroup takes from their initial values.
+__host__ __device__ inline int flow_nA(int T) { return T >= 4 ? T * (T + 1) / 2 - 9 : 0; }
 __host__ __device__ inline int flow_ntiles(int T, int Tp) {
     return flow_nA(T) + T * (T - 1) / 2 + 2 * T * Tp;
 }
@@ -29,7 +29,7 @@ __host__ __device__ inline int flow_ntiles(int T, int Tp) {
 __device__ inline int flow_decode(int g, int T, int Tp) {
     const int nA = flow_nA(T);
     int i, j;
-    if (g < nA) { flow_tri(g + 6, i, j); return flow_code(FT_A, i, j); }
+    if (g < nA) { flow_tri(g == 0 ? 6 : g + 9, i, j); return flow_code(FT_A, i, j); }   // (3,0), then rows >= 4
     g -= nA;
     const int nR = T * (T - 1) / 2;
     if (g < nR) { flow_tri(g, i, j); return flow_code(FT_R, i + 1, j); }
@@ -52,8 +52,8 @@ __host__ __device__ inline FlowTile flow_tile(int code, int T) {
     t.pub = 0;
     if (t.type == FT_A) {
         t.lo = 0;
-        // (k,k), (k,k-1): panels < k-2;  (k,k-2): all its panels (< k-2), finalized by diag
-        if (t.i <= t.j + 2) { t.hi = t.i - 3; t.fin = -1; t.pub = 1; }
+        // band tiles (k,k), (k,k-1), (k,k-2): panels < k-3 here, the rest and L(k,k-2) in diag
+        if (t.i <= t.j + 2) { t.hi = t.i - 4; t.fin = -1; t.pub = 1; }
         else { t.hi = t.j - 1; t.fin = t.j; }
     } else if (t.type == FT_R) {
         t.lo = (t.j < T) ? t.j : 0;

@@ -657,13 +657,20 @@ __device__ __forceinline__ void diag_second(FlowCtx& C, const DiagLds& B) {
     const int T = a.T;
     for (int j = 2; j < T; ++j) {
         WTile acc;
-        if (j >= 3) pub_wt(acc, C.P.H(2, j), C);
-        else wt_load<true>(acc, C.At(j, j - 2), a.lda);  // A(2,0): k_gram's value
+        if (j >= 4) pub_wt(acc, C.P.H(2, j), C);
+        else wt_load<true>(acc, C.At(j, j - 2), a.lda);  // A(2,0), A(3,1): k_gram's values
         if (a.trace && (threadIdx.x & 63) == 0) a.trace[4 * T + j] = flow_clock() - C.t0;
-        lds_wait_ge(&B.w()[DW_D], j - 2);
-        lds_wait_ge(&B.w()[DW_PRE6], j - 2);              // waves 6 / 7 are done with L2[j & 1]
-        lds_wait_ge(&B.w()[DW_PRE7], j - 2);
         WOp x, y;
+        if (j >= 3) {
+            // panel j-3: A(j,j-2) -= L(j,j-3) L(j-2,j-3)^T  (the worker's L, the chain's Ls of step j-2)
+            pub_op(x, C.P.L(j, j - 3), C);
+            lds_wait_ge(&B.w()[DW_LS], j - 2);
+            op_rows_lds_ld(y, B.Ls((j - 2) & 1), S);
+            wt_mma<true>(acc, x, y);
+        }
+        lds_wait_ge(&B.w()[DW_D], j - 2);
+        lds_wait_ge(&B.w()[DW_PRE6], j - 1);              // L2[j & 1] = L(j-2,j-4): last read by
+        lds_wait_ge(&B.w()[DW_PRE7], j - 2);              // wave 6 at j-1, wave 7 at j-2
         wt_to_lds_ld(acc, B.L2(j & 1), S);               // staging: A'(j,j-2) as the A operand
         asm volatile("" ::: "memory");
         op_rows_lds_ld(x, B.L2(j & 1), S);
@@ -687,9 +694,21 @@ __device__ __forceinline__ void diag_prefetch(FlowCtx& C, const DiagLds& B, bool
         const int pj = j & 1;
         double* dst = sub ? B.Ap(pj) : B.Cp(pj);
         WTile acc;
-        if (j >= 3) pub_wt(acc, C.P.H(sub ? 0 : 1, j), C);
+        if (j >= 4) pub_wt(acc, C.P.H(sub ? 0 : 1, j), C);
         else wt_load<true>(acc, sub ? C.At(j, j - 1) : C.At(j, j), a.lda);   // k_gram's values
         if (a.trace && (threadIdx.x & 63) == 0) a.trace[(sub ? 5 : 6) * T + j] = flow_clock() - C.t0;
+        if (j >= 3) {
+            // panel j-3 from the worker's L(j,j-3) and L(j-1,j-3) (wave 5, step j-1)
+            WOp x, y;
+            pub_op(x, C.P.L(j, j - 3), C);
+            if (sub) {
+                lds_wait_ge(&B.w()[DW_L2], j - 1);
+                op_rows_lds_ld(y, B.L2((j - 1) & 1), S);
+            } else {
+                y = x;
+            }
+            wt_mma<true>(acc, x, y);
+        }
         if (j >= 2) {
             WOp x, y;
             lds_wait_ge(&B.w()[DW_L2], j);

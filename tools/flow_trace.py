@@ -61,6 +61,23 @@ def main():
             ty, i, j = code >> 20, (code >> 10) & 1023, code & 1023
             if (ty, i, j) in want and lev >= kk - 5:
                 print(f"   {names[ty]}({i},{j}) lvl {lev:2d}: begin {b:7.2f} ready {r:7.2f} end {e:7.2f}  (work {e-r:5.2f})")
+    # lag of the L^{-1} / Z / alpha pipelines behind the chain: per level, latest item end - D_l published
+    print(" lvl  D_l    A-fin lag  R-fin lag  Y-fin lag  alpha lag   (us after D_l published)")
+    for lev in range(0, T, 3):
+        row = []
+        for kind in ("A", "R", "Y", "al"):
+            ends = []
+            for (wv, code, lv, b, r, e) in its:
+                ty, i, j = code >> 20, (code >> 10) & 1023, code & 1023
+                k2 = {0: "A", 1: ("Y" if j >= T else "R"), 2: "al"}[ty]
+                if k2 != kind:
+                    continue
+                # the item that completes level lev: finalize at lev (merged: update at lev-1) / alpha update at lev
+                if (kind in ("A", "R", "Y") and lv == lev - 1 and ((ty == 0 and j == lev) or (ty == 1 and i == lev))) or \
+                   (kind == "al" and lv == lev):
+                    ends.append(e)
+            row.append(max(ends) - pub[lev] if ends else float("nan"))
+        print(f" {lev:3d} {pub[lev]:7.2f} " + " ".join(f"{v:9.2f}" for v in row))
     dur = np.array([e - r for (_, _, _, b, r, e) in its])
     print(f"item work time (after waits): median {np.median(dur):.2f} us  p90 {np.percentile(dur, 90):.2f}  max {dur.max():.2f}")
 
