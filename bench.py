@@ -54,7 +54,7 @@ def pmc_traffic(kernel_prefix, nb):
     except (OSError, ValueError, KeyError):
         return None, None
     for name, v in kern.items():
-        if f"{kernel_prefix}<{nb}>" in name:
+        if f"{kernel_prefix}<{nb}>" in name or f"{kernel_prefix}(" in name:
             return v["hbm_bytes"], os.path.relpath(PMC_SUMMARY, ROOT)
     return None, None
 
@@ -106,13 +106,14 @@ def roofline(model, n, p, d, reps=10, pmc=True):
         "chol_steps": n ** 3 / 3 + n ** 3 / 3 + n * n * p + n * n * p,
         "grad": n ** 3 / 3 + n * n * p + n * (n + 1) / 2 * (4 * d + 10),
     }
-    launches = {"gram": 1, "chol_steps": T, "grad": 1}
+    flow = eng.flow() and nb == 32    # one persistent k_chol_flow launch, else T k_chol_step launches
+    launches = {"gram": 1, "chol_steps": 1 if flow else T, "grad": 1}
     dom = max(flops, key=lambda k: ms[names.index(k)])
     t_ms = ms[names.index(dom)]
     per_launch_ms = t_ms / launches[dom]
     per_launch_flop = flops[dom] / launches[dom]
     achieved = per_launch_flop / (per_launch_ms * 1e-3) / 1e12
-    kname = {"chol_steps": "k_chol_step", "gram": "k_gram", "grad": "k_grad"}[dom]
+    kname = {"chol_steps": "k_chol_flow" if flow else "k_chol_step", "gram": "k_gram", "grad": "k_grad"}[dom]
     traffic, tsrc = pmc_traffic(kname, nb) if pmc else (None, None)
     return {
         "kernel": kname,

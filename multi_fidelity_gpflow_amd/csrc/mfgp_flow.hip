@@ -211,11 +211,12 @@ __device__ __noinline__ bool flow_give_up(int* abortw, int* info, long long t0) 
     }
     return false;
 }
-// Wait for a published tile (row-major, ld 32): probe 64 of its elements (one 8-B sc1 load
-// per lane) until none is the sentinel, then the caller's full load re-checks every element.
+// Wait for a published tile (row-major, ld 32): probe its first line until no element is the
+// sentinel, then the caller's full load re-checks every element.
 __device__ __forceinline__ bool pub_probe_ok(const double* P) {
+    // one 128-B line (16 doubles) per probe: a poll costs one line of traffic, not 64
     const int l = threadIdx.x & 63;
-    return __ballot(is_sent(ld_coherent(P + 16 * l + (l & 15)))) == 0;
+    return __ballot(is_sent(ld_coherent(P + (l & 15)))) == 0;
 }
 __device__ __noinline__ void pub_wait(const double* P, int* abortw, int* info, long long t0) {
     for (int spin = 0;; ++spin) {
