@@ -57,7 +57,7 @@ __host__ __device__ inline FlowTile flow_tile(int code, int T) {
         else { t.hi = t.j - 1; t.fin = t.j; }
     } else if (t.type == FT_R) {
         t.lo = (t.j < T) ? t.j : 0;
-        t.hi = t.i - 1;
+        t.hi = t.i - 2;                         // panel i-1 enters the finalize through H_i
         t.fin = t.i;
     } else {
         t.lo = t.i;

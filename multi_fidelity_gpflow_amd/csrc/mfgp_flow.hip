@@ -161,6 +161,20 @@ __device__ __forceinline__ void op_cols_lds(WOp& o, const double* S) {
 #pragma unroll
         for (int s = 0; s < 8; ++s) o.v[b][s] = S[(8 * lq + s) * WLD + 16 * b + li];
 }
+// C += A B with the B side read from the per-wave LDS tile M untransposed (B[k][j] = M[k][j])
+__device__ __forceinline__ void wt_mma_lds_b(WTile& c, const WOp& a, const double* S) {
+    const int li = threadIdx.x & 15, lq = (threadIdx.x >> 4) & 3;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+        const double b0 = S[(8 * lq + s) * WLD + li], b1 = S[(8 * lq + s) * WLD + 16 + li];
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi) {
+            c.v[bi][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a.v[bi][s], b0, c.v[bi][0], 0, 0, 0);
+            c.v[bi][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a.v[bi][s], b1, c.v[bi][1], 0, 0, 0);
+        }
+    }
+}
 __device__ __forceinline__ double wave_sum64(double v) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -183,6 +197,7 @@ struct FlowPub {
         return tile(nL() + T + (c < T ? i * (i + 1) / 2 + c : T * (T + 1) / 2 + i * Tp + (c - T)));
     }
     __device__ double* H(int kind, int k) const { return tile(nL() + T + nX() + 3 * k + kind); }   // 0: (k,k-1) 1: (k,k) 2: (k,k-2)
+    __device__ double* Hk(int k) const { return tile(nL() + T + nX() + 3 * T + k); }   // H_k = D_k L(k,k-1)
 };
 
 struct FlowCtx {
@@ -298,22 +313,64 @@ __device__ __forceinline__ void pub_wt(WTile& t, const double* P, FlowCtx& C) {
 //   A(i,j): L(i,j) = A'(i,j) D_j^T;   R(i,c): X(i,c) = D_i R(i,c) (row block i of [L^{-1} | Z])
 __device__ __forceinline__ void flow_finalize_acc(FlowCtx& C, const FlowTile& t, const WTile& acc, const WOp& dop,
                                                   double* S) {
-    const FlowArgs& a = C.a;
-    const int T = a.T;
+    // L(i,j) = A'(i,j) D_j^T
     WTile out;
     WOp x;
     wt_to_lds(acc, S);
+    op_rows_lds(x, S);
     wt_zero(out);
-    if (t.type == FT_A) {
-        op_rows_lds(x, S);
-        wt_mma<false>(out, x, dop);                      // B[k][j'] = D_j[j'][k]
-        wt_store<true>(out, C.P.L(t.i, t.j), 32);
-        return;
+    wt_mma<false>(out, x, dop);                          // B[k][j'] = D_j[j'][k]
+    wt_store<true>(out, C.P.L(t.i, t.j), 32);
+}
+
+// A finalize with no update before it (tiles (i,0))
+__device__ __forceinline__ void flow_finalize(FlowCtx& C, const FlowTile& t, double* S) {
+    WTile acc;
+    WOp d;
+    wt_load<false>(acc, C.At(t.i, t.j), C.a.lda);
+    pub_op(d, C.P.D(t.fin), C);
+    flow_finalize_acc(C, t, acc, d, S);
+}
+
+// X(i,c) = D_i R''(i,c) - H_i X(i-1,c): row block i of [L^{-1} | Z], with R'' holding the panels
+// < i-1 and the last one folded in through H_i = D_i L(i,i-1) (diag publishes it), so a column
+// of L^{-1} / Z advances by one product per level once its previous block is out.
+__device__ __forceinline__ void flow_finalize_r(FlowCtx& C, const FlowTile& t, double* S) {
+    const FlowArgs& a = C.a;
+    const int T = a.T;
+    const int i = t.i;
+    {
+        WTile acc;
+        wt_load<false>(acc, C.Rt(i, t.j), a.ldr);
+        wt_to_lds(acc, S);
     }
-    op_cols_lds(x, S);                                   // B[k][j] = R[k][j]
-    wt_mma<false>(out, dop, x);                          // A[i'][k] = D_i[i'][k]
-    wt_store_t_sc1(out, C.P.X(t.i, t.j), 32);            // X^T (published first: it feeds others)
-    wt_store<false>(out, C.Xt(t.i, t.j), a.ldx);
+    const bool cpl = i >= 1;
+    const double* Pd = C.P.D(i);
+    const double* Ph = C.P.Hk(i);
+    const double* Pq = C.P.X(i - 1, t.j);
+    WOp d, h, q;
+    const long long tw = flow_clock();
+    bool waited = false;
+    for (int spin = 0;; ++spin) {
+        op_load_pub(d, Pd);
+        if (cpl) {
+            op_load_pub(h, Ph);
+            op_load_pub(q, Pq);
+        }
+        bool miss = op_missing(d);
+        if (cpl) miss = miss || op_missing(h) || op_missing(q);
+        if (!miss) break;
+        waited = true;
+        if ((spin & 7) == 7 && flow_give_up(C.a.flags, C.a.info, C.t0)) break;
+        __builtin_amdgcn_s_sleep(FLOW_SLEEP);
+    }
+    if (waited) C.waited += flow_clock() - tw;
+    WTile out;
+    wt_zero(out);
+    wt_mma_lds_b(out, d, S);                             // D_i R''   (B[k][j] = R''[k][j])
+    if (cpl) wt_mma<true>(out, h, q);                    // - H_i X(i-1,c)   (B[k][j] = X^T(i-1,c)[j][k])
+    wt_store_t_sc1(out, C.P.X(i, t.j), 32);              // X^T (published first: it feeds others)
+    wt_store<false>(out, C.Xt(i, t.j), a.ldx);
     if (t.j >= T) {
         // sum of Z^2 over the valid (n x p) part of this tile
         const int cy = t.j - T;
@@ -325,23 +382,13 @@ __device__ __forceinline__ void flow_finalize_acc(FlowCtx& C, const FlowTile& t,
             for (int bj = 0; bj < 2; ++bj)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int row = t.i * 32 + 16 * bi + lq + 4 * r, col = cy * 32 + 16 * bj + li;
+                    const int row = i * 32 + 16 * bi + lq + 4 * r, col = cy * 32 + 16 * bj + li;
                     const double z = out.v[bi][bj][r];
                     if (row < a.n && col < a.p) z2 += z * z;
                 }
         z2 = wave_sum64(z2);
-        if ((threadIdx.x & 63) == 0) a.zpart[t.i * a.Tp + cy] = z2;
+        if ((threadIdx.x & 63) == 0) a.zpart[i * a.Tp + cy] = z2;
     }
-}
-
-// A finalize with no update before it (tiles (i,0), Y tiles of row 0)
-__device__ __forceinline__ void flow_finalize(FlowCtx& C, const FlowTile& t, double* S) {
-    WTile acc;
-    WOp d;
-    if (t.type == FT_A) wt_load<false>(acc, C.At(t.i, t.j), C.a.lda);
-    else wt_load<false>(acc, C.Rt(t.i, t.j), C.a.ldr);
-    pub_op(d, C.P.D(t.fin), C);
-    flow_finalize_acc(C, t, acc, d, S);
 }
 
 // Update at level l; a tile's last update runs straight into its finalize (same registers,
@@ -351,7 +398,7 @@ __device__ __forceinline__ void flow_update(FlowCtx& C, const FlowTile& t, int l
     const int T = a.T;
     WTile acc;
     WOp x, y, d;
-    const bool fin = (l == t.hi) && (t.fin == l + 1);
+    const bool fin = (t.type == FT_A) && (l == t.hi) && (t.fin == l + 1);
     if (t.type == FT_A) {
         double* dst = C.At(t.i, t.j);
         wt_load<false>(acc, dst, a.lda);
@@ -379,22 +426,9 @@ __device__ __forceinline__ void flow_update(FlowCtx& C, const FlowTile& t, int l
     } else if (t.type == FT_R) {
         double* dst = C.Rt(t.i, t.j);
         wt_load<false>(acc, dst, a.ldr);
-        if (fin) {
-            op_load_pub(x, C.P.L(t.i, l));
-            op_load_pub(y, C.P.X(l, t.j));
-            op_load_pub(d, C.P.D(t.fin));
-            if (op_missing(x)) pub_retry(x, C.P.L(t.i, l), C);
-            if (op_missing(y)) pub_retry(y, C.P.X(l, t.j), C);
-        } else {
-            pub_op2(x, C.P.L(t.i, l), y, C.P.X(l, t.j), C);   // L(i,l), X(l,c)^T (B[k][j] = X(l,c)[k][j])
-        }
+        pub_op2(x, C.P.L(t.i, l), y, C.P.X(l, t.j), C);  // L(i,l), X(l,c)^T (B[k][j] = X(l,c)[k][j])
         wt_mma<true>(acc, x, y);                         // R(i,c) -= L(i,l) X(l,c)
-        if (fin) {
-            if (op_missing(d)) pub_retry(d, C.P.D(t.fin), C);
-            flow_finalize_acc(C, t, acc, d, S);
-        } else {
-            wt_store<false>(acc, dst, a.ldr);
-        }
+        wt_store<false>(acc, dst, a.ldr);
     } else {
         const int c = t.i, cy = t.j;
         double* al = a.alpha + (long)c * 32 * a.ldal + (long)cy * 32;
@@ -473,9 +507,10 @@ __device__ __forceinline__ void flow_worker(FlowCtx& C, int wid, double* S) {
             const int cs = pick(s);
             if (cs < 0) continue;
             const FlowTile t = flow_tile(cs, T);
-            if (t.fin == l && t.hi < t.lo) {
+            if (t.fin == l && (t.type == FT_R || t.hi < t.lo)) {
                 const long long i0 = flow_clock(), w0 = C.waited;
-                flow_finalize(C, t, S);
+                if (t.type == FT_R) flow_finalize_r(C, t, S);
+                else flow_finalize(C, t, S);
                 flow_item_log(C, wid, nitem++, cs, l, i0, w0);
             }
         }
@@ -561,6 +596,14 @@ __device__ __forceinline__ void op_rows_lds_ld(WOp& o, const double* S, int ld) 
     for (int b = 0; b < 2; ++b)
 #pragma unroll
         for (int s = 0; s < 8; ++s) o.v[b][s] = S[(16 * b + li) * ld + 8 * lq + s];
+}
+
+__device__ __forceinline__ void op_cols_lds_ld(WOp& o, const double* S, int ld) {
+    const int li = threadIdx.x & 15, lq = (threadIdx.x >> 4) & 3;
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int s = 0; s < 8; ++s) o.v[b][s] = S[(8 * lq + s) * ld + 16 * b + li];
 }
 
 __device__ __forceinline__ void diag_chain(FlowCtx& C, const DiagLds& B) {
@@ -686,6 +729,22 @@ __device__ __forceinline__ void diag_second(FlowCtx& C, const DiagLds& B) {
     }
 }
 
+// H_k = D_k L(k,k-1) for the L^{-1} / Z finalizes of row block k (wave 7, SIMD 3: MFMA work
+// stays off SIMD 0, where wave 0 factors).  D_k / L(k,k-1) stay in their LDS buffers until
+// the chain passes step k+2, which waits for this wave's prefetch of step k+2.
+__device__ __forceinline__ void diag_coupling(FlowCtx& C, const DiagLds& B, int k) {
+    constexpr int S = TileCfg<32>::S;
+    lds_wait_ge(&B.w()[DW_D], k);
+    lds_wait_ge(&B.w()[DW_LS], k);
+    WOp x, y;
+    op_rows_lds_ld(x, B.Db(k & 1), S);                   // A[i][k'] = D_k[i][k']
+    op_cols_lds_ld(y, B.Ls(k & 1), S);                   // B[k'][c] = L(k,k-1)[k'][c]
+    WTile hk;
+    wt_zero(hk);
+    wt_mma<false>(hk, x, y);
+    wt_store<true>(hk, C.P.Hk(k), 32);
+}
+
 __device__ __forceinline__ void diag_prefetch(FlowCtx& C, const DiagLds& B, bool sub) {
     constexpr int S = TileCfg<32>::S;
     const FlowArgs& a = C.a;
@@ -721,7 +780,9 @@ __device__ __forceinline__ void diag_prefetch(FlowCtx& C, const DiagLds& B, bool
         }
         wt_to_lds_ld(acc, dst, S);
         if ((threadIdx.x & 63) == 0) lds_put(done, j);
+        if (!sub && j >= 2) diag_coupling(C, B, j - 1);
     }
+    if (!sub && T >= 2) diag_coupling(C, B, T - 1);
 }
 
 __device__ __forceinline__ void flow_diag(FlowCtx& C, double* smem) {
@@ -754,7 +815,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void k_chol_flow(FlowArgs a) {
     flow_worker(C, (blockIdx.x - 1) * FLOW_WAVES + w, smem + w * 32 * WLD);
 }
 
-long flow_npub(int T, int Tp) { return 1024L * (T * (T - 1) / 2 + T + T * (T + 1) / 2 + T * Tp + 3 * T); }
+long flow_npub(int T, int Tp) { return 1024L * (T * (T - 1) / 2 + T + T * (T + 1) / 2 + T * Tp + 4 * T); }
 int flow_nflags(int T, int Tp) { (void)T; (void)Tp; return 1; }   // the abort word
 int flow_trace_count(int T, int nwg) { return 8 * T + (3 + 4 * FLOW_LOG) * FLOW_WAVES * (nwg - 1); }
 

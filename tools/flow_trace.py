@@ -78,6 +78,14 @@ def main():
                     ends.append(e)
             row.append(max(ends) - pub[lev] if ends else float("nan"))
         print(f" {lev:3d} {pub[lev]:7.2f} " + " ".join(f"{v:9.2f}" for v in row))
+    Tm = T - 1
+    print(f"-- tail: last items of row {Tm} R / Y tiles and alpha tiles (D_{Tm} published at {pub[Tm]:.2f})")
+    for (wv, code, lv, b, r, e) in sorted(its, key=lambda x: x[5]):
+        ty, i, j = code >> 20, (code >> 10) & 1023, code & 1023
+        if lv < Tm - 3:
+            continue
+        if (ty == 1 and i == Tm and (j in (0, 10, 20, 30, Tm - 1) or j >= T)) or (ty == 2 and i in (0, 20, Tm)):
+            print(f"   {names[ty]}({i},{j}) lvl {lv:2d}: begin {b:7.2f} ready {r:7.2f} end {e:7.2f}  (work {e-r:5.2f})")
     dur = np.array([e - r for (_, _, _, b, r, e) in its])
     print(f"item work time (after waits): median {np.median(dur):.2f} us  p90 {np.percentile(dur, 90):.2f}  max {dur.max():.2f}")
 
