@@ -94,7 +94,11 @@ __device__ inline void build_flow_owner(int T, int Tp, int W, int* own, int* fla
         const int L = flow_items(code, T);
         const int p = hist[L] + atomicAdd(&cur[L], 1);
         const int r = p / W, q = p % W;
-        const int w = (r & 1) ? W - 1 - q : q;
+        const int sn = (r & 1) ? W - 1 - q : q;
+        // snake position -> wave: first wave 0 of every workgroup, then wave 1, ...: the longest
+        // tiles get a SIMD of their own (waves w and w + 4 share one), spread over all CUs / XCDs
+        const int nwg = W / FLOW_WAVES;
+        const int w = (sn % nwg) * FLOW_WAVES + sn / nwg;
         if (r < FLOW_MAXOWN) own[w * FLOW_MAXOWN + r] = code;
     }
 }

@@ -73,7 +73,7 @@ def main():
                 if k2 != kind:
                     continue
                 # the item that completes level lev: finalize at lev (merged: update at lev-1) / alpha update at lev
-                if (kind in ("A", "R", "Y") and lv == lev - 1 and ((ty == 0 and j == lev) or (ty == 1 and i == lev))) or \
+                if (kind == "A" and lv == lev - 1 and j == lev) or (kind in ("R", "Y") and lv == lev and i == lev) or \
                    (kind == "al" and lv == lev):
                     ends.append(e)
             row.append(max(ends) - pub[lev] if ends else float("nan"))
