@@ -606,6 +606,23 @@ __device__ __forceinline__ void op_cols_lds_ld(WOp& o, const double* S, int ld) 
         for (int s = 0; s < 8; ++s) o.v[b][s] = S[(8 * lq + s) * ld + 16 * b + li];
 }
 
+// H_k = D_k L(k,k-1) for the L^{-1} / Z finalizes of row block k, formed by chain wave 1 while
+// wave 0 factors D_{k+1} (SIMD 1 is idle then; MFMA work of other waves on SIMD 0 would slow the
+// factor, and during the chain's tile products it would slow those).  D_k / L(k,k-1) stay in
+// their LDS buffers until step k+2, which wave 1 only reaches after this.
+__device__ __forceinline__ void diag_coupling(FlowCtx& C, const DiagLds& B, int k) {
+    constexpr int S = TileCfg<32>::S;
+    lds_wait_ge(&B.w()[DW_D], k);
+    lds_wait_ge(&B.w()[DW_LS], k);
+    WOp x, y;
+    op_rows_lds_ld(x, B.Db(k & 1), S);                   // A[i][k'] = D_k[i][k']
+    op_cols_lds_ld(y, B.Ls(k & 1), S);                   // B[k'][c] = L(k,k-1)[k'][c]
+    WTile hk;
+    wt_zero(hk);
+    wt_mma<false>(hk, x, y);
+    wt_store<true>(hk, C.P.Hk(k), 32);
+}
+
 __device__ __forceinline__ void diag_chain(FlowCtx& C, const DiagLds& B) {
     constexpr int S = TileCfg<32>::S;
     const FlowArgs& a = C.a;
@@ -638,6 +655,7 @@ __device__ __forceinline__ void diag_chain(FlowCtx& C, const DiagLds& B) {
             }
         }
         chain_bar(&B.w()[DW_BAR], epoch);
+        if (w == 1 && k >= 2) diag_coupling(C, B, k - 1);   // while wave 0 factors: SIMD 1 is idle
         if (w == 0) {
             lds_wait_ge(&B.w()[DW_DPUB], k - 2);    // wave 4 is done with Db[pk] (D_{k-2})
             if (a.trace && threadIdx.x == 0) a.trace[2 * T + k] = flow_clock() - C.t0;
@@ -645,6 +663,7 @@ __device__ __forceinline__ void diag_chain(FlowCtx& C, const DiagLds& B) {
             if (l == 0) lds_put(&B.w()[DW_D], k);
         }
     }
+    if (w == 1 && T >= 2) diag_coupling(C, B, T - 1);
 }
 
 
@@ -729,22 +748,6 @@ __device__ __forceinline__ void diag_second(FlowCtx& C, const DiagLds& B) {
     }
 }
 
-// H_k = D_k L(k,k-1) for the L^{-1} / Z finalizes of row block k (wave 7, SIMD 3: MFMA work
-// stays off SIMD 0, where wave 0 factors).  D_k / L(k,k-1) stay in their LDS buffers until
-// the chain passes step k+2, which waits for this wave's prefetch of step k+2.
-__device__ __forceinline__ void diag_coupling(FlowCtx& C, const DiagLds& B, int k) {
-    constexpr int S = TileCfg<32>::S;
-    lds_wait_ge(&B.w()[DW_D], k);
-    lds_wait_ge(&B.w()[DW_LS], k);
-    WOp x, y;
-    op_rows_lds_ld(x, B.Db(k & 1), S);                   // A[i][k'] = D_k[i][k']
-    op_cols_lds_ld(y, B.Ls(k & 1), S);                   // B[k'][c] = L(k,k-1)[k'][c]
-    WTile hk;
-    wt_zero(hk);
-    wt_mma<false>(hk, x, y);
-    wt_store<true>(hk, C.P.Hk(k), 32);
-}
-
 __device__ __forceinline__ void diag_prefetch(FlowCtx& C, const DiagLds& B, bool sub) {
     constexpr int S = TileCfg<32>::S;
     const FlowArgs& a = C.a;
@@ -780,9 +783,7 @@ __device__ __forceinline__ void diag_prefetch(FlowCtx& C, const DiagLds& B, bool
         }
         wt_to_lds_ld(acc, dst, S);
         if ((threadIdx.x & 63) == 0) lds_put(done, j);
-        if (!sub && j >= 2) diag_coupling(C, B, j - 1);
     }
-    if (!sub && T >= 2) diag_coupling(C, B, T - 1);
 }
 
 __device__ __forceinline__ void flow_diag(FlowCtx& C, double* smem) {
