@@ -562,7 +562,7 @@ struct DiagLds {
     __device__ int* bad() const { return reinterpret_cast<int*>(base + 10 * E + 32 * 33 + 64); }
     __device__ int* w() const { return bad() + 2; }
 };
-enum { DW_LS = 0, DW_D, DW_LPUB, DW_DPUB, DW_PRE6, DW_PRE7, DW_BAR, DW_L2, DW_N };
+enum { DW_LS = 0, DW_D, DW_LPUB, DW_DPUB, DW_PRE6, DW_PRE7, DW_BAR, DW_L2, DW_P2, DW_N };
 
 __device__ __forceinline__ int lds_get(const int* p) {
     return __hip_atomic_load(const_cast<int*>(p), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -655,6 +655,7 @@ __device__ __forceinline__ void diag_chain(FlowCtx& C, const DiagLds& B) {
             }
         }
         chain_bar(&B.w()[DW_BAR], epoch);
+        if (threadIdx.x == 0) lds_put(&B.w()[DW_P2], k);  // tile products of step k done
         if (w == 1 && k >= 2) diag_coupling(C, B, k - 1);   // while wave 0 factors: SIMD 1 is idle
         if (w == 0) {
             lds_wait_ge(&B.w()[DW_DPUB], k - 2);    // wave 4 is done with Db[pk] (D_{k-2})
@@ -727,11 +728,13 @@ __device__ __forceinline__ void diag_second(FlowCtx& C, const DiagLds& B) {
         if (j >= 3) {
             // panel j-3: A(j,j-2) -= L(j,j-3) L(j-2,j-3)^T  (the worker's L, the chain's Ls of step j-2)
             pub_op(x, C.P.L(j, j - 3), C);
-            lds_wait_ge(&B.w()[DW_LS], j - 2);
+            lds_wait_ge(&B.w()[DW_P2], j - 1);            // MFMA only once the chain's step j-1 products
+            lds_wait_ge(&B.w()[DW_LS], j - 2);            // are done (they share this CU's SIMDs)
             op_rows_lds_ld(y, B.Ls((j - 2) & 1), S);
             wt_mma<true>(acc, x, y);
         }
         lds_wait_ge(&B.w()[DW_D], j - 2);
+        lds_wait_ge(&B.w()[DW_P2], j - 1);
         lds_wait_ge(&B.w()[DW_PRE6], j - 1);              // L2[j & 1] = L(j-2,j-4): last read by
         lds_wait_ge(&B.w()[DW_PRE7], j - 2);              // wave 6 at j-1, wave 7 at j-2
         wt_to_lds_ld(acc, B.L2(j & 1), S);               // staging: A'(j,j-2) as the A operand
@@ -764,6 +767,7 @@ __device__ __forceinline__ void diag_prefetch(FlowCtx& C, const DiagLds& B, bool
             // panel j-3 from the worker's L(j,j-3) and L(j-1,j-3) (wave 5, step j-1)
             WOp x, y;
             pub_op(x, C.P.L(j, j - 3), C);
+            lds_wait_ge(&B.w()[DW_P2], j - 1);
             if (sub) {
                 lds_wait_ge(&B.w()[DW_L2], j - 1);
                 op_rows_lds_ld(y, B.L2((j - 1) & 1), S);
@@ -774,6 +778,7 @@ __device__ __forceinline__ void diag_prefetch(FlowCtx& C, const DiagLds& B, bool
         }
         if (j >= 2) {
             WOp x, y;
+            lds_wait_ge(&B.w()[DW_P2], j - 1);
             lds_wait_ge(&B.w()[DW_L2], j);
             op_rows_lds_ld(x, B.L2(pj), S);
             lds_wait_ge(&B.w()[DW_LS], j - 1);
