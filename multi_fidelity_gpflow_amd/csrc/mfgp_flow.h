@@ -8,7 +8,7 @@ namespace mfgp {
 
 // ---------------------------------------------------------------- tile catalogue
 // code = type << 20 | i << 10 | j ; R tiles use j = column tile c in [0, T + Tp)
-enum : int { FT_A = 0, FT_R = 1, FT_AL = 2 };
+enum : int { FT_A = 0, FT_R = 1, FT_AL = 2, FT_H = 3 };   // FT_H: coupling H_k = D_k L(k,k-1)
 __host__ __device__ inline int flow_code(int type, int i, int j) { return (type << 20) | (i << 10) | j; }
 
 __host__ __device__ inline void flow_tri(int t, int& i, int& j) {   // row-major lower triangle
@@ -23,7 +23,7 @@ __host__ __device__ inline void flow_tri(int t, int& i, int& j) {   // row-major
 // (k,k) of rows k <= 3, which the diag workgroup takes from their initial values.
 __host__ __device__ inline int flow_nA(int T) { return T >= 4 ? T * (T + 1) / 2 - 9 : 0; }
 __host__ __device__ inline int flow_ntiles(int T, int Tp) {
-    return flow_nA(T) + T * (T - 1) / 2 + 2 * T * Tp;
+    return flow_nA(T) + T * (T - 1) / 2 + 2 * T * Tp + (T > 1 ? T - 1 : 0);
 }
 
 __device__ inline int flow_decode(int g, int T, int Tp) {
@@ -36,7 +36,9 @@ __device__ inline int flow_decode(int g, int T, int Tp) {
     g -= nR;
     if (g < T * Tp) return flow_code(FT_R, g / Tp, T + g % Tp);
     g -= T * Tp;
-    return flow_code(FT_AL, g / Tp, g % Tp);
+    if (g < T * Tp) return flow_code(FT_AL, g / Tp, g % Tp);
+    g -= T * Tp;
+    return flow_code(FT_H, g + 1, 0);
 }
 
 // items of a tile: updates at levels [lo, hi] (hi < lo: none), finalize at level fin (-1: none),
@@ -59,10 +61,14 @@ __host__ __device__ inline FlowTile flow_tile(int code, int T) {
         t.lo = (t.j < T) ? t.j : 0;
         t.hi = t.i - 2;                         // panel i-1 enters the finalize through H_i
         t.fin = t.i;
-    } else {
+    } else if (t.type == FT_AL) {
         t.lo = t.i;
         t.hi = T - 1;
         t.fin = -1;
+    } else {   // FT_H: one item at level k, once D_k is out
+        t.lo = 0;
+        t.hi = -1;
+        t.fin = t.i;
     }
     return t;
 }

@@ -323,6 +323,19 @@ __device__ __forceinline__ void flow_finalize_acc(FlowCtx& C, const FlowTile& t,
     wt_store<true>(out, C.P.L(t.i, t.j), 32);
 }
 
+// H_k = D_k L(k,k-1) for the L^{-1} / Z finalizes of row block k (a worker item, so the MFMA
+// work stays off the diag workgroup's SIMDs)
+__device__ __forceinline__ void flow_coupling(FlowCtx& C, int k, double* S) {
+    WTile lt, out;
+    WOp d;
+    pub_wt(lt, C.P.L(k, k - 1), C);
+    wt_to_lds(lt, S);
+    pub_op(d, C.P.D(k), C);
+    wt_zero(out);
+    wt_mma_lds_b(out, d, S);                             // A[i][k'] = D_k[i][k'], B[k'][c] = L(k,k-1)[k'][c]
+    wt_store<true>(out, C.P.Hk(k), 32);
+}
+
 // A finalize with no update before it (tiles (i,0))
 __device__ __forceinline__ void flow_finalize(FlowCtx& C, const FlowTile& t, double* S) {
     WTile acc;
@@ -470,12 +483,14 @@ __device__ __forceinline__ void flow_item_log(const FlowCtx& C, int wid, int n, 
     e[3] = t1 - C.t0;
 }
 
-// Slot order of a worker wave: A tiles first (they feed the chain), nearest the diagonal
-// first; then the R / Y tiles, then alpha.  Items run level by level in this order.
+// Slot order of a worker wave: couplings H_k, then A tiles (they feed the chain), nearest the
+// diagonal first; then the R / Y tiles, then alpha.  Items run level by level in this order.
 __device__ __forceinline__ int flow_prio(int code) {
     if (code < 0) return 1 << 30;
     const FlowTile t = flow_tile(code, 1024);
-    return (t.type << 16) | (t.i << 8) | t.j;
+    // H_k first: the R finalizes of the same level wait for it (a later slot would deadlock)
+    const int rank = t.type == FT_H ? 0 : t.type + 1;
+    return (rank << 16) | (t.i << 8) | t.j;
 }
 
 __device__ __forceinline__ void flow_worker(FlowCtx& C, int wid, double* S) {
@@ -510,6 +525,7 @@ __device__ __forceinline__ void flow_worker(FlowCtx& C, int wid, double* S) {
             if (t.fin == l && (t.type == FT_R || t.hi < t.lo)) {
                 const long long i0 = flow_clock(), w0 = C.waited;
                 if (t.type == FT_R) flow_finalize_r(C, t, S);
+                else if (t.type == FT_H) flow_coupling(C, t.i, S);
                 else flow_finalize(C, t, S);
                 flow_item_log(C, wid, nitem++, cs, l, i0, w0);
             }
@@ -606,23 +622,6 @@ __device__ __forceinline__ void op_cols_lds_ld(WOp& o, const double* S, int ld) 
         for (int s = 0; s < 8; ++s) o.v[b][s] = S[(8 * lq + s) * ld + 16 * b + li];
 }
 
-// H_k = D_k L(k,k-1) for the L^{-1} / Z finalizes of row block k, formed by chain wave 1 while
-// wave 0 factors D_{k+1} (SIMD 1 is idle then; MFMA work of other waves on SIMD 0 would slow the
-// factor, and during the chain's tile products it would slow those).  D_k / L(k,k-1) stay in
-// their LDS buffers until step k+2, which wave 1 only reaches after this.
-__device__ __forceinline__ void diag_coupling(FlowCtx& C, const DiagLds& B, int k) {
-    constexpr int S = TileCfg<32>::S;
-    lds_wait_ge(&B.w()[DW_D], k);
-    lds_wait_ge(&B.w()[DW_LS], k);
-    WOp x, y;
-    op_rows_lds_ld(x, B.Db(k & 1), S);                   // A[i][k'] = D_k[i][k']
-    op_cols_lds_ld(y, B.Ls(k & 1), S);                   // B[k'][c] = L(k,k-1)[k'][c]
-    WTile hk;
-    wt_zero(hk);
-    wt_mma<false>(hk, x, y);
-    wt_store<true>(hk, C.P.Hk(k), 32);
-}
-
 __device__ __forceinline__ void diag_chain(FlowCtx& C, const DiagLds& B) {
     constexpr int S = TileCfg<32>::S;
     const FlowArgs& a = C.a;
@@ -656,7 +655,6 @@ __device__ __forceinline__ void diag_chain(FlowCtx& C, const DiagLds& B) {
         }
         chain_bar(&B.w()[DW_BAR], epoch);
         if (threadIdx.x == 0) lds_put(&B.w()[DW_P2], k);  // tile products of step k done
-        if (w == 1 && k >= 2) diag_coupling(C, B, k - 1);   // while wave 0 factors: SIMD 1 is idle
         if (w == 0) {
             lds_wait_ge(&B.w()[DW_DPUB], k - 2);    // wave 4 is done with Db[pk] (D_{k-2})
             if (a.trace && threadIdx.x == 0) a.trace[2 * T + k] = flow_clock() - C.t0;
@@ -664,7 +662,6 @@ __device__ __forceinline__ void diag_chain(FlowCtx& C, const DiagLds& B) {
             if (l == 0) lds_put(&B.w()[DW_D], k);
         }
     }
-    if (w == 1 && T >= 2) diag_coupling(C, B, T - 1);
 }
 
 

@@ -9,7 +9,7 @@ for small / ragged tile counts and small wave counts (several tiles per wave, wh
 items inside a wave matters)."""
 import pytest
 
-FT_A, FT_R, FT_AL = 0, 1, 2
+FT_A, FT_R, FT_AL, FT_H = 0, 1, 2, 3
 MAXOWN = 4
 
 
@@ -25,7 +25,7 @@ def n_a(T):
 
 
 def ntiles(T, Tp):
-    return n_a(T) + T * (T - 1) // 2 + 2 * T * Tp
+    return n_a(T) + T * (T - 1) // 2 + 2 * T * Tp + (T - 1 if T > 1 else 0)
 
 
 def decode(g, T, Tp):
@@ -41,7 +41,10 @@ def decode(g, T, Tp):
     if g < T * Tp:
         return (FT_R, g // Tp, T + g % Tp)
     g -= T * Tp
-    return (FT_AL, g // Tp, g % Tp)
+    if g < T * Tp:
+        return (FT_AL, g // Tp, g % Tp)
+    g -= T * Tp
+    return (FT_H, g + 1, 0)
 
 
 def tile(code, T):
@@ -52,8 +55,10 @@ def tile(code, T):
             return 0, i - 4, -1, True
         return 0, j - 1, j, False
     if ty == FT_R:
-        return (j if j < T else 0), i - 1, i, False
-    return i, T - 1, -1, False
+        return (j if j < T else 0), i - 2, i, False      # panel i-1 through H_i in the finalize
+    if ty == FT_AL:
+        return i, T - 1, -1, False
+    return 0, -1, i, False                              # FT_H: H_k = D_k L(k,k-1) at level k
 
 
 def items(code, T):
@@ -77,19 +82,21 @@ def owner_table(T, Tp, W):
 
 
 def prio(c):
-    return (c[0] << 16) | (c[1] << 8) | c[2]
+    rank = 0 if c[0] == FT_H else c[0] + 1          # flow_prio: H_k before the R finalizes needing it
+    return (rank << 16) | (c[1] << 8) | c[2]
 
 
 def wave_program(slots, T):
     """The item sequence of one worker wave (flow_worker): slots in priority order; per level
-    the stand-alone finalizes, then the updates (an A tile's last update carries its finalize)."""
+    the stand-alone finalizes (R, H, and A tiles without updates), then the updates (an A tile's
+    last update carries its finalize)."""
     slots = sorted([c for c in slots if c is not None], key=prio)
     last = max([max(tile(c, T)[1], tile(c, T)[2]) for c in slots] or [-1])
     prog = []
     for l in range(last + 1):
         for c in slots:
             lo, hi, fin, _ = tile(c, T)
-            if fin == l and hi < lo:
+            if fin == l and (c[0] in (FT_R, FT_H) or hi < lo):
                 prog.append(("fin", c, l))
         for c in slots:
             lo, hi, fin, _ = tile(c, T)
@@ -103,9 +110,17 @@ def needs_and_makes(item, T):
     kind, (ty, i, j), l = item
     lo, hi, fin, pub = tile((ty, i, j), T)
     need, make = [], []
-    if kind == "fin":                                 # stand-alone finalize: A (i,0), Y tiles of row 0
+    if kind == "fin":                                 # stand-alone finalize
         need.append(("D", fin))
-        make.append(("L", i, j) if ty == FT_A else ("X", i, j))
+        if ty == FT_A:
+            make.append(("L", i, j))
+        elif ty == FT_H:
+            need.append(("L", i, i - 1))
+            make.append(("Hk", i))
+        else:                                         # X(i,c) = D_i R'' - H_i X(i-1,c)
+            if i >= 1:
+                need += [("Hk", i), ("X", i - 1, j)]
+            make.append(("X", i, j))
         return need, make
     if ty == FT_A:
         need += [("L", i, l), ("L", j, l)]
@@ -116,9 +131,6 @@ def needs_and_makes(item, T):
             make.append(("H", i, j))
     elif ty == FT_R:
         need += [("L", i, l), ("X", l, j)]
-        if fin == l + 1:
-            need.append(("D", fin))
-            make.append(("X", i, j))
     else:
         need += [("X", l, i), ("X", l, T + j)]
     return need, make

@@ -53,13 +53,15 @@ def main():
     print("latest workers (start, done, waited):", [tuple(np.round(w[i], 1)) for i in late])
     W = (cnt.value - 8 * T) // (3 + 4 * 40)
     its = items(tr, T, W)
-    names = {0: "A", 1: "R", 2: "al"}
+    names = {0: "A", 1: "R", 2: "al", 3: "H"}
     for kk in (12, 20, 28):
         print(f"-- items feeding chain step {kk} (D_{kk-3} published at {pub[kk-3]:.2f}):")
-        want = {(0, kk, kk - 1), (0, kk, kk - 2), (0, kk, kk), (0, kk, kk - 3), (0, kk - 1, kk - 3)}
+        want = {(0, kk, kk - 1), (0, kk, kk - 2), (0, kk, kk), (0, kk, kk - 4), (0, kk - 1, kk - 4),
+                (0, kk, kk - 3), (0, kk - 1, kk - 5), (0, kk, kk - 5)}
+        print(f"   (D_{kk-5} {pub[kk-5]:.2f}  D_{kk-4} {pub[kk-4]:.2f}  D_{kk-3} {pub[kk-3]:.2f})")
         for (wv, code, lev, b, r, e) in its:
             ty, i, j = code >> 20, (code >> 10) & 1023, code & 1023
-            if (ty, i, j) in want and lev >= kk - 5:
+            if (ty, i, j) in want and lev >= kk - 7:
                 print(f"   {names[ty]}({i},{j}) lvl {lev:2d}: begin {b:7.2f} ready {r:7.2f} end {e:7.2f}  (work {e-r:5.2f})")
     # lag of the L^{-1} / Z / alpha pipelines behind the chain: per level, latest item end - D_l published
     print(" lvl  D_l    A-fin lag  R-fin lag  Y-fin lag  alpha lag   (us after D_l published)")
@@ -69,7 +71,7 @@ def main():
             ends = []
             for (wv, code, lv, b, r, e) in its:
                 ty, i, j = code >> 20, (code >> 10) & 1023, code & 1023
-                k2 = {0: "A", 1: ("Y" if j >= T else "R"), 2: "al"}[ty]
+                k2 = {0: "A", 1: ("Y" if j >= T else "R"), 2: "al", 3: "H"}[ty]
                 if k2 != kind:
                     continue
                 # the item that completes level lev: finalize at lev (merged: update at lev-1) / alpha update at lev
