@@ -156,6 +156,7 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
         const bool order = want_grad && h->grad_chunk + L.Tp < 2048;   // gram LDS holds the histogram
         if (order) { g.gorder = L.gorder; g.gT = L.T; g.gchunk = h->grad_chunk; g.gTp = L.Tp; }
         if (L.flow_wgs) { g.fown = L.own; g.fW = FLOW_WAVES * (L.flow_wgs - 1); g.fflags = L.flags; g.nfflags = L.nflags; g.fpub = L.pub; g.npub = L.npub; }
+        if (L.flow_wgs && h->flow_trace) g.dbg = L.trace + L.ntrace - 3 * 2048;   // k_gram timeline (diagnostic)
         launch_gram<NB>(g, L.T * (L.T + 1) / 2 + (order ? 1 : 0) + (L.flow_wgs ? 1 : 0), 1, s);
     }
     if (pm) pm->mark(s);

@@ -820,7 +820,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void k_chol_flow(FlowArgs a) {
 
 long flow_npub(int T, int Tp) { return 1024L * (T * (T - 1) / 2 + T + T * (T + 1) / 2 + T * Tp + 4 * T); }
 int flow_nflags(int T, int Tp) { (void)T; (void)Tp; return 1; }   // the abort word
-int flow_trace_count(int T, int nwg) { return 8 * T + (3 + 4 * FLOW_LOG) * FLOW_WAVES * (nwg - 1); }
+int flow_trace_count(int T, int nwg) { return 8 * T + (3 + 4 * FLOW_LOG) * FLOW_WAVES * (nwg - 1) + 3 * 2048; }
 
 void launch_chol_flow(const FlowArgs& a, int nwg, hipStream_t s) {
     static bool attr = false;

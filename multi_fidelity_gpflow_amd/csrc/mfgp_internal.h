@@ -30,6 +30,7 @@ struct GramArgs {
     // area with the sentinel
     int* fown; int fW; int* fflags; int nfflags;
     double* fpub; long npub;
+    long long* dbg;               // diagnostic per-workgroup timeline (nullptr: off)
 };
 
 // k_chol_flow (mfgp_flow.hip): persistent dataflow Cholesky + L^{-1} + Z + alpha, NB = 32, batch 1

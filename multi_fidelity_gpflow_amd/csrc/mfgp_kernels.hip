@@ -54,9 +54,80 @@ __device__ __forceinline__ void stage_rows(double* aL, double* aD, double* nL, d
 }
 
 // one Gram entry from staged rows (GPflow: dist = -2 a.b + (|a|^2 + |b|^2); k = v exp(-dist/2))
+// kernel scalars held in registers (one load each per workgroup, issued with the row loads)
+struct MFScal {
+    double vL_, vD_, rho_;
+    __device__ double vL() const { return vL_; }
+    __device__ double vD() const { return vD_; }
+    __device__ double rho() const { return rho_; }
+};
+
+// Both row blocks of a tile in ONE memory round trip: every X element, fidelity flag and
+// lengthscale a thread needs is loaded before any is used (the two-pass stage_rows took ~4
+// dependent global-load latencies).  Then aL = X / lL (GPflow divides; here X * rcp(lL), within
+// an ulp), squared norms and flags into LDS.
+template <int NB>
+__device__ __forceinline__ void stage_pair(double* aL1, double* aD1, double* nL1, double* nD1, double* f1,
+                                           double* aL2, double* aD2, double* nL2, double* nD2, double* f2,
+                                           const double* X1, long ldx1, int n1, int r01,
+                                           const double* X2, long ldx2, int n2, int r02,
+                                           int D, const double* theta, int rbf_only) {
+    constexpr int PER = (NB * MAXD + NTHREADS - 1) / NTHREADS;
+    double x1[PER], x2[PER], lL[PER], lD[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int e = threadIdx.x + q * NTHREADS;
+        if (e < NB * D) {
+            const int r = e / D, d = e % D;
+            x1[q] = (r01 + r < n1) ? X1[(long)(r01 + r) * ldx1 + d] : 0.0;
+            x2[q] = (r02 + r < n2) ? X2[(long)(r02 + r) * ldx2 + d] : 0.0;
+            lL[q] = theta[1 + d];
+            lD[q] = rbf_only ? 1.0 : theta[2 + D + d];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        if (threadIdx.x + q * NTHREADS < NB * D) {
+            lL[q] = rcp_nr(lL[q]);   // 1/l to <= 1 ulp: x * (1/l) for the IEEE division's ~30-op sequence
+            lD[q] = rcp_nr(lD[q]);
+        }
+    }
+    const int t = threadIdx.x;
+    double fv = -1.0;
+    if (t < NB) fv = (r01 + t < n1) ? (rbf_only ? 0.0 : X1[(long)(r01 + t) * ldx1 + D]) : -1.0;
+    else if (t < 2 * NB) fv = (r02 + t - NB < n2) ? (rbf_only ? 0.0 : X2[(long)(r02 + t - NB) * ldx2 + D]) : -1.0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int e = threadIdx.x + q * NTHREADS;
+        if (e < NB * D) {
+            const int r = e / D, d = e % D;
+            aL1[r * XS + d] = x1[q] * lL[q];
+            aL2[r * XS + d] = x2[q] * lL[q];
+            if (!rbf_only) { aD1[r * XS + d] = x1[q] * lD[q]; aD2[r * XS + d] = x2[q] * lD[q]; }
+        }
+    }
+    if (t < NB) f1[t] = fv;
+    else if (t < 2 * NB) f2[t - NB] = fv;
+    __syncthreads();
+    if (t < 2 * NB) {
+        const int r = t & (NB - 1);
+        const double* aL = (t < NB ? aL1 : aL2) + r * XS;
+        const double* aD = (t < NB ? aD1 : aD2) + r * XS;
+        double sL = 0.0, sD = 0.0;
+        for (int d = 0; d < D; ++d) {
+            const double a = aL[d];
+            sL += a * a;
+            if (!rbf_only) { const double b = aD[d]; sD += b * b; }
+        }
+        if (t < NB) { nL1[r] = sL; nD1[r] = sD; }
+        else { nL2[r] = sL; nD2[r] = sD; }
+    }
+}
+
+template <class TH>
 __device__ __forceinline__ double gram_entry(const double* aL1, const double* aD1, double nL1, double nD1, double f1,
                                              const double* aL2, const double* aD2, double nL2, double nD2, double f2,
-                                             int D, const MFTheta& th, int rbf_only) {
+                                             int D, const TH& th, int rbf_only) {
     if (rbf_only) {
         if (f1 < 0.0 || f2 < 0.0) return 0.0;
         double dot = 0.0;
@@ -76,6 +147,21 @@ __device__ __forceinline__ double gram_entry(const double* aL1, const double* aD
     for (int d = 0; d < D; ++d) dotD += aD1[d] * aD2[d];
     const double kD = th.vD() * exp(-0.5 * (-2.0 * dotD + (nD1 + nD2)));
     return kL * (rho * rho) + kD;                      // K_HH (linear.py:96)
+}
+
+// Sentinel fill of the k_chol_flow publication area (grid-stride over ALL workgroups of the
+// launch).  sc1 (write-through, line dropped from this XCD's L2): a plain store would leave a
+// clean copy of the sentinel in this XCD's L2 that the flow's sc1 polls could be served from.
+// Run LAST in a workgroup: the stores share the vmcnt queue with later loads, and a load's
+// data waits for every older store to be acknowledged.
+__device__ __forceinline__ void gram_fill_pub(const GramArgs& a) {
+#ifndef GRAM_DIAG_NOFILL
+    if (a.fpub && blockIdx.z == 0) {
+        unsigned long long* dst = reinterpret_cast<unsigned long long*>(a.fpub);
+        for (long e = blockIdx.x * (long)NTHREADS + threadIdx.x; e < a.npub; e += (long)gridDim.x * NTHREADS)
+            __hip_atomic_store(dst + e, FLOW_SENTINEL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#endif
 }
 
 template <int NB>
@@ -99,21 +185,23 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
                                                    // would shift the dynamic base off 16 B (G17)
 
     const int b = blockIdx.z;
-    if (a.fpub && b == 0) {
-        // sentinel fill of the k_chol_flow publication area, spread over the grid.  sc1 (write-
-        // through, line dropped from this XCD's L2): a plain store would leave a clean copy of
-        // the sentinel in this XCD's L2 that the flow's sc1 polls could be served from.
-        unsigned long long* dst = reinterpret_cast<unsigned long long*>(a.fpub);
-        for (long e = blockIdx.x * (long)NTHREADS + threadIdx.x; e < a.npub; e += (long)gridDim.x * NTHREADS)
-            __hip_atomic_store(dst + e, FLOW_SENTINEL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    const long long dbg_t0 = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+#ifdef GRAM_DIAG_EMPTY
+    if (a.padded) return;
+#endif
     if (a.gorder && blockIdx.x == gridDim.x - 1) {   // extra workgroup: k_grad task order
+#ifndef GRAM_DIAG_NOORDER
         if (b == 0) build_grad_order(a.gT, a.gchunk, a.gTp, a.gorder, reinterpret_cast<int*>(smem));
+#endif
+        gram_fill_pub(a);
         return;
     }
     if (a.fown && blockIdx.x == gridDim.x - 1 - (a.gorder ? 1 : 0)) {   // extra: flow owner table
+#ifndef GRAM_DIAG_NOOWNER
         if (b == 0) build_flow_owner(a.npad / NB, a.ppad / NB, a.fW, a.fown, a.fflags, a.nfflags,
                                      reinterpret_cast<int*>(smem));
+#endif
+        gram_fill_pub(a);
         return;
     }
     if (a.cnt && blockIdx.x == 0 && b == 0)
@@ -130,6 +218,16 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
         tj = blockIdx.x % a.tiles_c;
     }
     const MFTheta th{a.theta + b * a.stheta, a.D};
+    MFScal sc{0.0, 0.0, 0.0};
+    double noise = 0.0;
+    if (!a.nlf) {   // scalars first: their loads overlap the row loads of stage_pair
+        const double* tp = a.theta + b * a.stheta;
+        sc.vL_ = tp[0];
+        if (!a.rbf_only) { sc.vD_ = tp[1 + a.D]; sc.rho_ = tp[2 + 2 * a.D]; }
+        if (a.add_noise) noise = tp[kernel_theta_size(0, a.D) - 1];
+    } else if (a.add_noise) {
+        noise = a.theta[b * a.stheta + kernel_theta_size(a.nlf, a.D) - 1];
+    }
     const GraphTheta gth{a.theta + b * a.stheta, a.D, a.nlf};
     const double* X1 = a.X1 + b * a.sx1;
     const double* X2 = a.X2 + b * a.sx2;
@@ -146,19 +244,27 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
             }
         }
     } else {
-        stage_rows<NB>(aL1, aD1, nL1, nD1, f1, X1, a.ldx1, a.n1, ti * NB, a.D, th, a.rbf_only);
-        stage_rows<NB>(aL2, aD2, nL2, nD2, f2, X2, a.ldx2, a.n2, tj * NB, a.D, th, a.rbf_only);
+        stage_pair<NB>(aL1, aD1, nL1, nD1, f1, aL2, aD2, nL2, nD2, f2, X1, a.ldx1, a.n1, ti * NB,
+                       X2, a.ldx2, a.n2, tj * NB, a.D, a.theta + b * a.stheta, a.rbf_only);
     }
     __syncthreads();
+    if (a.dbg && threadIdx.x == 0) a.dbg[3 * blockIdx.x] = __builtin_amdgcn_s_memrealtime() - dbg_t0;   // stage time (ticks)
 
-    const double noise = a.add_noise ? a.theta[b * a.stheta + kernel_theta_size(a.nlf, a.D) - 1] : 0.0;
+#ifdef GRAM_DIAG_NOENTRY
+    if (a.padded) {
+        for (int e = threadIdx.x; e < NB * NB; e += NTHREADS) tile[(e / NB) * S + e % NB] = (ti == tj && e / NB == e % NB) ? 1.0 : 0.0;
+        __syncthreads();
+        tile_store<NB>(a.out + b * a.so + (long)ti * NB * a.ldo + tj * NB, a.ldo, tile);
+        return;
+    }
+#endif
     double* out = a.out + b * a.so;
     for (int e = threadIdx.x; e < NB * NB; e += NTHREADS) {
         const int r = e / NB, c = e % NB;
         const int gi = ti * NB + r, gj = tj * NB + c;
         double v = a.nlf ? graph_entry(aL1 + r * XS, aL2 + c * XS, (int)f1[r], (int)f2[c], gth)
                          : gram_entry(aL1 + r * XS, aD1 + r * XS, nL1[r], nD1[r], f1[r],
-                                      aL2 + c * XS, aD2 + c * XS, nL2[c], nD2[c], f2[c], a.D, th, a.rbf_only);
+                                      aL2 + c * XS, aD2 + c * XS, nL2[c], nD2[c], f2[c], a.D, sc, a.rbf_only);
         if (a.padded) {
             if (gi == gj) v = (gi < a.n1) ? v + noise + a.diag_add : 1.0;   // identity padding
             tile[r * S + c] = v;
@@ -167,7 +273,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
             if (gi < a.n1 && gj < a.n2) out[(long)gi * a.ldo + gj] = v;
         }
     }
-    if (!a.padded) return;
+    if (!a.padded) { gram_fill_pub(a); return; }
     if (a.R != nullptr) {
         // fused RHS init: R tile (ti, tj) of the identity part, and row block ti of Y
         double* Rb = a.R + b * a.sR;
@@ -185,8 +291,13 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
         }
     }
     __syncthreads();
+    if (a.dbg && threadIdx.x == 0) a.dbg[3 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - dbg_t0;
     tile_store<NB>(out + (long)ti * NB * a.ldo + tj * NB, a.ldo, tile);
+#ifdef GRAM_DIAG_NOFACTOR
+    if (false) {
+#else
     if (a.Dd != nullptr && ti == 0 && tj == 0) {
+#endif
         // fused factor of the first diagonal tile (step "-1" of the tile Cholesky)
         __syncthreads();
         tile_potrf_inv<NB>(tile, rtile, dg, &bad);
@@ -194,6 +305,8 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
         for (int r = threadIdx.x; r < NB; r += NTHREADS) a.ldiag[b * a.sL + r] = dg[r];
         if (threadIdx.x == 0) a.info[b] = bad;   // first writer of info in the sequence: initialises it
     }
+    gram_fill_pub(a);
+    if (a.dbg && threadIdx.x == 0) a.dbg[3 * blockIdx.x + 2] = __builtin_amdgcn_s_memrealtime() - dbg_t0;
 }
 
 size_t gram_smem_bytes(int nb) {

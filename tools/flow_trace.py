@@ -51,7 +51,13 @@ def main():
           f" max {w[:,2].max():.1f}")
     late = np.argsort(-w[:, 1])[:8]
     print("latest workers (start, done, waited):", [tuple(np.round(w[i], 1)) for i in late])
-    W = (cnt.value - 8 * T) // (3 + 4 * 40)
+    W = (cnt.value - 8 * T - 3 * 2048) // (3 + 4 * 40)
+    g = ws[off.value + 8 * (cnt.value - 3 * 2048): off.value + 8 * cnt.value].view(torch.int64).cpu().numpy().reshape(-1, 3)
+    g = g[g[:, 2] > 0].astype(np.float64) / 100.0
+    if len(g):
+        print(f"k_gram per workgroup (us since its start): staged median {np.median(g[:, 0]):.2f} max {g[:, 0].max():.2f};"
+              f" entries done median {np.median(g[:, 1]):.2f} max {g[:, 1].max():.2f}; end median {np.median(g[:, 2]):.2f}"
+              f" max {g[:, 2].max():.2f}")
     its = items(tr, T, W)
     names = {0: "A", 1: "R", 2: "al", 3: "H"}
     for kk in (12, 20, 28):
