@@ -45,10 +45,10 @@ struct Carve {
 struct GprLayout {
     int nb, npad, T, ppad, Tp, G, gstride, ng;
     double *A, *R, *Xo, *Dd, *ldiag, *alpha, *zpart, *gpart, *items;
-    int* gorder;   // k_grad workgroup -> task table, built by k_gram each call
+    int* gorder;   // k_grad workgroup -> task table (+ key), built or verified by k_gram each call
     int* cnt;   // reduce-arrival counter, zeroed by k_gram each call
     int ncnt;
-    // k_chol_flow (flow_wgs > 0): flags + owner table, both rebuilt by k_gram each call
+    // k_chol_flow (flow_wgs > 0): flags (zeroed) + owner table (built or verified) by k_gram each call
     int flow_wgs, nflags;
     int *flags, *own;
     double* pub;        // publication area (sentinel-filled by k_gram)
@@ -89,13 +89,13 @@ static GprLayout gpr_layout(int nb, int n, int p, int d, void* ws, int grad_chun
     L.items = c.take<double>((size_t)L.G + 8);
     L.ncnt = 1;
     L.cnt = c.take<int>((size_t)L.ncnt);
-    L.gorder = c.take<int>((size_t)L.ng);
+    L.gorder = c.take<int>((size_t)L.ng + SCHED_KEY);
     L.flow_wgs = flow_grid(nb, L.T, L.Tp, flow_wgs);
     L.nflags = L.flow_wgs ? flow_nflags(L.T, L.Tp) : 0;
     L.flags = c.take<int>((size_t)L.nflags * FLOW_FSTRIDE);
     L.npub = L.flow_wgs ? flow_npub(L.T, L.Tp) : 0;
     L.pub = c.take<double>((size_t)L.npub);
-    L.own = c.take<int>(L.flow_wgs ? (size_t)FLOW_WAVES * (L.flow_wgs - 1) * FLOW_MAXOWN : 0);
+    L.own = c.take<int>(L.flow_wgs ? (size_t)FLOW_WAVES * (L.flow_wgs - 1) * FLOW_MAXOWN + SCHED_KEY : 0);
     L.ntrace = L.flow_wgs ? flow_trace_count(L.T, L.flow_wgs) : 0;
     L.trace = c.take<long long>((size_t)L.ntrace);
     L.bytes = c.off + 256;

@@ -1416,4 +1416,58 @@ __device__ __forceinline__ double graph_entry(const double* xa, const double* xb
     return s + graph_k(xa, xb, m, th);
 }
 
+// ---------------------------------------------------------------- cached schedule tables
+// A schedule table (k_grad task order, k_chol_flow owner table) is a pure function of a few
+// shape parameters, so the workgroup that builds it keeps it in the workspace with a key
+// {magic, p0, p1, p2, hash of the contents} at tab[n .. n + 5) and skips the rebuild when a
+// later call finds both the key and the hash intact.  The hash is what makes this safe: the
+// workspace is shared with every other entry point, which may have overwritten any part of it.
+constexpr int SCHED_KEY = 5;
+__device__ inline unsigned sched_hash(const int* tab, int n, unsigned* sh) {
+    if (threadIdx.x == 0) *sh = 0u;
+    __syncthreads();
+    auto mix = [](int v, int e) {
+        unsigned t = (unsigned)v * 0x9E3779B1u + (unsigned)e * 0x85EBCA77u + 0x165667B1u;
+        t ^= t >> 15;
+        t *= 0x2C1B3C6Du;
+        return t ^ (t >> 12);
+    };
+    // 16-B loads, 8 in flight per thread: one memory round trip per 8 K ints (tab is 256-B
+    // aligned by the workspace carve)
+    unsigned h = 0u;
+    const int4* t4 = reinterpret_cast<const int4*>(tab);
+    const int n4 = n / 4;
+    for (int e0 = threadIdx.x; e0 < n4; e0 += 8 * blockDim.x) {
+        int4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int e = e0 + u * blockDim.x;
+            v[u] = e < n4 ? t4[e] : make_int4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int e = e0 + u * blockDim.x;
+            if (e < n4) h += mix(v[u].x, 4 * e) + mix(v[u].y, 4 * e + 1) + mix(v[u].z, 4 * e + 2) + mix(v[u].w, 4 * e + 3);
+        }
+    }
+    for (int e = 4 * n4 + threadIdx.x; e < n; e += blockDim.x) h += mix(tab[e], e);
+    atomicAdd(sh, h);
+    __syncthreads();
+    const unsigned r = *sh;
+    __syncthreads();
+    return r;
+}
+__device__ inline bool sched_cached(const int* tab, int n, int magic, int p0, int p1, int p2, unsigned* sh) {
+    const unsigned h = sched_hash(tab, n, sh);
+    const int* k = tab + n;
+    return k[0] == magic && k[1] == p0 && k[2] == p1 && k[3] == p2 && (unsigned)k[4] == h;
+}
+__device__ inline void sched_seal(int* tab, int n, int magic, int p0, int p1, int p2, unsigned* sh) {
+    __syncthreads();   // the table's stores (same CU: workgroup scope suffices)
+    const unsigned h = sched_hash(tab, n, sh);
+    if (threadIdx.x == 0) {
+        tab[n] = magic; tab[n + 1] = p0; tab[n + 2] = p1; tab[n + 3] = p2; tab[n + 4] = (int)h;
+    }
+}
+
 }  // namespace mfgp

@@ -79,13 +79,18 @@ __host__ __device__ inline int flow_items(int code, int T) {
 
 // Owner table: tiles by descending item count, dealt in snake order over the W worker waves
 // (slot r of wave w).  Run by ONE workgroup (k_gram's extra workgroup) before the flow launch;
-// it also zeroes the flags.  sh: >= 256 ints of LDS.
+// it also zeroes the flags.  sh: >= 257 ints of LDS.
+// own holds W * FLOW_MAXOWN + SCHED_KEY ints: a table found intact from an earlier call with the
+// same (T, Tp, W) is kept (sched_cached); the flags are zeroed every call.
+constexpr int FLOW_OWN_MAGIC = 0x464C4F57;
 __device__ inline void build_flow_owner(int T, int Tp, int W, int* own, int* flags, int nflags, int* sh) {
     int* hist = sh;          // [128] count per item count, then the start of its rank range
     int* cur = sh + 128;     // [128]
+    unsigned* hs = reinterpret_cast<unsigned*>(sh + 256);
+    for (int e = threadIdx.x; e < nflags; e += NTHREADS) flags[e * FLOW_FSTRIDE] = 0;
+    if (sched_cached(own, W * FLOW_MAXOWN, FLOW_OWN_MAGIC, T, Tp, W, hs)) return;
     for (int e = threadIdx.x; e < 128; e += NTHREADS) { hist[e] = 0; cur[e] = 0; }
     for (int e = threadIdx.x; e < W * FLOW_MAXOWN; e += NTHREADS) own[e] = -1;
-    for (int e = threadIdx.x; e < nflags; e += NTHREADS) flags[e * FLOW_FSTRIDE] = 0;
     __syncthreads();
     const int n = flow_ntiles(T, Tp);
     for (int g = threadIdx.x; g < n; g += blockDim.x) atomicAdd(&hist[flow_items(flow_decode(g, T, Tp), T)], 1);
@@ -107,6 +112,7 @@ __device__ inline void build_flow_owner(int T, int Tp, int W, int* own, int* fla
         const int w = (sn % nwg) * FLOW_WAVES + sn / nwg;
         if (r < FLOW_MAXOWN) own[w * FLOW_MAXOWN + r] = code;
     }
+    sched_seal(own, W * FLOW_MAXOWN, FLOW_OWN_MAGIC, T, Tp, W, hs);
 }
 
 }  // namespace mfgp

@@ -193,6 +193,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
 #ifndef GRAM_DIAG_NOORDER
         if (b == 0) build_grad_order(a.gT, a.gchunk, a.gTp, a.gorder, reinterpret_cast<int*>(smem));
 #endif
+        if (a.dbg && threadIdx.x == 0) a.dbg[3 * blockIdx.x + 2] = __builtin_amdgcn_s_memrealtime() - dbg_t0;
         gram_fill_pub(a);
         return;
     }
@@ -201,6 +202,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
         if (b == 0) build_flow_owner(a.npad / NB, a.ppad / NB, a.fW, a.fown, a.fflags, a.nfflags,
                                      reinterpret_cast<int*>(smem));
 #endif
+        if (a.dbg && threadIdx.x == 0) a.dbg[3 * blockIdx.x + 2] = __builtin_amdgcn_s_memrealtime() - dbg_t0;
         gram_fill_pub(a);
         return;
     }
@@ -281,12 +283,23 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
             const int r = e / NB, c = e % NB;
             Rb[(long)(ti * NB + r) * a.ldr + tj * NB + c] = (ti == tj && r == c) ? 1.0 : 0.0;
         }
-        if (tj == 0) {
+        if (tj == 0) {   // 8 loads in flight per thread before the stores
             const double* Yb = a.Y + b * a.sY;
-            for (int e = threadIdx.x; e < NB * a.ppad; e += NTHREADS) {
-                const int r = e / a.ppad, c = e % a.ppad;
-                const int gr = ti * NB + r;
-                Rb[(long)gr * a.ldr + a.npad + c] = (gr < a.n1 && c < a.p) ? Yb[(long)gr * a.ldy + c] : 0.0;
+            const int ne = NB * a.ppad;
+            for (int e0 = threadIdx.x; e0 < ne; e0 += 8 * NTHREADS) {
+                double v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int e = e0 + u * NTHREADS;
+                    const int r = e / a.ppad, c = e % a.ppad, gr = ti * NB + r;
+                    v[u] = (e < ne && gr < a.n1 && c < a.p) ? Yb[(long)gr * a.ldy + c] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int e = e0 + u * NTHREADS;
+                    const int r = e / a.ppad, c = e % a.ppad;
+                    if (e < ne) Rb[(long)(ti * NB + r) * a.ldr + a.npad + c] = v[u];
+                }
             }
         }
     }
@@ -571,9 +584,13 @@ __device__ __forceinline__ int grad_decode(int t, int T, int chunk, int Tp, int&
 // (longest first) and dealt in a snake over 256 slots, which evens out the MFMA work per
 // CU.  Placement only sets speed: any permutation gives the same result, because k_grad
 // indexes its partial sums by task, not by workgroup.  One workgroup; hist: LDS ints.
+// order holds ntask + SCHED_KEY ints; a table intact from an earlier call is kept.
+constexpr int GRAD_ORDER_MAGIC = 0x4F524431;
 __device__ void build_grad_order(int T, int chunk, int Tp, int* order, int* hist) {
     const int ntask = grad_tasks(T, chunk);
     const int lmax = chunk + Tp;
+    unsigned* hs = reinterpret_cast<unsigned*>(hist + lmax + 1);
+    if (sched_cached(order, ntask, GRAD_ORDER_MAGIC, T, chunk, Tp, hs)) return;
     for (int l = threadIdx.x; l <= lmax; l += NTHREADS) hist[l] = 0;
     __syncthreads();
     int i, j, ch;
@@ -595,6 +612,7 @@ __device__ void build_grad_order(int T, int chunk, int Tp, int* order, int* hist
         const int width = min(SLOTS, ntask - r * SLOTS);
         order[r * SLOTS + ((r & 1) ? width - 1 - k : k)] = t;
     }
+    sched_seal(order, ntask, GRAD_ORDER_MAGIC, T, chunk, Tp, hs);
 }
 
 

@@ -195,6 +195,44 @@ def test_flow_matches_step_schedule(n_lf, n_hf, p, eng):
     assert abs(vals[0][0] - lo) < 1e-10 * abs(lo)
 
 
+def test_schedule_tables_rebuilt_when_clobbered(eng):
+    """k_gram keeps the k_grad task order and the k_chol_flow owner table in the workspace with a
+    key + content hash and skips rebuilding them when both are intact (sched_cached).  A stale
+    table must never be used: results are bit-identical after (a) a call at another size, (b)
+    one corrupted table entry below an intact key, (c) the whole workspace overwritten."""
+    rng = np.random.default_rng(11)
+    D, p = 4, 2
+
+    def model(n_lf, n_hf):
+        X = np.vstack([np.hstack([rng.random((n_lf, D)), np.zeros((n_lf, 1))]),
+                       np.hstack([rng.random((n_hf, D)), np.ones((n_hf, 1))])])
+        Y = np.sin(X[:, :D] @ rng.standard_normal((D, p)) * 3.0)
+        return _model(X, Y, _params(D, p, seed=5))
+
+    big, small = model(900, 300), model(60, 30)
+    ref = big.log_marginal_likelihood_and_grad()
+    ws = eng.workspace("gpr", 0)
+    keys = {}
+    for name, magic in (("order", 0x4F524431), ("owner", 0x464C4F57)):
+        hits = np.nonzero(ws.view(torch.int32).cpu().numpy() == magic)[0]
+        assert len(hits) >= 1, name
+        keys[name] = int(hits[-1])
+
+    def same(v):
+        assert v[0] == ref[0]
+        np.testing.assert_array_equal(v[1], ref[1])
+
+    same(big.log_marginal_likelihood_and_grad())            # cached tables
+    small.log_marginal_likelihood_and_grad()                # (a) other shape: rebuilt, then back
+    same(big.log_marginal_likelihood_and_grad())
+    for name, k in keys.items():                            # (b) one entry below an intact key
+        w32 = ws.view(torch.int32)
+        w32[k - 7] = w32[k - 7] ^ 0x5A5A
+        same(big.log_marginal_likelihood_and_grad())
+    ws.view(torch.int32).random_(0, 1 << 30)                # (c) everything overwritten
+    same(big.log_marginal_likelihood_and_grad())
+
+
 def test_tile_size_invariance(eng, goku):
     m = _model(goku["X"], goku["Y"], _params(10, 64, seed=8))
     vals = []

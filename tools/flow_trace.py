@@ -53,6 +53,11 @@ def main():
     print("latest workers (start, done, waited):", [tuple(np.round(w[i], 1)) for i in late])
     W = (cnt.value - 8 * T - 3 * 2048) // (3 + 4 * 40)
     g = ws[off.value + 8 * (cnt.value - 3 * 2048): off.value + 8 * cnt.value].view(torch.int64).cpu().numpy().reshape(-1, 3)
+    gg = g.astype(np.float64) / 100.0
+    ext = [(i, gg[i, 2]) for i in range(len(gg)) if gg[i, 0] == 0 and gg[i, 2] > 0]
+    print("k_gram extra workgroups (index, us to done):", [(i, round(v, 2)) for i, v in ext])
+    print("k_gram WG 0 (staged, entries, done):", gg[0], " latest:",
+          [(int(i), gg[i, 2]) for i in np.argsort(-gg[:, 2])[:6]])
     g = g[g[:, 2] > 0].astype(np.float64) / 100.0
     if len(g):
         print(f"k_gram per workgroup (us since its start): staged median {np.median(g[:, 0]):.2f} max {g[:, 0].max():.2f};"
