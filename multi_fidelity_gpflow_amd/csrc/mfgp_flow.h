@@ -65,10 +65,11 @@ __host__ __device__ inline FlowTile flow_tile(int code, int T) {
         t.lo = t.i;
         t.hi = T - 1;
         t.fin = -1;
-    } else {   // FT_H: one item at level k, once D_k is out
+    } else {   // FT_H: one item at level k, once D_k is out; the last one (k = T-1) is formed by
+               // the diag workgroup itself (nothing else runs there by then), so it has no items
         t.lo = 0;
         t.hi = -1;
-        t.fin = t.i;
+        t.fin = t.i < T - 1 ? t.i : -1;
     }
     return t;
 }

@@ -308,6 +308,22 @@ __device__ __forceinline__ void pub_wt(WTile& t, const double* P, FlowCtx& C) {
     if (tw) C.waited += flow_clock() - tw;
 }
 
+// a published accumulator tile and a published operand in ONE round trip (the diag helpers'
+// inputs of a step: the band tile from its owner and the owner's L(j,j-3))
+__device__ __forceinline__ void pub_wt_op(WTile& t, const double* Pt, WOp& o, const double* Po, FlowCtx& C) {
+    wt_load<true>(t, Pt, 32);
+    op_load_pub(o, Po);
+    bool miss = false;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) miss |= is_sent(t.v[a][b][r]);
+    if (__ballot(miss) != 0) pub_wt(t, Pt, C);
+    if (op_missing(o)) pub_retry(o, Po, C);
+}
+
 // ---- worker items (one wave)
 // Finalize from the accumulator in registers; dop: D_j (A tiles) / D_i (R tiles) in operand form.
 //   A(i,j): L(i,j) = A'(i,j) D_j^T;   R(i,c): X(i,c) = D_i R(i,c) (row block i of [L^{-1} | Z])
@@ -328,9 +344,8 @@ __device__ __forceinline__ void flow_finalize_acc(FlowCtx& C, const FlowTile& t,
 __device__ __forceinline__ void flow_coupling(FlowCtx& C, int k, double* S) {
     WTile lt, out;
     WOp d;
-    pub_wt(lt, C.P.L(k, k - 1), C);
+    pub_wt_op(lt, C.P.L(k, k - 1), d, C.P.D(k), C);   // both inputs in one round trip
     wt_to_lds(lt, S);
-    pub_op(d, C.P.D(k), C);
     wt_zero(out);
     wt_mma_lds_b(out, d, S);                             // A[i][k'] = D_k[i][k'], B[k'][c] = L(k,k-1)[k'][c]
     wt_store<true>(out, C.P.Hk(k), 32);
@@ -352,23 +367,31 @@ __device__ __forceinline__ void flow_finalize_r(FlowCtx& C, const FlowTile& t, d
     const FlowArgs& a = C.a;
     const int T = a.T;
     const int i = t.i;
-    {
-        WTile acc;
-        wt_load<false>(acc, C.Rt(i, t.j), a.ldr);
-        wt_to_lds(acc, S);
-    }
     const bool cpl = i >= 1;
     const double* Pd = C.P.D(i);
     const double* Ph = C.P.Hk(i);
     const double* Pq = C.P.X(i - 1, t.j);
     WOp d, h, q;
     const long long tw = flow_clock();
-    bool waited = false;
-    for (int spin = 0;; ++spin) {
+    {   // R'' and the three published operands in one round trip (loads complete in order, so
+        // staging R'' waits for its own loads only)
+        WTile acc;
+        wt_load<false>(acc, C.Rt(i, t.j), a.ldr);
         op_load_pub(d, Pd);
         if (cpl) {
             op_load_pub(h, Ph);
             op_load_pub(q, Pq);
+        }
+        wt_to_lds(acc, S);
+    }
+    bool waited = false;
+    for (int spin = 0;; ++spin) {
+        if (spin > 0) {
+            op_load_pub(d, Pd);
+            if (cpl) {
+                op_load_pub(h, Ph);
+                op_load_pub(q, Pq);
+            }
         }
         bool miss = op_missing(d);
         if (cpl) miss = miss || op_missing(h) || op_missing(q);
@@ -709,6 +732,16 @@ __device__ __forceinline__ void diag_publisher(FlowCtx& C, const DiagLds& B) {
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (l == 0) lds_put(&B.w()[DW_DPUB], k);
+        if (k == T - 1 && k > 0) {
+            // the last coupling H_k = D_k L(k,k-1) from LDS: one hand-off less on the tail
+            WOp dr, lc;
+            op_rows_lds_ld(dr, D, S);                 // A[i][k'] = D_k[i][k']
+            op_cols_lds_ld(lc, B.Ls(pk), S);          // B[k'][c] = L(k,k-1)[k'][c]
+            WTile h;
+            wt_zero(h);
+            wt_mma<false>(h, dr, lc);
+            wt_store<true>(h, C.P.Hk(k), 32);
+        }
     }
 }
 
@@ -718,13 +751,15 @@ __device__ __forceinline__ void diag_second(FlowCtx& C, const DiagLds& B) {
     const int T = a.T;
     for (int j = 2; j < T; ++j) {
         WTile acc;
-        if (j >= 4) pub_wt(acc, C.P.H(2, j), C);
-        else wt_load<true>(acc, C.At(j, j - 2), a.lda);  // A(2,0), A(3,1): k_gram's values
-        if (a.trace && (threadIdx.x & 63) == 0) a.trace[4 * T + j] = flow_clock() - C.t0;
         WOp x, y;
+        if (j >= 4) pub_wt_op(acc, C.P.H(2, j), x, C.P.L(j, j - 3), C);
+        else {
+            wt_load<true>(acc, C.At(j, j - 2), a.lda);  // A(2,0), A(3,1): k_gram's values
+            if (j == 3) pub_op(x, C.P.L(j, j - 3), C);
+        }
+        if (a.trace && (threadIdx.x & 63) == 0) a.trace[4 * T + j] = flow_clock() - C.t0;
         if (j >= 3) {
             // panel j-3: A(j,j-2) -= L(j,j-3) L(j-2,j-3)^T  (the worker's L, the chain's Ls of step j-2)
-            pub_op(x, C.P.L(j, j - 3), C);
             lds_wait_ge(&B.w()[DW_P2], j - 1);            // MFMA only once the chain's step j-1 products
             lds_wait_ge(&B.w()[DW_LS], j - 2);            // are done (they share this CU's SIMDs)
             op_rows_lds_ld(y, B.Ls((j - 2) & 1), S);
@@ -757,13 +792,15 @@ __device__ __forceinline__ void diag_prefetch(FlowCtx& C, const DiagLds& B, bool
         const int pj = j & 1;
         double* dst = sub ? B.Ap(pj) : B.Cp(pj);
         WTile acc;
-        if (j >= 4) pub_wt(acc, C.P.H(sub ? 0 : 1, j), C);
-        else wt_load<true>(acc, sub ? C.At(j, j - 1) : C.At(j, j), a.lda);   // k_gram's values
+        WOp x, y;
+        if (j >= 4) pub_wt_op(acc, C.P.H(sub ? 0 : 1, j), x, C.P.L(j, j - 3), C);
+        else {
+            wt_load<true>(acc, sub ? C.At(j, j - 1) : C.At(j, j), a.lda);   // k_gram's values
+            if (j == 3) pub_op(x, C.P.L(j, j - 3), C);
+        }
         if (a.trace && (threadIdx.x & 63) == 0) a.trace[(sub ? 5 : 6) * T + j] = flow_clock() - C.t0;
         if (j >= 3) {
             // panel j-3 from the worker's L(j,j-3) and L(j-1,j-3) (wave 5, step j-1)
-            WOp x, y;
-            pub_op(x, C.P.L(j, j - 3), C);
             lds_wait_ge(&B.w()[DW_P2], j - 1);
             if (sub) {
                 lds_wait_ge(&B.w()[DW_L2], j - 1);

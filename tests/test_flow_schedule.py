@@ -58,7 +58,8 @@ def tile(code, T):
         return (j if j < T else 0), i - 2, i, False      # panel i-1 through H_i in the finalize
     if ty == FT_AL:
         return i, T - 1, -1, False
-    return 0, -1, i, False                              # FT_H: H_k = D_k L(k,k-1) at level k
+    return 0, -1, (i if i < T - 1 else -1), False       # FT_H: H_k = D_k L(k,k-1) at level k
+    #                                                     (H_{T-1}: the diag workgroup's publisher)
 
 
 def items(code, T):
@@ -163,6 +164,8 @@ def simulate(T, Tp, W, reverse=False):
         # diag chain: step k needs the chain's own L(k-1,k-2) etc. (internal) and the band inputs
         while dk < T and all(n in done for n in diag_needs(dk, T)):
             done |= {("D", dk), ("X", dk, dk), ("L", dk, dk - 1)}
+            if dk == T - 1:
+                done.add(("Hk", dk))
             if dk >= 2:
                 done.add(("L", dk, dk - 2))
             dk += 1
