@@ -64,8 +64,47 @@ __device__ __forceinline__ void wt_zero(WTile& t) {
 #pragma unroll
         for (int b = 0; b < 2; ++b) t.v[a][b] = f64x4{0.0, 0.0, 0.0, 0.0};
 }
+// Plain tile traffic of the worker items (A / R / alpha tiles, runtime leading dimension): the
+// row group's base (16a + 4r) * ld is wave-uniform (SGPR pair, global_load's saddr form) and the
+// lane's row / column is ONE 32-bit VGPR.  With per-lane 64-bit addresses the compiler hoists
+// the eight row addresses of every tile shape out of the item loop and spills them; their
+// reloads carry s_waitcnt vmcnt(0), which also waits for every older store of the wave.  The
+// empty asm keeps the lane offset opaque, so nothing derived from it is hoisted.
+__device__ __forceinline__ unsigned wt_lane_off(long ld) {
+    const int li = threadIdx.x & 15, lq = (threadIdx.x >> 4) & 3;
+    unsigned v = (unsigned)((lq * (int)ld + li) * 8);
+    asm volatile("" : "+v"(v));
+    return v;
+}
+__device__ __forceinline__ void wt_load_u(WTile& t, const double* P, long ld) {
+    const unsigned lo = wt_lane_off(ld);
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const char* row = reinterpret_cast<const char*>(P + (long)(16 * a + 4 * r) * ld);
+#pragma unroll
+            for (int b = 0; b < 2; ++b) t.v[a][b][r] = *reinterpret_cast<const double*>(row + lo + 128 * b);
+        }
+}
+__device__ __forceinline__ void wt_store_u(const WTile& t, double* P, long ld) {
+    const unsigned lo = wt_lane_off(ld);
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            char* row = reinterpret_cast<char*>(P + (long)(16 * a + 4 * r) * ld);
+#pragma unroll
+            for (int b = 0; b < 2; ++b) *reinterpret_cast<double*>(row + lo + 128 * b) = t.v[a][b][r];
+        }
+}
+
 template <bool SC1>
 __device__ __forceinline__ void wt_load(WTile& t, const double* P, long ld) {
+    if constexpr (!SC1) {
+        wt_load_u(t, P, ld);
+        return;
+    }
     const int li = threadIdx.x & 15, lq = (threadIdx.x >> 4) & 3;
 #pragma unroll
     for (int a = 0; a < 2; ++a)
@@ -79,6 +118,10 @@ __device__ __forceinline__ void wt_load(WTile& t, const double* P, long ld) {
 }
 template <bool SC1>
 __device__ __forceinline__ void wt_store(const WTile& t, double* P, long ld) {
+    if constexpr (!SC1) {
+        wt_store_u(t, P, ld);
+        return;
+    }
     const int li = threadIdx.x & 15, lq = (threadIdx.x >> 4) & 3;
 #pragma unroll
     for (int a = 0; a < 2; ++a)
@@ -205,6 +248,9 @@ struct FlowCtx {
     FlowPub P;
     long long t0;
     long long waited;   // worker: ticks spent re-polling (trace only)
+#ifdef FLOW_ITEM_PROBE
+    long long probe;    // diagnostic: time the item's operands were in registers
+#endif
     __device__ double* At(int i, int j) const { return a.A + (long)i * 32 * a.lda + (long)j * 32; }
     __device__ double* Rt(int i, int c) const { return a.R + (long)i * 32 * a.ldr + (long)c * 32; }
     __device__ double* Xt(int i, int c) const { return a.Xo + (long)i * 32 * a.ldx + (long)c * 32; }
@@ -438,21 +484,24 @@ __device__ __forceinline__ void flow_update(FlowCtx& C, const FlowTile& t, int l
     if (t.type == FT_A) {
         double* dst = C.At(t.i, t.j);
         wt_load<false>(acc, dst, a.lda);
-        if (fin) {
-            op_load_pub(x, C.P.L(t.i, l));
-            op_load_pub(y, C.P.L(t.j, l));
-            op_load_pub(d, C.P.D(t.fin));
-            if (op_missing(x)) pub_retry(x, C.P.L(t.i, l), C);
-            if (op_missing(y)) pub_retry(y, C.P.L(t.j, l), C);
-        } else if (t.j != t.i) {
+        if (t.j != t.i) {
             pub_op2(x, C.P.L(t.i, l), y, C.P.L(t.j, l), C);
         } else {
             pub_op(x, C.P.L(t.i, l), C);
             y = x;
         }
+#ifdef FLOW_ITEM_PROBE
+        {
+            double z = x.v[0][0] + y.v[1][7] + acc.v[1][1][3];
+            asm volatile("" : "+v"(z));
+            C.probe = flow_clock() + (z == 12345.678 ? 1 : 0);
+        }
+#endif
         wt_mma<true>(acc, x, y);                         // A(i,j) -= L(i,l) L(j,l)^T
         if (fin) {
-            if (op_missing(d)) pub_retry(d, C.P.D(t.fin), C);
+            // D_{l+1} is loaded only now: it is published ~one factor after L(j,l) (so an early
+            // load would nearly always miss), and holding it across the update spills registers
+            pub_op(d, C.P.D(t.fin), C);
             flow_finalize_acc(C, t, acc, d, S);
         } else if (t.pub && l == t.hi) {
             wt_store<true>(acc, C.P.H(t.i == t.j ? 1 : t.i == t.j + 1 ? 0 : 2, t.i), 32);
@@ -502,7 +551,11 @@ __device__ __forceinline__ void flow_item_log(const FlowCtx& C, int wid, int n, 
     const long long t1 = flow_clock();
     e[0] = ((long long)code << 8) | l;
     e[1] = i0 - C.t0;
+#ifdef FLOW_ITEM_PROBE
+    e[2] = C.probe - C.t0;
+#else
     e[2] = i0 + (C.waited - w0) - C.t0;
+#endif
     e[3] = t1 - C.t0;
 }
 
@@ -761,7 +814,8 @@ __device__ __forceinline__ void diag_second(FlowCtx& C, const DiagLds& B) {
         if (j >= 3) {
             // panel j-3: A(j,j-2) -= L(j,j-3) L(j-2,j-3)^T  (the worker's L, the chain's Ls of step j-2)
             lds_wait_ge(&B.w()[DW_P2], j - 1);            // MFMA only once the chain's step j-1 products
-            lds_wait_ge(&B.w()[DW_LS], j - 2);            // are done (they share this CU's SIMDs)
+            lds_wait_ge(&B.w()[DW_LS], j - 2);            // are done (they share this CU's SIMDs; an
+                                                          // earlier window in the factor measured slower)
             op_rows_lds_ld(y, B.Ls((j - 2) & 1), S);
             wt_mma<true>(acc, x, y);
         }
