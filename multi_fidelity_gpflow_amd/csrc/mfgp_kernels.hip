@@ -926,20 +926,33 @@ size_t grad_smem_bytes(int nb, int G, int nil2) {
 
 // Stage 2: LML, gradient output and the optional Keras-Adam step; run by the last
 // item workgroup of k_reduce_items to arrive.
+__device__ void adam_body(const FinArgs& a, int G, int s);
 __device__ void finalize_body(const FinArgs& a) {
     const int G = a.G ? a.G : theta_size(a.D);
     const double* items = a.items;
     const double LOG2PI = 1.8378770664093453;
-    double lml = -0.5 * ld_coherent(items) - (double)a.P * ld_coherent(items + 1) - 0.5 * (double)a.n * (double)a.P * LOG2PI;
-    if (a.info[0] != 0) lml = NAN;
+    // every input is read before the first store (the outputs may alias them as far as the
+    // compiler knows): one round trip instead of one per dependent group
+    const double i0 = ld_coherent(items), i1 = ld_coherent(items + 1);
+    const int info0 = a.info[0];
+    const int s = a.adam ? *a.step : 0;
+    const double g0 = (a.want_grad && (int)threadIdx.x < G) ? ld_coherent(items + 2 + threadIdx.x) : 0.0;
+    double lml = -0.5 * i0 - (double)a.P * i1 - 0.5 * (double)a.n * (double)a.P * LOG2PI;
+    if (info0 != 0) lml = NAN;
+    if (a.adam && info0 == 0) adam_body(a, G, s);
     if (threadIdx.x == 0) a.out[0] = lml;
-    if (a.want_grad)
-        for (int q = threadIdx.x; q < G; q += NTHREADS) a.out[1 + q] = ld_coherent(items + 2 + q);
+    if (a.want_grad) {
+        if ((int)threadIdx.x < G) a.out[1 + threadIdx.x] = g0;
+        for (int q = threadIdx.x + NTHREADS; q < G; q += NTHREADS) a.out[1 + q] = ld_coherent(items + 2 + q);
+    }
     if (!a.adam) return;
-    const double* gsh = items + 2;
-    const int s = *a.step;
     if (threadIdx.x == 0) a.loss_hist[s] = -lml;
-    if (a.info[0] != 0) return;   // non-PD: leave parameters untouched (host raises)
+    __syncthreads();   // every wave has read *a.step
+    if (threadIdx.x == 0 && info0 == 0) *a.step = s + 1;
+}
+
+__device__ void adam_body(const FinArgs& a, int G, int s) {
+    const double* gsh = a.items + 2;
     const double t = (double)(s + 1);
     const double alpha = a.lr * sqrt(1.0 - pow(a.b2, t)) / (1.0 - pow(a.b1, t));
     for (int q = threadIdx.x; q < G; q += NTHREADS) {
@@ -962,8 +975,6 @@ __device__ void finalize_body(const FinArgs& a) {
             a.theta[q] = tf_softplus(un) + (q == a.noise_index ? 1e-6 : 0.0);
         }
     }
-    __syncthreads();   // every wave has read *a.step
-    if (threadIdx.x == 0) *a.step = s + 1;
 }
 
 // Stage 1 of the step reduction: workgroup `it` sums item `it` of
@@ -975,8 +986,14 @@ __global__ __launch_bounds__(NTHREADS) void k_reduce_items(FinArgs a) {
     double s = 0.0;
     if (it == 0) {
         for (int e = threadIdx.x; e < a.nz; e += NTHREADS) s += a.zpart[e];
-    } else if (it == 1) {
-        for (int e = threadIdx.x; e < a.n; e += NTHREADS) s += log(a.ldiag[e]);
+    } else if (it == 1) {   // 8 loads in flight per thread before the logs
+        for (int e0 = threadIdx.x; e0 < a.n; e0 += 8 * NTHREADS) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = (e0 + u * NTHREADS < a.n) ? a.ldiag[e0 + u * NTHREADS] : 1.0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += log(v[u]);
+        }
     } else {
         const double* src = a.gpart + (long)(it - 2) * a.ng;
         double s1 = 0.0, s2 = 0.0, s3 = 0.0;
