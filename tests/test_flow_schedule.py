@@ -76,7 +76,11 @@ def owner_table(T, Tp, W):
     own = [[None] * MAXOWN for _ in range(W)]
     for p, c in enumerate(codes):
         r, q = divmod(p, W)
-        w = W - 1 - q if r & 1 else q
+        sn = W - 1 - q if r & 1 else q
+        # snake position -> wave: wave 0 of every workgroup first, then wave 1, ... (8 waves per
+        # workgroup; waves w and w + 4 share a SIMD)
+        nwg = W // 8
+        w = (sn % nwg) * 8 + sn // nwg if W % 8 == 0 else sn
         assert r < MAXOWN, "owner table overflow (the host falls back to step launches)"
         own[w][r] = c
     return own
@@ -203,7 +207,7 @@ def test_every_tile_owned_once(T, Tp):
 
 
 @pytest.mark.parametrize("T,Tp,W", [(1, 2, 8), (2, 1, 8), (3, 2, 5), (4, 2, 16), (6, 1, 9), (12, 2, 40),
-                                    (37, 2, 2040), (37, 2, 400), (20, 3, 120)])
+                                    (37, 2, 2040), (37, 2, 400), (20, 3, 120), (12, 2, 240), (30, 2, 1400)])
 @pytest.mark.parametrize("reverse", [False, True])
 def test_schedule_runs_to_completion(T, Tp, W, reverse):
     if ntiles(T, Tp) > W * MAXOWN:
