@@ -721,6 +721,11 @@ __device__ __forceinline__ void diag_chain(FlowCtx& C, const DiagLds& B) {
         for (int r = 0; r < 4; ++r) cij.v[0][r] = B.Cp(pk)[acc_row<32>(0, r) * S + acc_col<32>(0)];
         chain_bar(&B.w()[DW_BAR], epoch);
         if (threadIdx.x == 0) lds_put(&B.w()[DW_LS], k);
+#ifndef FLOW_SIMD1_SHARED
+        // only the lower blocks of A''(k,k) feed the factor: wave 1 (block (0,1)) skips the
+        // product and leaves SIMD 1 to wave 5 from the end of the first product on
+        if (w != 1)
+#endif
         tile_mma<32, false, true>(cij, B.Ls(pk), B.Ls(pk), -1.0);   // A''(k,k) -= L L^T
         {
             const int bi = w >> 1, bj = w & 1;
@@ -798,6 +803,13 @@ __device__ __forceinline__ void diag_publisher(FlowCtx& C, const DiagLds& B) {
     }
 }
 
+// wave 5 shares SIMD 1 with chain wave 1, whose last MFMA of a step is its block of the first
+// product (L(k,k-1)) unless FLOW_SIMD1_SHARED
+#ifdef FLOW_SIMD1_SHARED
+#define W5_GATE DW_P2
+#else
+#define W5_GATE DW_LS
+#endif
 __device__ __forceinline__ void diag_second(FlowCtx& C, const DiagLds& B) {
     constexpr int S = TileCfg<32>::S;
     const FlowArgs& a = C.a;
@@ -813,16 +825,18 @@ __device__ __forceinline__ void diag_second(FlowCtx& C, const DiagLds& B) {
         if (a.trace && (threadIdx.x & 63) == 0) a.trace[4 * T + j] = flow_clock() - C.t0;
         if (j >= 3) {
             // panel j-3: A(j,j-2) -= L(j,j-3) L(j-2,j-3)^T  (the worker's L, the chain's Ls of step j-2)
-            lds_wait_ge(&B.w()[DW_P2], j - 1);            // MFMA only once the chain's step j-1 products
-            lds_wait_ge(&B.w()[DW_LS], j - 2);            // are done (they share this CU's SIMDs; an
-                                                          // earlier window in the factor measured slower)
+            lds_wait_ge(&B.w()[W5_GATE], j - 1);          // MFMA only once the chain's step j-1 products
+            lds_wait_ge(&B.w()[DW_LS], j - 2);            // on SIMD 1 are done (an earlier window in the
+                                                          // factor, or none, measured slower)
+            if (a.trace && (threadIdx.x & 63) == 0) a.trace[8 * T + 3 * a.nwaves + 4 * FLOW_LOG * a.nwaves + j] = flow_clock() - C.t0;
             op_rows_lds_ld(y, B.Ls((j - 2) & 1), S);
             wt_mma<true>(acc, x, y);
         }
         lds_wait_ge(&B.w()[DW_D], j - 2);
-        lds_wait_ge(&B.w()[DW_P2], j - 1);
+        lds_wait_ge(&B.w()[W5_GATE], j - 1);
         lds_wait_ge(&B.w()[DW_PRE6], j - 1);              // L2[j & 1] = L(j-2,j-4): last read by
         lds_wait_ge(&B.w()[DW_PRE7], j - 2);              // wave 6 at j-1, wave 7 at j-2
+        if (a.trace && (threadIdx.x & 63) == 0) a.trace[8 * T + 3 * a.nwaves + 4 * FLOW_LOG * a.nwaves + T + j] = flow_clock() - C.t0;
         wt_to_lds_ld(acc, B.L2(j & 1), S);               // staging: A'(j,j-2) as the A operand
         asm volatile("" ::: "memory");
         op_rows_lds_ld(x, B.L2(j & 1), S);
@@ -911,7 +925,8 @@ __global__ __launch_bounds__(FLOW_THREADS) void k_chol_flow(FlowArgs a) {
 
 long flow_npub(int T, int Tp) { return 1024L * (T * (T - 1) / 2 + T + T * (T + 1) / 2 + T * Tp + 4 * T); }
 int flow_nflags(int T, int Tp) { (void)T; (void)Tp; return 1; }   // the abort word
-int flow_trace_count(int T, int nwg) { return 8 * T + (3 + 4 * FLOW_LOG) * FLOW_WAVES * (nwg - 1) + 3 * 2048; }
+// layout: chain / helper stamps [8T] | worker summaries + item logs | wave-5 detail [2T] | k_gram [3 x 2048]
+int flow_trace_count(int T, int nwg) { return 8 * T + (3 + 4 * FLOW_LOG) * FLOW_WAVES * (nwg - 1) + 2 * T + 3 * 2048; }
 
 void launch_chol_flow(const FlowArgs& a, int nwg, hipStream_t s) {
     static bool attr = false;
