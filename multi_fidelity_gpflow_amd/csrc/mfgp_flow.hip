@@ -327,6 +327,19 @@ __device__ __forceinline__ void pub_op(WOp& o, const double* P, FlowCtx& C) {
     op_load_pub(o, P);
     if (op_missing(o)) pub_retry(o, P, C);
 }
+// the same re-read in full per poll (no probe round trip once the tile lands)
+__device__ __forceinline__ void pub_op_direct(WOp& o, const double* P, FlowCtx& C) {
+    op_load_pub(o, P);
+    if (!op_missing(o)) return;
+    const long long tw = flow_clock();
+    for (int spin = 0;; ++spin) {
+        __builtin_amdgcn_s_sleep(FLOW_SLEEP);
+        op_load_pub(o, P);
+        if (!op_missing(o)) break;
+        if ((spin & 7) == 7 && flow_give_up(C.a.flags, C.a.info, C.t0)) break;
+    }
+    C.waited += flow_clock() - tw;
+}
 // two operands in one round trip
 __device__ __forceinline__ void pub_op2(WOp& x, const double* Px, WOp& y, const double* Py, FlowCtx& C) {
     op_load_pub(x, Px);
@@ -352,6 +365,26 @@ __device__ __forceinline__ void pub_wt(WTile& t, const double* P, FlowCtx& C) {
         pub_wait(P, C.a.flags, C.a.info, C.t0);
     }
     if (tw) C.waited += flow_clock() - tw;
+}
+
+// The diag helpers' inputs (waves 5-7): both re-read in full until complete, one round trip
+// per poll instead of probe + reload (only three waves of the launch poll this way)
+__device__ __forceinline__ void pub_wt_op_direct(WTile& t, const double* Pt, WOp& o, const double* Po,
+                                                 FlowCtx& C) {
+    for (int spin = 0;; ++spin) {
+        wt_load<true>(t, Pt, 32);
+        op_load_pub(o, Po);
+        bool miss = false;
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) miss |= is_sent(t.v[a][b][r]);
+        if (__ballot(miss) == 0 && !op_missing(o)) break;
+        if ((spin & 7) == 7 && flow_give_up(C.a.flags, C.a.info, C.t0)) break;
+        __builtin_amdgcn_s_sleep(FLOW_SLEEP);
+    }
 }
 
 // a published accumulator tile and a published operand in ONE round trip (the diag helpers'
@@ -501,7 +534,7 @@ __device__ __forceinline__ void flow_update(FlowCtx& C, const FlowTile& t, int l
         if (fin) {
             // D_{l+1} is loaded only now: it is published ~one factor after L(j,l) (so an early
             // load would nearly always miss), and holding it across the update spills registers
-            pub_op(d, C.P.D(t.fin), C);
+            pub_op_direct(d, C.P.D(t.fin), C);   // ~one wave per tile of the column polls it
             flow_finalize_acc(C, t, acc, d, S);
         } else if (t.pub && l == t.hi) {
             wt_store<true>(acc, C.P.H(t.i == t.j ? 1 : t.i == t.j + 1 ? 0 : 2, t.i), 32);
@@ -817,7 +850,7 @@ __device__ __forceinline__ void diag_second(FlowCtx& C, const DiagLds& B) {
     for (int j = 2; j < T; ++j) {
         WTile acc;
         WOp x, y;
-        if (j >= 4) pub_wt_op(acc, C.P.H(2, j), x, C.P.L(j, j - 3), C);
+        if (j >= 4) pub_wt_op_direct(acc, C.P.H(2, j), x, C.P.L(j, j - 3), C);
         else {
             wt_load<true>(acc, C.At(j, j - 2), a.lda);  // A(2,0), A(3,1): k_gram's values
             if (j == 3) pub_op(x, C.P.L(j, j - 3), C);
@@ -861,7 +894,7 @@ __device__ __forceinline__ void diag_prefetch(FlowCtx& C, const DiagLds& B, bool
         double* dst = sub ? B.Ap(pj) : B.Cp(pj);
         WTile acc;
         WOp x, y;
-        if (j >= 4) pub_wt_op(acc, C.P.H(sub ? 0 : 1, j), x, C.P.L(j, j - 3), C);
+        if (j >= 4) pub_wt_op_direct(acc, C.P.H(sub ? 0 : 1, j), x, C.P.L(j, j - 3), C);
         else {
             wt_load<true>(acc, sub ? C.At(j, j - 1) : C.At(j, j), a.lda);   // k_gram's values
             if (j == 3) pub_op(x, C.P.L(j, j - 3), C);
