@@ -451,7 +451,6 @@ __device__ __forceinline__ void flow_finalize_r(FlowCtx& C, const FlowTile& t, d
     const double* Ph = C.P.Hk(i);
     const double* Pq = C.P.X(i - 1, t.j);
     WOp d, h, q;
-    const long long tw = flow_clock();
     {   // R'' and the three published operands in one round trip (loads complete in order, so
         // staging R'' waits for its own loads only)
         WTile acc;
@@ -463,23 +462,13 @@ __device__ __forceinline__ void flow_finalize_r(FlowCtx& C, const FlowTile& t, d
         }
         wt_to_lds(acc, S);
     }
-    bool waited = false;
-    for (int spin = 0;; ++spin) {
-        if (spin > 0) {
-            op_load_pub(d, Pd);
-            if (cpl) {
-                op_load_pub(h, Ph);
-                op_load_pub(q, Pq);
-            }
-        }
-        bool miss = op_missing(d);
-        if (cpl) miss = miss || op_missing(h) || op_missing(q);
-        if (!miss) break;
-        waited = true;
-        if ((spin & 7) == 7 && flow_give_up(C.a.flags, C.a.info, C.t0)) break;
-        __builtin_amdgcn_s_sleep(FLOW_SLEEP);
+    // a missing operand is waited for with the one-line probe (hundreds of R / Z finalizes can be
+    // waiting at once: full re-reads of three tiles per poll would flood the fabric)
+    if (op_missing(d)) pub_retry(d, Pd, C);
+    if (cpl) {
+        if (op_missing(h)) pub_retry(h, Ph, C);
+        if (op_missing(q)) pub_retry(q, Pq, C);
     }
-    if (waited) C.waited += flow_clock() - tw;
     WTile out;
     wt_zero(out);
     wt_mma_lds_b(out, d, S);                             // D_i R''   (B[k][j] = R''[k][j])
