@@ -707,7 +707,8 @@ __device__ __forceinline__ void lds_wait_ge(const int* p, int v) {
 __device__ __forceinline__ void chain_bar(int* cnt, int& epoch) {
     epoch += 4;
     if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    lds_wait_ge(cnt, epoch);
+    while (__builtin_amdgcn_readfirstlane(lds_get(cnt)) < epoch) {}   // spin: a sleep's wake-up
+                                                                        // is on the chain (+1%)
 }
 
 // wave-level tile (accumulator layout) <-> LDS tile of stride ld
@@ -736,6 +737,11 @@ __device__ __forceinline__ void op_cols_lds_ld(WOp& o, const double* S, int ld) 
         for (int s = 0; s < 8; ++s) o.v[b][s] = S[(8 * lq + s) * ld + 16 * b + li];
 }
 
+// the chain waves (0-3) spin on their LDS words: a sleep's wake-up would sit on the critical
+// path (the waits of waves 4-7 keep sleeping: wave 4 shares SIMD 0 with the factor)
+__device__ __forceinline__ void lds_spin_ge(const int* p, int v) {
+    while (__builtin_amdgcn_readfirstlane(lds_get(p)) < v) {}
+}
 __device__ __forceinline__ void diag_chain(FlowCtx& C, const DiagLds& B) {
     constexpr int S = TileCfg<32>::S;
     const FlowArgs& a = C.a;
@@ -745,10 +751,10 @@ __device__ __forceinline__ void diag_chain(FlowCtx& C, const DiagLds& B) {
     for (int k = 1; k < T; ++k) {
         const int pk = k & 1;
         if (a.trace && threadIdx.x == 0) a.trace[k] = flow_clock() - C.t0;
-        lds_wait_ge(&B.w()[DW_PRE6], k);
-        lds_wait_ge(&B.w()[DW_PRE7], k);
-        lds_wait_ge(&B.w()[DW_D], k - 1);        // D_{k-1} in Db[pk ^ 1]
-        lds_wait_ge(&B.w()[DW_LPUB], k - 2);     // wave 4 is done with Ls[pk] (L(k-2,k-3))
+        lds_spin_ge(&B.w()[DW_PRE6], k);
+        lds_spin_ge(&B.w()[DW_PRE7], k);
+        lds_spin_ge(&B.w()[DW_D], k - 1);         // D_{k-1} in Db[pk ^ 1]
+        lds_spin_ge(&B.w()[DW_LPUB], k - 2);      // wave 4 is done with Ls[pk] (L(k-2,k-3))
         if (a.trace && threadIdx.x == 0) a.trace[T + k] = flow_clock() - C.t0;
         Acc<32> pl;
         acc_zero(pl);
@@ -775,7 +781,7 @@ __device__ __forceinline__ void diag_chain(FlowCtx& C, const DiagLds& B) {
         chain_bar(&B.w()[DW_BAR], epoch);
         if (threadIdx.x == 0) lds_put(&B.w()[DW_P2], k);  // tile products of step k done
         if (w == 0) {
-            lds_wait_ge(&B.w()[DW_DPUB], k - 2);    // wave 4 is done with Db[pk] (D_{k-2})
+            lds_spin_ge(&B.w()[DW_DPUB], k - 2);    // wave 4 is done with Db[pk] (D_{k-2})
             if (a.trace && threadIdx.x == 0) a.trace[2 * T + k] = flow_clock() - C.t0;
             tile_potrf_inv_w1_wave(B.fsc(), 33, B.fsc(), B.Db(pk), B.dg(pk), &B.bad()[pk]);
             if (l == 0) lds_put(&B.w()[DW_D], k);
