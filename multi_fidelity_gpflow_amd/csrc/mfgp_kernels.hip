@@ -164,6 +164,23 @@ __device__ __forceinline__ void gram_fill_pub(const GramArgs& a) {
 #endif
 }
 
+// Y block of R (rows < n1, columns < p; zero padding), a grid-stride slice per tile workgroup
+// of the padded launch (the extra workgroups after the T(T+1)/2 tiles do not take part)
+template <int NB>
+__device__ __forceinline__ void gram_copy_y(const GramArgs& a) {
+    if (a.R == nullptr) return;
+    const int T = a.npad / NB;
+    const long nt = (long)T * (T + 1) / 2;
+    const long ne = (long)a.npad * a.ppad;
+    const int b = blockIdx.z;
+    const double* Yb = a.Y + b * a.sY;
+    double* Rb = a.R + b * a.sR;
+    for (long e = blockIdx.x * (long)NTHREADS + threadIdx.x; e < ne; e += nt * NTHREADS) {
+        const int r = (int)(e / a.ppad), c = (int)(e % a.ppad);
+        Rb[(long)r * a.ldr + a.npad + c] = (r < a.n1 && c < a.p) ? Yb[(long)r * a.ldy + c] : 0.0;
+    }
+}
+
 template <int NB>
 __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
     constexpr int S = TileCfg<NB>::S;
@@ -283,25 +300,8 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
             const int r = e / NB, c = e % NB;
             Rb[(long)(ti * NB + r) * a.ldr + tj * NB + c] = (ti == tj && r == c) ? 1.0 : 0.0;
         }
-        if (tj == 0) {   // 8 loads in flight per thread before the stores
-            const double* Yb = a.Y + b * a.sY;
-            const int ne = NB * a.ppad;
-            for (int e0 = threadIdx.x; e0 < ne; e0 += 8 * NTHREADS) {
-                double v[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int e = e0 + u * NTHREADS;
-                    const int r = e / a.ppad, c = e % a.ppad, gr = ti * NB + r;
-                    v[u] = (e < ne && gr < a.n1 && c < a.p) ? Yb[(long)gr * a.ldy + c] : 0.0;
-                }
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int e = e0 + u * NTHREADS;
-                    const int r = e / a.ppad, c = e % a.ppad;
-                    if (e < ne) Rb[(long)(ti * NB + r) * a.ldr + a.npad + c] = v[u];
-                }
-            }
-        }
+        // the Y block of R is copied by every tile workgroup at its end (gram_copy_y), not by the
+        // column-0 ones: that copy kept the workgroup of the first diagonal factor the longest
     }
     __syncthreads();
     if (a.dbg && threadIdx.x == 0) a.dbg[3 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - dbg_t0;
@@ -318,6 +318,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
         for (int r = threadIdx.x; r < NB; r += NTHREADS) a.ldiag[b * a.sL + r] = dg[r];
         if (threadIdx.x == 0) a.info[b] = bad;   // first writer of info in the sequence: initialises it
     }
+    gram_copy_y<NB>(a);
     gram_fill_pub(a);
     if (a.dbg && threadIdx.x == 0) a.dbg[3 * blockIdx.x + 2] = __builtin_amdgcn_s_memrealtime() - dbg_t0;
 }
