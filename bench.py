@@ -43,7 +43,14 @@ FP64_PEAK_TFLOPS = 78.6   # MI355X dense FP64 (vector = matrix on gfx950), MI355
 HBM_PEAK_GBS = 8000.0
 # HBM bytes per dispatch from the committed rocprofv3 PMC passes (tools/profile_round.sh ->
 # tools/summarize_profile.py); the bench cannot count PMC on itself.
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01", "pmc_summary.json")
+def latest_pmc_summary():
+    """profiles/rNN/pmc_summary.json of the latest round that has one."""
+    import glob
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", "pmc_summary.json")))
+    return found[-1] if found else os.path.join(ROOT, "profiles", "r01", "pmc_summary.json")
+
+
+PMC_SUMMARY = latest_pmc_summary()
 
 
 def pmc_traffic(kernel_prefix, nb):
@@ -132,25 +139,61 @@ def roofline(model, n, p, d, reps=10, pmc=True):
     }
 
 
-def cpu_baseline(X, Y, budget_s=20.0):
-    """fp64 oracle (CPU restatement of the reference path) on this host's cores."""
-    from oracle import mfgp_oracle as O
-    try:
-        from threadpoolctl import threadpool_info
-        cores = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
-    except Exception:
-        cores = os.cpu_count() or 1
-    p0 = O.MFParams.initial(X.shape[1] - 1, Y.shape[1])
-    O.gpr_lml_and_grad(X, Y, p0)   # warm
-    t0 = time.perf_counter()
-    k = 0
-    while time.perf_counter() - t0 < budget_s or k < 3:
-        O.gpr_lml_and_grad(X, Y, p0)
-        k += 1
-    dt = time.perf_counter() - t0
-    return {"value": round(k / dt, 4), "unit": "LML value+grad evals/s", "cores": int(cores), "kind": "port",
-            "sample": f"{k} Goku LML value+grad evaluations (oracle/mfgp_oracle.py gpr_lml_and_grad, fp64 "
-                      f"NumPy/SciPy) at the initial theta, {dt:.1f} s"}
+def _median_rate(fn, min_evals=20, budget_s=6.0):
+    """evals/s from the median of >= min_evals timed calls after one warm-up,
+    stopping early at budget_s once min_evals are in (or after 3 if one call is that slow)."""
+    fn()
+    ts = []
+    t_start = time.perf_counter()
+    while len(ts) < min_evals:
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+        if time.perf_counter() - t_start > budget_s and len(ts) >= 3:
+            break
+    return 1.0 / float(np.median(ts)), len(ts)
+
+
+def cpu_baseline(X, Y):
+    """fp64 torch-CPU restatement of the reference path (oracle/torch_oracle.py, checked against
+    the KAT-pinned oracle/mfgp_oracle.py) on this host: all threads and 1 thread, value-only and
+    value+grad.  Bounded sample: <= ~6 s of CPU work per leg."""
+    from oracle import torch_oracle as TO
+    Xt = torch.as_tensor(X, dtype=torch.float64)
+    Yt = torch.as_tensor(Y, dtype=torch.float64)
+    args = TO.initial_args(X.shape[1] - 1)
+    nthreads = torch.get_num_threads()
+    legs = {}
+    for label, threads in (("all", nthreads), ("one", 1)):
+        torch.set_num_threads(threads)
+        try:
+            vg, nvg = _median_rate(lambda: TO.lml_and_grad(Xt, Yt, *args))
+            v, nv = _median_rate(lambda: TO.lml(Xt, Yt, *args))
+        finally:
+            torch.set_num_threads(nthreads)
+        legs[label] = {"threads": threads, "value_grad_evals_s": round(vg, 3), "value_evals_s": round(v, 3),
+                       "samples": [nvg, nv]}
+    return {"value": legs["all"]["value_grad_evals_s"], "unit": "LML value+grad evals/s",
+            "cores": nthreads, "kind": "port", "nproc": os.cpu_count(),
+            "value_only_evals_s": legs["all"]["value_evals_s"],
+            "one_core": legs["one"],
+            "train_1000_adam_s_est": round(1000.0 / legs["all"]["value_grad_evals_s"], 2),
+            "sample": (f"Goku (N={X.shape[0]}, P={Y.shape[1]}) fp64 LML value+grad and value-only evaluations at "
+                       f"the initial theta, oracle/torch_oracle.py (MKL Cholesky/TRSM/GEMM), median of >=20 "
+                       f"after warm-up (fewer if a leg exceeds ~6 s), torch threads {nthreads} and 1; "
+                       f"train_1000_adam_s_est = 1000 / value")}
+
+
+def spawn_ranks(n: int) -> int:
+    """python -m torch.distributed.run --nproc-per-node n bench.py <same args>, as a child."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def main():
@@ -167,6 +210,12 @@ def main():
     ap.add_argument("--config", choices=["goku", "synth"], default="goku",
                     help="goku: the BASELINE metric; synth: SURVEY §8(d) scale-up (N=18432, P=512, fp64)")
     args = ap.parse_args()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        # not launched by torchrun: start one rank per GPU (before this process touches the GPU)
+        sys.exit(spawn_ranks(args.gpus))
+    if world_env is not None and int(world_env) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}")
     if args.config == "synth":
         args.no_cpu_baseline = True
         args.no_train_predict = True
@@ -203,6 +252,8 @@ def main():
     else:
         sess = model.adam_session(0.1, K + W, graph=True, graph_chunk=50 if args.config == "goku" else 2)
     sess.run(W)
+    if hasattr(sess, "prepare"):
+        sess.prepare(K)   # capture every graph the timed run replays: the timed region is replay-only
     sess.sync()
     if world > 1:
         dist.barrier()

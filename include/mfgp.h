@@ -62,6 +62,11 @@ int mfgp_get_tile(mfgp_handle_t h);
  * Results agree to rounding; a workspace must be sized under the setting it is used with. */
 int mfgp_set_flow(mfgp_handle_t h, int enable);   /* 2: flow + diagnostic timeline */
 int mfgp_get_flow(mfgp_handle_t h);
+/* Bound of every k_chol_flow hand-off wait, in microseconds from the start of that wait
+ * (default 50000).  On expiry the launch drains and info = MFGP_FLOW_TIMEOUT: a scheduling
+ * failure (not every workgroup resident, e.g. another kernel holding CUs), not a numerical one.
+ * 0 makes any wait that polls 8 times give up (diagnostic: exercises the abort path). */
+int mfgp_set_flow_timeout_us(mfgp_handle_t h, long long us);
 /* Where the flow timeline sits inside an mfgp_gpr_* workspace (diagnostic): `count` int64
  * ticks of the 100 MHz device clock from byte `offset`: per step k the diag workgroup's step
  * start [k], A' ready [T+k], factor start [2T+k], D_k published [3T+k], owner hand-offs of
@@ -120,6 +125,17 @@ int mfgp_gpr_predict_workspace_size(mfgp_handle_t h, int n, int p, int d, int ns
 int mfgp_gpr_predict(mfgp_handle_t h, int n, int p, int d, int nstar, const double* X, int ldx, const double* Y,
                      int ldy, const double* Xs, int ldxs, const double* theta, void* ws, size_t ws_bytes,
                      double* mean, int ldm, double* var, int* info);
+
+/* GPR.predict_f(Xnew, full_cov=True) (GPflow base_conditional full_cov branch: fvar =
+ * Knn - A^T A, A = L^{-1} Kmn, the same [nstar, nstar] block for every output; the Python
+ * layer tiles it to [p, nstar, nstar]).  nlf = 0: LinearMultiFidelityKernel (theta as
+ * mfgp_gpr_*); nlf = m >= 1: GraphMultiFidelityKernel (theta as mfgp_gmf_*, K(X*, X*)
+ * carries the kernel's 1e-6 jitter like graph.py:96).  mean / var as mfgp_gpr_predict;
+ * cov [nstar][ldc]. */
+int mfgp_gpr_predict_cov_workspace_size(mfgp_handle_t h, int nlf, int n, int p, int d, int nstar, size_t* bytes);
+int mfgp_gpr_predict_cov(mfgp_handle_t h, int nlf, int n, int p, int d, int nstar, const double* X, int ldx,
+                         const double* Y, int ldy, const double* Xs, int ldxs, const double* theta, void* ws,
+                         size_t ws_bytes, double* mean, int ldm, double* var, double* cov, int ldc, int* info);
 
 /* GraphMultiFidelityKernel / GraphMultiFidelityGPModel (mfgpflow/graph.py:7-188) with
  * nlf = m LF sources (fidelity flags 0..m-1 LF, m HF; 1 <= m <= 4).  theta layout

@@ -30,6 +30,7 @@ SIGNATURES = {
     "mfgp_get_tile": [_p],
     "mfgp_set_flow": [_p, _i],
     "mfgp_get_flow": [_p],
+    "mfgp_set_flow_timeout_us": [_p, C.c_longlong],
     "mfgp_gpr_flow_trace": [_p, _i, _i, _i, C.POINTER(C.c_size_t), C.POINTER(_i)],
     "mfgp_rbf_gram": [_p, _i, _i, _i, _p, _i, _p, _i, _p, _p, _i],
     "mfgp_mf_gram": [_p, _i, _i, _i, _p, _i, _p, _i, _p, _d, _p, _i],
@@ -42,6 +43,8 @@ SIGNATURES = {
     "mfgp_theta_from_u": [_p, _p, _p, _i, _i],
     "mfgp_gpr_predict_workspace_size": [_p, _i, _i, _i, _i, C.POINTER(_sz)],
     "mfgp_gpr_predict": [_p, _i, _i, _i, _i, _p, _i, _p, _i, _p, _i, _p, _p, _sz, _p, _i, _p, _p],
+    "mfgp_gpr_predict_cov_workspace_size": [_p, _i, _i, _i, _i, _i, C.POINTER(_sz)],
+    "mfgp_gpr_predict_cov": [_p, _i, _i, _i, _i, _i, _p, _i, _p, _i, _p, _i, _p, _p, _sz, _p, _i, _p, _p, _i, _p],
     "mfgp_potrf_inv_workspace_size": [_p, _i, _i, C.POINTER(_sz)],
     "mfgp_potrf_inv": [_p, _i, _i, _p, _i, _l, _p, _sz, _p, _i, _l, _p, _p],
     "mfgp_svgp_workspace_size": [_p, _i, _i, _i, _i, _i, C.POINTER(_sz)],
@@ -69,6 +72,28 @@ _handles = {}
 
 class MFGPError(RuntimeError):
     pass
+
+
+MFGP_FLOW_TIMEOUT = -100   # include/mfgp.h: info written when a k_chol_flow hand-off stalled
+
+
+class FlowTimeoutError(MFGPError):
+    """The persistent Cholesky (k_chol_flow) gave up on a stalled hand-off (info = MFGP_FLOW_TIMEOUT):
+    a scheduling failure (e.g. another kernel holding CUs, so not every workgroup was resident),
+    not a numerical one.  Re-run with the launch-per-step schedule (``Engine.set_flow(False)`` or
+    MFGP_FLOW=0)."""
+
+
+def info_error(v: int, what: str):
+    """The exception for a nonzero device info word (None for 0)."""
+    if v == 0:
+        return None
+    if v == MFGP_FLOW_TIMEOUT:
+        return FlowTimeoutError(f"{what}: the persistent Cholesky timed out waiting for a hand-off "
+                                f"(info {v}); set MFGP_FLOW=0 / Engine.set_flow(False) to use the step schedule")
+    from .models import CholeskyError
+    return CholeskyError(f"{what}: Cholesky decomposition was not successful "
+                         f"(non-positive pivot at row {v}); the input might not be valid.")
 
 
 def load(path: str = None):

@@ -21,6 +21,7 @@ struct mfgp_handle_s {
     int flow_wgs;   // k_chol_flow grid (one workgroup per CU); 0: launch-per-step Cholesky
     int ncu;        // compute units of the device
     int flow_trace; // k_chol_flow writes its diagnostic timeline into the workspace
+    long long flow_timeout;   // k_chol_flow hand-off wait bound (100 MHz ticks)
 };
 
 namespace mfgp {
@@ -171,6 +172,7 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
         fa.T = L.T; fa.Tp = L.Tp; fa.n = n; fa.p = p;
         fa.trace = h->flow_trace ? L.trace : nullptr;
         fa.nwaves = FLOW_WAVES * (L.flow_wgs - 1);
+        fa.timeout = h->flow_timeout;
         launch_chol_flow(fa, L.flow_wgs, s);
     } else {
         CholArgs c{};
@@ -309,10 +311,12 @@ struct PredLayout {
     GprLayout g;
     int nspad, Ts;
     double *Kmn, *Am, *kdiag;
+    double *Kss, *Cov;   // full_cov only: K(X*, X*) and Kss - A^T A (nspad x nspad)
     size_t bytes;
 };
 
-static PredLayout pred_layout(int nb, int n, int p, int d, int nstar, void* ws, int grad_chunk, int nlf = 0) {
+static PredLayout pred_layout(int nb, int n, int p, int d, int nstar, void* ws, int grad_chunk, int nlf = 0,
+                              int full_cov = 0) {
     PredLayout P;
     P.g = gpr_layout(nb, n, p, d, ws, grad_chunk, nlf);
     P.Ts = ceil_div(nstar > 0 ? nstar : 1, nb);
@@ -322,15 +326,27 @@ static PredLayout pred_layout(int nb, int n, int p, int d, int nstar, void* ws, 
     P.Kmn = c.take<double>((size_t)P.g.npad * P.nspad);
     P.Am = c.take<double>((size_t)P.g.npad * P.nspad);
     P.kdiag = c.take<double>(P.nspad);
+    const size_t sq = full_cov ? (size_t)P.nspad * P.nspad : 0;
+    P.Kss = c.take<double>(sq);
+    P.Cov = c.take<double>(sq);
     P.bytes = c.off + 256;
     return P;
+}
+
+__global__ void k_copy_block(const double* src, long lds, double* dst, long ldd, int rows, int cols) {
+    const long total = (long)rows * cols;
+    for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const int r = (int)(e / cols), c = (int)(e % cols);
+        dst[(long)r * ldd + c] = src[(long)r * lds + c];
+    }
 }
 
 template <int NB>
 static int predict_impl(mfgp_handle_t h, int n, int p, int d, int nstar, const double* X, int ldx, const double* Y,
                         int ldy, const double* Xs, int ldxs, const double* theta, void* ws, size_t ws_bytes,
-                        double* mean, int ldm, double* var, int* info, int nlf = 0) {
-    const PredLayout P = pred_layout(NB, n, p, d, nstar, ws, h->grad_chunk, nlf);
+                        double* mean, int ldm, double* var, int* info, int nlf = 0, double* cov = nullptr,
+                        int ldc = 0) {
+    const PredLayout P = pred_layout(NB, n, p, d, nstar, ws, h->grad_chunk, nlf, cov != nullptr);
     if (ws_bytes < P.bytes) return MFGP_ERR_WORKSPACE;
     hipStream_t s = h->stream;
     const GprLayout& L = P.g;
@@ -348,6 +364,28 @@ static int predict_impl(mfgp_handle_t h, int n, int p, int d, int nstar, const d
     PredAArgs pa{L.Xo, ldr, P.Kmn, (long)P.nspad, P.Am, (long)P.nspad, P.Ts};
     PredOutArgs po{P.Am, (long)P.nspad, L.Xo, ldr, P.kdiag, mean, (long)ldm, var, L.T, L.Tp, nstar, p};
     launch_pred<NB>(pa, po, L.T, s);
+    if (cov) {
+        // base_conditional(full_cov=True): Kss - A^T A with A = L^{-1} Kmn (padded rows of A are 0)
+        (void)hipMemsetAsync(P.Kss, 0, sizeof(double) * (size_t)P.nspad * P.nspad, s);
+        GramArgs gs{};
+        gs.X1 = Xs; gs.ldx1 = ldxs; gs.n1 = nstar;
+        gs.X2 = Xs; gs.ldx2 = ldxs; gs.n2 = nstar;
+        gs.theta = theta; gs.D = d; gs.rbf_only = 0;
+        gs.out = P.Kss; gs.ldo = P.nspad; gs.padded = 0; gs.tiles_c = P.Ts; gs.nlf = nlf;
+        gs.diag_add = nlf ? GRAPH_JITTER : 0.0;   // graph.py:96 adds the jitter inside K(X*, X*) too
+        launch_gram<NB>(gs, P.Ts * P.Ts, 1, s);
+        BgemmArgs b{};
+        b.A = P.Am; b.lda = P.nspad;
+        b.B = P.Am; b.ldb = P.nspad;
+        b.Cin = P.Kss; b.ldc = P.nspad; b.beta = 1.0;
+        b.D = P.Cov; b.ldd = P.nspad;
+        b.alpha = -1.0;
+        b.Mt = P.Ts; b.Nt = P.Ts; b.Kt = L.T;
+        launch_bgemm(NB, s, 1, 0, b, 1);
+        const long tot = (long)nstar * nstar;
+        hipLaunchKernelGGL(k_copy_block, dim3((int)std::min<long>((tot + 255) / 256, 2048)), dim3(256), 0, s, P.Cov,
+                           (long)P.nspad, cov, (long)ldc, nstar, nstar);
+    }
     return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;
 }
 
@@ -408,6 +446,7 @@ int mfgp_create(int device, mfgp_handle_t* out) {
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 0;
     h->ncu = ncu;
     h->flow_wgs = ncu;
+    h->flow_timeout = FLOW_TIMEOUT_TICKS;
     if (const char* fl = getenv("MFGP_FLOW")) if (atoi(fl) == 0) h->flow_wgs = 0;
     if (const char* gc = getenv("MFGP_GRAD_CHUNK")) h->grad_chunk = std::max(1, atoi(gc));
     const char* env = getenv("MFGP_TILE");
@@ -452,6 +491,13 @@ int mfgp_gpr_flow_trace(mfgp_handle_t h, int n, int p, int d, size_t* offset, in
     const GprLayout L = gpr_layout(h->nb, n, p, d, base, h->grad_chunk, 0, h->flow_wgs);
     *offset = (size_t)(reinterpret_cast<char*>(L.trace) - base);
     *count = L.ntrace;
+    return MFGP_OK;
+}
+
+int mfgp_set_flow_timeout_us(mfgp_handle_t h, long long us) {
+    CHECK_H(h);
+    if (us < 0) return MFGP_ERR_ARG;
+    h->flow_timeout = us * 100;   // s_memrealtime: 100 MHz
     return MFGP_OK;
 }
 
@@ -649,6 +695,30 @@ int mfgp_gpr_predict(mfgp_handle_t h, int n, int p, int d, int nstar, const doub
         return predict_impl<64>(h, n, p, d, nstar, X, ldx, Y, ldy, Xs, ldxs, theta, ws, ws_bytes, mean, ldm, var,
                                 info);
     return predict_impl<32>(h, n, p, d, nstar, X, ldx, Y, ldy, Xs, ldxs, theta, ws, ws_bytes, mean, ldm, var, info);
+}
+
+int mfgp_gpr_predict_cov_workspace_size(mfgp_handle_t h, int nlf, int n, int p, int d, int nstar, size_t* bytes) {
+    CHECK_H(h);
+    CHECK_D(d);
+    if (nlf < 0 || nlf > MFGP_MAX_LF || n < 1 || p < 1 || nstar < 0 || !bytes) return MFGP_ERR_ARG;
+    *bytes = pred_layout(h->nb, n, p, d, nstar, nullptr, h->grad_chunk, nlf, 1).bytes;
+    return MFGP_OK;
+}
+
+int mfgp_gpr_predict_cov(mfgp_handle_t h, int nlf, int n, int p, int d, int nstar, const double* X, int ldx,
+                         const double* Y, int ldy, const double* Xs, int ldxs, const double* theta, void* ws,
+                         size_t ws_bytes, double* mean, int ldm, double* var, double* cov, int ldc, int* info) {
+    CHECK_H(h);
+    CHECK_D(d);
+    if (nlf < 0 || nlf > MFGP_MAX_LF) return MFGP_ERR_ARG;
+    if (n < 1 || p < 1 || nstar < 0 || !X || !Y || !theta || !ws || !info) return MFGP_ERR_ARG;
+    if (nstar == 0) return MFGP_OK;
+    if (!Xs || !mean || !var || !cov || ldc < nstar) return MFGP_ERR_ARG;
+    if (h->nb == 64)
+        return predict_impl<64>(h, n, p, d, nstar, X, ldx, Y, ldy, Xs, ldxs, theta, ws, ws_bytes, mean, ldm, var,
+                                info, nlf, cov, ldc);
+    return predict_impl<32>(h, n, p, d, nstar, X, ldx, Y, ldy, Xs, ldxs, theta, ws, ws_bytes, mean, ldm, var, info,
+                            nlf, cov, ldc);
 }
 
 int mfgp_potrf_inv_workspace_size(mfgp_handle_t h, int n, int batch, size_t* bytes) {

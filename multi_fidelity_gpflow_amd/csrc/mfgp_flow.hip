@@ -31,7 +31,8 @@
 // Published X tiles are stored transposed (X^T) so that every MFMA operand is a row-major read
 // along the contraction index: lane (li, lq) loads 8 consecutive doubles of row 16b + li,
 // contraction indices 8 lq .. 8 lq + 7 (the k order inside an MFMA sum is free).
-// Every wait is bounded (FLOW_TIMEOUT_TICKS of the 100 MHz realtime clock): on expiry the wave
+// Every wait is bounded (FlowArgs::timeout ticks of the 100 MHz realtime clock, counted from the start
+// of that wait; default FLOW_TIMEOUT_TICKS, mfgp_set_flow_timeout_us): on expiry the wave
 // raises the abort word, writes info = MFGP_FLOW_TIMEOUT and runs on, so the grid drains.
 #include "../../include/mfgp.h"
 #include "mfgp_device.h"
@@ -40,7 +41,6 @@
 
 namespace mfgp {
 
-constexpr long long FLOW_TIMEOUT_TICKS = 5000000;   // 50 ms (s_memrealtime is 100 MHz)
 #ifndef FLOW_SLEEP
 #define FLOW_SLEEP 1
 #endif
@@ -259,11 +259,11 @@ struct FlowCtx {
 __device__ __forceinline__ bool is_sent(double v) {
     return (unsigned long long)__double_as_longlong(v) == FLOW_SENTINEL;
 }
-// Give-up path of every poll: abort word + info after FLOW_TIMEOUT_TICKS (or someone else's abort).
-__device__ __noinline__ bool flow_give_up(int* abortw, int* info, long long t0) {
+// Give-up path of every poll: abort word + info after `lim` ticks of this wait (or someone else's abort).
+__device__ __noinline__ bool flow_give_up(int* abortw, int* info, long long t0, long long lim) {
     if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(abortw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
         return true;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > FLOW_TIMEOUT_TICKS) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > lim) {
         if ((threadIdx.x & 63) == 0) {
             __hip_atomic_store(abortw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(info, MFGP_FLOW_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -279,10 +279,13 @@ __device__ __forceinline__ bool pub_probe_ok(const double* P) {
     const int l = threadIdx.x & 63;
     return __ballot(is_sent(ld_coherent(P + (l & 15)))) == 0;
 }
-__device__ __noinline__ void pub_wait(const double* P, int* abortw, int* info, long long t0) {
+// Every wait's bound counts from the start of THAT wait (a long but progressing factorization
+// never trips it; only a hand-off that stalls for FlowArgs::timeout ticks does).
+__device__ __noinline__ void pub_wait(const double* P, int* abortw, int* info, long long lim) {
+    const long long t0 = __builtin_amdgcn_s_memrealtime();
     for (int spin = 0;; ++spin) {
         if (pub_probe_ok(P)) return;
-        if ((spin & 7) == 7 && flow_give_up(abortw, info, t0)) return;
+        if ((spin & 7) == 7 && flow_give_up(abortw, info, t0, lim)) return;
         __builtin_amdgcn_s_sleep(FLOW_SLEEP);
     }
 }
@@ -296,8 +299,8 @@ __device__ __forceinline__ void pub_probe2(const double* Px, const double* Py, F
     const bool okx = __ballot(is_sent(px)) == 0, oky = __ballot(is_sent(py)) == 0;
     if (!okx || !oky) {
         const long long tw = flow_clock();
-        if (!okx) pub_wait(Px, C.a.flags, C.a.info, C.t0);
-        if (!oky) pub_wait(Py, C.a.flags, C.a.info, C.t0);
+        if (!okx) pub_wait(Px, C.a.flags, C.a.info, C.a.timeout);
+        if (!oky) pub_wait(Py, C.a.flags, C.a.info, C.a.timeout);
         C.waited += flow_clock() - tw;
     }
 }
@@ -331,8 +334,8 @@ __device__ __forceinline__ bool op_missing(const WOp& o) {
 __device__ __forceinline__ void pub_retry(WOp& o, const double* P, FlowCtx& C) {
     const long long tw = flow_clock();
     for (;;) {
-        if (flow_give_up(C.a.flags, C.a.info, C.t0)) break;
-        pub_wait(P, C.a.flags, C.a.info, C.t0);
+        if (flow_give_up(C.a.flags, C.a.info, tw, C.a.timeout)) break;
+        pub_wait(P, C.a.flags, C.a.info, C.a.timeout);
         op_load_pub(o, P);
         if (!op_missing(o)) break;
     }
@@ -351,7 +354,7 @@ __device__ __forceinline__ void pub_op_direct(WOp& o, const double* P, FlowCtx& 
         __builtin_amdgcn_s_sleep(FLOW_SLEEP);
         op_load_pub(o, P);
         if (!op_missing(o)) break;
-        if ((spin & 7) == 7 && flow_give_up(C.a.flags, C.a.info, C.t0)) break;
+        if ((spin & 7) == 7 && flow_give_up(C.a.flags, C.a.info, tw, C.a.timeout)) break;
     }
     C.waited += flow_clock() - tw;
 }
@@ -377,8 +380,8 @@ __device__ __forceinline__ void pub_wt(WTile& t, const double* P, FlowCtx& C) {
                 for (int r = 0; r < 4; ++r) miss |= is_sent(t.v[a][b][r]);
         if (__ballot(miss) == 0) break;
         if (spin == 0) tw = flow_clock();
-        if (flow_give_up(C.a.flags, C.a.info, C.t0)) break;
-        pub_wait(P, C.a.flags, C.a.info, C.t0);
+        if (flow_give_up(C.a.flags, C.a.info, tw, C.a.timeout)) break;
+        pub_wait(P, C.a.flags, C.a.info, C.a.timeout);
     }
     if (tw) C.waited += flow_clock() - tw;
 }
@@ -387,6 +390,7 @@ __device__ __forceinline__ void pub_wt(WTile& t, const double* P, FlowCtx& C) {
 // per poll instead of probe + reload (only three waves of the launch poll this way)
 __device__ __forceinline__ void pub_wt_op_direct(WTile& t, const double* Pt, WOp& o, const double* Po,
                                                  FlowCtx& C) {
+    const long long tw = flow_clock();
     for (int spin = 0;; ++spin) {
         wt_load<true>(t, Pt, 32);
         op_load_pub(o, Po);
@@ -398,7 +402,7 @@ __device__ __forceinline__ void pub_wt_op_direct(WTile& t, const double* Pt, WOp
 #pragma unroll
                 for (int r = 0; r < 4; ++r) miss |= is_sent(t.v[a][b][r]);
         if (__ballot(miss) == 0 && !op_missing(o)) break;
-        if ((spin & 7) == 7 && flow_give_up(C.a.flags, C.a.info, C.t0)) break;
+        if ((spin & 7) == 7 && flow_give_up(C.a.flags, C.a.info, tw, C.a.timeout)) break;
         __builtin_amdgcn_s_sleep(FLOW_SLEEP);
     }
 }

@@ -56,7 +56,9 @@ struct FlowArgs {
     int T, Tp, n, p;
     long long* trace;             // diagnostic timeline (nullptr: off), flow_trace_count entries
     int nwaves;                   // worker waves (trace layout)
+    long long timeout;            // bound of every hand-off wait, 100 MHz ticks (FLOW_TIMEOUT_TICKS)
 };
+constexpr long long FLOW_TIMEOUT_TICKS = 5000000;   // 50 ms (s_memrealtime is 100 MHz)
 int flow_trace_count(int T, int nwg);
 
 struct CholArgs {
@@ -123,6 +125,21 @@ struct PredOutArgs {
     double* var;                      // nstar
     int T, Tp, nstar, p;
 };
+
+// Batched fp64 MFMA GEMM (k_bgemm, mfgp_svgp_grad.hip), NB x NB output tiles:
+// D = alpha * op(A) diag(s) op(B) [* diag(colscale)] + beta * Cin + x y^T   (tril: zero j > i)
+struct BgemmArgs {
+    const double* A; long lda; long sA;
+    const double* B; long ldb; long sB;
+    const double* s; long ss;              // k scaling (nullptr: none)
+    const double* colscale; long scs;      // output column scaling (nullptr: none)
+    const double* Cin; long ldc; long sC; double beta;
+    const double* x; long sx; const double* y; long sy;   // rank-1 term (nullptr: none)
+    double* D; long ldd; long sD;
+    double alpha;
+    int Mt, Nt, Kt, tril;
+};
+void launch_bgemm(int nb, hipStream_t st, int ta, int tb, const BgemmArgs& a, int batch);
 
 constexpr int MAXD_HOST = 32;
 

@@ -26,20 +26,7 @@ namespace mfgp {
 
 static inline int cdv(int a, int b) { return (a + b - 1) / b; }
 
-// ---------------------------------------------------------------- batched GEMM
-// D = alpha * op(A) diag(s) op(B) [* diag(colscale)] + beta * Cin + x y^T   (tril: zero j > i)
-struct BgemmArgs {
-    const double* A; long lda; long sA;
-    const double* B; long ldb; long sB;
-    const double* s; long ss;              // k scaling (nullptr: none)
-    const double* colscale; long scs;      // output column scaling (nullptr: none)
-    const double* Cin; long ldc; long sC; double beta;
-    const double* x; long sx; const double* y; long sy;   // rank-1 term (nullptr: none)
-    double* D; long ldd; long sD;
-    double alpha;
-    int Mt, Nt, Kt, tril;
-};
-
+// ---------------------------------------------------------------- batched GEMM (BgemmArgs: mfgp_internal.h)
 template <int NB, bool TA, bool TB>
 __global__ __launch_bounds__(NTHREADS) void k_bgemm(BgemmArgs a) {
     constexpr int S = TileCfg<NB>::S;
@@ -101,6 +88,11 @@ static void bgemm(hipStream_t st, int ta, int tb, const BgemmArgs& a, int batch)
     else if (!ta && tb) hipLaunchKernelGGL((k_bgemm<NB, false, true>), g, dim3(NTHREADS), sm, st, a);
     else if (ta && !tb) hipLaunchKernelGGL((k_bgemm<NB, true, false>), g, dim3(NTHREADS), sm, st, a);
     else hipLaunchKernelGGL((k_bgemm<NB, true, true>), g, dim3(NTHREADS), sm, st, a);
+}
+
+void launch_bgemm(int nb, hipStream_t st, int ta, int tb, const BgemmArgs& a, int batch) {
+    if (nb == 64) bgemm<64>(st, ta, tb, a, batch);
+    else bgemm<32>(st, ta, tb, a, batch);
 }
 
 // plain square product helper on Mpad x Mpad batched matrices

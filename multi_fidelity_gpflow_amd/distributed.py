@@ -158,6 +158,7 @@ class SharedThetaTrainer:
 
     def finish(self):
         """Write theta back into the model (device path) and its loss_history."""
+        from ._lib import MFGP_FLOW_TIMEOUT, info_error
         from .models import CholeskyError
         if not hasattr(self, "u"):
             return
@@ -165,5 +166,8 @@ class SharedThetaTrainer:
         self.tm.set_u(self.u.cpu().numpy())
         h = self.hist_t[:self.done].cpu().numpy()
         self.model.loss_history = [np.float64(v) for v in h]
-        if int(self.info.item()) != 0 or not np.all(np.isfinite(h)):
+        v = int(self.info.item())
+        if v == MFGP_FLOW_TIMEOUT:
+            raise info_error(v, "shared-theta optimize")
+        if v != 0 or not np.all(np.isfinite(h)):
             raise CholeskyError("shared-theta optimize: Cholesky failed")

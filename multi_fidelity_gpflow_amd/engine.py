@@ -87,6 +87,10 @@ class Engine:
         """Cholesky schedule of the LML path: persistent dataflow launch (True) or one launch per step."""
         check(self.lib.mfgp_set_flow(self.h, 1 if enable else 0), "mfgp_set_flow")
 
+    def set_flow_timeout_us(self, us: int):
+        """Bound of every k_chol_flow hand-off wait (default 50000 us; 0: diagnostic abort path)."""
+        check(self.lib.mfgp_set_flow_timeout_us(self.h, int(us)), "mfgp_set_flow_timeout_us")
+
     # ------------------------------------------------------------ kernels
     def rbf_gram(self, X1: torch.Tensor, X2: torch.Tensor, params: torch.Tensor) -> torch.Tensor:
         n1, d = X1.shape
@@ -110,24 +114,39 @@ class Engine:
         check(self.lib.mfgp_mf_kdiag(self.h, n, dp1 - 1, ptr(X), dp1, ptr(theta), ptr(out)), "mfgp_mf_kdiag")
         return out
 
-    def gpr_lml(self, X, Y, theta, want_grad=False):
+    def gpr_workspace_bytes(self, n: int, p: int, d: int) -> int:
+        return self._size(self.lib.mfgp_gpr_workspace_size, n, p, d)
+
+    def private_workspace(self, nbytes: int) -> torch.Tensor:
+        """A workspace owned by its caller (a training session keeps it for the life of its
+        recorded graphs; the shared grow-only buffers may be replaced under them)."""
+        return torch.empty(int(nbytes), dtype=torch.uint8, device=self.device)
+
+    def gpr_lml(self, X, Y, theta, want_grad=False, ws=None):
         n, dp1 = X.shape
         p = Y.shape[1]
         d = dp1 - 1
-        nbytes = self._size(self.lib.mfgp_gpr_workspace_size, n, p, d)
-        ws = self.workspace("gpr", nbytes)
+        nbytes = self.gpr_workspace_bytes(n, p, d)
+        if ws is None:
+            ws = self.workspace("gpr", nbytes)
+        elif ws.numel() < nbytes:
+            raise MFGPError("gpr_lml: private workspace too small")
         out = torch.empty((1 + theta_size(d),), dtype=torch.float64, device=self.device)
         info = torch.empty((1,), dtype=torch.int32, device=self.device)
         check(self.lib.mfgp_gpr_lml(self.h, n, p, d, ptr(X), dp1, ptr(Y), p, ptr(theta), int(want_grad), ptr(ws),
                                     ws.numel(), ptr(out), ptr(info)), "mfgp_gpr_lml")
         return out, info
 
-    def gpr_adam_step(self, X, Y, st: "AdamState", loss_hist: torch.Tensor, out: torch.Tensor, info: torch.Tensor):
+    def gpr_adam_step(self, X, Y, st: "AdamState", loss_hist: torch.Tensor, out: torch.Tensor, info: torch.Tensor,
+                      ws: torch.Tensor = None):
         n, dp1 = X.shape
         p = Y.shape[1]
         d = dp1 - 1
-        nbytes = self._size(self.lib.mfgp_gpr_workspace_size, n, p, d)
-        ws = self.workspace("gpr", nbytes)
+        nbytes = self.gpr_workspace_bytes(n, p, d)
+        if ws is None:
+            ws = self.workspace("gpr", nbytes)
+        elif ws.numel() < nbytes:
+            raise MFGPError("gpr_adam_step: private workspace too small")
         check(self.lib.mfgp_gpr_adam_step(self.h, n, p, d, ptr(X), dp1, ptr(Y), p, ptr(st.theta), ptr(st.u),
                                           ptr(st.m), ptr(st.v), ptr(st.trainable), ptr(st.tie), ptr(st.step), st.lr, st.b1,
                                           st.b2, st.eps, ptr(loss_hist), ptr(ws), ws.numel(), ptr(out), ptr(info)),
@@ -151,6 +170,23 @@ class Engine:
               "mfgp_gpr_predict")
         return mean, var, info
 
+    def gpr_predict_cov(self, nlf, X, Y, Xs, theta):
+        """predict_f(full_cov=True): mean [ns, p], var [ns], cov [ns, ns] (nlf 0: linear MF kernel)."""
+        n, dp1 = X.shape
+        p = Y.shape[1]
+        d = dp1 - 1
+        ns = Xs.shape[0]
+        nbytes = self._size(self.lib.mfgp_gpr_predict_cov_workspace_size, nlf, n, p, d, ns)
+        ws = self.workspace("pred_cov", nbytes)
+        mean = torch.empty((ns, p), dtype=torch.float64, device=self.device)
+        var = torch.empty((ns,), dtype=torch.float64, device=self.device)
+        cov = torch.empty((ns, ns), dtype=torch.float64, device=self.device)
+        info = torch.empty((1,), dtype=torch.int32, device=self.device)
+        check(self.lib.mfgp_gpr_predict_cov(self.h, nlf, n, p, d, ns, ptr(X), dp1, ptr(Y), p, ptr(Xs), Xs.shape[1],
+                                            ptr(theta), ptr(ws), ws.numel(), ptr(mean), p, ptr(var), ptr(cov), ns,
+                                            ptr(info)), "mfgp_gpr_predict_cov")
+        return mean, var, cov, info
+
     # ---- GraphMultiFidelityKernel (graph.py) with nlf LF sources
     def gmf_gram(self, nlf, X1, X2, theta, diag_add=0.0):
         n1, dp1 = X1.shape
@@ -166,12 +202,18 @@ class Engine:
         check(self.lib.mfgp_gmf_kdiag(self.h, nlf, n, dp1 - 1, ptr(X), dp1, ptr(theta), ptr(out)), "mfgp_gmf_kdiag")
         return out
 
-    def gmf_lml(self, nlf, X, Y, theta, want_grad=False, out=None, info=None):
+    def gmf_workspace_bytes(self, nlf, n, p, d) -> int:
+        return self._size(self.lib.mfgp_gmf_gpr_workspace_size, nlf, n, p, d)
+
+    def gmf_lml(self, nlf, X, Y, theta, want_grad=False, out=None, info=None, ws=None):
         n, dp1 = X.shape
         p = Y.shape[1]
         d = dp1 - 1
-        nbytes = self._size(self.lib.mfgp_gmf_gpr_workspace_size, nlf, n, p, d)
-        ws = self.workspace("gmf", nbytes)
+        nbytes = self.gmf_workspace_bytes(nlf, n, p, d)
+        if ws is None:
+            ws = self.workspace("gmf", nbytes)
+        elif ws.numel() < nbytes:
+            raise MFGPError("gmf_lml: private workspace too small")
         if out is None:
             out = torch.empty((1 + theta.numel(),), dtype=torch.float64, device=self.device)
         if info is None:
@@ -230,8 +272,11 @@ class Engine:
                                       ptr(info)), "mfgp_svgp_elbo")
         return out, g_mu, g_var, info
 
+    def svgp_grad_workspace_bytes(self, n, m, L, p, d) -> int:
+        return self._size(self.lib.mfgp_svgp_grad_workspace_size, n, m, L, p, d)
+
     def svgp_elbo_grad(self, X, Y, Z, thetas, q_mu, q_sqrt, W, noise, scale, kl_mult, jitter, out, g_mu, g_var,
-                       gZ, gtheta, gq_mu, gq_sqrt, gW, gnoise, info):
+                       gZ, gtheta, gq_mu, gq_sqrt, gW, gnoise, info, ws=None):
         """Gradient of VE*scale - kl_mult*KL w.r.t. the constrained SVGP parameters (all device
         tensors, written in place; noise is a device scalar)."""
         n, dp1 = X.shape
@@ -239,8 +284,11 @@ class Engine:
         p = Y.shape[1]
         m = Z.shape[0]
         L = thetas.shape[0]
-        nbytes = self._size(self.lib.mfgp_svgp_grad_workspace_size, n, m, L, p, d)
-        ws = self.workspace("svgp_grad", nbytes)
+        nbytes = self.svgp_grad_workspace_bytes(n, m, L, p, d)
+        if ws is None:
+            ws = self.workspace("svgp_grad", nbytes)
+        elif ws.numel() < nbytes:
+            raise MFGPError("svgp_elbo_grad: private workspace too small")
         check(self.lib.mfgp_svgp_elbo_grad(self.h, n, m, L, p, d, ptr(X), dp1, ptr(Y), Y.stride(0), ptr(Z), dp1,
                                            ptr(thetas), ptr(q_mu), ptr(q_sqrt), ptr(W), ptr(noise), float(scale),
                                            float(kl_mult), float(jitter), ptr(ws), ws.numel(), ptr(out), ptr(g_mu),

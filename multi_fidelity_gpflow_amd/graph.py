@@ -18,6 +18,7 @@ import torch
 
 from .engine import Engine, to_dev
 from .kernels import GraphMultiFidelityKernel
+from ._lib import MFGP_FLOW_TIMEOUT, info_error
 from .models import CholeskyError, Gaussian, _StepRunner
 from .params import Module, Sigmoid, Softplus, as_result, set_trainable
 
@@ -70,10 +71,9 @@ class GraphMultiFidelityGPModel(Module):
 
     @staticmethod
     def _raise_info(info, what):
-        bad = int(info.max().item())
-        if bad != 0:
-            raise CholeskyError(f"{what}: Cholesky decomposition was not successful (non-positive pivot at row "
-                                f"{bad - 1}); the input might not be valid.")
+        err = info_error(int(info.reshape(-1)[0].item()), what)
+        if err is not None:
+            raise err
 
     # ------------------------------------------------------------ GPR surface
     def log_marginal_likelihood(self):
@@ -98,18 +98,27 @@ class GraphMultiFidelityGPModel(Module):
     def predict_f(self, Xnew, full_cov: bool = False, full_output_cov: bool = False):
         """GPR.predict_f(full_cov=False).  (The reference's K(X, Xnew) adds tf.eye(len(X)) and
         fails unless len(Xnew) == len(X); the engine computes K(X, Xnew) without it.)"""
-        if full_cov or full_output_cov:
-            raise NotImplementedError("predict_f(full_cov=True) is not provided by the MI355X engine yet")
+        if full_output_cov:
+            raise NotImplementedError("predict_f(full_output_cov=True): GPR has no output covariance to return")
         eng, X, Y = self._device_data()
         Xs = to_dev(Xnew, eng.device)
         th = torch.tensor(self._theta(), dtype=torch.float64, device=eng.device)
+        if full_cov:   # [P, N*, N*]; K(X*, X*) carries the kernel's 1e-6 jitter (graph.py:96)
+            mean, _, cov, info = eng.gpr_predict_cov(self.num_LF, X, Y, Xs, th)
+            self._raise_info(info, "predict_f")
+            return as_result(mean), as_result(cov[None].expand(Y.shape[1], -1, -1).contiguous())
         mean, var, info = eng.gmf_predict(self.num_LF, X, Y, Xs, th)
         self._raise_info(info, "predict_f")
         return as_result(mean), as_result(var[:, None].expand(-1, Y.shape[1]).contiguous())
 
     def predict_y(self, Xnew, full_cov: bool = False, full_output_cov: bool = False):
         mean, var = self.predict_f(Xnew, full_cov, full_output_cov)
-        return mean, as_result(var + float(self.likelihood.variance.numpy()))
+        noise = float(self.likelihood.variance.numpy())
+        if full_cov:
+            var = var.as_subclass(torch.Tensor).clone()
+            var.diagonal(dim1=-2, dim2=-1).add_(noise)
+            return mean, as_result(var)
+        return mean, as_result(var + noise)
 
     # ------------------------------------------------------------ training
     def optimize(self, max_iters=1000, learning_rate=0.01, use_adam=True, unfix_noise_after=500, verbose=False,
@@ -216,13 +225,16 @@ class _GraphAdamSession:
             self.hist = torch.zeros((self.max_iters,), **f64)
             self.out = torch.zeros((1 + G,), **f64)
             self.info = torch.zeros((1,), dtype=torch.int32, device=dev)
-            self._lml()   # sizes the workspace outside capture
+            n, p, d = self.X.shape[0], self.Y.shape[1], self.X.shape[1] - 1
+            self.ws = self.eng.private_workspace(self.eng.gmf_workspace_bytes(self.model.num_LF, n, p, d))
+            self._lml()   # builds the schedule tables outside capture
         self.b1, self.b2 = float(np.float32(0.9)), float(np.float32(0.999))
         self.done = 0
         self.runner = _StepRunner(self._step, chunk if graph else 0)
 
     def _lml(self):
-        self.eng.gmf_lml(self.model.num_LF, self.X, self.Y, self.theta, want_grad=True, out=self.out, info=self.info)
+        self.eng.gmf_lml(self.model.num_LF, self.X, self.Y, self.theta, want_grad=True, out=self.out, info=self.info,
+                         ws=self.ws)
 
     def _step(self):
         self._lml()
@@ -248,5 +260,8 @@ class _GraphAdamSession:
                 prm.unconstrained_variable = arr
         h = self.hist[:self.done].cpu().numpy()
         self.model.loss_history = [np.float64(v) for v in h]
-        if int(self.info.item()) != 0 or not np.all(np.isfinite(h)):
+        v = int(self.info.item())
+        if v == MFGP_FLOW_TIMEOUT:
+            raise info_error(v, "optimize")
+        if v != 0 or not np.all(np.isfinite(h)):
             raise CholeskyError("optimize: Cholesky failed")

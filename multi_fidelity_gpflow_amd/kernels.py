@@ -177,10 +177,16 @@ class SeparateIndependent(Combination):
     """gpflow.kernels.SeparateIndependent (singlebin_svgp.py:47)."""
 
     def K(self, X, X2=None, full_output_cov=False):
-        return as_result(torch.stack([torch.Tensor(k.K(X, X2)) for k in self.kernels], dim=0))
+        """[L, N, N2] (GPflow SeparateIndependent.K, full_output_cov=False)."""
+        if full_output_cov:
+            raise NotImplementedError("SeparateIndependent.K(full_output_cov=True) is not used by the reference")
+        return as_result(torch.stack([k.K(X, X2).as_subclass(torch.Tensor) for k in self.kernels], dim=0))
 
     def K_diag(self, X, full_output_cov=False):
-        return as_result(torch.stack([torch.Tensor(k.K_diag(X)) for k in self.kernels], dim=1))
+        """[N, L] (GPflow SeparateIndependent.K_diag, full_output_cov=False)."""
+        if full_output_cov:
+            raise NotImplementedError("SeparateIndependent.K_diag(full_output_cov=True) is not used by the reference")
+        return as_result(torch.stack([k.K_diag(X).as_subclass(torch.Tensor) for k in self.kernels], dim=1))
 
 
 class LinearCoregionalization(Combination):

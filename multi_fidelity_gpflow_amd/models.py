@@ -22,7 +22,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from ._lib import MFGPError
+from ._lib import MFGP_FLOW_TIMEOUT, MFGPError, info_error
 from .engine import AdamState, Engine, theta_size, to_dev
 from .kernels import LinearMultiFidelityKernel
 from .params import Module, Parameter, as_result, positive, set_trainable
@@ -129,10 +129,9 @@ class MultiFidelityGPModel(Module):
 
     @staticmethod
     def _raise_info(info: torch.Tensor, what: str):
-        v = int(info.reshape(-1)[0].item())
-        if v != 0:
-            raise CholeskyError(f"{what}: Cholesky decomposition was not successful "
-                                f"(non-positive pivot at row {v}); the input might not be valid.")
+        err = info_error(int(info.reshape(-1)[0].item()), what)
+        if err is not None:
+            raise err
 
     # ------------------------------------------------------------ GPR surface
     def log_marginal_likelihood(self):
@@ -158,18 +157,29 @@ class MultiFidelityGPModel(Module):
         return float(o[0]), o[1:]
 
     def predict_f(self, Xnew, full_cov: bool = False, full_output_cov: bool = False):
-        if full_cov or full_output_cov:
-            raise NotImplementedError("predict_f(full_cov=True) is not provided by the MI355X engine yet")
+        """GPflow GPR.predict_f (mirror at linear.py:237-286): mean [N*, P]; var [N*, P]
+        (full_cov=False) or [P, N*, N*] (full_cov=True, base_conditional's tiled Knn - AᵀA)."""
+        if full_output_cov:
+            raise NotImplementedError("predict_f(full_output_cov=True): GPR has no output covariance to return")
         eng, X, Y = self._device_data()
         Xs = to_dev(Xnew, eng.device)
         theta = torch.tensor(self._theta_map().theta(), dtype=torch.float64, device=eng.device)
+        if full_cov:
+            mean, _, cov, info = eng.gpr_predict_cov(0, X, Y, Xs, theta)
+            self._raise_info(info, "predict_f")
+            return as_result(mean), as_result(cov[None].expand(Y.shape[1], -1, -1).contiguous())
         mean, var, info = eng.gpr_predict(X, Y, Xs, theta)
         self._raise_info(info, "predict_f")
         return as_result(mean), as_result(var[:, None].expand(-1, Y.shape[1]).contiguous())
 
     def predict_y(self, Xnew, full_cov: bool = False, full_output_cov: bool = False):
         mean, var = self.predict_f(Xnew, full_cov, full_output_cov)
-        return mean, as_result(var + float(self.likelihood.variance.numpy()))
+        noise = float(self.likelihood.variance.numpy())
+        if full_cov:   # Gaussian.predict_mean_and_var adds the noise on the diagonal
+            var = var.as_subclass(torch.Tensor).clone()
+            var.diagonal(dim1=-2, dim2=-1).add_(noise)
+            return mean, as_result(var)
+        return mean, as_result(var + noise)
 
     # ------------------------------------------------------------ training
     def optimize(self, max_iters=1000, learning_rate=0.01, use_adam=True, unfix_noise_after=500, verbose=True,
@@ -267,18 +277,23 @@ class AdamSession:
         self.tm = model._theta_map()
         self.stream = torch.cuda.Stream(self.eng.device)
         self.max_iters = max(int(max_iters), 1)
+        # every buffer the recorded graphs point at is allocated on the session's stream and
+        # owned by the session for its lifetime (no shared grow-only workspace under a graph)
+        self.stream.wait_stream(torch.cuda.current_stream(self.eng.device))
         with torch.cuda.stream(self.stream):
             self.st = AdamState(self.eng.device, self.tm.u(), self.tm.trainable(), self.tm.tie(), lr)
             self.hist = torch.zeros((self.max_iters,), dtype=torch.float64, device=self.eng.device)
             self.out = torch.empty((1 + theta_size(self.tm.d),), dtype=torch.float64, device=self.eng.device)
             self.info = torch.zeros((1,), dtype=torch.int32, device=self.eng.device)
+            n, p, d = self.X.shape[0], self.Y.shape[1], self.tm.d
+            self.ws = self.eng.private_workspace(self.eng.gpr_workspace_bytes(n, p, d))
             self.eng.theta_from_u(self.st.u, self.st.theta, self.tm.noise_index)
-            self.eng.gpr_lml(self.X, self.Y, self.st.theta, want_grad=False)   # sizes the workspace
+            self.eng.gpr_lml(self.X, self.Y, self.st.theta, want_grad=False, ws=self.ws)   # builds schedule tables
         self.done = 0
         self.runner = _StepRunner(self._step, chunk if graph else 0)
 
     def _step(self):
-        self.eng.gpr_adam_step(self.X, self.Y, self.st, self.hist, self.out, self.info)
+        self.eng.gpr_adam_step(self.X, self.Y, self.st, self.hist, self.out, self.info, ws=self.ws)
 
     def run(self, n: int):
         if self.done + n > self.max_iters:
@@ -286,6 +301,11 @@ class AdamSession:
         with torch.cuda.stream(self.stream):
             self.runner.run(n)
         self.done += n
+
+    def prepare(self, n: int):
+        """Capture the step graphs a later run(n) replays (nothing executes)."""
+        with torch.cuda.stream(self.stream):
+            self.runner.prepare(n)
 
     def sync(self):
         self.stream.synchronize()
@@ -299,9 +319,12 @@ class AdamSession:
         h = self.hist[:self.done].cpu().numpy()
         self.model.loss_history = [np.float64(v) for v in h]
         self.tm.set_u(self.st.u.cpu().numpy())
-        if int(self.info.item()) != 0 or not np.all(np.isfinite(h)):
+        v = int(self.info.item())
+        if v != 0 or not np.all(np.isfinite(h)):
             bad = int(np.argmax(~np.isfinite(h))) if not np.all(np.isfinite(h)) else len(h) - 1
             self.model.loss_history = self.model.loss_history[:bad + 1]
+            if v == MFGP_FLOW_TIMEOUT:
+                raise info_error(v, f"optimize (by iteration {bad})")
             raise CholeskyError(f"optimize: Cholesky failed at iteration {bad}")
 
 
@@ -323,6 +346,17 @@ class _StepRunner:
                     self.step()
             self.graphs[n] = g
         return g
+
+    def prepare(self, n: int):
+        """Capture (without running) every graph that run(n) will replay, so a later
+        run(n) is replay-only (bench.py captures before its timed region)."""
+        if self.chunk <= 0 or n < 4:
+            return
+        full, rem = divmod(n, self.chunk)
+        if full:
+            self._graph(self.chunk)
+        if rem >= 4:
+            self._graph(rem)
 
     def run(self, n: int):
         if self.chunk <= 0 or n < 4:

@@ -295,6 +295,8 @@ class _SVGPTrainer:
             self.g_mu = torch.empty((L, n), **f64)
             self.g_var = torch.empty((L, n), **f64)
             self.info = torch.zeros((L,), dtype=torch.int32, device=dev)
+            # owned by the trainer for the life of its graphs (not the engine's shared buffer)
+            self.ws = eng.private_workspace(eng.svgp_grad_workspace_bytes(n, m, L, p, d))
         self.scale = (model.num_data / n) if model.num_data else 1.0
         self.b1, self.b2 = float(np.float32(0.9)), float(np.float32(0.999))
         self.done = 0
@@ -322,7 +324,7 @@ class _SVGPTrainer:
                                 self.view(c, "q_sqrt"), W, self.view(c, "noise"), self.scale, self.klm,
                                 DEFAULT_JITTER, self.out, self.g_mu, self.g_var, self.view(g, "Z"),
                                 self.view(g, "theta"), self.view(g, "q_mu"), self.view(g, "q_sqrt"), gW,
-                                self.view(g, "noise"), self.info)
+                                self.view(g, "noise"), self.info, ws=self.ws)
 
     def _step(self):
         self._grad()
@@ -431,6 +433,20 @@ class LatentMFCoregionalizationSVGP(_SVGPBase):
         fires: the noise keeps the trainable flag it has.)"""
         self._optimize(data, max_iters, initial_lr, None, kl_multiplier, False, graph, graph_chunk, verbose, 100)
 
+    def save_model(self, filename="latent_mf_svgp.pkl"):
+        """linear_svgp.py:206-212 (parameter_dict pickled)."""
+        super().save_model(filename)
+
+    @staticmethod
+    def load_model(filename, *args):
+        """linear_svgp.py:214-221: rebuild with the constructor arguments, then
+        multiple_assign the saved parameter_dict."""
+        with open(filename, "rb") as f:
+            params = pickle.load(f)
+        model = LatentMFCoregionalizationSVGP(*args)
+        multiple_assign(model, params)
+        return model
+
 
 class SingleBinSVGP(_SVGPBase):
     """mfgpflow/singlebin_svgp.py:20-62 constructor semantics (Z values are ignored;
@@ -451,6 +467,10 @@ class SingleBinSVGP(_SVGPBase):
         """singlebin_svgp.py:64-97: Adam + CosineDecay(initial_lr, max_iters) on -ELBO;
         loss_history restarts; the noise becomes trainable after iteration unfix_noise_after."""
         self._optimize(data, max_iters, initial_lr, unfix_noise_after, 1.0, True, graph, graph_chunk, verbose, 10)
+
+    def save_model(self, filename="svgp_model.pkl"):
+        """singlebin_svgp.py:99-110 (parameter_dict pickled)."""
+        super().save_model(filename)
 
     @staticmethod
     def load_model(filename, X, Y, kernel_L, kernel_delta, num_outputs, Z):

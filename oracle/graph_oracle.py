@@ -77,6 +77,17 @@ def predict_f(X, Y, Xs, prm, noise):
     return mean, var
 
 
+def predict_f_full_cov(X, Y, Xs, prm, noise):
+    """GPR.predict_f(full_cov=True): Knn = K(X*, X*) as the kernel computes it (with its 1e-6
+    jitter, graph.py:96), cov = Knn − AᵀA (one block for every output)."""
+    K = graph_K(X, X, prm) + noise * torch.eye(X.shape[0], dtype=torch.float64)
+    L = torch.linalg.cholesky(K)
+    Kmn = graph_K(X, Xs, prm, jitter=False)
+    A = torch.linalg.solve_triangular(L, Kmn, upper=False)
+    V = torch.linalg.solve_triangular(L, Y, upper=False)
+    return A.T @ V, graph_K(Xs, Xs, prm) - A.T @ A
+
+
 class GraphTrainer:
     """GraphMultiFidelityGPModel.optimize(use_adam=True) (graph.py:154-174): Adam (constant
     float32 lr) on the unconstrained kernel variances / lengthscales / rho (Softplus) and

@@ -230,6 +230,19 @@ def gpr_predict_f(X, Y, Xnew, p: MFParams):
     return mean, np.tile(var[:, None], (1, Y.shape[1]))
 
 
+def gpr_predict_f_full_cov(X, Y, Xnew, p: MFParams):
+    """gpflow GPR.predict_f(full_cov=True) → base_conditional(full_cov=True, white=False):
+    fvar = Knn − AᵀA with Knn = K(X*, X*), tiled to [P, N*, N*]."""
+    K = mf_K(X, None, p)
+    K[np.diag_indices_from(K)] += p.noise
+    Lm = np.linalg.cholesky(K)
+    Kmn = mf_K(X, Xnew, p)
+    A = sla.solve_triangular(Lm, Kmn, lower=True)
+    cov = mf_K(Xnew, None, p) - A.T @ A
+    mean = sla.solve_triangular(Lm.T, A, lower=False).T @ Y
+    return mean, np.tile(cov[None], (Y.shape[1], 1, 1))
+
+
 # ---------------------------------------------------------------- unconstrained vector
 def pack_unconstrained(p: MFParams, with_noise=False):
     """Trainable unconstrained vector [vL, lL(D), vD, lD(D), rho0, (noise)]."""

@@ -1,0 +1,158 @@
+"""GPflow API surface beyond the LML hot loop, on the HIP path (round-2 additions).
+
+* ``predict_f(full_cov=True)`` / ``predict_y(full_cov=True)`` — GPflow base_conditional's
+  full-covariance branch (Knn − AᵀA, tiled to [P, N*, N*]) for the linear and graph models,
+  against oracle/mfgp_oracle.py and oracle/graph_oracle.py: 1e-9 abs (fp64).
+* ``SeparateIndependent.K`` / ``K_diag`` (singlebin_svgp.py:47) stack per-bin device Grams.
+* The persistent Cholesky's timeout path raises ``FlowTimeoutError`` (not a numerical
+  ``CholeskyError``), and the next call on the same workspace is correct again.
+* Training sessions own their workspaces: two interleaved sessions reproduce their solo
+  trajectories bit for bit; a prepared (pre-captured) run replays the same steps.
+"""
+import numpy as np
+import pytest
+import torch
+
+import multi_fidelity_gpflow_amd as M
+from multi_fidelity_gpflow_amd._lib import FlowTimeoutError
+from multi_fidelity_gpflow_amd.engine import Engine
+from oracle import graph_oracle as GO
+from oracle import mfgp_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    e = Engine.get()
+    yield e
+    e.set_flow(True)
+    e.set_flow_timeout_us(50000)
+
+
+def _model(d, theta_seed=None):
+    D = d["X"].shape[1] - 1
+    m = M.MultiFidelityGPModel(d["X"], d["Y"], M.SquaredExponential(lengthscales=np.ones(D)),
+                               M.SquaredExponential(lengthscales=np.ones(D)))
+    if theta_seed is not None:
+        rng = np.random.default_rng(theta_seed)
+        m.kernel.kernel_L.lengthscales.assign(0.5 + rng.random(D))
+        m.kernel.kernel_delta.lengthscales.assign(0.5 + rng.random(D))
+        m.kernel.kernel_L.variance.assign(0.5 + rng.random())
+        m.kernel.kernel_delta.variance.assign(0.1 + rng.random())
+        m.kernel.rho.assign(np.full((d["Y"].shape[1], 1), 0.5 + rng.random()))
+    return m
+
+
+def _oracle_params(m, D, P):
+    k = m.kernel
+    return O.MFParams(float(k.kernel_L.variance.numpy()), np.broadcast_to(k.kernel_L.lengthscales.numpy(), (D,)).copy(),
+                      float(k.kernel_delta.variance.numpy()),
+                      np.broadcast_to(k.kernel_delta.lengthscales.numpy(), (D,)).copy(),
+                      np.array(k.rho.numpy()), float(m.likelihood.variance.numpy()))
+
+
+@pytest.mark.parametrize("which", ["hbs", "goku"])
+def test_predict_full_cov(which, hbs, goku, eng):
+    d = hbs if which == "hbs" else goku
+    D, P = d["X"].shape[1] - 1, d["Y"].shape[1]
+    m = _model(d, theta_seed=11)
+    Xs = d["Xtest"]
+    mean, cov = m.predict_f(Xs, full_cov=True)
+    mo, co = O.gpr_predict_f_full_cov(d["X"], d["Y"], Xs, _oracle_params(m, D, P))
+    assert tuple(cov.shape) == (P, Xs.shape[0], Xs.shape[0])
+    np.testing.assert_allclose(mean.numpy(), mo, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(cov.numpy(), co, rtol=0, atol=1e-9)
+    # the diagonal is the full_cov=False variance
+    _, var = m.predict_f(Xs)
+    np.testing.assert_allclose(np.diagonal(cov.numpy()[0]), var.numpy()[:, 0], rtol=0, atol=1e-12)
+    _, ycov = m.predict_y(Xs, full_cov=True)
+    np.testing.assert_allclose(np.diagonal(ycov.numpy()[1]) - np.diagonal(cov.numpy()[1]), 1e-3, rtol=1e-9)
+
+
+def test_graph_predict_full_cov(eng):
+    rng = np.random.default_rng(3)
+    D, P = 3, 4
+    Xs_, Ys_ = [], []
+    w = rng.standard_normal((D, P))
+    for s, n in enumerate((40, 30, 12)):
+        x = rng.uniform(0, 1, (n, D))
+        Xs_.append(np.hstack([x, np.full((n, 1), float(s))]))
+        Ys_.append(np.sin(3 * x @ w) * (1 + 0.3 * s))
+    X, Y = np.vstack(Xs_), np.vstack(Ys_)
+    kLs = [M.SquaredExponential(lengthscales=np.full(D, 0.8), variance=1.2) for _ in range(2)]
+    kd = M.SquaredExponential(lengthscales=np.full(D, 0.6), variance=0.3)
+    mod = M.GraphMultiFidelityGPModel(X, Y, kLs, kd)
+    Xt = np.hstack([rng.uniform(0, 1, (9, D)), np.full((9, 1), 2.0)])
+    mean, cov = mod.predict_f(Xt, full_cov=True)
+    k = mod.kernel
+    ks = k.kernel_Ls + [k.kernel_delta]
+    f64 = dict(dtype=torch.float64)
+    prm = dict(v=torch.tensor([float(kk.variance.numpy()) for kk in ks], **f64),
+               l=torch.tensor(np.stack([kk.lengthscale_vector(D) for kk in ks]), **f64),
+               rho=torch.tensor(k.rho.numpy()[:, 0], **f64), rhoLF=torch.tensor(k.rho_LF.numpy(), **f64))
+    mo, co = GO.predict_f_full_cov(torch.tensor(X), torch.tensor(Y), torch.tensor(Xt), prm, 1e-3)
+    np.testing.assert_allclose(mean.numpy(), mo.numpy(), rtol=0, atol=1e-9)
+    np.testing.assert_allclose(cov.numpy()[2], co.numpy(), rtol=0, atol=1e-9)
+
+
+def test_separate_independent_K(hbs, eng):
+    kern = [M.LinearMultiFidelityKernel(M.SquaredExponential(lengthscales=np.full(5, 0.5 + 0.2 * i)),
+                                        M.SquaredExponential(lengthscales=np.ones(5)), 1) for i in range(3)]
+    si = M.kernels.SeparateIndependent(kern)
+    X = hbs["X"]
+    K = si.K(X)
+    Kd = si.K_diag(X)
+    assert tuple(K.shape) == (3, X.shape[0], X.shape[0]) and tuple(Kd.shape) == (X.shape[0], 3)
+    for i, k in enumerate(kern):
+        np.testing.assert_array_equal(K.numpy()[i], k.K(X).numpy())
+        np.testing.assert_array_equal(Kd.numpy()[:, i], k.K_diag(X).numpy())
+
+
+def test_flow_timeout_is_not_a_cholesky_error(goku, eng):
+    """mfgp_set_flow_timeout_us(0): any hand-off that polls 8 times gives up -> the launch drains
+    with info = MFGP_FLOW_TIMEOUT -> FlowTimeoutError; the next call (default bound) is correct."""
+    eng.set_flow(True)
+    if not eng.flow():
+        pytest.skip("persistent Cholesky not available on this device")
+    m = _model(goku)
+    ref = m.log_marginal_likelihood_and_grad()
+    eng.set_flow_timeout_us(0)
+    try:
+        with pytest.raises(FlowTimeoutError):
+            m.log_marginal_likelihood_and_grad()
+    finally:
+        eng.set_flow_timeout_us(50000)
+    again = m.log_marginal_likelihood_and_grad()
+    assert again[0] == ref[0]
+    np.testing.assert_array_equal(again[1], ref[1])
+
+
+def test_interleaved_sessions_own_their_workspaces(hbs, goku, eng):
+    """Two live Adam sessions (different sizes) interleaved on one engine reproduce their solo
+    trajectories exactly: neither writes the other's workspace."""
+    solo = []
+    for d in (hbs, goku):
+        m = _model(d)
+        m.optimize(max_iters=60, learning_rate=0.1, verbose=False)
+        solo.append(np.array(m.loss_history))
+    ma, mb = _model(hbs), _model(goku)
+    sa, sb = ma.adam_session(0.1, 60), mb.adam_session(0.1, 60)
+    for _ in range(6):
+        sa.run(10)
+        sb.run(10)
+    sa.finish()
+    sb.finish()
+    np.testing.assert_array_equal(np.array(ma.loss_history), solo[0])
+    np.testing.assert_array_equal(np.array(mb.loss_history), solo[1])
+
+
+def test_prepared_run_matches(hbs, eng):
+    m1, m2 = _model(hbs), _model(hbs)
+    s1 = m1.adam_session(0.1, 80, graph_chunk=50)
+    s1.run(5)
+    s1.prepare(75)    # captures the 50-step and 25-step graphs, runs nothing
+    s1.run(75)
+    s1.finish()
+    m2.optimize(max_iters=80, learning_rate=0.1, verbose=False, graph=False)
+    np.testing.assert_array_equal(np.array(m1.loss_history), np.array(m2.loss_history))

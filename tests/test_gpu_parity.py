@@ -253,9 +253,18 @@ def test_adam_trajectory_kats(which, hbs, goku, kats, eng):
                                M.SquaredExponential(lengthscales=np.ones(D)))
     m.optimize(max_iters=1000, use_adam=True, learning_rate=0.1, unfix_noise_after=500, verbose=False)
     assert len(m.loss_history) == 1000
+    # Bit-level region (<= 500): 1e-10.  The dynamics turn chaotic near iteration 520 (a 1e-13
+    # perturbation grows to 1e-6 by 540, tests/test_oracle_kats.py) and then re-converge: the HIP
+    # path measured 3.4e-8 / 4.1e-9 / 3.1e-9 at HBS 600 / 700 / 800 (round 2), so 600-800 are held
+    # to 1e-7; iteration 900 (the oracle itself is 1.5e-5 off at Goku) keeps 1e-4.
+    errs = {}
     for k, v in kats[key]["values"].items():
         k = int(k)
-        assert abs(-m.loss_history[k] - v) < (1e-10 if k <= 500 else 1e-4) * abs(v), (k, -m.loss_history[k], v)
+        errs[k] = abs(-m.loss_history[k] - v) / abs(v)
+    print(which, {k: f"{e:.2e}" for k, e in sorted(errs.items())})
+    for k, e in errs.items():
+        tol = 1e-10 if k <= 500 else (1e-7 if k <= 800 else 1e-4)
+        assert e < tol, (k, e, tol)
     # noise never trained in the Adam path (Appendix C-2)
     assert float(m.likelihood.variance.numpy()) == pytest.approx(1e-3, rel=1e-12)
 

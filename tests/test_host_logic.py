@@ -101,3 +101,46 @@ def test_compute_without_gpu_fails_loudly():
     m = _model()
     with pytest.raises(M.MFGPError):
         m.log_marginal_likelihood()
+
+
+def test_svgp_save_load_roundtrip(hbs, tmp_path):
+    """save_model / load_model of both SVGP emulators (linear_svgp.py:206-221,
+    singlebin_svgp.py:99-135): parameter_dict pickled, re-applied with multiple_assign onto a
+    model rebuilt from the constructor arguments.  Host only (no compute)."""
+    X, Y = hbs["X"], hbs["Y"]
+    kL = M.SquaredExponential(lengthscales=np.ones(5))
+    kD = M.SquaredExponential(lengthscales=np.ones(5))
+    args = (X, Y, kL, kD, 4, 12, Y.shape[1])
+    lat = M.LatentMFCoregionalizationSVGP(*args)
+    lat.kernel.kernels[1].kernel_L.lengthscales.assign(np.linspace(0.3, 0.9, 5))
+    lat.q_mu.assign(np.arange(12 * 4, dtype=float).reshape(12, 4) * 0.01)
+    lat.kernel.W.assign(lat.kernel.W.numpy() * 1.5)
+    f = str(tmp_path / "lat.pkl")
+    lat.save_model(f)
+    back = M.LatentMFCoregionalizationSVGP.load_model(f, *args)
+    for (n1, p1), (n2, p2) in zip(lat.parameters_with_names(), back.parameters_with_names()):
+        assert n1 == n2
+        np.testing.assert_array_equal(p1.numpy(), p2.numpy())
+    sb = M.SingleBinSVGP(X, Y[:, :3], kL, kD, 3, np.zeros((10, 6)))
+    sb.q_mu.assign(np.ones((10, 3)) * 0.5)
+    f2 = str(tmp_path / "sb.pkl")
+    sb.save_model(f2)
+    back2 = M.SingleBinSVGP.load_model(f2, X, Y[:, :3], kL, kD, 3, np.zeros((10, 6)))
+    np.testing.assert_array_equal(back2.q_mu.numpy(), sb.q_mu.numpy())
+
+
+def test_torch_cpu_baseline_matches_oracle(hbs):
+    """oracle/torch_oracle.py (bench.py's timed CPU baseline) agrees with the KAT-pinned
+    oracle/mfgp_oracle.py: LML 1e-13 rel, gradient 1e-10 of the largest component."""
+    import torch
+    from oracle import torch_oracle as TO
+    X, Y = hbs["X"], hbs["Y"]
+    rng = np.random.default_rng(2)
+    p = O.MFParams(1.3, 0.5 + rng.random(5), 0.4, 0.5 + rng.random(5), np.full((49, 1), 0.8), 2e-3)
+    lo, go = O.gpr_lml_and_grad(X, Y, p)
+    gv = np.concatenate([[go["vL"]], go["lL"], [go["vD"]], go["lD"], [go["rho0"]], [go["noise"]]])
+    args = (p.vL, torch.tensor(p.lL), p.vD, torch.tensor(p.lD), p.rho0, p.noise)
+    l1, g1 = TO.lml_and_grad(torch.tensor(X), torch.tensor(Y), *args)
+    assert abs(l1 - lo) < 1e-13 * abs(lo)
+    assert abs(TO.lml(torch.tensor(X), torch.tensor(Y), *args) - lo) < 1e-13 * abs(lo)
+    np.testing.assert_allclose(g1.numpy(), gv, rtol=0, atol=1e-10 * np.abs(gv).max())
