@@ -40,6 +40,7 @@ sys.path.insert(0, ROOT)
 
 GOKU = os.path.join(ROOT, "tests", "golden", "data", "matter_power_1128_Box1000_Part750_36_Box1000_Part3000_z0")
 FP64_PEAK_TFLOPS = 78.6   # MI355X dense FP64 (vector = matrix on gfx950), MI355X_MICROARCH.md
+FP32_PEAK_TFLOPS = 157.3  # MI355X dense FP32 (v_mfma_f32_32x32x2_f32 = the f32 vector rate), MI355X_MICROARCH.md
 HBM_PEAK_GBS = 8000.0
 # HBM bytes per dispatch from the committed rocprofv3 PMC passes (tools/profile_round.sh ->
 # tools/summarize_profile.py); the bench cannot count PMC on itself.
@@ -80,11 +81,11 @@ def broadcast_inputs(rank, world, device):
     return broadcast_arrays(arrays, rank, world, device)
 
 
-def make_model(X, Yr):
+def make_model(X, Yr, dtype=None):
     import multi_fidelity_gpflow_amd as M
     d = X.shape[1] - 1
     return M.MultiFidelityGPModel(X, Yr, M.SquaredExponential(lengthscales=np.ones(d), variance=1.0),
-                                  M.SquaredExponential(lengthscales=np.ones(d), variance=1.0))
+                                  M.SquaredExponential(lengthscales=np.ones(d), variance=1.0), dtype=dtype)
 
 
 def step_flops(n, p, d):
@@ -136,6 +137,47 @@ def roofline(model, n, p, d, reps=10, pmc=True):
         "avg_launch_us": round(per_launch_ms * 1e3, 3),
         "flop_per_launch": per_launch_flop,
         "phase_ms": {k: round(float(v), 4) for k, v in zip(names, ms)},
+    }
+
+
+def roofline_f32(model, reps=3, pmc=True):
+    """fp32 path: hipEvents around every launch of one value+grad evaluation (serial schedule,
+    launch stream), summed per phase.  The dominant kernel is the trailing update k32_update
+    (K = 128 * panel); achieved = the tile flops it performs (all but the strictly upper half of
+    the diagonal tiles) / its summed launch time."""
+    from multi_fidelity_gpflow_amd.engine import gpr_phase_times_ex
+    eng, X, Y = model._device_data()
+    theta = torch.tensor(model._theta_map().theta(), dtype=torch.float64, device=eng.device)
+    gpr_phase_times_ex(eng, X, Y, theta)   # warm
+    acc = {}
+    for _ in range(reps):
+        for k, (ms, fl, la) in gpr_phase_times_ex(eng, X, Y, theta).items():
+            a = acc.setdefault(k, [0.0, fl, la])
+            a[0] += ms / reps
+    dom = max(acc, key=lambda k: acc[k][0])
+    ms, fl, la = acc[dom]
+    achieved = fl / (ms * 1e-3) / 1e12
+    kname = {"update_out": "k32_update", "update_in": "k32_update", "grad": "k32_grad", "diag": "k32_diag",
+             "panel": "k32_panel", "gram": "k32_gram", "alpha": "k32_alpha", "finalize": "k32_zsum"}[dom]
+    traffic, tsrc = pmc_traffic(kname, 0) if pmc else (None, None)
+    return {
+        "kernel": kname + (" (trailing update, K = 128 x panel)" if dom == "update_out" else ""),
+        "bound": "mfma",
+        "achieved": round(achieved, 3),
+        "peak": FP32_PEAK_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
+        "traffic": traffic,
+        "traffic_unit": "bytes per step summed over the kernel's launches (FETCH_SIZE x2 + WRITE_SIZE)",
+        "traffic_source": tsrc,
+        "launches_per_step": la,
+        "avg_launch_us": round(ms * 1e3 / max(la, 1), 3),
+        "flop_per_launch": fl / max(la, 1),
+        "phase_ms": {k: round(v[0], 4) for k, v in acc.items()},
+        "phase_tflops": {k: round(v[1] / (v[0] * 1e-3) / 1e12, 2) if v[0] > 0 and v[1] > 0 else None
+                         for k, v in acc.items()},
+        "phase_launches": {k: v[2] for k, v in acc.items()},
+        "serial_sum_ms": round(sum(v[0] for v in acc.values()), 3),
     }
 
 
@@ -208,7 +250,8 @@ def main():
                     help="shard: per-shard-theta bin blocks (no inner-loop collective); shared: one model, "
                          "one all-reduce of 1+G doubles per step (reference-parity mode, SURVEY 8(e))")
     ap.add_argument("--config", choices=["goku", "synth"], default="goku",
-                    help="goku: the BASELINE metric; synth: SURVEY §8(d) scale-up (N=18432, P=512, fp64)")
+                    help="goku: the BASELINE metric (fp64); synth: BASELINE configs[4] / SURVEY §8(d) "
+                         "(N=18432, P=512, fp32)")
     args = ap.parse_args()
     world_env = os.environ.get("WORLD_SIZE")
     if world_env is None and args.gpus > 1:
@@ -243,7 +286,9 @@ def main():
     b0, b1 = bin_block(P, rank, world)
     Yr = np.ascontiguousarray(Y[:, b0:b1])
 
-    model = make_model(X, Yr)
+    synth = args.config == "synth"
+    dtype = "float32" if synth else None
+    model = make_model(X, Yr, dtype)
     K, W = args.steps, args.warmup
     if args.mode == "shared":
         from multi_fidelity_gpflow_amd.distributed import SharedThetaTrainer
@@ -273,7 +318,7 @@ def main():
     # train + predict wall-clock (notebook protocol, fresh model)
     tp = None
     if not args.no_train_predict:
-        m2 = make_model(X, Yr)
+        m2 = make_model(X, Yr, dtype)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -287,7 +332,7 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             tp = float(t.item())
 
-    roof = roofline(model, n, Yr.shape[1], d, pmc=args.config == "goku")
+    roof = roofline_f32(model) if synth else roofline(model, n, Yr.shape[1], d)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(X, Y)
@@ -295,7 +340,6 @@ def main():
     if rank == 0:
         shared = args.mode == "shared"
         value = (K if shared else world * K) / dt
-        synth = args.config == "synth"
         line = {
             "metric": ("LML evals/sec (synthetic 16384LF/2048HF D=10 P=512, value+grad+Adam step)" if synth else
                        "LML evals/sec (Goku 1128LF/36HF multi-bin, value+grad+Adam step)"),
@@ -308,7 +352,7 @@ def main():
             "higher_is_better": True,
             "scaling": "strong" if shared else "weak",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": "f32" if synth else "f64",
             "data": ("synthetic (SURVEY §8(d) recipe, seed 20251015), built on every rank" if synth else
                      "Goku z=0 P(k) (reference data files, tests/golden/data), RCCL-broadcast from rank 0"),
             "config": {"workload": "synth_multibin_adam_step" if synth else "goku_multibin_adam_step",

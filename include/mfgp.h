@@ -221,6 +221,46 @@ int mfgp_svgp_predict(mfgp_handle_t h, int nstar, int m, int l, int p, int d, co
  * writes C (16x16 row-major, device). */
 int mfgp_selftest_mfma(mfgp_handle_t h, double* out);
 
+/* ---- dtype-generic forms (mfgp_mf_gram(h, dtype, ...)).
+ * dtype MFGP_F64: X / Y / K / mean / var are double and the call is exactly the fp64 entry point
+ * of the same name without "_ex".  dtype MFGP_F32: those arrays are float (device, row-major);
+ * theta, out and the Adam state stay double.  The fp32 path is the BASELINE "Synth" config's
+ * (N_L = 16384, N_H = 2048, D = 10, P = 512): the reference forces fp64 (linear.py:63-64), so
+ * its semantics are the fp64 ones computed in fp32 -- r^2 in direct-difference form (not
+ * GPflow's expanded form, which cancels in fp32), every GEMM on v_mfma_f32_32x32x2_f32, the
+ * LML / gradient reductions in fp64.  Tolerances against the fp64 oracle: DESIGN.md §9. */
+#define MFGP_F64 0
+#define MFGP_F32 1
+/* fp32 path: 128-wide tile columns per outer Cholesky panel (default 4; env MFGP_F32_PANEL). */
+int mfgp_set_f32_panel(mfgp_handle_t h, int tiles);
+/* fp32 path: 1 (default; env MFGP_F32_LOOKAHEAD) factors the next panel on a high-priority side
+ * stream beside the trailing update (fork / join events, graph-capturable); 0: one stream. */
+int mfgp_set_f32_lookahead(mfgp_handle_t h, int enable);
+/* LinearMultiFidelityKernel.K (linear.py:55-104), as mfgp_mf_gram. */
+int mfgp_mf_gram_ex(mfgp_handle_t h, int dtype, int n1, int n2, int d, const void* X1, int ldx1, const void* X2,
+                    int ldx2, const double* theta, double diag_add, void* K, int ldk);
+/* GPR.log_marginal_likelihood (+ gradient), as mfgp_gpr_workspace_size / mfgp_gpr_lml. */
+int mfgp_gpr_workspace_size_ex(mfgp_handle_t h, int dtype, int n, int p, int d, size_t* bytes);
+int mfgp_gpr_lml_ex(mfgp_handle_t h, int dtype, int n, int p, int d, const void* X, int ldx, const void* Y, int ldy,
+                    const double* theta, int want_grad, void* ws, size_t ws_bytes, double* out, int* info);
+/* One optimize(use_adam=True) iteration (linear.py:200-214), as mfgp_gpr_adam_step. */
+int mfgp_gpr_adam_step_ex(mfgp_handle_t h, int dtype, int n, int p, int d, const void* X, int ldx, const void* Y,
+                          int ldy, double* theta, double* u, double* m, double* v, const unsigned char* trainable,
+                          const int* tie, int* step, double lr, double beta1, double beta2, double eps,
+                          double* loss_hist, void* ws, size_t ws_bytes, double* out, int* info);
+/* GPR.predict_f(full_cov=False) (linear.py:237-286), as mfgp_gpr_predict; mean / var in dtype. */
+int mfgp_gpr_predict_workspace_size_ex(mfgp_handle_t h, int dtype, int n, int p, int d, int nstar, size_t* bytes);
+int mfgp_gpr_predict_ex(mfgp_handle_t h, int dtype, int n, int p, int d, int nstar, const void* X, int ldx,
+                        const void* Y, int ldy, const void* Xs, int ldxs, const double* theta, void* ws,
+                        size_t ws_bytes, void* mean, int ldm, void* var, int* info);
+/* Diagnostic: one LML value+grad evaluation with hipEvents around its launches; synchronises.
+ * Per phase (HOST arrays of nphase entries): ms, flops performed (fp32 only) and launch count.
+ * fp32 phases: [gram, diag factors, panels, in-panel updates, trailing updates, alpha, gradient,
+ * reductions]; fp64: mfgp_gpr_lml_phase_times' five phases. */
+int mfgp_gpr_phase_times_ex(mfgp_handle_t h, int dtype, int n, int p, int d, const void* X, int ldx, const void* Y,
+                            int ldy, const double* theta, void* ws, size_t ws_bytes, double* out, int* info,
+                            float* ms, double* flops, int* launches, int nphase);
+
 #ifdef __cplusplus
 }
 #endif

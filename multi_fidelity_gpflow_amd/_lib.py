@@ -63,7 +63,22 @@ SIGNATURES = {
     "mfgp_gmf_gpr_predict_workspace_size": [_p, _i, _i, _i, _i, _i, C.POINTER(_sz)],
     "mfgp_gmf_gpr_predict": [_p, _i, _i, _i, _i, _i, _p, _i, _p, _i, _p, _i, _p, _p, _sz, _p, _i, _p, _p],
     "mfgp_selftest_mfma": [_p, _p],
+    # dtype-generic forms (MFGP_F64 = 0, MFGP_F32 = 1)
+    "mfgp_set_f32_panel": [_p, _i],
+    "mfgp_set_f32_lookahead": [_p, _i],
+    "mfgp_mf_gram_ex": [_p, _i, _i, _i, _i, _p, _i, _p, _i, _p, _d, _p, _i],
+    "mfgp_gpr_workspace_size_ex": [_p, _i, _i, _i, _i, C.POINTER(_sz)],
+    "mfgp_gpr_lml_ex": [_p, _i, _i, _i, _i, _p, _i, _p, _i, _p, _i, _p, _sz, _p, _p],
+    "mfgp_gpr_adam_step_ex": [_p, _i, _i, _i, _i, _p, _i, _p, _i, _p, _p, _p, _p, _p, _p, _p, _d, _d, _d, _d, _p,
+                              _p, _sz, _p, _p],
+    "mfgp_gpr_phase_times_ex": [_p, _i, _i, _i, _i, _p, _i, _p, _i, _p, _p, _sz, _p, _p, C.POINTER(C.c_float),
+                                C.POINTER(_d), C.POINTER(_i), _i],
+    "mfgp_gpr_predict_workspace_size_ex": [_p, _i, _i, _i, _i, _i, C.POINTER(_sz)],
+    "mfgp_gpr_predict_ex": [_p, _i, _i, _i, _i, _i, _p, _i, _p, _i, _p, _i, _p, _p, _sz, _p, _i, _p, _p],
 }
+
+MFGP_F64 = 0
+MFGP_F32 = 1
 
 _lib = None
 _lock = threading.Lock()

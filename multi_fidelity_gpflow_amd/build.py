@@ -8,7 +8,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 ROOT = os.path.dirname(HERE)
-SOURCES = ["mfgp_kernels.hip", "mfgp_flow.hip", "mfgp_capi.hip", "mfgp_svgp.hip", "mfgp_svgp_grad.hip"]
+SOURCES = ["mfgp_kernels.hip", "mfgp_flow.hip", "mfgp_capi.hip", "mfgp_svgp.hip", "mfgp_svgp_grad.hip", "mfgp_f32.hip"]
 OUT = os.path.join(HERE, "libmfgp.so")
 
 

@@ -22,6 +22,10 @@ struct mfgp_handle_s {
     int ncu;        // compute units of the device
     int flow_trace; // k_chol_flow writes its diagnostic timeline into the workspace
     long long flow_timeout;   // k_chol_flow hand-off wait bound (100 MHz ticks)
+    int f32_panel;  // fp32 path: 128-wide tile columns per outer panel (trailing-update K = 128 * f32_panel)
+    int f32_lookahead;          // fp32 sweep: factor the next panel beside the trailing update
+    hipStream_t side;           // its high-priority side stream + fork / join events (created with the handle)
+    hipEvent_t ev_fork, ev_join;
 };
 
 namespace mfgp {
@@ -410,6 +414,85 @@ int svgp_predict_impl(hipStream_t s, int nb, int n, int m, int l, int p, int d, 
                       const double* W, double jitter, void* ws, size_t ws_bytes, double* g_mu, double* g_var,
                       double* f_mu, double* f_var, int* info);
 
+// ---------------------------------------------------------------- fp32 path (mfgp_f32.hip)
+struct F32Layout {
+    F32Args a;
+    double* items;
+    int ntask, G;
+    size_t bytes;
+};
+
+// ns > 0: predict rows; want_grad: identity rows + alpha + gradient partials
+static F32Layout f32_layout(int n, int p, int d, int ns, int want_grad, int panel, void* ws) {
+    F32Layout L{};
+    F32Args& a = L.a;
+    const int TB = F32_TILE;
+    a.T = ceil_div(n, TB);
+    a.Tp = ceil_div(p, TB);
+    a.Ts = ns > 0 ? ceil_div(ns, TB) : 0;
+    a.Ti = want_grad ? a.T : 0;
+    a.W = panel;
+    a.ld = (long)a.T * TB;
+    a.n = n; a.p = p; a.ns = ns; a.D = d;
+    Carve c(ws);
+    a.M = c.take<float>((size_t)(a.T + a.Tp + a.Ts + a.Ti) * TB * a.ld);
+    a.Dd = c.take<float>((size_t)a.T * TB * TB);
+    a.ldiag = c.take<double>((size_t)a.T * TB);
+    a.ldal = (long)a.Tp * TB;
+    a.alpha = c.take<float>(want_grad ? (size_t)a.ld * a.ldal : 0);
+    a.nz = 256;
+    a.zpart = c.take<double>((size_t)a.nz);
+    L.ntask = a.T * (a.T + 1) / 2;
+    L.G = theta_size(d);
+    a.gpart = c.take<double>(want_grad ? (size_t)L.G * L.ntask : 0);
+    L.items = c.take<double>((size_t)L.G + 8);
+    a.cnt = c.take<int>(1);
+    L.bytes = c.off + 256;
+    return L;
+}
+
+static int f32_value_grad(mfgp_handle_t h, int n, int p, int d, const float* X, int ldx, const float* Y, int ldy,
+                          double* theta, int want_grad, void* ws, size_t ws_bytes, double* out, int* info,
+                          const FinArgs* adam, F32Marks* mk = nullptr) {
+    F32Layout L = f32_layout(n, p, d, 0, want_grad, h->f32_panel, ws);
+    if (ws_bytes < L.bytes) return MFGP_ERR_WORKSPACE;
+    hipStream_t s = h->stream;
+    F32Args& a = L.a;
+    a.info = info; a.X = X; a.ldx = ldx; a.Y = Y; a.ldy = ldy; a.theta = theta;
+    if (h->f32_lookahead) launch_f32_sweep(a, s, mk, h->side, h->ev_fork, h->ev_join);
+    else launch_f32_sweep(a, s, mk);
+    if (want_grad) launch_f32_grad(a, s, mk);
+    if (mk) mk->begin(s, F32_FIN);
+    launch_f32_zsum(a, s);
+    FinArgs f{};
+    if (adam) f = *adam;
+    f.zpart = a.zpart; f.nz = a.nz;
+    f.ldiag = a.ldiag; f.n = n;
+    f.gpart = a.gpart; f.ng = L.ntask; f.gstride = 0;
+    f.info = info; f.P = p; f.D = d; f.want_grad = want_grad;
+    f.out = out;
+    f.adam = adam != nullptr;
+    f.items = L.items;
+    f.G = L.G;
+    f.cnt = a.cnt;
+    hipLaunchKernelGGL(k_reduce_items, dim3(2 + (want_grad ? L.G : 0)), dim3(NTHREADS), 0, s, f);
+    if (mk) mk->end(s, 0.0);
+    return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;
+}
+
+static int f32_predict(mfgp_handle_t h, int n, int p, int d, int ns, const float* X, int ldx, const float* Y, int ldy,
+                       const float* Xs, int ldxs, const double* theta, void* ws, size_t ws_bytes, float* mean, int ldm,
+                       float* var, int* info) {
+    F32Layout L = f32_layout(n, p, d, ns, 0, h->f32_panel, ws);
+    if (ws_bytes < L.bytes) return MFGP_ERR_WORKSPACE;
+    F32Args& a = L.a;
+    a.info = info; a.X = X; a.ldx = ldx; a.Y = Y; a.ldy = ldy; a.Xs = Xs; a.ldxs = ldxs; a.theta = theta;
+    if (h->f32_lookahead) launch_f32_sweep(a, h->stream, nullptr, h->side, h->ev_fork, h->ev_join);
+    else launch_f32_sweep(a, h->stream);
+    launch_f32_predict(a, mean, ldm, var, h->stream);
+    return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;
+}
+
 }  // namespace mfgp
 
 using namespace mfgp;
@@ -447,6 +530,21 @@ int mfgp_create(int device, mfgp_handle_t* out) {
     h->ncu = ncu;
     h->flow_wgs = ncu;
     h->flow_timeout = FLOW_TIMEOUT_TICKS;
+    h->f32_panel = 4;
+    h->f32_lookahead = 1;
+    if (const char* la = getenv("MFGP_F32_LOOKAHEAD")) h->f32_lookahead = atoi(la) != 0;
+    {
+        int lo = 0, hi = 0;
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        (void)hipSetDevice(device);
+        if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
+        if (hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, hi) != hipSuccess) h->side = nullptr;
+        if (hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) != hipSuccess) h->ev_fork = nullptr;
+        if (hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess) h->ev_join = nullptr;
+        if (cur >= 0) (void)hipSetDevice(cur);
+    }
+    if (const char* fp = getenv("MFGP_F32_PANEL")) h->f32_panel = std::max(1, atoi(fp));
     if (const char* fl = getenv("MFGP_FLOW")) if (atoi(fl) == 0) h->flow_wgs = 0;
     if (const char* gc = getenv("MFGP_GRAD_CHUNK")) h->grad_chunk = std::max(1, atoi(gc));
     const char* env = getenv("MFGP_TILE");
@@ -456,6 +554,11 @@ int mfgp_create(int device, mfgp_handle_t* out) {
 }
 
 int mfgp_destroy(mfgp_handle_t h) {
+    if (h) {
+        if (h->side) (void)hipStreamDestroy(h->side);
+        if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+        if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+    }
     free(h);
     return MFGP_OK;
 }
@@ -814,6 +917,141 @@ int mfgp_selftest_mfma(mfgp_handle_t h, double* out) {
     if (!out) return MFGP_ERR_ARG;
     hipLaunchKernelGGL(k_selftest_mfma, dim3(1), dim3(64), 0, h->stream, out);
     return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;
+}
+
+// ---------------------------------------------------------------- dtype-generic forms
+#define CHECK_DT(dt) \
+    if ((dt) != MFGP_F64 && (dt) != MFGP_F32) return MFGP_ERR_ARG
+
+int mfgp_set_f32_panel(mfgp_handle_t h, int tiles) {
+    CHECK_H(h);
+    if (tiles < 1 || tiles > 64) return MFGP_ERR_ARG;
+    h->f32_panel = tiles;
+    return MFGP_OK;
+}
+
+int mfgp_set_f32_lookahead(mfgp_handle_t h, int enable) {
+    CHECK_H(h);
+    h->f32_lookahead = enable != 0;
+    return MFGP_OK;
+}
+
+int mfgp_mf_gram_ex(mfgp_handle_t h, int dtype, int n1, int n2, int d, const void* X1, int ldx1, const void* X2,
+                    int ldx2, const double* theta, double diag_add, void* K, int ldk) {
+    CHECK_H(h);
+    CHECK_D(d);
+    CHECK_DT(dtype);
+    if (dtype == MFGP_F64)
+        return mfgp_mf_gram(h, n1, n2, d, (const double*)X1, ldx1, (const double*)X2, ldx2, theta, diag_add,
+                            (double*)K, ldk);
+    if (n1 < 1 || n2 < 1 || !X1 || !X2 || !theta || !K || ldx1 < d + 1 || ldx2 < d + 1 || ldk < n2)
+        return MFGP_ERR_ARG;
+    launch_f32_gram_dense((const float*)X1, ldx1, n1, (const float*)X2, ldx2, n2, d, theta, (float)diag_add,
+                          (float*)K, ldk, h->stream);
+    return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;
+}
+
+int mfgp_gpr_workspace_size_ex(mfgp_handle_t h, int dtype, int n, int p, int d, size_t* bytes) {
+    CHECK_H(h);
+    CHECK_D(d);
+    CHECK_DT(dtype);
+    if (dtype == MFGP_F64) return mfgp_gpr_workspace_size(h, n, p, d, bytes);
+    if (n < 1 || p < 1 || !bytes) return MFGP_ERR_ARG;
+    *bytes = f32_layout(n, p, d, 0, 1, h->f32_panel, nullptr).bytes;
+    return MFGP_OK;
+}
+
+int mfgp_gpr_lml_ex(mfgp_handle_t h, int dtype, int n, int p, int d, const void* X, int ldx, const void* Y, int ldy,
+                    const double* theta, int want_grad, void* ws, size_t ws_bytes, double* out, int* info) {
+    CHECK_H(h);
+    CHECK_D(d);
+    CHECK_DT(dtype);
+    if (dtype == MFGP_F64)
+        return mfgp_gpr_lml(h, n, p, d, (const double*)X, ldx, (const double*)Y, ldy, theta, want_grad, ws, ws_bytes,
+                            out, info);
+    if (n < 1 || p < 1 || !X || !Y || !theta || !ws || !out || !info || ldx < d + 1 || ldy < p) return MFGP_ERR_ARG;
+    return f32_value_grad(h, n, p, d, (const float*)X, ldx, (const float*)Y, ldy, (double*)theta, want_grad, ws,
+                          ws_bytes, out, info, nullptr);
+}
+
+int mfgp_gpr_adam_step_ex(mfgp_handle_t h, int dtype, int n, int p, int d, const void* X, int ldx, const void* Y,
+                          int ldy, double* theta, double* u, double* m, double* v, const unsigned char* trainable,
+                          const int* tie, int* step, double lr, double beta1, double beta2, double eps,
+                          double* loss_hist, void* ws, size_t ws_bytes, double* out, int* info) {
+    CHECK_H(h);
+    CHECK_D(d);
+    CHECK_DT(dtype);
+    if (dtype == MFGP_F64)
+        return mfgp_gpr_adam_step(h, n, p, d, (const double*)X, ldx, (const double*)Y, ldy, theta, u, m, v, trainable,
+                                  tie, step, lr, beta1, beta2, eps, loss_hist, ws, ws_bytes, out, info);
+    if (n < 1 || p < 1 || !X || !Y || !theta || !u || !m || !v || !trainable || !step || !loss_hist || !ws ||
+        !out || !info || ldx < d + 1 || ldy < p)
+        return MFGP_ERR_ARG;
+    FinArgs f{};
+    f.theta = theta; f.u = u; f.m = m; f.v = v; f.trainable = trainable; f.tie = tie; f.step = step;
+    f.lr = lr; f.b1 = beta1; f.b2 = beta2; f.eps = eps; f.loss_hist = loss_hist;
+    f.noise_index = theta_size(d) - 1;
+    return f32_value_grad(h, n, p, d, (const float*)X, ldx, (const float*)Y, ldy, theta, 1, ws, ws_bytes, out, info,
+                          &f);
+}
+
+int mfgp_gpr_phase_times_ex(mfgp_handle_t h, int dtype, int n, int p, int d, const void* X, int ldx, const void* Y,
+                            int ldy, const double* theta, void* ws, size_t ws_bytes, double* out, int* info,
+                            float* ms, double* flops, int* launches, int nphase) {
+    CHECK_H(h);
+    CHECK_D(d);
+    CHECK_DT(dtype);
+    if (!ms || nphase < 1) return MFGP_ERR_ARG;
+    if (dtype == MFGP_F64) {
+        float m5[5] = {};
+        const int rc = mfgp_gpr_lml_phase_times(h, n, p, d, (const double*)X, ldx, (const double*)Y, ldy, theta, ws,
+                                                ws_bytes, out, info, m5);
+        for (int i = 0; i < nphase; ++i) {
+            ms[i] = i < 5 ? m5[i] : 0.0f;
+            if (flops) flops[i] = 0.0;
+            if (launches) launches[i] = 0;
+        }
+        return rc;
+    }
+    if (n < 1 || p < 1 || !X || !Y || !theta || !ws || !out || !info) return MFGP_ERR_ARG;
+    F32Marks* mk = new F32Marks();
+    const int rc = f32_value_grad(h, n, p, d, (const float*)X, ldx, (const float*)Y, ldy, (double*)theta, 1, ws,
+                                  ws_bytes, out, info, nullptr, mk);
+    float all[F32_NPHASE];
+    mk->collect(all);
+    for (int i = 0; i < nphase; ++i) {
+        ms[i] = i < F32_NPHASE ? all[i] : 0.0f;
+        if (flops) flops[i] = i < F32_NPHASE ? mk->flops[i] : 0.0;
+        if (launches) launches[i] = i < F32_NPHASE ? mk->launches[i] : 0;
+    }
+    delete mk;
+    return rc;
+}
+
+int mfgp_gpr_predict_workspace_size_ex(mfgp_handle_t h, int dtype, int n, int p, int d, int nstar, size_t* bytes) {
+    CHECK_H(h);
+    CHECK_D(d);
+    CHECK_DT(dtype);
+    if (dtype == MFGP_F64) return mfgp_gpr_predict_workspace_size(h, n, p, d, nstar, bytes);
+    if (n < 1 || p < 1 || nstar < 0 || !bytes) return MFGP_ERR_ARG;
+    *bytes = f32_layout(n, p, d, nstar > 0 ? nstar : 1, 0, h->f32_panel, nullptr).bytes;
+    return MFGP_OK;
+}
+
+int mfgp_gpr_predict_ex(mfgp_handle_t h, int dtype, int n, int p, int d, int nstar, const void* X, int ldx,
+                        const void* Y, int ldy, const void* Xs, int ldxs, const double* theta, void* ws,
+                        size_t ws_bytes, void* mean, int ldm, void* var, int* info) {
+    CHECK_H(h);
+    CHECK_D(d);
+    CHECK_DT(dtype);
+    if (dtype == MFGP_F64)
+        return mfgp_gpr_predict(h, n, p, d, nstar, (const double*)X, ldx, (const double*)Y, ldy, (const double*)Xs,
+                                ldxs, theta, ws, ws_bytes, (double*)mean, ldm, (double*)var, info);
+    if (n < 1 || p < 1 || nstar < 0 || !X || !Y || !theta || !ws || !info) return MFGP_ERR_ARG;
+    if (nstar == 0) return MFGP_OK;
+    if (!Xs || !mean || !var || ldx < d + 1 || ldy < p || ldxs < d + 1 || ldm < p) return MFGP_ERR_ARG;
+    return f32_predict(h, n, p, d, nstar, (const float*)X, ldx, (const float*)Y, ldy, (const float*)Xs, ldxs, theta,
+                       ws, ws_bytes, (float*)mean, ldm, (float*)var, info);
 }
 
 }  // extern "C"

@@ -1,0 +1,872 @@
+// mfgp_f32.hip — the fp32 instance of the GPR hot path (BASELINE configs[4], "Synth":
+// N_L = 16384, N_H = 2048, D = 10, P = 512).  The reference forces fp64
+// (mfgpflow/linear.py:63-64); fp32 is this engine's added capability, with the same
+// semantics as the fp64 path (linear.py:55-136 kernel, GPflow GPR LML / gradient / predict).
+//
+// At N = 18432 the factorization is 2.1 TFLOP (N^3/3): MFMA-throughput-bound, not
+// chain-latency-bound like Goku's 1164.  Everything is therefore ONE tall matrix M (fp32,
+// row-major, ld = Npad, 128 x 128 tiles) factored by a right-looking blocked Cholesky whose
+// every stage is an NT GEMM (both operands read along the contraction index):
+//
+//   row tiles [0, T)                  A = K + s2 I   (lower tiles)          -> L
+//   row tiles [T, T+Tp)               Y^T                                  -> Z^T = (L^-1 Y)^T
+//   row tiles [T+Tp, T+Tp+Ts)         K(X*, X)  (predict only)             -> (L^-1 Kmn)^T
+//   row tiles [T+Tp+Ts, +Ti)          I         (gradient only)            -> L^-T
+//
+// Factoring the first N columns of [K; B] gives B L^-T in the bottom rows, so the solves and
+// the explicit inverse come out of the same sweep as the factor.  L^-T's rows are exactly the
+// operands K^-1 = L^-T L^-1 needs in NT form, and alpha = K^-1 Y = L^-T Z the same.
+//
+// Sweep: outer panels of W tiles (W*128 columns).  Inside a panel, per tile column k: factor
+// the 128 x 128 diagonal block in registers (k32_diag, also D_k = L_kk^-1), form the panel
+// L(r,k) = M(r,k) D_k^T for every live row tile (k32_panel), update the remaining panel columns
+// (k32_update, K = 128).  Then ONE trailing update of everything right of the panel with
+// K = W*128 (k32_update): the C tile read-modify-write is paid once per panel, not per column.
+//
+// GEMM core: 128 x 128 output per 256-thread workgroup, 4 waves of 64 x 64 (2 x 2 blocks of
+// v_mfma_f32_32x32x2_f32), BK = 32, LDS double buffer with register staging.  LDS rows are
+// [row][k] with a 36-float stride: each lane reads 4 consecutive k of its row with one
+// ds_read_b128 (the k order inside an MFMA sum is free as long as A and B agree), and the
+// 16-lane groups of ds_read_b128 land on distinct banks.
+#include "mfgp_device.h"
+#include "mfgp_internal.h"
+
+namespace mfgp {
+namespace f32 {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int TB = F32_TILE;          // 128
+constexpr int BK = 32;
+constexpr int LDL = BK + 4;           // LDS row stride (floats)
+constexpr int GT = 256;               // threads of the GEMM-shaped kernels
+constexpr int STAGE = 2 * TB * LDL;   // floats per LDS stage (A + B)
+constexpr size_t GEMM_SMEM = 2 * STAGE * sizeof(float);   // 73,728 B: two workgroups per CU
+
+// ---------------------------------------------------------------- GEMM core
+struct Acc {
+    f32x16 c[2][2];
+};
+
+__device__ __forceinline__ void acc_zero(Acc& a) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) a.c[m][n][r] = 0.0f;
+}
+
+// Output element (m, n, reg) of this lane: MFMA 32x32 C/D map (col = lane & 31,
+// row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)) inside the wave's 64 x 64 quarter.
+__device__ __forceinline__ int acc_row(int m, int reg) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    return (w >> 1) * 64 + m * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+}
+__device__ __forceinline__ int acc_col(int n) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    return (w & 1) * 64 + n * 32 + (lane & 31);
+}
+
+struct StageRegs {
+    f32x4 a[4], b[4];
+};
+
+// thread t moves rows t/8 + 32q, floats 4(t%8) .. +3 of the 128 x 32 A and B slabs
+__device__ __forceinline__ void stage_fetch(StageRegs& s, const float* __restrict__ A, long lda,
+                                            const float* __restrict__ B, long ldb, int k) {
+    const int r = threadIdx.x >> 3, c4 = (threadIdx.x & 7) * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        s.a[q] = *reinterpret_cast<const f32x4*>(A + (long)(r + 32 * q) * lda + k + c4);
+        s.b[q] = *reinterpret_cast<const f32x4*>(B + (long)(r + 32 * q) * ldb + k + c4);
+    }
+}
+__device__ __forceinline__ void stage_put(float* sm, const StageRegs& s) {
+    const int r = threadIdx.x >> 3, c4 = (threadIdx.x & 7) * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        *reinterpret_cast<f32x4*>(sm + (r + 32 * q) * LDL + c4) = s.a[q];
+        *reinterpret_cast<f32x4*>(sm + TB * LDL + (r + 32 * q) * LDL + c4) = s.b[q];
+    }
+}
+__device__ __forceinline__ void stage_mma(Acc& acc, const float* sm) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const float* sa = sm + ((w >> 1) * 64 + (lane & 31)) * LDL + 4 * (lane >> 5);
+    const float* sb = sm + TB * LDL + ((w & 1) * 64 + (lane & 31)) * LDL + 4 * (lane >> 5);
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 8) {
+        const f32x4 a0 = *reinterpret_cast<const f32x4*>(sa + kk);
+        const f32x4 a1 = *reinterpret_cast<const f32x4*>(sa + 32 * LDL + kk);
+        const f32x4 b0 = *reinterpret_cast<const f32x4*>(sb + kk);
+        const f32x4 b1 = *reinterpret_cast<const f32x4*>(sb + 32 * LDL + kk);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            acc.c[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b0[s], acc.c[0][0], 0, 0, 0);
+            acc.c[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b1[s], acc.c[0][1], 0, 0, 0);
+            acc.c[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b0[s], acc.c[1][0], 0, 0, 0);
+            acc.c[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b1[s], acc.c[1][1], 0, 0, 0);
+        }
+    }
+}
+
+// acc += A[0:128, 0:32 nk] * B[0:128, 0:32 nk]^T (row-major, 16-B aligned rows).  Ends with a
+// barrier, so two calls may follow each other on the same LDS.
+__device__ __forceinline__ void gemm_nt(Acc& acc, const float* __restrict__ A, long lda, const float* __restrict__ B,
+                                        long ldb, int nk, float* smem) {
+    StageRegs st;
+    stage_fetch(st, A, lda, B, ldb, 0);
+    stage_put(smem, st);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const bool more = kt + 1 < nk;
+        if (more) stage_fetch(st, A, lda, B, ldb, (kt + 1) * BK);
+        stage_mma(acc, smem + (kt & 1) * STAGE);
+        if (more) stage_put(smem + ((kt + 1) & 1) * STAGE, st);
+        __syncthreads();
+    }
+}
+
+__device__ __forceinline__ void acc_store(const Acc& a, float* __restrict__ C, long ld) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) C[(long)acc_row(m, r) * ld + acc_col(n)] = a.c[m][n][r];
+}
+// C -= acc, all C loads issued before the first store
+__device__ __forceinline__ void acc_sub_into(const Acc& a, float* __restrict__ C, long ld) {
+    float v[2][2][16];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[m][n][r] = C[(long)acc_row(m, r) * ld + acc_col(n)];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) C[(long)acc_row(m, r) * ld + acc_col(n)] = v[m][n][r] - a.c[m][n][r];
+}
+
+// ---------------------------------------------------------------- geometry
+__host__ __device__ inline int rows_B(const F32Args& a, int k1) {   // live bottom row tiles after k1 columns
+    return a.Tp + a.Ts + (k1 < a.Ti ? k1 : a.Ti);
+}
+__host__ __device__ inline long row_off(const F32Args& a, int rt) { return (long)rt * TB * a.ld; }
+__host__ __device__ inline int id0(const F32Args& a) { return a.T + a.Tp + a.Ts; }   // first identity row tile
+
+// identity-region tiles the gram launch initialises: row tile c, columns from the start of c's
+// panel (earlier columns are never read)
+__host__ __device__ inline long ident_tiles(const F32Args& a) {
+    long s = 0;
+    for (int c = 0; c < a.Ti; ++c) s += a.T - (c / a.W) * a.W;
+    return s;
+}
+
+// ---------------------------------------------------------------- MF kernel tile (fp32)
+// SquaredExponential in direct-difference form (the expanded
+// |a|^2 + |b|^2 - 2 a.b of GPflow cancels catastrophically in fp32; in fp64 the two agree to
+// ~1e-14, in fp32 the difference form keeps K's diagonal exact and PD-ness intact).
+// Rows are staged transposed, [d][row], scaled by 1/l: xs1L, xs1D (tile rows), xs2L, xs2D (tile
+// columns); flags f (0 LF, 1 HF, 2 any other value -> zero row, -1 beyond n).
+struct GramSmem {
+    float* x1L; float* x1D; float* x2L; float* x2D; float* f1; float* f2;
+};
+__device__ __forceinline__ GramSmem gram_smem(float* base, int D) {
+    GramSmem g;
+    g.x1L = base; g.x1D = g.x1L + D * TB; g.x2L = g.x1D + D * TB; g.x2D = g.x2L + D * TB;
+    g.f1 = g.x2D + D * TB; g.f2 = g.f1 + TB;
+    return g;
+}
+size_t gram_smem_bytes32(int D) { return sizeof(float) * (4 * (size_t)D * TB + 2 * TB); }
+
+__device__ __forceinline__ float fid_code(float f) { return f == 0.0f ? 0.0f : (f == 1.0f ? 1.0f : 2.0f); }
+
+__device__ void gram_stage(const GramSmem& g, const float* X1, long ldx1, int n1, int r1,
+                           const float* X2, long ldx2, int n2, int r2, int D, const double* theta) {
+    for (int e = threadIdx.x; e < TB * D; e += blockDim.x) {
+        const int r = e % TB, d = e / TB;   // consecutive threads: consecutive rows of one dim
+        const float il = (float)(1.0 / theta[1 + d]);
+        const float ild = (float)(1.0 / theta[2 + D + d]);
+        const float x1 = (r1 + r < n1) ? X1[(long)(r1 + r) * ldx1 + d] : 0.0f;
+        const float x2 = (r2 + r < n2) ? X2[(long)(r2 + r) * ldx2 + d] : 0.0f;
+        g.x1L[d * TB + r] = x1 * il; g.x1D[d * TB + r] = x1 * ild;
+        g.x2L[d * TB + r] = x2 * il; g.x2D[d * TB + r] = x2 * ild;
+    }
+    for (int r = threadIdx.x; r < TB; r += blockDim.x) {
+        g.f1[r] = (r1 + r < n1) ? fid_code(X1[(long)(r1 + r) * ldx1 + D]) : -1.0f;
+        g.f2[r] = (r2 + r < n2) ? fid_code(X2[(long)(r2 + r) * ldx2 + D]) : -1.0f;
+    }
+}
+
+// 128 x 128 tile of LinearMultiFidelityKernel.K (linear.py:55-104) from staged rows; thread t
+// owns rows (t >> 4) + 16 i and columns 4 (t & 15) + 64 jj + q (i < 8, jj < 2, q < 4).
+__device__ void gram_tile_vals(const GramSmem& g, int D, const double* theta, float v[8][8]) {
+    const int t = threadIdx.x;
+    const int rb = t >> 4, cb = (t & 15) * 4;
+    float s2[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s2[i][j] = 0.0f;
+    for (int d = 0; d < D; ++d) {
+        float a[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] = g.x1L[d * TB + rb + 16 * i];
+        const f32x4 b0 = *reinterpret_cast<const f32x4*>(g.x2L + d * TB + cb);
+        const f32x4 b1 = *reinterpret_cast<const f32x4*>(g.x2L + d * TB + cb + 64);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float u0 = a[i] - b0[q], u1 = a[i] - b1[q];
+                s2[i][q] = fmaf(u0, u0, s2[i][q]);
+                s2[i][4 + q] = fmaf(u1, u1, s2[i][4 + q]);
+            }
+    }
+    const float vL = (float)theta[0], vD = (float)theta[1 + D], rho = (float)theta[2 + 2 * D];
+    bool hh = false;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float f1 = g.f1[rb + 16 * i], f2 = g.f2[cb + (j & 3) + 64 * (j >> 2)];
+            const float kL = vL * __expf(-0.5f * s2[i][j]);
+            float val = 0.0f;
+            if (f1 == 0.0f && f2 == 0.0f) val = kL;
+            else if ((f1 == 0.0f && f2 == 1.0f) || (f1 == 1.0f && f2 == 0.0f)) val = kL * rho;
+            else if (f1 == 1.0f && f2 == 1.0f) { val = kL * (rho * rho); hh = true; }
+            v[i][j] = val;
+        }
+    if (__syncthreads_or(hh)) {   // HF x HF entries also get K_delta (linear.py:96); tile-uniform
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s2[i][j] = 0.0f;
+        for (int d = 0; d < D; ++d) {
+            float a[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) a[i] = g.x1D[d * TB + rb + 16 * i];
+            const f32x4 b0 = *reinterpret_cast<const f32x4*>(g.x2D + d * TB + cb);
+            const f32x4 b1 = *reinterpret_cast<const f32x4*>(g.x2D + d * TB + cb + 64);
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float u0 = a[i] - b0[q], u1 = a[i] - b1[q];
+                    s2[i][q] = fmaf(u0, u0, s2[i][q]);
+                    s2[i][4 + q] = fmaf(u1, u1, s2[i][4 + q]);
+                }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float f1 = g.f1[rb + 16 * i], f2 = g.f2[cb + (j & 3) + 64 * (j >> 2)];
+                if (f1 == 1.0f && f2 == 1.0f) v[i][j] += vD * __expf(-0.5f * s2[i][j]);
+            }
+    }
+}
+
+__device__ __forceinline__ void tri_decode32(long t, int& i, int& j) {
+    int r = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+    while ((long)(r + 1) * (r + 2) / 2 <= t) ++r;
+    while ((long)r * (r + 1) / 2 > t) --r;
+    i = r;
+    j = (int)(t - (long)r * (r + 1) / 2);
+}
+
+// ---------------------------------------------------------------- K1: gram + RHS rows + identity
+// blockIdx ranges: [A lower tiles][Y^T tiles Tp x T][K(X*,X) tiles Ts x T][identity fill]
+__global__ __launch_bounds__(GT) void k32_gram(F32Args a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    long b = blockIdx.x;
+    const long nA = (long)a.T * (a.T + 1) / 2, nY = (long)a.Tp * a.T, nS = (long)a.Ts * a.T;
+    if (b == 0) {
+        if (threadIdx.x == 0) *a.info = 0;
+        if (a.cnt && threadIdx.x == 0) *a.cnt = 0;
+    }
+    const int t = threadIdx.x;
+    if (b < nA || (b >= nA + nY && b < nA + nY + nS)) {
+        // kernel tile: A (ti, tj) of K(X, X) + s2 I, or (st, tj) of K(X*, X)
+        int ti, tj;
+        const bool isA = b < nA;
+        const float* X1;
+        long ldx1;
+        int n1, rt;
+        if (isA) {
+            tri_decode32(b, ti, tj);
+            X1 = a.X; ldx1 = a.ldx; n1 = a.n; rt = ti;
+        } else {
+            const long s = b - nA - nY;
+            ti = (int)(s / a.T); tj = (int)(s % a.T);
+            X1 = a.Xs; ldx1 = a.ldxs; n1 = a.ns; rt = a.T + a.Tp + ti;
+        }
+        const GramSmem g = gram_smem(smem, a.D);
+        gram_stage(g, X1, ldx1, n1, ti * TB, a.X, a.ldx, a.n, tj * TB, a.D, a.theta);
+        __syncthreads();
+        float v[8][8];
+        gram_tile_vals(g, a.D, a.theta, v);
+        const float noise = (float)a.theta[2 * a.D + 3];
+        const int rb = t >> 4, cb = (t & 15) * 4;
+        float* out = a.M + row_off(a, rt) + (long)tj * TB;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int r = rb + 16 * i;
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj) {
+                f32x4 w;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int c = cb + 64 * jj + q;
+                    float x = v[i][4 * jj + q];
+                    if (isA && ti == tj && r == c) x = (ti * TB + r < a.n) ? x + noise : 1.0f;   // identity padding
+                    w[q] = x;
+                }
+                *reinterpret_cast<f32x4*>(out + (long)r * a.ld + cb + 64 * jj) = w;
+            }
+        }
+        return;
+    }
+    if (b < nA + nY) {   // Y^T tile (pt, it): M[T + pt][it] = Y[it rows][pt cols]^T
+        const long s = b - nA;
+        const int pt = (int)(s / a.T), it = (int)(s % a.T);
+        float* tile = smem;   // [i][p], stride TB + 1
+        for (int e = t; e < TB * TB; e += GT) {
+            const int i = e / TB, p = e % TB;
+            const int gi = it * TB + i, gp = pt * TB + p;
+            tile[i * (TB + 1) + p] = (gi < a.n && gp < a.p) ? a.Y[(long)gi * a.ldy + gp] : 0.0f;
+        }
+        __syncthreads();
+        float* out = a.M + row_off(a, a.T + pt) + (long)it * TB;
+        for (int e = t; e < TB * TB; e += GT) {
+            const int p = e / TB, i = e % TB;
+            out[(long)p * a.ld + i] = tile[i * (TB + 1) + p];
+        }
+        return;
+    }
+    // identity fill: row tile c, column tiles from the start of c's panel
+    long s = b - nA - nY - nS;
+    int c = 0;
+    for (; c < a.Ti; ++c) {
+        const long cnt = a.T - (c / a.W) * a.W;
+        if (s < cnt) break;
+        s -= cnt;
+    }
+    if (c >= a.Ti) return;
+    const int j = (c / a.W) * a.W + (int)s;
+    float* out = a.M + row_off(a, id0(a) + c) + (long)j * TB;
+    for (int e = t; e < TB * TB / 4; e += GT) {
+        const int r = e / (TB / 4), c4 = (e % (TB / 4)) * 4;
+        f32x4 w = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (j == c && r >= c4 && r < c4 + 4) w[r - c4] = 1.0f;
+        *reinterpret_cast<f32x4*>(out + (long)r * a.ld + c4) = w;
+    }
+}
+
+// ---------------------------------------------------------------- K2a: diagonal block factor
+// L_kk = chol(M(k,k)) and D_k = L_kk^-1 of one 128 x 128 block in ONE workgroup of 16 waves:
+// wave w holds rows 8w .. 8w+7 of the running A and of the running inverse Y (= I at the
+// start), lane l columns l and l + 64 (16 + 16 floats in registers).  Both stay UNSCALED:
+// pivot j reads column j of A (its pivot d_j = A(j,j)) and row j of Y from LDS and applies
+//   A(r,c) -= A(r,j) A(c,j) / d_j   (c > j)        Y(r,c) -= A(r,j) Y(j,c) / d_j   (c <= j < r)
+// as two FMAs per element (masked operands, no branches), then the owners publish column /
+// row j+1 (double buffered): ONE barrier per pivot.  The scaling is applied once at the end:
+// L(r,c) = A(r,c) / sqrt(d_c), D(r,c) = Y(r,c) / sqrt(d_r).  A wave whose rows are all <= j has
+// nothing left to update and only takes the barrier.
+constexpr int DIAG_THREADS = 1024;
+
+__global__ __launch_bounds__(DIAG_THREADS) void k32_diag(F32Args a, int k) {
+    __shared__ float col[2][TB];   // A(., j), unscaled
+    __shared__ float row[2][TB];   // Y(j, .), unscaled
+    __shared__ float piv[TB];      // d_j (bad pivots replaced by 1)
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int r0 = 8 * w;
+    float* Mkk = a.M + row_off(a, k) + (long)k * TB;
+    float A[8][2], Y[8][2];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int r = r0 + q, c = l + 64 * h;
+            A[q][h] = Mkk[(long)r * a.ld + c];   // upper entries are read too (never used)
+            Y[q][h] = (r == c) ? 1.0f : 0.0f;
+        }
+    if (l == 0) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) col[0][r0 + q] = A[q][0];
+    }
+    if (w == 0) { row[0][l] = Y[0][0]; row[0][l + 64] = Y[0][1]; }
+    __syncthreads();
+    int bad = 0;
+    for (int j = 0; j < TB; ++j) {
+        const int b = j & 1;
+        const float d = col[b][j];
+        const bool ok = d > 0.0f;   // false for NaN too
+        if (!ok && bad == 0) bad = j + 1;
+        const float dd = ok ? d : 1.0f;
+        if (threadIdx.x == 0) piv[j] = dd;
+        if (r0 + 7 > j) {   // wave-uniform: some row of this wave is below the pivot
+            const float invd = 1.0f / dd;
+            float cr[8], cy[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                cr[q] = col[b][r0 + q] * invd;
+                cy[q] = (r0 + q > j) ? cr[q] : 0.0f;
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int c = l + 64 * h;
+                const float xa = (c > j) ? col[b][c] : 0.0f;    // A(c, j)
+                const float xy = (c <= j) ? row[b][c] : 0.0f;   // Y(j, c)
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    A[q][h] = fmaf(-cr[q], xa, A[q][h]);
+                    Y[q][h] = fmaf(-cy[q], xy, Y[q][h]);
+                }
+            }
+        }
+        if (j + 1 < TB) {   // publish column j+1 of A and row j+1 of Y
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                if (l + 64 * h == j + 1) {
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) col[b ^ 1][r0 + q] = A[q][h];
+                }
+            }
+            if ((j + 1) >> 3 == w) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    if (r0 + q == j + 1) { row[b ^ 1][l] = Y[q][0]; row[b ^ 1][l + 64] = Y[q][1]; }
+            }
+        }
+        __syncthreads();
+    }
+    float* Dk = a.Dd + (long)k * TB * TB;
+    float rs[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) rs[q] = rsqrtf(piv[r0 + q]);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int c = l + 64 * h;
+        const float sc = sqrtf(piv[c]), rc = 1.0f / sc;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int r = r0 + q;
+            if (c < r) Mkk[(long)r * a.ld + c] = A[q][h] * rc;
+            else if (c == r) { Mkk[(long)r * a.ld + c] = sc; a.ldiag[k * TB + r] = (double)sc; }
+            Dk[r * TB + c] = (c <= r) ? Y[q][h] * rs[q] : 0.0f;   // upper part zero: full-tile operand
+        }
+    }
+    if (threadIdx.x == 0 && bad && k * TB + bad - 1 < a.n && *a.info == 0) *a.info = k * TB + bad;
+}
+
+// ---------------------------------------------------------------- K2b: panel  M(r,k) <- M(r,k) D_k^T
+// row tiles: A rows k+1 .. T-1, then the live bottom rows (Y^T, K(X*,X), identity rows <= k)
+__global__ __launch_bounds__(GT, 2) void k32_panel(F32Args a, int k) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int b = blockIdx.x;
+    const int nA = a.T - k - 1;
+    const int rt = (b < nA) ? k + 1 + b : a.T + (b - nA);
+    float* Mr = a.M + row_off(a, rt) + (long)k * TB;
+    Acc acc;
+    acc_zero(acc);
+    gemm_nt(acc, Mr, a.ld, a.Dd + (long)k * TB * TB, TB, TB / BK, smem);
+    acc_store(acc, Mr, a.ld);
+}
+
+// ---------------------------------------------------------------- K2c: update
+// M(r, j) -= sum_{k in [k0,k1)} L(r,k) L(j,k)^T for columns j in [jb, je): A rows r >= j, then
+// every live bottom row.  Inside a panel (k1 = k0 + 1) and the trailing update (K = W*128).
+__host__ __device__ inline long update_tiles(const F32Args& a, int k1, int jb, int je) {
+    long s = 0;
+    for (int j = jb; j < je; ++j) s += a.T - j;
+    return s + (long)rows_B(a, k1) * (je - jb);
+}
+
+__global__ __launch_bounds__(GT, 2) void k32_update(F32Args a, int k0, int k1, int jb, int je) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    long b = blockIdx.x;
+    int rt = -1, jt = jb;
+    for (int j = jb; j < je; ++j) {
+        const int cnt = a.T - j;
+        if (b < cnt) { rt = j + (int)b; jt = j; break; }
+        b -= cnt;
+    }
+    if (rt < 0) {
+        const int nB = rows_B(a, k1);
+        rt = a.T + (int)(b % nB);
+        jt = jb + (int)(b / nB);
+    }
+    const long koff = (long)k0 * TB;
+    Acc acc;
+    acc_zero(acc);
+    gemm_nt(acc, a.M + row_off(a, rt) + koff, a.ld, a.M + row_off(a, jt) + koff, a.ld, (k1 - k0) * (TB / BK), smem);
+    acc_sub_into(acc, a.M + row_off(a, rt) + (long)jt * TB, a.ld);
+}
+
+// ---------------------------------------------------------------- K3: alpha = K^-1 Y = L^-T Z
+// alpha[a][p] = sum_{i >= a} L^-T[a][i] Z^T[p][i]   (tile (at, pt), contraction from tile at)
+__global__ __launch_bounds__(GT, 2) void k32_alpha(F32Args a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int at = blockIdx.x / a.Tp, pt = blockIdx.x % a.Tp;
+    const long koff = (long)at * TB;
+    Acc acc;
+    acc_zero(acc);
+    gemm_nt(acc, a.M + row_off(a, id0(a) + at) + koff, a.ld, a.M + row_off(a, a.T + pt) + koff, a.ld,
+            (a.T - at) * (TB / BK), smem);
+    acc_store(acc, a.alpha + (long)at * TB * a.ldal + (long)pt * TB, a.ldal);
+}
+
+// ---------------------------------------------------------------- K5: gradient
+// Lower tile (I, J): W = alpha_I alpha_J^T - P sum_{l >= I} L^-T(I,l) L^-T(J,l)^T, contracted
+// with dK/dtheta recomputed from X (the fp64 k_grad epilogue in fp32; per-tile sums in fp64).
+// gpart[q][task] = 1/2 sum W dK/dtheta_q over the tile (x2 for the mirrored upper tile).
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <int DT>   // compile-time bound on D (DT >= D): per-dimension sums stay in registers
+__global__ __launch_bounds__(GT, 2) void k32_grad(F32Args a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int task = blockIdx.x;
+    int I, J;
+    tri_decode32(task, I, J);
+    {
+        Acc acc;
+        acc_zero(acc);
+        const long koff = (long)I * TB;
+        gemm_nt(acc, a.M + row_off(a, id0(a) + I) + koff, a.ld, a.M + row_off(a, id0(a) + J) + koff, a.ld,
+                (a.T - I) * (TB / BK), smem);
+        const float negP = -(float)a.p;
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc.c[m][n][r] *= negP;
+        gemm_nt(acc, a.alpha + (long)I * TB * a.ldal, a.ldal, a.alpha + (long)J * TB * a.ldal, a.ldal,
+                a.Tp * (TB / BK), smem);
+        // W tile (x 1/2 on the diagonal tile; x 1 off it: the mirrored upper tile) into LDS
+        const float wscale = (I == J) ? 0.5f : 1.0f;
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) smem[acc_row(m, r) * (TB + 1) + acc_col(n)] = acc.c[m][n][r] * wscale;
+    }
+    // raw inputs of the two row tiles [d][row], flags, inverse squared lengthscales, reduction slots
+    const int D = a.D;
+    float* xi = smem + TB * (TB + 1);
+    float* xj = xi + D * TB;
+    float* fi = xj + D * TB;
+    float* fj = fi + TB;
+    float* il2 = fj + TB;   // [2][D]
+    double* red = reinterpret_cast<double*>(il2 + 2 * MAXD_HOST);   // [G][4]
+    for (int e = threadIdx.x; e < TB * D; e += GT) {
+        const int r = e % TB, d = e / TB;
+        const int gi = I * TB + r, gj = J * TB + r;
+        xi[d * TB + r] = gi < a.n ? a.X[(long)gi * a.ldx + d] : 0.0f;
+        xj[d * TB + r] = gj < a.n ? a.X[(long)gj * a.ldx + d] : 0.0f;
+    }
+    for (int r = threadIdx.x; r < TB; r += GT) {
+        const int gi = I * TB + r, gj = J * TB + r;
+        fi[r] = gi < a.n ? fid_code(a.X[(long)gi * a.ldx + D]) : -1.0f;
+        fj[r] = gj < a.n ? fid_code(a.X[(long)gj * a.ldx + D]) : -1.0f;
+    }
+    if (threadIdx.x < 2 * D) {
+        const int src = threadIdx.x / D, d = threadIdx.x % D;
+        const double l = a.theta[src == 0 ? 1 + d : 2 + D + d];
+        il2[threadIdx.x] = (float)(1.0 / (l * l));
+    }
+    __syncthreads();
+    const float vL = (float)a.theta[0], vD = (float)a.theta[1 + D], rho = (float)a.theta[2 + 2 * D];
+    // thread: column c = t & 127, rows (t >> 7) + 2 i (a wave shares its row: broadcast reads)
+    const int c = threadIdx.x & (TB - 1);
+    float xc[DT], il[DT], ild[DT], tl[DT], td[DT];
+#pragma unroll
+    for (int d = 0; d < DT; ++d) {
+        const bool on = d < D;
+        xc[d] = on ? xj[d * TB + c] : 0.0f;
+        il[d] = on ? il2[d] : 0.0f;
+        ild[d] = on ? il2[D + d] : 0.0f;
+        tl[d] = 0.0f;
+        td[d] = 0.0f;
+    }
+    const float f2 = fj[c];
+    const bool L2 = f2 == 0.0f, H2 = f2 == 1.0f;
+    const float sj = L2 ? 1.0f : (H2 ? rho : 0.0f), hj = H2 ? 1.0f : 0.0f;
+    float gvL = 0.0f, gvD = 0.0f, grho = 0.0f, gno = 0.0f;
+    for (int r = threadIdx.x >> 7; r < TB; r += 2) {
+        const float f1 = fi[r];
+        const bool L1 = f1 == 0.0f, H1 = f1 == 1.0f;
+        const float w = smem[r * (TB + 1) + c];
+        if (!((L1 || H1) && (L2 || H2))) continue;
+        float df2[DT];
+        float s2 = 0.0f, s2d = 0.0f;
+#pragma unroll
+        for (int d = 0; d < DT; ++d) {
+            const float df = (d < D ? xi[d * TB + r] : 0.0f) - xc[d];
+            df2[d] = df * df;
+            s2 = fmaf(df2[d], il[d], s2);
+            s2d = fmaf(df2[d], ild[d], s2d);
+        }
+        const float kL = vL * __expf(-0.5f * s2);
+        const float kD = (H1 && H2) ? vD * __expf(-0.5f * s2d) : 0.0f;
+        const float si = L1 ? 1.0f : rho, hi = H1 ? 1.0f : 0.0f;
+        const float cL = w * si * sj * kL, cD = w * hi * hj * kD;
+        gvL += cL;
+        gvD += cD;
+        grho += w * (hi * sj + si * hj) * kL;
+        if (I == J && r == c && I * TB + r < a.n) gno += w;
+#pragma unroll
+        for (int d = 0; d < DT; ++d) {
+            tl[d] = fmaf(cL, df2[d], tl[d]);
+            td[d] = fmaf(cD, df2[d], td[d]);
+        }
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int G = theta_size(D);
+    auto put = [&](int q, float v) {
+        const double s = wave_sum_d((double)v);
+        if (lane == 0) red[q * 4 + wv] = s;
+    };
+    put(0, gvL);
+    put(1 + D, gvD);
+    put(2 + 2 * D, grho);
+    put(3 + 2 * D, gno);
+#pragma unroll
+    for (int d = 0; d < DT; ++d) {
+        if (d < D) {
+            put(1 + d, tl[d]);
+            put(2 + D + d, td[d]);
+        }
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < G; q += GT) {
+        double v = (red[q * 4] + red[q * 4 + 1]) + (red[q * 4 + 2] + red[q * 4 + 3]);
+        if (q == 0) v /= a.theta[0];
+        else if (q <= D) { const double l = a.theta[q]; v /= l * l * l; }
+        else if (q == 1 + D) v /= a.theta[1 + D];
+        else if (q <= 1 + 2 * D) { const double l = a.theta[q]; v /= l * l * l; }
+        a.gpart[(long)q * gridDim.x + task] = v;
+    }
+}
+
+size_t grad_smem_bytes32(int D) {
+    const size_t epi = sizeof(float) * ((size_t)TB * (TB + 1) + 2 * (size_t)D * TB + 2 * TB + 2 * MAXD_HOST) +
+                       sizeof(double) * 4 * (size_t)theta_size(D);
+    return GEMM_SMEM > epi ? GEMM_SMEM : epi;
+}
+
+// ---------------------------------------------------------------- K4 input: sum Z^2 partials
+__global__ __launch_bounds__(GT) void k32_zsum(F32Args a) {
+    __shared__ double red[4];
+    const f32x4* Z = reinterpret_cast<const f32x4*>(a.M + row_off(a, a.T));
+    const long total = (long)a.Tp * TB * a.ld / 4;
+    double s = 0.0;
+    for (long e = blockIdx.x * (long)GT + threadIdx.x; e < total; e += (long)gridDim.x * GT) {
+        const f32x4 v = Z[e];
+        s += (double)(v[0] * v[0]) + (double)(v[1] * v[1]) + (double)(v[2] * v[2]) + (double)(v[3] * v[3]);
+    }
+    s = wave_sum_d(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) a.zpart[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// ---------------------------------------------------------------- K6: predict
+// mean[s][p] = sum_i (L^-1 Kmn)^T[s][i] Z^T[p][i]
+__global__ __launch_bounds__(GT, 2) void k32_pred_mean(F32Args a, float* mean, long ldm) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int st = blockIdx.x / a.Tp, pt = blockIdx.x % a.Tp;
+    Acc acc;
+    acc_zero(acc);
+    gemm_nt(acc, a.M + row_off(a, a.T + a.Tp + st), a.ld, a.M + row_off(a, a.T + pt), a.ld, a.T * (TB / BK), smem);
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int gs = st * TB + acc_row(m, r), gp = pt * TB + acc_col(n);
+                if (gs < a.ns && gp < a.p) mean[(long)gs * ldm + gp] = acc.c[m][n][r];
+            }
+}
+
+// var[s] = K_diag(x*_s) - sum_i A[i][s]^2 (linear.py:106-136 for K_diag); one wave per row
+__global__ __launch_bounds__(GT) void k32_pred_var(F32Args a, float* var) {
+    const int s = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (s >= a.ns) return;
+    const f32x4* row = reinterpret_cast<const f32x4*>(a.M + row_off(a, a.T + a.Tp) + (long)s * a.ld);
+    double acc = 0.0;
+    for (long e = lane; e < a.ld / 4; e += 64) {
+        const f32x4 v = row[e];
+        acc += (double)(v[0] * v[0] + v[1] * v[1]) + (double)(v[2] * v[2] + v[3] * v[3]);
+    }
+    acc = wave_sum_d(acc);
+    if (lane == 0) {
+        const float f = a.Xs[(long)s * a.ldxs + a.D];
+        const double vL = a.theta[0], vD = a.theta[1 + a.D], rho = a.theta[2 + 2 * a.D];
+        const double kd = f == 0.0f ? vL : (f == 1.0f ? rho * rho * vL + vD : 0.0);
+        var[s] = (float)(kd - acc);
+    }
+}
+
+// ---------------------------------------------------------------- dense gram (mfgp_mf_gram_ex f32)
+__global__ __launch_bounds__(GT) void k32_gram_dense(const float* X1, long ldx1, int n1, const float* X2, long ldx2,
+                                                     int n2, int D, const double* theta, float diag_add, float* K,
+                                                     long ldk, int tc) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int ti = blockIdx.x / tc, tj = blockIdx.x % tc;
+    const GramSmem g = gram_smem(smem, D);
+    gram_stage(g, X1, ldx1, n1, ti * TB, X2, ldx2, n2, tj * TB, D, theta);
+    __syncthreads();
+    float v[8][8];
+    gram_tile_vals(g, D, theta, v);
+    const int t = threadIdx.x, rb = t >> 4, cb = (t & 15) * 4;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int gi = ti * TB + rb + 16 * i, gj = tj * TB + cb + (j & 3) + 64 * (j >> 2);
+            if (gi < n1 && gj < n2) K[(long)gi * ldk + gj] = v[i][j] + (gi == gj ? diag_add : 0.0f);
+        }
+}
+
+}  // namespace f32
+
+// ---------------------------------------------------------------- host launchers
+using namespace f32;
+
+size_t f32_gemm_smem() { return GEMM_SMEM; }
+
+int f32_ident_fill_tiles(const F32Args& a) { return (int)ident_tiles(a); }
+
+// The whole sweep: gram (+ RHS rows, identity), then per panel of W tile columns: factor,
+// panel, in-panel updates; then the trailing update.  want_grad: alpha and gradient partials;
+// always: sum Z^2 partials (a.nz workgroups).
+static void f32_gram(const F32Args& a, hipStream_t s, F32Marks* mk) {
+    const long nA = (long)a.T * (a.T + 1) / 2;
+    const long ngram = nA + (long)a.Tp * a.T + (long)a.Ts * a.T + ident_tiles(a);
+    const size_t glds = gram_smem_bytes32(a.D) > (size_t)TB * (TB + 1) * 4 ? gram_smem_bytes32(a.D)
+                                                                           : (size_t)TB * (TB + 1) * 4;
+    if (mk) mk->begin(s, F32_GRAM);
+    hipLaunchKernelGGL(k32_gram, dim3((unsigned)ngram), dim3(GT), glds, s, a);
+    if (mk) mk->end(s, 0.0);
+}
+
+constexpr double TILE_FL = 2.0 * TB * TB;   // flops of one 128 x 128 output tile per unit of K
+
+// F(panel): per tile column k of [k0, k1): diagonal factor, panel, update of the panel's
+// remaining columns
+static void f32_panel_factor(const F32Args& a, int k0, int k1, hipStream_t s, F32Marks* mk) {
+    for (int k = k0; k < k1; ++k) {
+        if (mk) mk->begin(s, F32_DIAG);
+        hipLaunchKernelGGL(k32_diag, dim3(1), dim3(DIAG_THREADS), 0, s, a, k);
+        if (mk) mk->end(s, (double)TB * TB * TB * 2.0 / 3.0);
+        const int np = (a.T - k - 1) + rows_B(a, k + 1);
+        if (np > 0) {
+            if (mk) mk->begin(s, F32_PANEL);
+            hipLaunchKernelGGL(k32_panel, dim3(np), dim3(GT), GEMM_SMEM, s, a, k);
+            if (mk) mk->end(s, TILE_FL * TB * np);
+        }
+        if (k + 1 < k1) {
+            const long nt = update_tiles(a, k + 1, k + 1, k1);
+            if (mk) mk->begin(s, F32_UPD_IN);
+            hipLaunchKernelGGL(k32_update, dim3((unsigned)nt), dim3(GT), GEMM_SMEM, s, a, k, k + 1, k + 1, k1);
+            // useful work: every tile but the strictly upper half of the diagonal tiles
+            if (mk) mk->end(s, TILE_FL * TB * (nt - 0.5 * (k1 - k - 1) * (TB - 1) / TB));
+        }
+    }
+}
+
+// U(panel, [jb, je)): columns jb .. je-1 updated with the panel's K = (k1 - k0) * 128
+static void f32_trailing(const F32Args& a, int k0, int k1, int jb, int je, hipStream_t s, F32Marks* mk) {
+    if (jb >= je) return;
+    const long nt = update_tiles(a, k1, jb, je);
+    if (mk) mk->begin(s, F32_UPD_OUT);
+    hipLaunchKernelGGL(k32_update, dim3((unsigned)nt), dim3(GT), GEMM_SMEM, s, a, k0, k1, jb, je);
+    if (mk) mk->end(s, TILE_FL * TB * (k1 - k0) * (nt - 0.5 * (je - jb) * (TB - 1) / TB));
+}
+
+// The sweep.  With a side stream (and no timing marks): one-panel lookahead -- the next panel's
+// columns are updated first, then the rest of the trailing update (main stream) runs beside the
+// next panel's factorization (side stream, high priority), which is the critical path; both
+// read panel K's columns only and write disjoint column ranges.  Fork / join through events,
+// so the sequence stays hipGraph-capturable.
+void launch_f32_sweep(const F32Args& a, hipStream_t s, F32Marks* mk, hipStream_t side, hipEvent_t fork,
+                      hipEvent_t join) {
+    f32_gram(a, s, mk);
+    const bool ahead = side && fork && join && !mk;
+    const int W = a.W;
+    auto pend = [&](int k0) { return (k0 + W < a.T) ? k0 + W : a.T; };
+    f32_panel_factor(a, 0, pend(0), s, mk);
+    for (int k0 = 0; k0 < a.T; k0 += W) {
+        const int k1 = pend(k0);
+        if (k1 >= a.T) break;
+        const int k2 = pend(k1);
+        if (!ahead) {
+            f32_trailing(a, k0, k1, k1, a.T, s, mk);
+            f32_panel_factor(a, k1, k2, s, mk);
+            continue;
+        }
+        f32_trailing(a, k0, k1, k1, k2, s, mk);
+        if (k2 < a.T) {
+            (void)hipEventRecord(fork, s);
+            (void)hipStreamWaitEvent(side, fork, 0);
+            f32_trailing(a, k0, k1, k2, a.T, s, mk);
+            f32_panel_factor(a, k1, k2, side, mk);
+            (void)hipEventRecord(join, side);
+            (void)hipStreamWaitEvent(s, join, 0);
+        } else {
+            f32_panel_factor(a, k1, k2, s, mk);
+        }
+    }
+}
+
+void launch_f32_grad(const F32Args& a, hipStream_t s, F32Marks* mk) {
+    const double tile_fl = TILE_FL;
+    if (mk) mk->begin(s, F32_ALPHA);
+    hipLaunchKernelGGL(k32_alpha, dim3(a.T * a.Tp), dim3(GT), GEMM_SMEM, s, a);
+    if (mk) mk->end(s, tile_fl * TB * a.Tp * (double)a.T * (a.T + 1) / 2);
+    const dim3 g(a.T * (a.T + 1) / 2);
+    const size_t lds = grad_smem_bytes32(a.D);
+    if (mk) mk->begin(s, F32_GRAD);
+    if (a.D <= 4) hipLaunchKernelGGL(k32_grad<4>, g, dim3(GT), lds, s, a);
+    else if (a.D <= 8) hipLaunchKernelGGL(k32_grad<8>, g, dim3(GT), lds, s, a);
+    else if (a.D <= 12) hipLaunchKernelGGL(k32_grad<12>, g, dim3(GT), lds, s, a);
+    else if (a.D <= 16) hipLaunchKernelGGL(k32_grad<16>, g, dim3(GT), lds, s, a);
+    else hipLaunchKernelGGL(k32_grad<32>, g, dim3(GT), lds, s, a);
+    if (mk) {   // sum over lower tiles (I, J) of K = (T - I) tiles + Ppad
+        double kt = 0.0;
+        for (int I = 0; I < a.T; ++I) kt += (double)(I + 1) * ((a.T - I) * TB + a.Tp * TB);
+        mk->end(s, tile_fl * kt);
+    }
+}
+
+void launch_f32_zsum(const F32Args& a, hipStream_t s) {
+    hipLaunchKernelGGL(k32_zsum, dim3(a.nz), dim3(GT), 0, s, a);
+}
+
+void launch_f32_predict(const F32Args& a, float* mean, long ldm, float* var, hipStream_t s) {
+    hipLaunchKernelGGL(k32_pred_mean, dim3(a.Ts * a.Tp), dim3(GT), GEMM_SMEM, s, a, mean, ldm);
+    hipLaunchKernelGGL(k32_pred_var, dim3((a.ns + 3) / 4), dim3(GT), 0, s, a, var);
+}
+
+void launch_f32_gram_dense(const float* X1, long ldx1, int n1, const float* X2, long ldx2, int n2, int D,
+                           const double* theta, float diag_add, float* K, long ldk, hipStream_t s) {
+    const int tr = (n1 + TB - 1) / TB, tc = (n2 + TB - 1) / TB;
+    hipLaunchKernelGGL(k32_gram_dense, dim3(tr * tc), dim3(GT), gram_smem_bytes32(D), s, X1, ldx1, n1, X2, ldx2, n2,
+                       D, theta, diag_add, K, ldk, tc);
+}
+
+}  // namespace mfgp

@@ -143,6 +143,70 @@ void launch_bgemm(int nb, hipStream_t st, int ta, int tb, const BgemmArgs& a, in
 
 constexpr int MAXD_HOST = 32;
 
+// fp32 path (mfgp_f32.hip): one tall row-major matrix M, 128 x 128 tiles, ld = Npad; row tiles
+// [A = K + s2 I: T][Y^T: Tp][K(X*, X): Ts][I: Ti] (see the file header).
+constexpr int F32_TILE = 128;
+struct F32Args {
+    float* M; long ld;                    // tall matrix, ld = Npad
+    int T, Tp, Ts, Ti;                    // row-tile counts of the four regions
+    int W;                                // tile columns per outer panel
+    float* Dd;                            // T diagonal inverses D_k = L_kk^-1 (128 x 128, upper zero)
+    double* ldiag;                        // diag(L), Npad
+    int* info;                            // LAPACK-style, zeroed by k32_gram
+    const float* X; long ldx; int n;      // inputs [n, D+1]
+    const float* Y; long ldy; int p;      // targets [n, p]
+    const float* Xs; long ldxs; int ns;   // predict inputs [ns, D+1] (Ts > 0)
+    const double* theta; int D;           // constrained theta (fp64, include/mfgp.h layout)
+    float* alpha; long ldal;              // K^-1 Y, Npad x Ppad (gradient)
+    double* zpart; int nz;                // sum Z^2 partials (nz workgroups)
+    double* gpart;                        // [G][T(T+1)/2] gradient partials
+    int* cnt;                             // k_reduce_items arrival counter, zeroed by k32_gram
+};
+size_t f32_gemm_smem();
+// Diagnostic timing of the fp32 launches (never on the hot path): events around every launch,
+// summed per category after a sync; flops = the tile work each category performed.
+enum F32Phase { F32_GRAM = 0, F32_DIAG, F32_PANEL, F32_UPD_IN, F32_UPD_OUT, F32_ALPHA, F32_GRAD, F32_FIN, F32_NPHASE };
+struct F32Marks {
+    static constexpr int MAXEV = 4096;
+    hipEvent_t ev[MAXEV];
+    int cat[MAXEV / 2];
+    int n = 0;
+    double flops[F32_NPHASE] = {};
+    int launches[F32_NPHASE] = {};
+    void begin(hipStream_t s, int c) {
+        if (n + 2 > MAXEV) return;
+        (void)hipEventCreate(&ev[n]);
+        (void)hipEventCreate(&ev[n + 1]);
+        cat[n / 2] = c;
+        (void)hipEventRecord(ev[n], s);
+    }
+    void end(hipStream_t s, double fl) {
+        if (n + 2 > MAXEV) return;
+        (void)hipEventRecord(ev[n + 1], s);
+        flops[cat[n / 2]] += fl;
+        launches[cat[n / 2]] += 1;
+        n += 2;
+    }
+    void collect(float* ms) {   // synchronises; ms[F32_NPHASE]
+        for (int c = 0; c < F32_NPHASE; ++c) ms[c] = 0.0f;
+        if (n) (void)hipEventSynchronize(ev[n - 1]);
+        for (int i = 0; i < n; i += 2) {
+            float t = 0.0f;
+            (void)hipEventElapsedTime(&t, ev[i], ev[i + 1]);
+            ms[cat[i / 2]] += t;
+        }
+        for (int i = 0; i < n; ++i) (void)hipEventDestroy(ev[i]);
+        n = 0;
+    }
+};
+void launch_f32_sweep(const F32Args& a, hipStream_t s, F32Marks* mk = nullptr, hipStream_t side = nullptr,
+                      hipEvent_t fork = nullptr, hipEvent_t join = nullptr);
+void launch_f32_grad(const F32Args& a, hipStream_t s, F32Marks* mk = nullptr);
+void launch_f32_zsum(const F32Args& a, hipStream_t s);
+void launch_f32_predict(const F32Args& a, float* mean, long ldm, float* var, hipStream_t s);
+void launch_f32_gram_dense(const float* X1, long ldx1, int n1, const float* X2, long ldx2, int n2, int D,
+                           const double* theta, float diag_add, float* K, long ldk, hipStream_t s);
+
 size_t gram_smem_bytes(int nb);
 size_t chol_smem_bytes(int nb);
 size_t grad_smem_bytes(int nb, int G, int nil2);

@@ -25,13 +25,31 @@ def default_device() -> torch.device:
     return torch.device("cuda", torch.cuda.current_device())
 
 
-def to_dev(x, device: torch.device) -> torch.Tensor:
-    """float64, contiguous, on `device` (numpy / list / torch accepted)."""
+def to_dev(x, device: torch.device, dtype: torch.dtype = torch.float64) -> torch.Tensor:
+    """`dtype` (default float64), contiguous, on `device` (numpy / list / torch accepted)."""
     if isinstance(x, torch.Tensor):
         t = x.detach()
     else:
         t = torch.as_tensor(np.asarray(x, dtype=np.float64))
-    return t.to(device=device, dtype=torch.float64).contiguous()
+    return t.to(device=device, dtype=dtype).contiguous()
+
+
+def dtype_code(t: torch.Tensor) -> int:
+    """include/mfgp.h dtype of a data tensor: MFGP_F32 for float32, MFGP_F64 for float64."""
+    if t.dtype == torch.float32:
+        return _lib.MFGP_F32
+    if t.dtype == torch.float64:
+        return _lib.MFGP_F64
+    raise MFGPError(f"unsupported data dtype {t.dtype} (float64 or float32)")
+
+
+def resolve_dtype(dtype) -> torch.dtype:
+    """Model compute dtype: None / 'float64' / torch.float64 -> float64; 'float32' / torch.float32 -> float32."""
+    if dtype is None or dtype in ("float64", "f64", torch.float64, np.float64):
+        return torch.float64
+    if dtype in ("float32", "f32", torch.float32, np.float32):
+        return torch.float32
+    raise MFGPError(f"unsupported compute dtype {dtype!r} (float64 or float32)")
 
 
 class Engine:
@@ -101,11 +119,12 @@ class Engine:
         return K
 
     def mf_gram(self, X1: torch.Tensor, X2: torch.Tensor, theta: torch.Tensor, diag_add: float = 0.0) -> torch.Tensor:
+        """K(X1, X2) in X1's dtype (float64: mfgp_mf_gram; float32: mfgp_mf_gram_ex)."""
         n1, dp1 = X1.shape
         n2 = X2.shape[0]
-        K = torch.empty((n1, n2), dtype=torch.float64, device=self.device)
-        check(self.lib.mfgp_mf_gram(self.h, n1, n2, dp1 - 1, ptr(X1), dp1, ptr(X2), X2.shape[1], ptr(theta),
-                                    float(diag_add), ptr(K), n2), "mfgp_mf_gram")
+        K = torch.empty((n1, n2), dtype=X1.dtype, device=self.device)
+        check(self.lib.mfgp_mf_gram_ex(self.h, dtype_code(X1), n1, n2, dp1 - 1, ptr(X1), dp1, ptr(X2), X2.shape[1],
+                                       ptr(theta), float(diag_add), ptr(K), n2), "mfgp_mf_gram_ex")
         return K
 
     def mf_kdiag(self, X: torch.Tensor, theta: torch.Tensor) -> torch.Tensor:
@@ -114,8 +133,16 @@ class Engine:
         check(self.lib.mfgp_mf_kdiag(self.h, n, dp1 - 1, ptr(X), dp1, ptr(theta), ptr(out)), "mfgp_mf_kdiag")
         return out
 
-    def gpr_workspace_bytes(self, n: int, p: int, d: int) -> int:
-        return self._size(self.lib.mfgp_gpr_workspace_size, n, p, d)
+    def gpr_workspace_bytes(self, n: int, p: int, d: int, dtype: torch.dtype = torch.float64) -> int:
+        return self._size(self.lib.mfgp_gpr_workspace_size_ex, dtype_code(torch.empty(0, dtype=dtype)), n, p, d)
+
+    def set_f32_panel(self, tiles: int):
+        """fp32 path: 128-wide tile columns per outer Cholesky panel (trailing-update K = 128 * tiles)."""
+        check(self.lib.mfgp_set_f32_panel(self.h, int(tiles)), "mfgp_set_f32_panel")
+
+    def set_f32_lookahead(self, enable: bool):
+        """fp32 path: factor the next panel on a side stream beside the trailing update (default on)."""
+        check(self.lib.mfgp_set_f32_lookahead(self.h, 1 if enable else 0), "mfgp_set_f32_lookahead")
 
     def private_workspace(self, nbytes: int) -> torch.Tensor:
         """A workspace owned by its caller (a training session keeps it for the life of its
@@ -126,15 +153,17 @@ class Engine:
         n, dp1 = X.shape
         p = Y.shape[1]
         d = dp1 - 1
-        nbytes = self.gpr_workspace_bytes(n, p, d)
+        nbytes = self.gpr_workspace_bytes(n, p, d, X.dtype)
         if ws is None:
-            ws = self.workspace("gpr", nbytes)
+            ws = self.workspace("gpr" if X.dtype == torch.float64 else "gpr32", nbytes)
         elif ws.numel() < nbytes:
             raise MFGPError("gpr_lml: private workspace too small")
+        if Y.dtype != X.dtype:
+            raise MFGPError("gpr_lml: X and Y must share a dtype")
         out = torch.empty((1 + theta_size(d),), dtype=torch.float64, device=self.device)
         info = torch.empty((1,), dtype=torch.int32, device=self.device)
-        check(self.lib.mfgp_gpr_lml(self.h, n, p, d, ptr(X), dp1, ptr(Y), p, ptr(theta), int(want_grad), ptr(ws),
-                                    ws.numel(), ptr(out), ptr(info)), "mfgp_gpr_lml")
+        check(self.lib.mfgp_gpr_lml_ex(self.h, dtype_code(X), n, p, d, ptr(X), dp1, ptr(Y), p, ptr(theta),
+                                       int(want_grad), ptr(ws), ws.numel(), ptr(out), ptr(info)), "mfgp_gpr_lml_ex")
         return out, info
 
     def gpr_adam_step(self, X, Y, st: "AdamState", loss_hist: torch.Tensor, out: torch.Tensor, info: torch.Tensor,
@@ -142,15 +171,15 @@ class Engine:
         n, dp1 = X.shape
         p = Y.shape[1]
         d = dp1 - 1
-        nbytes = self.gpr_workspace_bytes(n, p, d)
+        nbytes = self.gpr_workspace_bytes(n, p, d, X.dtype)
         if ws is None:
-            ws = self.workspace("gpr", nbytes)
+            ws = self.workspace("gpr" if X.dtype == torch.float64 else "gpr32", nbytes)
         elif ws.numel() < nbytes:
             raise MFGPError("gpr_adam_step: private workspace too small")
-        check(self.lib.mfgp_gpr_adam_step(self.h, n, p, d, ptr(X), dp1, ptr(Y), p, ptr(st.theta), ptr(st.u),
-                                          ptr(st.m), ptr(st.v), ptr(st.trainable), ptr(st.tie), ptr(st.step), st.lr, st.b1,
-                                          st.b2, st.eps, ptr(loss_hist), ptr(ws), ws.numel(), ptr(out), ptr(info)),
-              "mfgp_gpr_adam_step")
+        check(self.lib.mfgp_gpr_adam_step_ex(self.h, dtype_code(X), n, p, d, ptr(X), dp1, ptr(Y), p, ptr(st.theta),
+                                             ptr(st.u), ptr(st.m), ptr(st.v), ptr(st.trainable), ptr(st.tie),
+                                             ptr(st.step), st.lr, st.b1, st.b2, st.eps, ptr(loss_hist), ptr(ws),
+                                             ws.numel(), ptr(out), ptr(info)), "mfgp_gpr_adam_step_ex")
 
     def theta_from_u(self, u: torch.Tensor, theta: torch.Tensor, noise_index: int):
         check(self.lib.mfgp_theta_from_u(self.h, ptr(u), ptr(theta), u.numel(), noise_index), "mfgp_theta_from_u")
@@ -160,14 +189,15 @@ class Engine:
         p = Y.shape[1]
         d = dp1 - 1
         ns = Xs.shape[0]
-        nbytes = self._size(self.lib.mfgp_gpr_predict_workspace_size, n, p, d, ns)
-        ws = self.workspace("pred", nbytes)
-        mean = torch.empty((ns, p), dtype=torch.float64, device=self.device)
-        var = torch.empty((ns,), dtype=torch.float64, device=self.device)
+        dt = dtype_code(X)
+        nbytes = self._size(self.lib.mfgp_gpr_predict_workspace_size_ex, dt, n, p, d, ns)
+        ws = self.workspace("pred" if X.dtype == torch.float64 else "pred32", nbytes)
+        mean = torch.empty((ns, p), dtype=X.dtype, device=self.device)
+        var = torch.empty((ns,), dtype=X.dtype, device=self.device)
         info = torch.empty((1,), dtype=torch.int32, device=self.device)
-        check(self.lib.mfgp_gpr_predict(self.h, n, p, d, ns, ptr(X), dp1, ptr(Y), p, ptr(Xs), Xs.shape[1],
-                                        ptr(theta), ptr(ws), ws.numel(), ptr(mean), p, ptr(var), ptr(info)),
-              "mfgp_gpr_predict")
+        check(self.lib.mfgp_gpr_predict_ex(self.h, dt, n, p, d, ns, ptr(X), dp1, ptr(Y), p, ptr(Xs), Xs.shape[1],
+                                           ptr(theta), ptr(ws), ws.numel(), ptr(mean), p, ptr(var), ptr(info)),
+              "mfgp_gpr_predict_ex")
         return mean, var, info
 
     def gpr_predict_cov(self, nlf, X, Y, Xs, theta):
@@ -340,6 +370,27 @@ class AdamState:
         self.tie = torch.tensor(tie.astype(np.int32), device=device)
         self.step = torch.zeros((1,), dtype=torch.int32, device=device)
         self.lr, self.b1, self.b2, self.eps = f32(lr), f32(b1), f32(b2), float(eps)
+
+
+F32_PHASES = ["gram", "diag", "panel", "update_in", "update_out", "alpha", "grad", "finalize"]
+
+
+def gpr_phase_times_ex(eng: Engine, X, Y, theta):
+    """One value+grad evaluation with hipEvents around every launch (diagnostic).  Returns
+    {phase: (ms, flops performed, launches)}: fp32 phases F32_PHASES; fp64 the five of gpr_phase_times."""
+    n, dp1 = X.shape
+    p = Y.shape[1]
+    d = dp1 - 1
+    nbytes = eng.gpr_workspace_bytes(n, p, d, X.dtype)
+    ws = eng.workspace("gpr" if X.dtype == torch.float64 else "gpr32", nbytes)
+    out = torch.empty((1 + theta_size(d),), dtype=torch.float64, device=eng.device)
+    info = torch.empty((1,), dtype=torch.int32, device=eng.device)
+    k = len(F32_PHASES)
+    ms, fl, la = (C.c_float * k)(), (C.c_double * k)(), (C.c_int * k)()
+    check(eng.lib.mfgp_gpr_phase_times_ex(eng.h, dtype_code(X), n, p, d, ptr(X), dp1, ptr(Y), p, ptr(theta), ptr(ws),
+                                          ws.numel(), ptr(out), ptr(info), ms, fl, la, k), "mfgp_gpr_phase_times_ex")
+    names = F32_PHASES if X.dtype == torch.float32 else ["pre", "gram", "chol_steps", "grad", "finalize"]
+    return {nm: (float(ms[i]), float(fl[i]), int(la[i])) for i, nm in enumerate(names)}
 
 
 def gpr_phase_times(eng: Engine, X, Y, theta):

@@ -14,7 +14,7 @@ import copy
 import numpy as np
 import torch
 
-from .engine import Engine, theta_size, to_dev
+from .engine import Engine, resolve_dtype, theta_size, to_dev
 from .params import Module, Parameter, as_result, positive, set_trainable
 
 
@@ -90,10 +90,13 @@ class LinearMultiFidelityKernel(Kernel):
     def theta(self, d: int, device, ith_output_dim: int = 0, noise: float = 0.0) -> torch.Tensor:
         return torch.tensor(self.theta_vector(d, ith_output_dim, noise), dtype=torch.float64, device=device)
 
-    def K(self, X, X2=None, ith_output_dim=0):
+    def K(self, X, X2=None, ith_output_dim=0, dtype=None):
+        """linear.py:55-104 (fp64, as the reference forces); dtype="float32" selects the fp32 path
+        (this engine's addition, include/mfgp.h mfgp_mf_gram_ex)."""
         eng = Engine.get()
-        X1 = to_dev(X, eng.device)
-        X2d = X1 if X2 is None else to_dev(X2, eng.device)
+        dt = resolve_dtype(dtype)
+        X1 = to_dev(X, eng.device, dt)
+        X2d = X1 if X2 is None else to_dev(X2, eng.device, dt)
         d = X1.shape[1] - 1
         return as_result(eng.mf_gram(X1, X2d, self.theta(d, eng.device, ith_output_dim)))
 

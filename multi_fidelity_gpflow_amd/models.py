@@ -23,7 +23,7 @@ import numpy as np
 import torch
 
 from ._lib import MFGP_FLOW_TIMEOUT, MFGPError, info_error
-from .engine import AdamState, Engine, theta_size, to_dev
+from .engine import AdamState, Engine, resolve_dtype, theta_size, to_dev
 from .kernels import LinearMultiFidelityKernel
 from .params import Module, Parameter, as_result, positive, set_trainable
 
@@ -92,9 +92,14 @@ class _ThetaMap:
 
 
 class MultiFidelityGPModel(Module):
-    """GPR with the linear multi-fidelity kernel and a shared Gram over P outputs."""
+    """GPR with the linear multi-fidelity kernel and a shared Gram over P outputs.
 
-    def __init__(self, X, Y, kernel_L, kernel_delta):
+    ``dtype`` (this engine's addition; the reference forces fp64, linear.py:63-64): ``None`` /
+    ``"float64"`` runs the fp64 path; ``"float32"`` keeps X, Y on the device in fp32 and runs
+    the fp32 path (include/mfgp.h ``*_ex`` with MFGP_F32: the BASELINE "Synth" config).  The
+    parameters, the LML, its gradient and the Adam state stay fp64 either way."""
+
+    def __init__(self, X, Y, kernel_L, kernel_delta, dtype=None):
         Xh = np.asarray(X.cpu().numpy() if isinstance(X, torch.Tensor) else X, dtype=np.float64)
         Yh = np.asarray(Y.cpu().numpy() if isinstance(Y, torch.Tensor) else Y, dtype=np.float64)
         if Yh.ndim == 1:
@@ -106,6 +111,7 @@ class MultiFidelityGPModel(Module):
         self.num_output_dims = num_output_dims
         self.mean_function = None
         self._Xh, self._Yh = Xh, Yh
+        self.dtype = resolve_dtype(dtype)
         self._dev = None
         self.loss_history = []
 
@@ -117,7 +123,7 @@ class MultiFidelityGPModel(Module):
     def _device_data(self):
         eng = Engine.get()
         if self._dev is None or self._dev[0].device != eng.device:
-            self._dev = (to_dev(self._Xh, eng.device), to_dev(self._Yh, eng.device))
+            self._dev = (to_dev(self._Xh, eng.device, self.dtype), to_dev(self._Yh, eng.device, self.dtype))
         return eng, self._dev[0], self._dev[1]
 
     @property
@@ -162,8 +168,10 @@ class MultiFidelityGPModel(Module):
         if full_output_cov:
             raise NotImplementedError("predict_f(full_output_cov=True): GPR has no output covariance to return")
         eng, X, Y = self._device_data()
-        Xs = to_dev(Xnew, eng.device)
+        Xs = to_dev(Xnew, eng.device, self.dtype)
         theta = torch.tensor(self._theta_map().theta(), dtype=torch.float64, device=eng.device)
+        if full_cov and self.dtype != torch.float64:
+            raise NotImplementedError("predict_f(full_cov=True) runs on the fp64 path only (dtype=None)")
         if full_cov:
             mean, _, cov, info = eng.gpr_predict_cov(0, X, Y, Xs, theta)
             self._raise_info(info, "predict_f")
@@ -286,7 +294,7 @@ class AdamSession:
             self.out = torch.empty((1 + theta_size(self.tm.d),), dtype=torch.float64, device=self.eng.device)
             self.info = torch.zeros((1,), dtype=torch.int32, device=self.eng.device)
             n, p, d = self.X.shape[0], self.Y.shape[1], self.tm.d
-            self.ws = self.eng.private_workspace(self.eng.gpr_workspace_bytes(n, p, d))
+            self.ws = self.eng.private_workspace(self.eng.gpr_workspace_bytes(n, p, d, self.X.dtype))
             self.eng.theta_from_u(self.st.u, self.st.theta, self.tm.noise_index)
             self.eng.gpr_lml(self.X, self.Y, self.st.theta, want_grad=False, ws=self.ws)   # builds schedule tables
         self.done = 0

@@ -1,0 +1,147 @@
+"""fp32 path (include/mfgp.h *_ex with MFGP_F32; csrc/mfgp_f32.hip) against the fp64 CPU oracle
+and against the HIP fp64 path, through the C-ABI.
+
+The reference forces fp64 (mfgpflow/linear.py:63-64); BASELINE configs[4] ("Synth", N_L = 16384,
+N_H = 2048, D = 10, P = 512) asks for fp32.  fp32 results differ from fp64 by the conditioning of
+K + s2 I (s2 = 1e-3), so the tolerances here are measured, with margin:
+
+  size                        LML (rel)   gradient (rel. to max |g|)  mean (rel. to max |mean|)  var (abs)
+  n <= 2300 vs oracle         1e-4        3e-4                        1e-2                       5e-5
+  Synth 18432 x 512 vs f64    4e-3        1.5e-2                      2e-2                       5e-4
+
+(measured round 2: <= 2.0e-5 / 5.3e-5 / 2.0e-3 / 4.7e-6 small, 8.4e-4 / 2.7e-3 at Synth).
+Properties that hold to rounding of the fp64 reductions at any size: additivity of the LML over
+output columns (one shared factorization), identical results with and without the lookahead
+schedule and for every panel width that tiles the same way."""
+import numpy as np
+import pytest
+import torch
+
+import multi_fidelity_gpflow_amd as M
+from multi_fidelity_gpflow_amd.data import synthetic_multifidelity
+from multi_fidelity_gpflow_amd.engine import Engine
+from multi_fidelity_gpflow_amd.models import CholeskyError
+from oracle import mfgp_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    e = Engine.get()
+    yield e
+    e.set_f32_panel(4)
+    e.set_f32_lookahead(True)
+
+
+def _model(X, Y, dtype="float32"):
+    d = X.shape[1] - 1
+    return M.MultiFidelityGPModel(X, Y, M.SquaredExponential(lengthscales=np.ones(d)),
+                                  M.SquaredExponential(lengthscales=np.ones(d)), dtype=dtype)
+
+
+def _gvec(go):
+    return np.concatenate([[go["vL"]], go["lL"], [go["vD"]], go["lD"], [go["rho0"]], [go["noise"]]])
+
+
+def test_f32_gram_matches_oracle(eng):
+    rng = np.random.default_rng(3)
+    X1 = np.hstack([rng.uniform(0, 1, (300, 10)), (rng.random((300, 1)) < 0.3).astype(float)])
+    X2 = np.hstack([rng.uniform(0, 1, (200, 10)), (rng.random((200, 1)) < 0.5).astype(float)])
+    X1[7, -1] = 0.5   # non-{0,1} fidelity: zero row (linear.py:67-70).  (0.9999999999999999, the KMeans
+    # centre of Appendix C-3, rounds to exactly 1.0f: in fp32 such a row is an HF row)
+    p = O.MFParams(1.3, 0.4 + rng.random(10), 0.6, 0.5 + rng.random(10), np.full((1, 1), 0.8), 1e-3)
+    theta = torch.tensor(np.concatenate([[p.vL], p.lL, [p.vD], p.lD, [0.8], [1e-3]]), dtype=torch.float64,
+                         device=eng.device)
+    K = eng.mf_gram(torch.tensor(X1, dtype=torch.float32, device=eng.device),
+                    torch.tensor(X2, dtype=torch.float32, device=eng.device), theta).cpu().numpy()
+    Ko = O.mf_K(X1.astype(np.float32).astype(np.float64), X2.astype(np.float32).astype(np.float64), p)
+    assert K.dtype == np.float32
+    assert np.max(np.abs(K - Ko)) < 2e-6
+    assert np.all(K[7] == 0.0)
+
+
+@pytest.mark.parametrize("n_lf,n_hf,p,panel", [(200, 50, 3, 1), (200, 50, 3, 4), (500, 100, 20, 2),
+                                               (2000, 300, 130, 4)])
+def test_f32_lml_grad_predict_vs_oracle(eng, n_lf, n_hf, p, panel):
+    eng.set_f32_panel(panel)
+    X, Y, Xt, _ = synthetic_multifidelity(n_lf, n_hf, 10, p, 64, seed=1)
+    m = _model(X, Y)
+    lml, g = m.log_marginal_likelihood_and_grad()
+    p0 = O.MFParams.initial(10, p)
+    lo, go = O.gpr_lml_and_grad(X, Y, p0)
+    gov = _gvec(go)
+    assert abs(lml - lo) / abs(lo) < 1e-4
+    assert np.max(np.abs(g - gov)) / np.max(np.abs(gov)) < 3e-4
+    mean, var = m.predict_f(Xt)
+    mo, vo = O.gpr_predict_f(X, Y, Xt, p0)
+    assert mean.dtype == torch.float32 and tuple(mean.shape) == (64, p) and tuple(var.shape) == (64, p)
+    assert np.max(np.abs(mean.numpy() - mo)) / np.max(np.abs(mo)) < 1e-2
+    assert np.max(np.abs(var.numpy() - vo)) < 5e-5
+
+
+def test_f32_schedules_agree_bitwise(eng):
+    """Lookahead (side stream) vs one stream: the same kernels on the same data, so the same bits."""
+    X, Y, _, _ = synthetic_multifidelity(900, 200, 10, 40, 8, seed=2)
+    m = _model(X, Y)
+    res = []
+    for la in (False, True):
+        eng.set_f32_lookahead(la)
+        res.append(m.log_marginal_likelihood_and_grad())
+    assert res[0][0] == res[1][0] and np.array_equal(res[0][1], res[1][1])
+
+
+def test_f32_adam_matches_oracle_trajectory(eng):
+    X, Y, _, _ = synthetic_multifidelity(300, 60, 10, 4, 8, seed=4)
+    m = _model(X, Y)
+    m.optimize(max_iters=30, learning_rate=0.1, verbose=False)
+    _, ho = O.adam_train(X, Y, O.MFParams.initial(10, 4), max_iters=30, learning_rate=0.1)
+    h = np.array(m.loss_history)
+    assert len(h) == 30
+    err = np.max(np.abs(h - ho) / np.abs(ho))
+    print(f"fp32 Adam trajectory max rel err vs oracle {err:.2e}")
+    assert err < 2e-3
+    assert h[-1] < 0.5 * h[0]
+
+
+def test_f32_non_pd_raises(eng):
+    X, Y, _, _ = synthetic_multifidelity(200, 40, 10, 2, 8, seed=5)
+    Xd = torch.tensor(X, dtype=torch.float32, device=eng.device)
+    Yd = torch.tensor(Y, dtype=torch.float32, device=eng.device)
+    theta = torch.tensor(np.concatenate([[1.0], np.ones(10), [1.0], np.ones(10), [1.0], [-5.0]]),
+                         dtype=torch.float64, device=eng.device)   # K - 5 I: not PD
+    out, info = eng.gpr_lml(Xd, Yd, theta, want_grad=True)
+    assert int(info.item()) >= 1
+    assert not np.isfinite(out[0].item())
+    with pytest.raises(CholeskyError):
+        M.MultiFidelityGPModel._raise_info(info, "log_marginal_likelihood")
+
+
+@pytest.fixture(scope="module")
+def synth():
+    return synthetic_multifidelity()
+
+
+def test_f32_synth_full_size_vs_f64_path(eng, synth):
+    """BASELINE configs[4] at full size (N = 18432, P = 512): fp32 against the HIP fp64 path (the
+    CPU oracle would take minutes), additivity over the bins, and predict_f on 2048 HF points."""
+    X, Y, Xt, _ = synth
+    eng.set_f32_panel(4)
+    m32 = _model(X, Y)
+    l32, g32 = m32.log_marginal_likelihood_and_grad()
+    m64 = _model(X, Y, None)
+    l64, g64 = m64.log_marginal_likelihood_and_grad()
+    print(f"Synth LML f32 {l32:.4f} f64 {l64:.4f} rel {abs(l32 - l64) / abs(l64):.2e}; "
+          f"grad maxrel {np.max(np.abs(g32 - g64)) / np.max(np.abs(g64)):.2e}")
+    assert abs(l32 - l64) / abs(l64) < 4e-3
+    assert np.max(np.abs(g32 - g64)) / np.max(np.abs(g64)) < 1.5e-2
+    la = _model(X, Y[:, :256]).log_marginal_likelihood()
+    lb = _model(X, Y[:, 256:]).log_marginal_likelihood()
+    assert abs(float(la) + float(lb) - l32) / abs(l32) < 1e-9
+    mu32, v32 = m32.predict_f(Xt)
+    mu64, v64 = m64.predict_f(Xt)
+    mu32, v32, mu64, v64 = mu32.numpy(), v32.numpy(), mu64.numpy(), v64.numpy()
+    print(f"Synth predict mean maxrel {np.max(np.abs(mu32 - mu64)) / np.max(np.abs(mu64)):.2e}, "
+          f"var maxabs {np.max(np.abs(v32 - v64)):.2e}")
+    assert np.max(np.abs(mu32 - mu64)) / np.max(np.abs(mu64)) < 2e-2
+    assert np.max(np.abs(v32 - v64)) < 5e-4
