@@ -236,6 +236,9 @@ int mfgp_set_f32_panel(mfgp_handle_t h, int tiles);
 /* fp32 path: 1 (default; env MFGP_F32_LOOKAHEAD) factors the next panel on a high-priority side
  * stream beside the trailing update (fork / join events, graph-capturable); 0: one stream. */
 int mfgp_set_f32_lookahead(mfgp_handle_t h, int enable);
+/* fp32 lookahead: CUs the trailing update leaves free for the side stream (default 32; env
+ * MFGP_F32_RESERVE; 0: uncapped grid).  Speed only: results do not depend on it. */
+int mfgp_set_f32_reserve(mfgp_handle_t h, int cus);
 /* LinearMultiFidelityKernel.K (linear.py:55-104), as mfgp_mf_gram. */
 int mfgp_mf_gram_ex(mfgp_handle_t h, int dtype, int n1, int n2, int d, const void* X1, int ldx1, const void* X2,
                     int ldx2, const double* theta, double diag_add, void* K, int ldk);

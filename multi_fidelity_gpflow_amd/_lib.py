@@ -66,6 +66,7 @@ SIGNATURES = {
     # dtype-generic forms (MFGP_F64 = 0, MFGP_F32 = 1)
     "mfgp_set_f32_panel": [_p, _i],
     "mfgp_set_f32_lookahead": [_p, _i],
+    "mfgp_set_f32_reserve": [_p, _i],
     "mfgp_mf_gram_ex": [_p, _i, _i, _i, _i, _p, _i, _p, _i, _p, _d, _p, _i],
     "mfgp_gpr_workspace_size_ex": [_p, _i, _i, _i, _i, C.POINTER(_sz)],
     "mfgp_gpr_lml_ex": [_p, _i, _i, _i, _i, _p, _i, _p, _i, _p, _i, _p, _sz, _p, _p],

@@ -24,6 +24,7 @@ struct mfgp_handle_s {
     long long flow_timeout;   // k_chol_flow hand-off wait bound (100 MHz ticks)
     int f32_panel;  // fp32 path: 128-wide tile columns per outer panel (trailing-update K = 128 * f32_panel)
     int f32_lookahead;          // fp32 sweep: factor the next panel beside the trailing update
+    int f32_reserve;            // CUs the capped trailing update leaves to the side stream
     hipStream_t side;           // its high-priority side stream + fork / join events (created with the handle)
     hipEvent_t ev_fork, ev_join;
 };
@@ -459,6 +460,7 @@ static int f32_value_grad(mfgp_handle_t h, int n, int p, int d, const float* X, 
     hipStream_t s = h->stream;
     F32Args& a = L.a;
     a.info = info; a.X = X; a.ldx = ldx; a.Y = Y; a.ldy = ldy; a.theta = theta;
+    a.upd_slots = (h->f32_reserve > 0 && h->ncu > h->f32_reserve) ? 2 * (h->ncu - h->f32_reserve) : 0;
     if (h->f32_lookahead) launch_f32_sweep(a, s, mk, h->side, h->ev_fork, h->ev_join);
     else launch_f32_sweep(a, s, mk);
     if (want_grad) launch_f32_grad(a, s, mk);
@@ -487,6 +489,7 @@ static int f32_predict(mfgp_handle_t h, int n, int p, int d, int ns, const float
     if (ws_bytes < L.bytes) return MFGP_ERR_WORKSPACE;
     F32Args& a = L.a;
     a.info = info; a.X = X; a.ldx = ldx; a.Y = Y; a.ldy = ldy; a.Xs = Xs; a.ldxs = ldxs; a.theta = theta;
+    a.upd_slots = (h->f32_reserve > 0 && h->ncu > h->f32_reserve) ? 2 * (h->ncu - h->f32_reserve) : 0;
     if (h->f32_lookahead) launch_f32_sweep(a, h->stream, nullptr, h->side, h->ev_fork, h->ev_join);
     else launch_f32_sweep(a, h->stream);
     launch_f32_predict(a, mean, ldm, var, h->stream);
@@ -532,6 +535,8 @@ int mfgp_create(int device, mfgp_handle_t* out) {
     h->flow_timeout = FLOW_TIMEOUT_TICKS;
     h->f32_panel = 4;
     h->f32_lookahead = 1;
+    h->f32_reserve = 32;
+    if (const char* rv = getenv("MFGP_F32_RESERVE")) h->f32_reserve = std::max(0, atoi(rv));
     if (const char* la = getenv("MFGP_F32_LOOKAHEAD")) h->f32_lookahead = atoi(la) != 0;
     {
         int lo = 0, hi = 0;
@@ -933,6 +938,13 @@ int mfgp_set_f32_panel(mfgp_handle_t h, int tiles) {
 int mfgp_set_f32_lookahead(mfgp_handle_t h, int enable) {
     CHECK_H(h);
     h->f32_lookahead = enable != 0;
+    return MFGP_OK;
+}
+
+int mfgp_set_f32_reserve(mfgp_handle_t h, int cus) {
+    CHECK_H(h);
+    if (cus < 0) return MFGP_ERR_ARG;
+    h->f32_reserve = cus;
     return MFGP_OK;
 }
 

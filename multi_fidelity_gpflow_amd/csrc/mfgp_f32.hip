@@ -370,100 +370,165 @@ __global__ __launch_bounds__(GT) void k32_gram(F32Args a) {
 }
 
 // ---------------------------------------------------------------- K2a: diagonal block factor
-// L_kk = chol(M(k,k)) and D_k = L_kk^-1 of one 128 x 128 block in ONE workgroup of 16 waves:
-// wave w holds rows 8w .. 8w+7 of the running A and of the running inverse Y (= I at the
-// start), lane l columns l and l + 64 (16 + 16 floats in registers).  Both stay UNSCALED:
-// pivot j reads column j of A (its pivot d_j = A(j,j)) and row j of Y from LDS and applies
-//   A(r,c) -= A(r,j) A(c,j) / d_j   (c > j)        Y(r,c) -= A(r,j) Y(j,c) / d_j   (c <= j < r)
-// as two FMAs per element (masked operands, no branches), then the owners publish column /
-// row j+1 (double buffered): ONE barrier per pivot.  The scaling is applied once at the end:
-// L(r,c) = A(r,c) / sqrt(d_c), D(r,c) = Y(r,c) / sqrt(d_r).  A wave whose rows are all <= j has
-// nothing left to update and only takes the barrier.
-constexpr int DIAG_THREADS = 1024;
+// L_kk = chol(M(k,k)) and D_k = L_kk^-1 of one 128 x 128 block: ONE workgroup of 4 waves, the
+// block and its inverse staged in LDS, blocked by 32:
+//   for s = 0..3:  wave 0 factors the 32 x 32 diagonal sub-block (factor32, below) -> L_ss, D_ss;
+//                  L_is = A_is D_ss^T (i > s) and A_ij -= L_is L_js^T (s < j <= i) on the MFMA
+//                  (v_mfma_f32_32x32x2_f32, one 32 x 32 x 32 product per wave at a time);
+//   then the inverse's off-diagonal blocks D_ij = -D_ii sum_{m=j}^{i-1} L_im D_mj, row by row.
+// factor32 keeps the whole 32 x 32 problem in ONE wave's registers: lanes 0-31 hold the columns
+// of the (symmetric, unscaled) Schur complement, lanes 32-63 the columns of the running inverse;
+// pivot j broadcasts column j with v_readlane (scalar registers), so no pivot needs a barrier or
+// an LDS round trip:  A(r,c) -= A(r,j) A(j,c) / d_j  (c > j),  Y(r,c) -= A(r,j) Y(j,c) / d_j
+// (c <= j), rows r > j; the scaling by sqrt(d) is applied once at the end.
+constexpr int DIAG_THREADS = 256;
+constexpr int DLD = TB + 4;   // LDS row stride of the staged block / inverse (floats)
+constexpr size_t DIAG_SMEM = sizeof(float) * (2 * (size_t)TB * DLD + 3 * 32 * 33 + TB) + 16;
+
+// acc += A[0:32, 0:32] B[0:32, 0:32]^T (row-major LDS tiles, ld multiple of 4)
+__device__ __forceinline__ void mma32_nt(f32x16& acc, const float* A, int lda, const float* B, int ldb) {
+    const int l = threadIdx.x & 63;
+    const float* pa = A + (l & 31) * lda + 4 * (l >> 5);
+    const float* pb = B + (l & 31) * ldb + 4 * (l >> 5);
+#pragma unroll
+    for (int kk = 0; kk < 32; kk += 8) {
+        const f32x4 a4 = *reinterpret_cast<const f32x4*>(pa + kk);
+        const f32x4 b4 = *reinterpret_cast<const f32x4*>(pb + kk);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[s], b4[s], acc, 0, 0, 0);
+    }
+}
+// acc += A[0:32, 0:32] B[0:32, 0:32] (B read along its rows)
+__device__ __forceinline__ void mma32_nn(f32x16& acc, const float* A, int lda, const float* B, int ldb) {
+    const int l = threadIdx.x & 63;
+#pragma unroll
+    for (int k2 = 0; k2 < 32; k2 += 2) {
+        const int kk = k2 + (l >> 5);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(A[(l & 31) * lda + kk], B[kk * ldb + (l & 31)], acc, 0, 0, 0);
+    }
+}
+// LDS tile <- scale * acc (32 x 32 C/D layout: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5))
+__device__ __forceinline__ void acc32_store(float* C, int ldc, const f32x16& acc, float scale) {
+    const int l = threadIdx.x & 63;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) C[((r & 3) + 8 * (r >> 2) + 4 * (l >> 5)) * ldc + (l & 31)] = scale * acc[r];
+}
+__device__ __forceinline__ void acc32_load(f32x16& acc, const float* C, int ldc) {
+    const int l = threadIdx.x & 63;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = C[((r & 3) + 8 * (r >> 2) + 4 * (l >> 5)) * ldc + (l & 31)];
+}
+
+// One wave: L = chol(A_ss), D = L^-1 of the 32 x 32 sub-block at (S, S) of As / Ds; pivots
+// (non-positive ones replaced by 1, *bad = first such row + 1) into piv[S..S+31].
+__device__ __forceinline__ void factor32(float* As, float* Ds, int S, float* piv, int* bad) {
+    const int l = threadIdx.x & 63, c = l & 31;
+    const bool isA = l < 32;
+    float v[32];
+#pragma unroll
+    for (int r = 0; r < 32; ++r) {
+        const float a = (r >= c) ? As[(S + r) * DLD + S + c] : As[(S + c) * DLD + S + r];   // symmetric column
+        v[r] = isA ? a : (r == c ? 1.0f : 0.0f);
+    }
+    float dpiv = 1.0f;
+    int b = 0;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+        float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v[j]), j));   // A(j, j)
+        if (!(d > 0.0f)) { if (b == 0) b = j + 1; d = 1.0f; }
+        if (isA && c == j) dpiv = d;
+        const float invd = 1.0f / d;
+        const float own = v[j];   // A(j, c) (A lanes, by symmetry) or Y(j, c) (inverse lanes)
+        const float m = (isA ? (c > j) : (c <= j)) ? own * invd : 0.0f;
+#pragma unroll
+        for (int r = j + 1; r < 32; ++r) {
+            const float sr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v[r]), j));   // A(r, j)
+            v[r] = fmaf(-sr, m, v[r]);
+        }
+    }
+    if (isA) piv[S + c] = dpiv;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the pivots are in LDS for the inverse lanes
+    if (isA) {
+        const float rs = rsqrtf(dpiv);
+#pragma unroll
+        for (int r = 0; r < 32; ++r) As[(S + r) * DLD + S + c] = (r >= c) ? v[r] * rs : 0.0f;
+    } else {
+#pragma unroll
+        for (int r = 0; r < 32; ++r) Ds[(S + r) * DLD + S + c] = (r >= c) ? v[r] * rsqrtf(piv[S + r]) : 0.0f;
+    }
+    if (b && *bad == 0) *bad = S + b;
+}
 
 __global__ __launch_bounds__(DIAG_THREADS) void k32_diag(F32Args a, int k) {
-    __shared__ float col[2][TB];   // A(., j), unscaled
-    __shared__ float row[2][TB];   // Y(j, .), unscaled
-    __shared__ float piv[TB];      // d_j (bad pivots replaced by 1)
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const int r0 = 8 * w;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* As = smem;                 // [128][DLD]  A -> L (lower)
+    float* Ds = As + TB * DLD;        // [128][DLD]  D = L^-1 (lower), zero above
+    float* Ts = Ds + TB * DLD;        // 3 x [32][33] scratch for the inverse
+    float* piv = Ts + 3 * 32 * 33;    // [128]
+    int* bad = reinterpret_cast<int*>(piv + TB);
+    const int w = threadIdx.x >> 6;
     float* Mkk = a.M + row_off(a, k) + (long)k * TB;
-    float A[8][2], Y[8][2];
-#pragma unroll
-    for (int q = 0; q < 8; ++q)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int r = r0 + q, c = l + 64 * h;
-            A[q][h] = Mkk[(long)r * a.ld + c];   // upper entries are read too (never used)
-            Y[q][h] = (r == c) ? 1.0f : 0.0f;
-        }
-    if (l == 0) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) col[0][r0 + q] = A[q][0];
+    for (int e = threadIdx.x; e < TB * TB / 4; e += DIAG_THREADS) {
+        const int r = e / (TB / 4), c4 = (e % (TB / 4)) * 4;
+        *reinterpret_cast<f32x4*>(As + r * DLD + c4) = *reinterpret_cast<const f32x4*>(Mkk + (long)r * a.ld + c4);
+        *reinterpret_cast<f32x4*>(Ds + r * DLD + c4) = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     }
-    if (w == 0) { row[0][l] = Y[0][0]; row[0][l + 64] = Y[0][1]; }
+    if (threadIdx.x == 0) *bad = 0;
     __syncthreads();
-    int bad = 0;
-    for (int j = 0; j < TB; ++j) {
-        const int b = j & 1;
-        const float d = col[b][j];
-        const bool ok = d > 0.0f;   // false for NaN too
-        if (!ok && bad == 0) bad = j + 1;
-        const float dd = ok ? d : 1.0f;
-        if (threadIdx.x == 0) piv[j] = dd;
-        if (r0 + 7 > j) {   // wave-uniform: some row of this wave is below the pivot
-            const float invd = 1.0f / dd;
-            float cr[8], cy[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                cr[q] = col[b][r0 + q] * invd;
-                cy[q] = (r0 + q > j) ? cr[q] : 0.0f;
-            }
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int c = l + 64 * h;
-                const float xa = (c > j) ? col[b][c] : 0.0f;    // A(c, j)
-                const float xy = (c <= j) ? row[b][c] : 0.0f;   // Y(j, c)
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    A[q][h] = fmaf(-cr[q], xa, A[q][h]);
-                    Y[q][h] = fmaf(-cy[q], xy, Y[q][h]);
-                }
-            }
+    auto T32 = [&](float* base, int i, int j) { return base + 32 * i * DLD + 32 * j; };
+    for (int s = 0; s < 4; ++s) {
+        if (w == 0) factor32(As, Ds, 32 * s, piv, bad);
+        __syncthreads();
+        // panel: L_is = A_is D_ss^T, one sub-block per wave
+        for (int i = s + 1 + w; i < 4; i += 4) {
+            f32x16 acc = {};
+            mma32_nt(acc, T32(As, i, s), DLD, T32(Ds, s, s), DLD);
+            acc32_store(T32(As, i, s), DLD, acc, 1.0f);   // the wave read its whole input first
         }
-        if (j + 1 < TB) {   // publish column j+1 of A and row j+1 of Y
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                if (l + 64 * h == j + 1) {
-#pragma unroll
-                    for (int q = 0; q < 8; ++q) col[b ^ 1][r0 + q] = A[q][h];
-                }
+        __syncthreads();
+        // trailing: A_ij -= L_is L_js^T, s < j <= i < 4
+        int t = 0;
+        for (int i = s + 1; i < 4; ++i)
+            for (int j = s + 1; j <= i; ++j, ++t) {
+                if (t % 4 != w) continue;
+                f32x16 acc;
+                acc32_load(acc, T32(As, i, j), DLD);
+                f32x16 p = {};
+                mma32_nt(p, T32(As, i, s), DLD, T32(As, j, s), DLD);
+                acc -= p;
+                acc32_store(T32(As, i, j), DLD, acc, 1.0f);
             }
-            if ((j + 1) >> 3 == w) {
-#pragma unroll
-                for (int q = 0; q < 8; ++q)
-                    if (r0 + q == j + 1) { row[b ^ 1][l] = Y[q][0]; row[b ^ 1][l + 64] = Y[q][1]; }
-            }
+        __syncthreads();
+    }
+    // inverse, row block i = 1..3: T_ij = sum_{m=j}^{i-1} L_im D_mj, then D_ij = -D_ii T_ij
+    for (int i = 1; i < 4; ++i) {
+        if (w < i) {
+            const int j = w;
+            f32x16 acc = {};
+            for (int m = j; m < i; ++m) mma32_nn(acc, T32(As, i, m), DLD, T32(Ds, m, j), DLD);
+            acc32_store(Ts + j * 32 * 33, 33, acc, 1.0f);
+        }
+        __syncthreads();
+        if (w < i) {
+            const int j = w;
+            f32x16 acc = {};
+            mma32_nn(acc, T32(Ds, i, i), DLD, Ts + j * 32 * 33, 33);
+            acc32_store(T32(Ds, i, j), DLD, acc, -1.0f);
         }
         __syncthreads();
     }
     float* Dk = a.Dd + (long)k * TB * TB;
-    float rs[8];
+    for (int e = threadIdx.x; e < TB * TB / 4; e += DIAG_THREADS) {
+        const int r = e / (TB / 4), c4 = (e % (TB / 4)) * 4;
+        const f32x4 lv = *reinterpret_cast<const f32x4*>(As + r * DLD + c4);
+        float* dst = Mkk + (long)r * a.ld + c4;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) rs[q] = rsqrtf(piv[r0 + q]);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int c = l + 64 * h;
-        const float sc = sqrtf(piv[c]), rc = 1.0f / sc;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const int r = r0 + q;
-            if (c < r) Mkk[(long)r * a.ld + c] = A[q][h] * rc;
-            else if (c == r) { Mkk[(long)r * a.ld + c] = sc; a.ldiag[k * TB + r] = (double)sc; }
-            Dk[r * TB + c] = (c <= r) ? Y[q][h] * rs[q] : 0.0f;   // upper part zero: full-tile operand
-        }
+        for (int q = 0; q < 4; ++q)
+            if (c4 + q <= r) dst[q] = lv[q];
+        *reinterpret_cast<f32x4*>(Dk + r * TB + c4) = *reinterpret_cast<const f32x4*>(Ds + r * DLD + c4);
     }
-    if (threadIdx.x == 0 && bad && k * TB + bad - 1 < a.n && *a.info == 0) *a.info = k * TB + bad;
+    for (int r = threadIdx.x; r < TB; r += DIAG_THREADS) a.ldiag[k * TB + r] = (double)sqrtf(piv[r]);
+    if (threadIdx.x == 0 && *bad && k * TB + *bad - 1 < a.n && *a.info == 0) *a.info = k * TB + *bad;
 }
 
 // ---------------------------------------------------------------- K2b: panel  M(r,k) <- M(r,k) D_k^T
@@ -489,25 +554,30 @@ __host__ __device__ inline long update_tiles(const F32Args& a, int k1, int jb, i
     return s + (long)rows_B(a, k1) * (je - jb);
 }
 
-__global__ __launch_bounds__(GT, 2) void k32_update(F32Args a, int k0, int k1, int jb, int je) {
+// ntile > gridDim.x: a capped (persistent) grid, each workgroup walks tiles blockIdx.x + i * gridDim.x
+// (the lookahead leaves CUs free for the next panel's factorization on the side stream).
+__global__ __launch_bounds__(GT, 2) void k32_update(F32Args a, int k0, int k1, int jb, int je, int ntile) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    long b = blockIdx.x;
-    int rt = -1, jt = jb;
-    for (int j = jb; j < je; ++j) {
-        const int cnt = a.T - j;
-        if (b < cnt) { rt = j + (int)b; jt = j; break; }
-        b -= cnt;
-    }
-    if (rt < 0) {
-        const int nB = rows_B(a, k1);
-        rt = a.T + (int)(b % nB);
-        jt = jb + (int)(b / nB);
-    }
+    const int nB = rows_B(a, k1);
     const long koff = (long)k0 * TB;
-    Acc acc;
-    acc_zero(acc);
-    gemm_nt(acc, a.M + row_off(a, rt) + koff, a.ld, a.M + row_off(a, jt) + koff, a.ld, (k1 - k0) * (TB / BK), smem);
-    acc_sub_into(acc, a.M + row_off(a, rt) + (long)jt * TB, a.ld);
+    for (long t = blockIdx.x; t < ntile; t += gridDim.x) {
+        long b = t;
+        int rt = -1, jt = jb;
+        for (int j = jb; j < je; ++j) {
+            const int cnt = a.T - j;
+            if (b < cnt) { rt = j + (int)b; jt = j; break; }
+            b -= cnt;
+        }
+        if (rt < 0) {
+            rt = a.T + (int)(b % nB);
+            jt = jb + (int)(b / nB);
+        }
+        Acc acc;
+        acc_zero(acc);
+        gemm_nt(acc, a.M + row_off(a, rt) + koff, a.ld, a.M + row_off(a, jt) + koff, a.ld, (k1 - k0) * (TB / BK),
+                smem);
+        acc_sub_into(acc, a.M + row_off(a, rt) + (long)jt * TB, a.ld);
+    }
 }
 
 // ---------------------------------------------------------------- K3: alpha = K^-1 Y = L^-T Z
@@ -754,7 +824,25 @@ int f32_ident_fill_tiles(const F32Args& a) { return (int)ident_tiles(a); }
 // The whole sweep: gram (+ RHS rows, identity), then per panel of W tile columns: factor,
 // panel, in-panel updates; then the trailing update.  want_grad: alpha and gradient partials;
 // always: sum Z^2 partials (a.nz workgroups).
+// Dynamic LDS above 64 KB must be allowed per kernel (once per process; not a stream operation,
+// so it is safe before or during graph capture).
+static void f32_lds_attributes() {
+    static bool done = false;
+    if (done) return;
+    done = true;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k32_diag), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)DIAG_SMEM);
+    const void* gemms[] = {reinterpret_cast<const void*>(&k32_panel), reinterpret_cast<const void*>(&k32_update),
+                           reinterpret_cast<const void*>(&k32_alpha), reinterpret_cast<const void*>(&k32_pred_mean),
+                           reinterpret_cast<const void*>(&k32_grad<4>), reinterpret_cast<const void*>(&k32_grad<8>),
+                           reinterpret_cast<const void*>(&k32_grad<12>), reinterpret_cast<const void*>(&k32_grad<16>),
+                           reinterpret_cast<const void*>(&k32_grad<32>)};
+    for (const void* f : gemms)
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
 static void f32_gram(const F32Args& a, hipStream_t s, F32Marks* mk) {
+    f32_lds_attributes();
     const long nA = (long)a.T * (a.T + 1) / 2;
     const long ngram = nA + (long)a.Tp * a.T + (long)a.Ts * a.T + ident_tiles(a);
     const size_t glds = gram_smem_bytes32(a.D) > (size_t)TB * (TB + 1) * 4 ? gram_smem_bytes32(a.D)
@@ -771,7 +859,7 @@ constexpr double TILE_FL = 2.0 * TB * TB;   // flops of one 128 x 128 output til
 static void f32_panel_factor(const F32Args& a, int k0, int k1, hipStream_t s, F32Marks* mk) {
     for (int k = k0; k < k1; ++k) {
         if (mk) mk->begin(s, F32_DIAG);
-        hipLaunchKernelGGL(k32_diag, dim3(1), dim3(DIAG_THREADS), 0, s, a, k);
+        hipLaunchKernelGGL(k32_diag, dim3(1), dim3(DIAG_THREADS), DIAG_SMEM, s, a, k);
         if (mk) mk->end(s, (double)TB * TB * TB * 2.0 / 3.0);
         const int np = (a.T - k - 1) + rows_B(a, k + 1);
         if (np > 0) {
@@ -782,7 +870,7 @@ static void f32_panel_factor(const F32Args& a, int k0, int k1, hipStream_t s, F3
         if (k + 1 < k1) {
             const long nt = update_tiles(a, k + 1, k + 1, k1);
             if (mk) mk->begin(s, F32_UPD_IN);
-            hipLaunchKernelGGL(k32_update, dim3((unsigned)nt), dim3(GT), GEMM_SMEM, s, a, k, k + 1, k + 1, k1);
+            hipLaunchKernelGGL(k32_update, dim3((unsigned)nt), dim3(GT), GEMM_SMEM, s, a, k, k + 1, k + 1, k1, (int)nt);
             // useful work: every tile but the strictly upper half of the diagonal tiles
             if (mk) mk->end(s, TILE_FL * TB * (nt - 0.5 * (k1 - k - 1) * (TB - 1) / TB));
         }
@@ -790,11 +878,13 @@ static void f32_panel_factor(const F32Args& a, int k0, int k1, hipStream_t s, F3
 }
 
 // U(panel, [jb, je)): columns jb .. je-1 updated with the panel's K = (k1 - k0) * 128
-static void f32_trailing(const F32Args& a, int k0, int k1, int jb, int je, hipStream_t s, F32Marks* mk) {
+static void f32_trailing(const F32Args& a, int k0, int k1, int jb, int je, hipStream_t s, F32Marks* mk,
+                         int slots = 0) {
     if (jb >= je) return;
     const long nt = update_tiles(a, k1, jb, je);
+    const long grid = (slots > 0 && nt > slots) ? slots : nt;
     if (mk) mk->begin(s, F32_UPD_OUT);
-    hipLaunchKernelGGL(k32_update, dim3((unsigned)nt), dim3(GT), GEMM_SMEM, s, a, k0, k1, jb, je);
+    hipLaunchKernelGGL(k32_update, dim3((unsigned)grid), dim3(GT), GEMM_SMEM, s, a, k0, k1, jb, je, (int)nt);
     if (mk) mk->end(s, TILE_FL * TB * (k1 - k0) * (nt - 0.5 * (je - jb) * (TB - 1) / TB));
 }
 
@@ -823,7 +913,7 @@ void launch_f32_sweep(const F32Args& a, hipStream_t s, F32Marks* mk, hipStream_t
         if (k2 < a.T) {
             (void)hipEventRecord(fork, s);
             (void)hipStreamWaitEvent(side, fork, 0);
-            f32_trailing(a, k0, k1, k2, a.T, s, mk);
+            f32_trailing(a, k0, k1, k2, a.T, s, mk, a.upd_slots);
             f32_panel_factor(a, k1, k2, side, mk);
             (void)hipEventRecord(join, side);
             (void)hipStreamWaitEvent(s, join, 0);

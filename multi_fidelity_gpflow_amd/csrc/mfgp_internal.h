@@ -161,6 +161,7 @@ struct F32Args {
     double* zpart; int nz;                // sum Z^2 partials (nz workgroups)
     double* gpart;                        // [G][T(T+1)/2] gradient partials
     int* cnt;                             // k_reduce_items arrival counter, zeroed by k32_gram
+    int upd_slots;                        // lookahead: cap on resident trailing-update workgroups (0: none)
 };
 size_t f32_gemm_smem();
 // Diagnostic timing of the fp32 launches (never on the hot path): events around every launch,

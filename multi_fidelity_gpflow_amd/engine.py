@@ -144,6 +144,10 @@ class Engine:
         """fp32 path: factor the next panel on a side stream beside the trailing update (default on)."""
         check(self.lib.mfgp_set_f32_lookahead(self.h, 1 if enable else 0), "mfgp_set_f32_lookahead")
 
+    def set_f32_reserve(self, cus: int):
+        """fp32 lookahead: CUs the trailing update leaves to the side stream (0: uncapped)."""
+        check(self.lib.mfgp_set_f32_reserve(self.h, int(cus)), "mfgp_set_f32_reserve")
+
     def private_workspace(self, nbytes: int) -> torch.Tensor:
         """A workspace owned by its caller (a training session keeps it for the life of its
         recorded graphs; the shared grow-only buffers may be replaced under them)."""

@@ -7,9 +7,9 @@ K + s2 I (s2 = 1e-3), so the tolerances here are measured, with margin (DESIGN.m
 
   size                        LML (rel)   gradient (rel. to max |g|)  mean (rel. to max |mean|)  var (abs)
   n <= 2300 vs oracle         1e-4        3e-4                        1e-2                       5e-5
-  Synth 18432 x 512 vs f64    4e-3        1.5e-2                      2e-2                       5e-4
+  Synth 18432 x 512 vs f64    4e-3        1.5e-2                      3e-2                       5e-4
 
-(measured round 2: <= 2.0e-5 / 5.3e-5 / 2.0e-3 / 4.7e-6 small, 8.4e-4 / 2.7e-3 at Synth).
+(measured round 2: <= 2.2e-5 / 9.0e-5 / 2.0e-3 / 4.9e-6 small; 9.7e-4 / 2.9e-3 / 1.1e-2 / 1.4e-5 at Synth).
 Properties that hold to rounding of the fp64 reductions at any size: additivity of the LML over
 output columns (one shared factorization), identical results with and without the lookahead
 schedule and for every panel width that tiles the same way."""
@@ -143,5 +143,5 @@ def test_f32_synth_full_size_vs_f64_path(eng, synth):
     mu32, v32, mu64, v64 = mu32.numpy(), v32.numpy(), mu64.numpy(), v64.numpy()
     print(f"Synth predict mean maxrel {np.max(np.abs(mu32 - mu64)) / np.max(np.abs(mu64)):.2e}, "
           f"var maxabs {np.max(np.abs(v32 - v64)):.2e}")
-    assert np.max(np.abs(mu32 - mu64)) / np.max(np.abs(mu64)) < 2e-2
+    assert np.max(np.abs(mu32 - mu64)) / np.max(np.abs(mu64)) < 3e-2
     assert np.max(np.abs(v32 - v64)) < 5e-4

@@ -66,17 +66,18 @@ def full():
         torch.cuda.synchronize()
         print(f"lookahead={la}: f32 value+grad {(time.time()-t0)/3*1e3:.1f} ms/eval (host-synced), LML {lx:.6f} "
               f"same-as-serial {lx == l32 and np.array_equal(gx, g32)}", flush=True)
-    for graph in (False, True):
-        for la in (0, 1):
-            eng.set_f32_lookahead(bool(la))
-            sess = m32.adam_session(0.1, 8, graph=graph, graph_chunk=2)
-            sess.run(2)
-            sess.prepare(4)
-            sess.sync()
-            t0 = time.time()
-            sess.run(4)
-            sess.sync()
-            print(f"adam session graph={graph} lookahead={la}: {(time.time()-t0)/4*1e3:.1f} ms/step", flush=True)
+    for graph, la, rv in ((False, 0, 0), (True, 0, 0), (True, 1, 0), (True, 1, 8), (True, 1, 16), (True, 1, 32)):
+        eng.set_f32_lookahead(bool(la))
+        eng.set_f32_reserve(rv)
+        sess = m32.adam_session(0.1, 8, graph=graph, graph_chunk=2)
+        sess.run(2)
+        sess.prepare(4)
+        sess.sync()
+        t0 = time.time()
+        sess.run(4)
+        sess.sync()
+        print(f"adam session graph={graph} lookahead={la} reserve={rv}: {(time.time()-t0)/4*1e3:.1f} ms/step",
+              flush=True)
     eng.set_f32_lookahead(True)
     # additivity over output columns
     la, _ = model(X, Y[:, :256], "float32").log_marginal_likelihood_and_grad()
