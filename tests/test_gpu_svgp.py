@@ -189,6 +189,50 @@ def test_singlebin_training_kat(hbs, kats):
             assert abs(got - ref[str(i)]) < 2e-6 * abs(ref[str(i)]), (i, got, ref[str(i)])
 
 
+def test_goku_singlebin_training_kat(goku, kats):
+    """notebooks/demo: goku power spectra.ipynb:350-353: SingleBinSVGP (M=300 KMeans centres,
+    L=P=64) optimize(max_iters=1000, initial_lr=0.1) -- -ELBO after Adam steps 0/10/20/30 (the
+    oracle meets them to <= 1.5e-9, tests/test_oracle_kats.py)."""
+    X, Y = goku["X"], goku["Y"]
+    ref = kats["goku_singlebin_svgp_neg_elbo"]["values"]
+    m = M.SingleBinSVGP(X, Y, M.SquaredExponential(lengthscales=np.ones(10)),
+                        M.SquaredExponential(lengthscales=np.ones(10)), 64, Z=np.zeros((300, 11)))
+    tr = M.svgp._SVGPTrainer(m, (X, Y), max_iters=1000, initial_lr=0.1, graph=True, graph_chunk=10)
+    errs = {}
+    for i in range(31):
+        tr.run(1)
+        if str(i) in ref:
+            got = -tr.elbo_now()
+            errs[i] = abs(got - ref[str(i)]) / abs(ref[str(i)])
+    print("goku singlebin -ELBO rel err", {k: f"{v:.1e}" for k, v in errs.items()})
+    for i, e in errs.items():   # measured 1.3e-11 / 6.7e-10 / 1.2e-8 / 5.6e-8 (round 2)
+        assert e < (1e-8 if i <= 10 else 5e-7), (i, e)
+
+
+@pytest.mark.parametrize("which", ["latent15", "singlebin64"])
+def test_goku_elbo_grad_vs_autograd(goku, which):
+    """Gradients at the Goku size (M=300 KMeans centres with their 2 fractional-fidelity rows,
+    N=1164, P=64): latent L=15 and single-bin L=P=64, against torch autograd through the oracle."""
+    X, Y = goku["X"], goku["Y"]
+    D, P = X.shape[1] - 1, Y.shape[1]
+    if which == "latent15":
+        m = M.LatentMFCoregionalizationSVGP(X, Y, M.SquaredExponential(lengthscales=np.ones(D)),
+                                            M.SquaredExponential(lengthscales=np.ones(D)), num_latents=15,
+                                            num_inducing=300, num_outputs=P, w_type='diagonal',
+                                            window_fraction=0.4, scale=0.2)
+        _randomize(m, 31)
+        e, gd = m.elbo_and_grad((X, Y))
+        eo, ga = _autograd_grads(m, X, Y, m.kernel.W.numpy(), num_data=X.shape[0])
+    else:
+        m = M.SingleBinSVGP(X, Y, M.SquaredExponential(lengthscales=np.ones(D)),
+                            M.SquaredExponential(lengthscales=np.ones(D)), P, Z=np.zeros((300, D + 1)))
+        _randomize(m, 32)
+        e, gd = m.elbo_and_grad((X, Y))
+        eo, ga = _autograd_grads(m, X, Y)
+    assert abs(e - eo) < 1e-7 * abs(eo)
+    _check_grads(gd, ga, 1e-5)
+
+
 def test_latent_training_matches_oracle(hbs):
     """20 optimize() steps of the latent model vs. the same Adam/CosineDecay loop on the
     torch-CPU oracle (autograd gradients)."""

@@ -61,6 +61,39 @@ def test_singlebin_svgp_trace(hbs, kats):
             assert rel(float(tr.neg_elbo().detach()), ref[str(i)]) < 1e-9, i
 
 
+def test_goku_kmeans_fixture(goku, kats):
+    """tests/golden/goku_kmeans_z300.npy (tests/golden/make_goku_kmeans_z.py) is the reference's
+    KMeans(300, random_state=42) on the Goku inputs: recomputed here and checked against the
+    rows the notebook printed."""
+    import os
+    from sklearn.cluster import KMeans
+    from conftest import GOLDEN
+    Zf = np.load(os.path.join(GOLDEN, "goku_kmeans_z300.npy"))
+    Z = KMeans(n_clusters=300, random_state=42).fit(goku["X"]).cluster_centers_
+    np.testing.assert_allclose(Z, Zf, rtol=1e-12, atol=1e-14)   # KMeans sums in thread order: ulp-level
+    k = kats["goku_kmeans_z300_rows"]
+    cols = [0, 1, 2, 8, 9, 10]   # numpy's summarised print: first and last three columns
+    np.testing.assert_allclose(Zf[:3][:, cols], k["first_rows"], rtol=5e-9, atol=5e-12)
+    np.testing.assert_allclose(Zf[-3:][:, cols], k["last_rows"], rtol=5e-9, atol=5e-12)
+    assert int(np.sum((Zf[:, -1] != 0) & (Zf[:, -1] != 1))) == 2   # SURVEY Appendix C-3
+
+
+@pytest.mark.slow
+def test_goku_singlebin_svgp_trace(goku, kats):
+    """The oracle trainer against the Goku SingleBinSVGP -ELBO trace (M=300, L=P=64; ~1 min):
+    measured 1e-12 / 1.2e-12 / 2.2e-10 / 1.5e-9 at steps 0 / 10 / 20 / 30."""
+    import os
+    from conftest import GOLDEN
+    from oracle.svgp_oracle import SingleBinTrainer
+    Z = np.load(os.path.join(GOLDEN, "goku_kmeans_z300.npy"))
+    tr = SingleBinTrainer(goku["X"], goku["Y"], Z, lr=0.1, max_iters=1000)
+    ref = kats["goku_singlebin_svgp_neg_elbo"]["values"]
+    for i in range(31):
+        tr.step()
+        if str(i) in ref:
+            assert rel(float(tr.neg_elbo().detach()), ref[str(i)]) < 1e-8, i
+
+
 def test_hbs_kmeans_inducing_points(hbs, kats):
     from sklearn.cluster import KMeans
     Z = KMeans(n_clusters=50, random_state=42).fit(hbs["X"]).cluster_centers_
