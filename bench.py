@@ -44,26 +44,27 @@ FP32_PEAK_TFLOPS = 157.3  # MI355X dense FP32 (v_mfma_f32_32x32x2_f32 = the f32 
 HBM_PEAK_GBS = 8000.0
 # HBM bytes per dispatch from the committed rocprofv3 PMC passes (tools/profile_round.sh ->
 # tools/summarize_profile.py); the bench cannot count PMC on itself.
-def latest_pmc_summary():
-    """profiles/rNN/pmc_summary.json of the latest round that has one."""
+def latest_pmc_summary(config="goku"):
+    """profiles/rNN/<config>/pmc_summary.json (or round 1's profiles/r01/pmc_summary.json for Goku) of
+    the latest round that has one."""
     import glob
-    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", "pmc_summary.json")))
-    return found[-1] if found else os.path.join(ROOT, "profiles", "r01", "pmc_summary.json")
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", config, "pmc_summary.json")))
+    if not found and config == "goku":
+        found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", "pmc_summary.json")))
+    return found[-1] if found else None
 
 
-PMC_SUMMARY = latest_pmc_summary()
-
-
-def pmc_traffic(kernel_prefix, nb):
+def pmc_traffic(kernel_prefix, nb, config="goku"):
     """(bytes per dispatch, source) of the dominant kernel from the committed PMC summary."""
+    path = latest_pmc_summary(config)
     try:
-        with open(PMC_SUMMARY) as f:
+        with open(path) as f:
             kern = json.load(f)["kernels"]
-    except (OSError, ValueError, KeyError):
+    except (TypeError, OSError, ValueError, KeyError):
         return None, None
     for name, v in kern.items():
         if f"{kernel_prefix}<{nb}>" in name or f"{kernel_prefix}(" in name:
-            return v["hbm_bytes"], os.path.relpath(PMC_SUMMARY, ROOT)
+            return v["hbm_bytes"], os.path.relpath(path, ROOT)
     return None, None
 
 
@@ -142,9 +143,11 @@ def roofline(model, n, p, d, reps=10, pmc=True):
 
 def roofline_f32(model, reps=3, pmc=True):
     """fp32 path: hipEvents around every launch of one value+grad evaluation (serial schedule,
-    launch stream), summed per phase.  The dominant kernel is the trailing update k32_update
-    (K = 128 * panel); achieved = the tile flops it performs (all but the strictly upper half of
-    the diagonal tiles) / its summed launch time."""
+    launch stream), summed per phase.  The dominant kernel is the tile update k32_update (the
+    in-panel updates, K = 128, and the trailing updates, K = 128 * panel); achieved = the tile
+    flops its launches perform (all but the strictly upper half of the diagonal tiles) / their
+    summed launch time; traffic = the committed PMC mean bytes per k32_update dispatch x its
+    launches per step."""
     from multi_fidelity_gpflow_amd.engine import gpr_phase_times_ex
     eng, X, Y = model._device_data()
     theta = torch.tensor(model._theta_map().theta(), dtype=torch.float64, device=eng.device)
@@ -154,14 +157,23 @@ def roofline_f32(model, reps=3, pmc=True):
         for k, (ms, fl, la) in gpr_phase_times_ex(eng, X, Y, theta).items():
             a = acc.setdefault(k, [0.0, fl, la])
             a[0] += ms / reps
-    dom = max(acc, key=lambda k: acc[k][0])
-    ms, fl, la = acc[dom]
+    kn = {"update_out": "k32_update", "update_in": "k32_update", "grad": "k32_grad", "diag": "k32_diag",
+          "panel": "k32_panel", "gram": "k32_gram", "alpha": "k32_alpha", "finalize": "k32_zsum"}
+    per_kernel = {}
+    for k, (ms_, fl_, la_) in acc.items():
+        e = per_kernel.setdefault(kn[k], [0.0, 0.0, 0])
+        e[0] += ms_
+        e[1] += fl_
+        e[2] += la_
+    kname = max(per_kernel, key=lambda k: per_kernel[k][0])
+    ms, fl, la = per_kernel[kname]
     achieved = fl / (ms * 1e-3) / 1e12
-    kname = {"update_out": "k32_update", "update_in": "k32_update", "grad": "k32_grad", "diag": "k32_diag",
-             "panel": "k32_panel", "gram": "k32_gram", "alpha": "k32_alpha", "finalize": "k32_zsum"}[dom]
-    traffic, tsrc = pmc_traffic(kname, 0) if pmc else (None, None)
+    traffic, tsrc = pmc_traffic(kname, 0, "synth") if pmc else (None, None)
+    if traffic is not None:
+        traffic = int(traffic * la)
     return {
-        "kernel": kname + (" (trailing update, K = 128 x panel)" if dom == "update_out" else ""),
+        "kernel": kname + (" (in-panel K = 128 and trailing K = 128 x panel tile updates)"
+                           if kname == "k32_update" else ""),
         "bound": "mfma",
         "achieved": round(achieved, 3),
         "peak": FP32_PEAK_TFLOPS,
@@ -226,6 +238,99 @@ def cpu_baseline(X, Y):
                        f"train_1000_adam_s_est = 1000 / value")}
 
 
+def svgp_elbo_flops(n, m, L, p, d):
+    """one SVGP ELBO evaluation L[(M(M+1)/2 + MN)(3D+6) + M^3/3 + 2M^2 N] + 4NLP."""
+    return L * ((m * (m + 1) / 2 + m * n) * (3 * d + 6) + m ** 3 / 3 + 2 * m * m * n) + 4 * n * L * p
+
+
+def bench_svgp(args):
+    """BASELINE configs[3]: the Goku SVGP models of notebooks/demo: goku power spectra.ipynb --
+    SingleBinSVGP (M=300 KMeans centres, L=P=64; cell 10, 1000 iterations, published 2237.47 s on
+    the M1) and LatentMFCoregionalizationSVGP (L=15, M=300; published 1020.22 s for 2000).  A step
+    is one optimize() iteration: ELBO + analytic gradient + Keras Adam with the CosineDecay
+    schedule, replayed from hipGraphs (graphs captured in warm-up).  N > 1: each rank trains the
+    single-bin model of its own bin block (per-shard Z / noise, no collective)."""
+    import multi_fidelity_gpflow_amd as M
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+    X, Y, Xt, Yt = broadcast_inputs(rank, world, device)
+    n, d, P = X.shape[0], X.shape[1] - 1, Y.shape[1]
+    from multi_fidelity_gpflow_amd.distributed import bin_block
+    b0, b1 = bin_block(P, rank, world)
+    Yr = np.ascontiguousarray(Y[:, b0:b1])
+    pr = Yr.shape[1]
+    K, W = args.steps, args.warmup
+    kern = lambda: M.SquaredExponential(lengthscales=np.ones(d))
+
+    def timed(model, max_iters):
+        tr = M.svgp._SVGPTrainer(model, (X, Yr), max_iters=max_iters, initial_lr=0.1, graph=True, graph_chunk=10)
+        tr.run(W)
+        with torch.cuda.stream(tr.stream):
+            tr.runner.prepare(K)   # capture every graph the timed run replays
+        tr.sync()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        tr.run(K)
+        tr.sync()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([dt], dtype=torch.float64, device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        return dt, tr
+
+    sb = M.SingleBinSVGP(X, Yr, kern(), kern(), pr, Z=np.zeros((300, d + 1)))
+    dt_sb, _ = timed(sb, K + W)
+    lat = M.LatentMFCoregionalizationSVGP(X, Yr, kern(), kern(), num_latents=15, num_inducing=300, num_outputs=pr,
+                                          w_type="diagonal", window_fraction=0.4, scale=0.2)
+    dt_lat, _ = timed(lat, max(K + W, 2000))
+    # notebook protocol for the single-bin model: a fresh model, optimize(max_iters=1000, initial_lr=0.1)
+    train_s = None
+    if not args.no_train_predict:
+        m2 = M.SingleBinSVGP(X, Yr, kern(), kern(), pr, Z=np.zeros((300, d + 1)))
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        m2.optimize((X, Yr), max_iters=1000, initial_lr=0.1, unfix_noise_after=500)
+        m2.predict_f(Xt)
+        torch.cuda.synchronize()
+        train_s = time.perf_counter() - t1
+    if rank == 0:
+        value = world * K / dt_sb
+        fl = svgp_elbo_flops(n, 300, pr, pr, d)
+        achieved = fl * K / dt_sb / 1e12
+        line = {
+            "metric": "SVGP optimize iterations/s (Goku SingleBinSVGP M=300, L=P=64: ELBO + gradient + Adam)",
+            "value": round(value, 3), "unit": "iters/s", "n_gpus": world, "steps": K, "warmup": W,
+            "ms_per_step": round(dt_sb / K * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64",
+            "data": "Goku z=0 P(k) (reference data files, tests/golden/data), RCCL-broadcast from rank 0",
+            "config": {"workload": "goku_singlebin_svgp_step", "n": n, "d": d, "m": 300, "latents": pr,
+                       "bins_per_rank": pr, "parallelism": f"bins{world}" if world > 1 else "single"},
+            "latent_l15": {"ms_per_step": round(dt_lat / K * 1e3, 4), "iters_per_s": round(world * K / dt_lat, 3),
+                           "published_m1_s_per_iter": round(1020.22 / 2000, 4)},
+            "train_1000_predict_s": None if train_s is None else round(train_s, 3),
+            "published_m1": {"train_1000_s": 2237.47, "source": "notebooks/demo: goku power spectra.ipynb:451"},
+            "roofline": {"kernel": "whole optimize() iteration (SURVEY §8(d) ELBO-value flops only; the gradient's "
+                                   "reverse pass is not counted, so this is a lower bound)",
+                         "bound": "mfma", "achieved": round(achieved, 4), "peak": FP64_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 5), "traffic": None,
+                         "flop_per_step": fl},
+            "cpu_baseline": None,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
 def spawn_ranks(n: int) -> int:
     """python -m torch.distributed.run --nproc-per-node n bench.py <same args>, as a child."""
     import socket
@@ -249,7 +354,7 @@ def main():
     ap.add_argument("--mode", choices=["shard", "shared"], default="shard",
                     help="shard: per-shard-theta bin blocks (no inner-loop collective); shared: one model, "
                          "one all-reduce of 1+G doubles per step (reference-parity mode, SURVEY 8(e))")
-    ap.add_argument("--config", choices=["goku", "synth"], default="goku",
+    ap.add_argument("--config", choices=["goku", "synth", "goku_svgp"], default="goku",
                     help="goku: the BASELINE metric (fp64); synth: BASELINE configs[4] / SURVEY §8(d) "
                          "(N=18432, P=512, fp32)")
     args = ap.parse_args()
@@ -262,6 +367,8 @@ def main():
     if args.config == "synth":
         args.no_cpu_baseline = True
         args.no_train_predict = True
+    if args.config == "goku_svgp":
+        return bench_svgp(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

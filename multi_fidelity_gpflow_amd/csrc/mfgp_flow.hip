@@ -472,9 +472,11 @@ __device__ __forceinline__ void flow_finalize_r(FlowCtx& C, const FlowTile& t, d
     const double* Pq = C.P.X(i - 1, t.j);
     WOp d, h, q;
     {   // R'' and the three published operands in one round trip (loads complete in order, so
-        // staging R'' waits for its own loads only)
+        // staging R'' waits for its own loads only).  R's identity block is never stored: a tile
+        // (j+1, j) of it has no update before its finalize, so R'' is its initial value, zero.
         WTile acc;
-        wt_load<false>(acc, C.Rt(i, t.j), a.ldr);
+        if (t.j < T && i == t.j + 1) wt_zero(acc);
+        else wt_load<false>(acc, C.Rt(i, t.j), a.ldr);
         op_load_pub(d, Pd);
         if (cpl) {
             op_load_pub(h, Ph);
@@ -552,7 +554,9 @@ __device__ __forceinline__ void flow_update(FlowCtx& C, const FlowTile& t, int l
         }
     } else if (t.type == FT_R) {
         double* dst = C.Rt(t.i, t.j);
-        wt_load<false>(acc, dst, a.ldr);
+        // identity block: the first update (level j) starts from the initial value, zero (i > j + 1)
+        if (t.j < T && l == t.j) wt_zero(acc);
+        else wt_load<false>(acc, dst, a.ldr);
         pub_op2(x, C.P.L(t.i, l), y, C.P.X(l, t.j), C);  // L(i,l), X(l,c)^T (B[k][j] = X(l,c)[k][j])
         wt_mma<true>(acc, x, y);                         // R(i,c) -= L(i,l) X(l,c)
         wt_store<false>(acc, dst, a.ldr);

@@ -293,8 +293,9 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
         }
     }
     if (!a.padded) { gram_fill_pub(a); return; }
-    if (a.R != nullptr) {
-        // fused RHS init: R tile (ti, tj) of the identity part, and row block ti of Y
+    if (a.R != nullptr && a.fown == nullptr) {
+        // fused RHS init: R tile (ti, tj) of the identity part, and row block ti of Y (the
+        // persistent k_chol_flow never reads R's identity block: it starts those tiles from zero)
         double* Rb = a.R + b * a.sR;
         for (int e = threadIdx.x; e < NB * NB; e += NTHREADS) {
             const int r = e / NB, c = e % NB;
