@@ -248,9 +248,6 @@ struct FlowCtx {
     FlowPub P;
     long long t0;
     long long waited;   // worker: ticks spent re-polling (trace only)
-#ifdef FLOW_ITEM_PROBE
-    long long probe;    // diagnostic: time the item's operands were in registers
-#endif
     __device__ double* At(int i, int j) const { return a.A + (long)i * 32 * a.lda + (long)j * 32; }
     __device__ double* Rt(int i, int c) const { return a.R + (long)i * 32 * a.ldr + (long)c * 32; }
     __device__ double* Xt(int i, int c) const { return a.Xo + (long)i * 32 * a.ldx + (long)c * 32; }
@@ -534,13 +531,6 @@ __device__ __forceinline__ void flow_update(FlowCtx& C, const FlowTile& t, int l
             pub_op(x, C.P.L(t.i, l), C);
             y = x;
         }
-#ifdef FLOW_ITEM_PROBE
-        {
-            double z = x.v[0][0] + y.v[1][7] + acc.v[1][1][3];
-            asm volatile("" : "+v"(z));
-            C.probe = flow_clock() + (z == 12345.678 ? 1 : 0);
-        }
-#endif
         wt_mma<true>(acc, x, y);                         // A(i,j) -= L(i,l) L(j,l)^T
         if (fin) {
             // D_{l+1} is loaded only now: it is published ~one factor after L(j,l) (so an early
@@ -597,11 +587,7 @@ __device__ __forceinline__ void flow_item_log(const FlowCtx& C, int wid, int n, 
     const long long t1 = flow_clock();
     e[0] = ((long long)code << 8) | l;
     e[1] = i0 - C.t0;
-#ifdef FLOW_ITEM_PROBE
-    e[2] = C.probe - C.t0;
-#else
     e[2] = i0 + (C.waited - w0) - C.t0;
-#endif
     e[3] = t1 - C.t0;
 }
 
@@ -773,11 +759,9 @@ __device__ __forceinline__ void diag_chain(FlowCtx& C, const DiagLds& B) {
         for (int r = 0; r < 4; ++r) cij.v[0][r] = B.Cp(pk)[acc_row<32>(0, r) * S + acc_col<32>(0)];
         chain_bar(&B.w()[DW_BAR], epoch);
         if (threadIdx.x == 0) lds_put(&B.w()[DW_LS], k);
-#ifndef FLOW_SIMD1_SHARED
         // only the lower blocks of A''(k,k) feed the factor: wave 1 (block (0,1)) skips the
         // product and leaves SIMD 1 to wave 5 from the end of the first product on
         if (w != 1)
-#endif
         tile_mma<32, false, true>(cij, B.Ls(pk), B.Ls(pk), -1.0);   // A''(k,k) -= L L^T
         {
             const int bi = w >> 1, bj = w & 1;
@@ -856,12 +840,8 @@ __device__ __forceinline__ void diag_publisher(FlowCtx& C, const DiagLds& B) {
 }
 
 // wave 5 shares SIMD 1 with chain wave 1, whose last MFMA of a step is its block of the first
-// product (L(k,k-1)) unless FLOW_SIMD1_SHARED
-#ifdef FLOW_SIMD1_SHARED
-#define W5_GATE DW_P2
-#else
+// product (L(k,k-1))
 #define W5_GATE DW_LS
-#endif
 __device__ __forceinline__ void diag_second(FlowCtx& C, const DiagLds& B) {
     constexpr int S = TileCfg<32>::S;
     const FlowArgs& a = C.a;

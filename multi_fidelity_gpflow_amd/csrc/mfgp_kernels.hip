@@ -155,13 +155,11 @@ __device__ __forceinline__ double gram_entry(const double* aL1, const double* aD
 // Run LAST in a workgroup: the stores share the vmcnt queue with later loads, and a load's
 // data waits for every older store to be acknowledged.
 __device__ __forceinline__ void gram_fill_pub(const GramArgs& a) {
-#ifndef GRAM_DIAG_NOFILL
     if (a.fpub && blockIdx.z == 0) {
         unsigned long long* dst = reinterpret_cast<unsigned long long*>(a.fpub);
         for (long e = blockIdx.x * (long)NTHREADS + threadIdx.x; e < a.npub; e += (long)gridDim.x * NTHREADS)
             __hip_atomic_store(dst + e, FLOW_SENTINEL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-#endif
 }
 
 // Y block of R (rows < n1, columns < p; zero padding), a grid-stride slice per tile workgroup
@@ -203,22 +201,15 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
 
     const int b = blockIdx.z;
     const long long dbg_t0 = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
-#ifdef GRAM_DIAG_EMPTY
-    if (a.padded) return;
-#endif
     if (a.gorder && blockIdx.x == gridDim.x - 1) {   // extra workgroup: k_grad task order
-#ifndef GRAM_DIAG_NOORDER
         if (b == 0) build_grad_order(a.gT, a.gchunk, a.gTp, a.gorder, reinterpret_cast<int*>(smem));
-#endif
         if (a.dbg && threadIdx.x == 0) a.dbg[3 * blockIdx.x + 2] = __builtin_amdgcn_s_memrealtime() - dbg_t0;
         gram_fill_pub(a);
         return;
     }
     if (a.fown && blockIdx.x == gridDim.x - 1 - (a.gorder ? 1 : 0)) {   // extra: flow owner table
-#ifndef GRAM_DIAG_NOOWNER
         if (b == 0) build_flow_owner(a.npad / NB, a.ppad / NB, a.fW, a.fown, a.fflags, a.nfflags,
                                      reinterpret_cast<int*>(smem));
-#endif
         if (a.dbg && threadIdx.x == 0) a.dbg[3 * blockIdx.x + 2] = __builtin_amdgcn_s_memrealtime() - dbg_t0;
         gram_fill_pub(a);
         return;
@@ -269,14 +260,6 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
     __syncthreads();
     if (a.dbg && threadIdx.x == 0) a.dbg[3 * blockIdx.x] = __builtin_amdgcn_s_memrealtime() - dbg_t0;   // stage time (ticks)
 
-#ifdef GRAM_DIAG_NOENTRY
-    if (a.padded) {
-        for (int e = threadIdx.x; e < NB * NB; e += NTHREADS) tile[(e / NB) * S + e % NB] = (ti == tj && e / NB == e % NB) ? 1.0 : 0.0;
-        __syncthreads();
-        tile_store<NB>(a.out + b * a.so + (long)ti * NB * a.ldo + tj * NB, a.ldo, tile);
-        return;
-    }
-#endif
     double* out = a.out + b * a.so;
     for (int e = threadIdx.x; e < NB * NB; e += NTHREADS) {
         const int r = e / NB, c = e % NB;
@@ -307,11 +290,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
     __syncthreads();
     if (a.dbg && threadIdx.x == 0) a.dbg[3 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - dbg_t0;
     tile_store<NB>(out + (long)ti * NB * a.ldo + tj * NB, a.ldo, tile);
-#ifdef GRAM_DIAG_NOFACTOR
-    if (false) {
-#else
     if (a.Dd != nullptr && ti == 0 && tj == 0) {
-#endif
         // fused factor of the first diagonal tile (step "-1" of the tile Cholesky)
         __syncthreads();
         tile_potrf_inv<NB>(tile, rtile, dg, &bad);
@@ -544,15 +523,12 @@ __global__ void k_rhs_init(double* R, long ldr, long sR, int npad, int ppad, con
 }
 
 // ============================================================ K5: gradient
-#ifndef MFGP_GRAD_NBUF1
-#define MFGP_GRAD_NBUF1 0
-#endif
 // k_grad LDS: NBUF operand buffers (2: double-buffered m-loop, one barrier per item;
-// NB = 64 tiles are 33 KB each, so one).  MFGP_GRAD_NBUF1 forces one at NB = 32.
+// NB = 64 tiles are 33 KB each, so one).
 // After the loop the region is reused: raw rows xi, xj, flags fi, fj, then the
 // per-quad gradient partials R [G][GRAD_RLD] and the inverse squared lengthscales.
 template <int NB>
-constexpr int GRAD_NBUF = (NB == 32 && !MFGP_GRAD_NBUF1) ? 2 : 1;
+constexpr int GRAD_NBUF = (NB == 32) ? 2 : 1;
 constexpr int GRAD_RLD = 65;   // 64 quad partials per gradient entry, +1 against bank conflicts
 template <int NB>
 constexpr int GRAD_RED_OFF = (2 * NB * XS + 2 * NB + 1) & ~1;
@@ -928,43 +904,44 @@ size_t grad_smem_bytes(int nb, int G, int nil2) {
 
 // Stage 2: LML, gradient output and the optional Keras-Adam step; run by the last
 // item workgroup of k_reduce_items to arrive.
-__device__ void adam_body(const FinArgs& a, int G, int s);
+__device__ void adam_body(const FinArgs& a, int G, int s, const double* gsh, const int* tsh);
+constexpr int FIN_MAXG = 254;   // theta entries staged in LDS (graph kernel: <= 186)
 __device__ void finalize_body(const FinArgs& a) {
     const int G = a.G ? a.G : theta_size(a.D);
-    const double* items = a.items;
     const double LOG2PI = 1.8378770664093453;
-    // every input is read before the first store (the outputs may alias them as far as the
-    // compiler knows): one round trip instead of one per dependent group
-    const double i0 = ld_coherent(items), i1 = ld_coherent(items + 1);
+    // every input in ONE round trip into LDS, before the first store (the outputs may alias them
+    // as far as the compiler knows; a dependent sc1 load per tied entry cost ~8 us per step)
+    __shared__ double gsh[FIN_MAXG + 2];   // [sum Z^2, sum log L_ii, grad_0 .. grad_{G-1}]
+    __shared__ int tsh[FIN_MAXG];
+    for (int q = threadIdx.x; q < G + 2 && q < FIN_MAXG + 2; q += NTHREADS) gsh[q] = ld_coherent(a.items + q);
+    if (a.adam && a.tie)
+        for (int q = threadIdx.x; q < G && q < FIN_MAXG; q += NTHREADS) tsh[q] = a.tie[q];
     const int info0 = a.info[0];
     const int s = a.adam ? *a.step : 0;
-    const double g0 = (a.want_grad && (int)threadIdx.x < G) ? ld_coherent(items + 2 + threadIdx.x) : 0.0;
-    double lml = -0.5 * i0 - (double)a.P * i1 - 0.5 * (double)a.n * (double)a.P * LOG2PI;
+    __syncthreads();
+    double lml = -0.5 * gsh[0] - (double)a.P * gsh[1] - 0.5 * (double)a.n * (double)a.P * LOG2PI;
     if (info0 != 0) lml = NAN;
-    if (a.adam && info0 == 0) adam_body(a, G, s);
+    if (a.adam && info0 == 0) adam_body(a, G, s, gsh + 2, a.tie ? tsh : nullptr);
     if (threadIdx.x == 0) a.out[0] = lml;
-    if (a.want_grad) {
-        if ((int)threadIdx.x < G) a.out[1 + threadIdx.x] = g0;
-        for (int q = threadIdx.x + NTHREADS; q < G; q += NTHREADS) a.out[1 + q] = ld_coherent(items + 2 + q);
-    }
+    if (a.want_grad)
+        for (int q = threadIdx.x; q < G; q += NTHREADS) a.out[1 + q] = gsh[2 + q];
     if (!a.adam) return;
     if (threadIdx.x == 0) a.loss_hist[s] = -lml;
     __syncthreads();   // every wave has read *a.step
     if (threadIdx.x == 0 && info0 == 0) *a.step = s + 1;
 }
 
-__device__ void adam_body(const FinArgs& a, int G, int s) {
-    const double* gsh = a.items + 2;
+__device__ void adam_body(const FinArgs& a, int G, int s, const double* gsh, const int* tsh) {
     const double t = (double)(s + 1);
     const double alpha = a.lr * sqrt(1.0 - pow(a.b2, t)) / (1.0 - pow(a.b1, t));
     for (int q = threadIdx.x; q < G; q += NTHREADS) {
         if (a.trainable[q]) {
             const double uq = a.u[q];
-            double gc = ld_coherent(gsh + q);
-            if (a.tie) {   // a variable shared by several theta entries gets the summed gradient
+            double gc = gsh[q];
+            if (tsh) {   // a variable shared by several theta entries gets the summed gradient
                 gc = 0.0;
                 for (int r = 0; r < G; ++r)
-                    if (a.tie[r] == a.tie[q]) gc += ld_coherent(gsh + r);
+                    if (tsh[r] == tsh[q]) gc += gsh[r];
             }
             const double g = (-gc) / (exp(-uq) + 1.0);   // loss = -lml; TF SoftplusGrad form
             double mq = a.m[q], vq = a.v[q];

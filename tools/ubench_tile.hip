@@ -7,7 +7,7 @@
 #include <string.h>
 #include <math.h>
 static double prev[64 * 64];
-#include "../multi_fidelity_gpflow_amd/csrc/mfgp_device.h"
+#include "factor_variants.h"
 using namespace mfgp;
 
 

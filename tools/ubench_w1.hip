@@ -5,7 +5,7 @@
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
-#include "../multi_fidelity_gpflow_amd/csrc/mfgp_device.h"
+#include "factor_variants.h"
 using namespace mfgp;
 constexpr int NB = 32;
 
