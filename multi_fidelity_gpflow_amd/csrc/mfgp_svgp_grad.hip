@@ -19,6 +19,8 @@
 // All products are batched over latents and run on v_mfma_f64_16x16x4 tiles (k_bgemm).
 #include <algorithm>
 
+#include <type_traits>
+
 #include "mfgp_device.h"
 #include "mfgp_internal.h"
 
@@ -263,8 +265,8 @@ __global__ __launch_bounds__(NTHREADS) void k_kgrad(const double* P1, long ld1, 
                                                     int n2, const double* Wt, long ldw, long sW, const double* thetas,
                                                     int G, int D, double zf, int nbc, double* gth_part,
                                                     double* gz_part) {
-    __shared__ double red[NTHREADS];
-    __shared__ double zs[KG_ROWS][DC + 1];
+    __shared__ double wred[NTHREADS / 64][2 * DC + 4];
+    __shared__ double zsw[NTHREADS / 64][KG_ROWS][DC + 1];
     const int l = blockIdx.z;
     const int at = blockIdx.x / nbc, bc = blockIdx.x % nbc;
     const int t = threadIdx.x;
@@ -272,13 +274,19 @@ __global__ __launch_bounds__(NTHREADS) void k_kgrad(const double* P1, long ld1, 
     const int a = at * KG_ROWS + ar;
     const MFTheta th{thetas + (long)l * G, D};
     const double vL = th.vL(), vD = th.vD(), rho = th.rho();
-    double gl[DC], gd[DC], gz[DC], il[DC], id[DC];
+    // inverse lengthscales of the latent in LDS (every thread reads the same word: a broadcast),
+    // which keeps 2 DC doubles out of the register file of the pair loop
+    __shared__ double il[DC], id[DC];
+    if (t < DC) {
+        il[t] = (t < D) ? 1.0 / th.lL(t) : 0.0;
+        id[t] = (t < D) ? 1.0 / th.lD(t) : 0.0;
+    }
+    __syncthreads();
+    double gl[DC], gd[DC], gz[DC];
     double gvL = 0.0, gvD = 0.0, grho = 0.0;
 #pragma unroll
     for (int d = 0; d < DC; ++d) {
         gl[d] = 0.0; gd[d] = 0.0; gz[d] = 0.0;
-        il[d] = (d < D) ? 1.0 / th.lL(d) : 0.0;   // inverse lengthscales hoisted out of the pair loop
-        id[d] = (d < D) ? 1.0 / th.lD(d) : 0.0;
     }
     if (a < n1) {
         const double fa = P1[(long)a * ld1 + D];
@@ -325,35 +333,38 @@ __global__ __launch_bounds__(NTHREADS) void k_kgrad(const double* P1, long ld1, 
             }
         }
     }
-    // theta partials: block reduction per entry (G entries in the MFTheta layout)
-    auto reduce_store = [&](double v, int q) {
-        red[t] = v;
-        __syncthreads();
-        for (int o = NTHREADS / 2; o > 0; o >>= 1) {
-            if (t < o) red[t] += red[t + o];
-            __syncthreads();
-        }
-        if (t == 0) gth_part[((long)l * gridDim.x + blockIdx.x) * G + q] = red[0];
-        __syncthreads();
+    // theta partials: wave shuffles, one LDS slot per (entry, wave), ONE barrier (a tree
+    // reduction per entry cost 9 barriers x G entries, ten times the pair loop itself)
+    const int lane = t & 63, wv = t >> 6;
+    auto put = [&](double v, int q) {
+        v = wave_sum(v);
+        if (lane == 0) wred[wv][q] = v;
     };
-    reduce_store(gvL, 0);
-    for (int d = 0; d < D; ++d) reduce_store(gl[d < DC ? d : 0] * (d < DC ? 1.0 : 0.0), 1 + d);
-    reduce_store(gvD, 1 + D);
-    for (int d = 0; d < D; ++d) reduce_store(gd[d < DC ? d : 0] * (d < DC ? 1.0 : 0.0), 2 + D + d);
-    reduce_store(grho, 2 + 2 * D);
-    if (t == 0) gth_part[((long)l * gridDim.x + blockIdx.x) * G + (G - 1)] = 0.0;   // noise slot
-    // z partials: rows of this tile, summed over the 8 column lanes
-    for (int e = t; e < KG_ROWS * (DC + 1); e += NTHREADS) (&zs[0][0])[e] = 0.0;
-    __syncthreads();
-    for (int s8 = 0; s8 < NTHREADS / KG_ROWS; ++s8) {
-        if (bs == s8)
-            for (int d = 0; d < D && d < DC; ++d) zs[ar][d] += gz[d];
-        __syncthreads();
+    put(gvL, 0);
+#pragma unroll
+    for (int d = 0; d < DC; ++d)
+        if (d < D) put(gl[d], 1 + d);
+    put(gvD, 1 + D);
+#pragma unroll
+    for (int d = 0; d < DC; ++d)
+        if (d < D) put(gd[d], 2 + D + d);
+    put(grho, 2 + 2 * D);
+    // z partials of the tile's rows: the two column lanes of a row that share a wave (lanes
+    // ar and ar + 32) by one shuffle, the four waves through LDS
+#pragma unroll
+    for (int d = 0; d < DC; ++d) {
+        const double v = gz[d] + __shfl_xor(gz[d], 32, 64);
+        if (lane < 32 && d < D) zsw[wv][ar][d] = v;
     }
+    __syncthreads();
+    for (int q = t; q < G; q += NTHREADS)
+        gth_part[((long)l * gridDim.x + blockIdx.x) * G + q] =
+            (q == G - 1) ? 0.0 : (wred[0][q] + wred[1][q]) + (wred[2][q] + wred[3][q]);   // noise slot: 0
     for (int e = t; e < KG_ROWS * D; e += NTHREADS) {
         const int r = e / D, d = e % D;
         const int ag = at * KG_ROWS + r;
-        gz_part[(((long)l * gridDim.x + blockIdx.x) * KG_ROWS + r) * D + d] = (ag < n1) ? zf * zs[r][d] : 0.0;
+        const double v = (zsw[0][r][d] + zsw[1][r][d]) + (zsw[2][r][d] + zsw[3][r][d]);
+        gz_part[(((long)l * gridDim.x + blockIdx.x) * KG_ROWS + r) * D + d] = (ag < n1) ? zf * v : 0.0;
     }
 }
 
@@ -570,17 +581,19 @@ static int svgp_grad_run(hipStream_t s, int n, int m, int L, int p, int d, const
     hipLaunchKernelGGL(k_glq_final, dim3(std::min(cdv(m * m, 256), 1024), 1, L), dim3(256), 0, s, g.gLq, Lq, m, mpad,
                        mm, kl_mult, gq_sqrt);
     // 8. kernel / inducing-point derivative sums
-    if (d <= 16) {
-        launch_kgrad<16>(s, Z, ldz, m, Z, ldz, m, g.Sig, mpad, mm, thetas, G, d, 2.0, g.n_at, g.nbc_uu, L, g.gth_uu,
+    // compile-time bound on d: the per-dimension accumulators stay in registers
+    auto kgrad = [&](auto dc) {
+        constexpr int DC = decltype(dc)::value;
+        launch_kgrad<DC>(s, Z, ldz, m, Z, ldz, m, g.Sig, mpad, mm, thetas, G, d, 2.0, g.n_at, g.nbc_uu, L, g.gth_uu,
                          g.gz_uu);
-        launch_kgrad<16>(s, Z, ldz, m, X, ldx, n, g.Kbar, npad, mn, thetas, G, d, 1.0, g.n_at, g.nbc_uf, L, g.gth_uf,
+        launch_kgrad<DC>(s, Z, ldz, m, X, ldx, n, g.Kbar, npad, mn, thetas, G, d, 1.0, g.n_at, g.nbc_uf, L, g.gth_uf,
                          g.gz_uf);
-    } else {
-        launch_kgrad<32>(s, Z, ldz, m, Z, ldz, m, g.Sig, mpad, mm, thetas, G, d, 2.0, g.n_at, g.nbc_uu, L, g.gth_uu,
-                         g.gz_uu);
-        launch_kgrad<32>(s, Z, ldz, m, X, ldx, n, g.Kbar, npad, mn, thetas, G, d, 1.0, g.n_at, g.nbc_uf, L, g.gth_uf,
-                         g.gz_uf);
-    }
+    };
+    if (d <= 4) kgrad(std::integral_constant<int, 4>{});
+    else if (d <= 8) kgrad(std::integral_constant<int, 8>{});
+    else if (d <= 12) kgrad(std::integral_constant<int, 12>{});
+    else if (d <= 16) kgrad(std::integral_constant<int, 16>{});
+    else kgrad(std::integral_constant<int, 32>{});
     hipLaunchKernelGGL(k_kff_grad, dim3(L), dim3(NTHREADS), 0, s, X, (long)ldx, n, g.beta, npad, thetas, G, d,
                        g.gth_kff);
     const int tot = L * G + m * (d + 1) + 1;
