@@ -228,7 +228,7 @@ int mfgp_selftest_mfma(mfgp_handle_t h, double* out);
  * (N_L = 16384, N_H = 2048, D = 10, P = 512): the reference forces fp64 (linear.py:63-64), so
  * its semantics are the fp64 ones computed in fp32 -- r^2 in direct-difference form (not
  * GPflow's expanded form, which cancels in fp32), every GEMM on v_mfma_f32_32x32x2_f32, the
- * LML / gradient reductions in fp64.  Tolerances against the fp64 oracle: DESIGN.md §9. */
+ * LML / gradient reductions in fp64.  Tolerances against the fp64 oracle: DESIGN.md §8. */
 #define MFGP_F64 0
 #define MFGP_F32 1
 /* fp32 path: 128-wide tile columns per outer Cholesky panel (default 4; env MFGP_F32_PANEL). */

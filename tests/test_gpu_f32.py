@@ -3,7 +3,7 @@ and against the HIP fp64 path, through the C-ABI.
 
 The reference forces fp64 (mfgpflow/linear.py:63-64); BASELINE configs[4] ("Synth", N_L = 16384,
 N_H = 2048, D = 10, P = 512) asks for fp32.  fp32 results differ from fp64 by the conditioning of
-K + s2 I (s2 = 1e-3), so the tolerances here are measured, with margin (DESIGN.md §9):
+K + s2 I (s2 = 1e-3), so the tolerances here are measured, with margin (DESIGN.md §8):
 
   size                        LML (rel)   gradient (rel. to max |g|)  mean (rel. to max |mean|)  var (abs)
   n <= 2300 vs oracle         1e-4        3e-4                        1e-2                       5e-5
