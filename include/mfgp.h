@@ -231,7 +231,7 @@ int mfgp_selftest_mfma(mfgp_handle_t h, double* out);
  * LML / gradient reductions in fp64.  Tolerances against the fp64 oracle: DESIGN.md §8. */
 #define MFGP_F64 0
 #define MFGP_F32 1
-/* fp32 path: 128-wide tile columns per outer Cholesky panel (default 4; env MFGP_F32_PANEL). */
+/* fp32 path: 128-wide tile columns per outer Cholesky panel (default 6; env MFGP_F32_PANEL). */
 int mfgp_set_f32_panel(mfgp_handle_t h, int tiles);
 /* fp32 path: 1 (default; env MFGP_F32_LOOKAHEAD) factors the next panel on a high-priority side
  * stream beside the trailing update (fork / join events, graph-capturable); 0: one stream. */

@@ -533,7 +533,7 @@ int mfgp_create(int device, mfgp_handle_t* out) {
     h->ncu = ncu;
     h->flow_wgs = ncu;
     h->flow_timeout = FLOW_TIMEOUT_TICKS;
-    h->f32_panel = 4;
+    h->f32_panel = 6;
     h->f32_lookahead = 1;
     h->f32_reserve = 32;
     if (const char* rv = getenv("MFGP_F32_RESERVE")) h->f32_reserve = std::max(0, atoi(rv));

@@ -112,19 +112,48 @@ __device__ __forceinline__ void stage_mma(Acc& acc, const float* sm) {
 }
 
 // acc += A[0:128, 0:32 nk] * B[0:128, 0:32 nk]^T (row-major, 16-B aligned rows).  Ends with a
-// barrier, so two calls may follow each other on the same LDS.
+// barrier, so two calls may follow each other on the same LDS.  Global loads run TWO K-steps
+// ahead of the MFMAs (two register stages, the loop unrolled by two so each stage is a
+// compile-time register set): at ~4k MFMA cycles per K-step, one step of lead did not cover the
+// L2 / Infinity Cache latency under load.  Cpre (optional): the C tile this workgroup will
+// update, loaded into *cv during the last K-step, so the epilogue does not start with a
+// round trip to memory.
+__device__ __forceinline__ void c_tile_load(float (&cv)[2][2][16], const float* __restrict__ C, long ld) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) cv[m][n][r] = C[(long)acc_row(m, r) * ld + acc_col(n)];
+}
+
 __device__ __forceinline__ void gemm_nt(Acc& acc, const float* __restrict__ A, long lda, const float* __restrict__ B,
-                                        long ldb, int nk, float* smem) {
-    StageRegs st;
-    stage_fetch(st, A, lda, B, ldb, 0);
-    stage_put(smem, st);
+                                        long ldb, int nk, float* smem, const float* Cpre = nullptr, long ldc = 0,
+                                        float (*cv)[2][16] = nullptr) {
+    StageRegs s0, s1;
+    stage_fetch(s0, A, lda, B, ldb, 0);
+    if (nk > 1) stage_fetch(s1, A, lda, B, ldb, BK);
+    stage_put(smem, s0);
+    if (nk > 2) stage_fetch(s0, A, lda, B, ldb, 2 * BK);
     __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-        const bool more = kt + 1 < nk;
-        if (more) stage_fetch(st, A, lda, B, ldb, (kt + 1) * BK);
-        stage_mma(acc, smem + (kt & 1) * STAGE);
-        if (more) stage_put(smem + ((kt + 1) & 1) * STAGE, st);
+    // invariant at even kt: buffer 0 holds step kt, s1 step kt+1, s0 step kt+2
+    for (int kt = 0; kt < nk; kt += 2) {
+        if (Cpre && kt + 1 >= nk) c_tile_load(*reinterpret_cast<float(*)[2][2][16]>(cv), Cpre, ldc);
+        stage_mma(acc, smem);
+        if (kt + 1 < nk) {
+            stage_put(smem + STAGE, s1);
+            if (kt + 3 < nk) stage_fetch(s1, A, lda, B, ldb, (kt + 3) * BK);
+        }
         __syncthreads();
+        if (kt + 1 < nk) {
+            if (Cpre && kt + 2 >= nk) c_tile_load(*reinterpret_cast<float(*)[2][2][16]>(cv), Cpre, ldc);
+            stage_mma(acc, smem + STAGE);
+            if (kt + 2 < nk) {
+                stage_put(smem, s0);
+                if (kt + 4 < nk) stage_fetch(s0, A, lda, B, ldb, (kt + 4) * BK);
+            }
+            __syncthreads();
+        }
     }
 }
 
@@ -136,21 +165,19 @@ __device__ __forceinline__ void acc_store(const Acc& a, float* __restrict__ C, l
 #pragma unroll
             for (int r = 0; r < 16; ++r) C[(long)acc_row(m, r) * ld + acc_col(n)] = a.c[m][n][r];
 }
-// C -= acc, all C loads issued before the first store
+// C -= acc, one 32 x 32 block at a time (16 loads in flight, then 16 stores: the registers the
+// loads need stay within the GEMM loop's budget)
 __device__ __forceinline__ void acc_sub_into(const Acc& a, float* __restrict__ C, long ld) {
-    float v[2][2][16];
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
-        for (int n = 0; n < 2; ++n)
+        for (int n = 0; n < 2; ++n) {
+            float v[16];
 #pragma unroll
-            for (int r = 0; r < 16; ++r) v[m][n][r] = C[(long)acc_row(m, r) * ld + acc_col(n)];
+            for (int r = 0; r < 16; ++r) v[r] = C[(long)acc_row(m, r) * ld + acc_col(n)];
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-        for (int n = 0; n < 2; ++n)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) C[(long)acc_row(m, r) * ld + acc_col(n)] = v[m][n][r] - a.c[m][n][r];
+            for (int r = 0; r < 16; ++r) C[(long)acc_row(m, r) * ld + acc_col(n)] = v[r] - a.c[m][n][r];
+        }
 }
 
 // ---------------------------------------------------------------- geometry
