@@ -51,4 +51,15 @@ def test_host_only_entry_points(lib):
     # argument validation happens before any device work
     assert lib.mfgp_gpr_lml(h, 0, 1, 1, None, 2, None, 1, None, 0, None, 0, None, None) == -1
     assert lib.mfgp_mf_gram(h, 4, 4, 1, None, 2, None, 2, None, 0.0, None, 4) == -1
+    # dtype-generic forms: MFGP_F64 (0) is the fp64 entry, MFGP_F32 (1) the fp32 tall-matrix layout
+    s64, s32 = C.c_size_t(), C.c_size_t()
+    assert lib.mfgp_gpr_workspace_size_ex(h, 0, 1164, 64, 10, C.byref(s64)) == 0
+    assert lib.mfgp_gpr_workspace_size(h, 1164, 64, 10, C.byref(sz)) == 0 and s64.value == sz.value
+    assert lib.mfgp_gpr_workspace_size_ex(h, 1, 18432, 512, 10, C.byref(s32)) == 0
+    # M = (T + Tp + T) x 128 rows of Npad floats (K, Y^T, identity rows) = 2.76 GB at the Synth config
+    assert 2.7e9 < s32.value < 2.9e9
+    assert lib.mfgp_gpr_workspace_size_ex(h, 2, 1164, 64, 10, C.byref(sz)) == -1     # unknown dtype
+    assert lib.mfgp_gpr_lml_ex(h, 1, 0, 1, 1, None, 2, None, 1, None, 0, None, 0, None, None) == -1
+    assert lib.mfgp_set_f32_panel(h, 0) == -1 and lib.mfgp_set_f32_panel(h, 6) == 0
+    assert lib.mfgp_set_f32_reserve(h, -1) == -1 and lib.mfgp_set_f32_reserve(h, 32) == 0
     assert lib.mfgp_destroy(h) == 0
