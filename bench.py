@@ -289,8 +289,8 @@ def bench_svgp(args):
 
     sb = M.SingleBinSVGP(X, Yr, kern(), kern(), pr, Z=np.zeros((300, d + 1)))
     dt_sb, _ = timed(sb, K + W)
-    lat = M.LatentMFCoregionalizationSVGP(X, Yr, kern(), kern(), num_latents=15, num_inducing=300, num_outputs=pr,
-                                          w_type="diagonal", window_fraction=0.4, scale=0.2)
+    lat = M.LatentMFCoregionalizationSVGP(X, Yr, kern(), kern(), num_latents=min(15, pr), num_inducing=300,
+                                          num_outputs=pr, w_type="diagonal", window_fraction=0.4, scale=0.2)
     dt_lat, _ = timed(lat, max(K + W, 2000))
     # notebook protocol for the single-bin model: a fresh model, optimize(max_iters=1000, initial_lr=0.1)
     train_s = None
@@ -314,7 +314,8 @@ def bench_svgp(args):
             "data": "Goku z=0 P(k) (reference data files, tests/golden/data), RCCL-broadcast from rank 0",
             "config": {"workload": "goku_singlebin_svgp_step", "n": n, "d": d, "m": 300, "latents": pr,
                        "bins_per_rank": pr, "parallelism": f"bins{world}" if world > 1 else "single"},
-            "latent_l15": {"ms_per_step": round(dt_lat / K * 1e3, 4), "iters_per_s": round(world * K / dt_lat, 3),
+            "latent_l15": {"latents": min(15, pr), "ms_per_step": round(dt_lat / K * 1e3, 4),
+                           "iters_per_s": round(world * K / dt_lat, 3),
                            "published_m1_s_per_iter": round(1020.22 / 2000, 4)},
             "train_1000_predict_s": None if train_s is None else round(train_s, 3),
             "published_m1": {"train_1000_s": 2237.47, "source": "notebooks/demo: goku power spectra.ipynb:451"},

@@ -30,7 +30,7 @@ pytestmark = pytest.mark.gpu
 def eng():
     e = Engine.get()
     yield e
-    e.set_f32_panel(4)
+    e.set_f32_panel(6)   # the handle default (mfgp_capi.hip)
     e.set_f32_lookahead(True)
 
 

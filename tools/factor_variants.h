@@ -629,4 +629,269 @@ __device__ __forceinline__ void tile_potrf_inv_w2_acc(f64x4 aA, double* __restri
 // NB = 32 uses the single-wave form (9.1k shader clocks vs 12.7k for the 4-wave MFMA 4-pivot
 // form and 15.5k for the pivot form: tools/ubench_w1.hip, tools/ubench_tile.hip).
 
+// ---------------------------------------------------------------- split diag factor (lost)
+// Measured round 2 (tools/ubench_w1.hip, "s2 lds"): A wave alone 5.0-5.5k clocks, but the whole
+// factor 7.9k against 8.2k for w1: whoever re-derives the 4x4 LDL^T for the inverse (the L wave,
+// ~950 clocks a round) trails the A wave, and the last round's LDL -> R update -> scale chain is
+// a ~1.2k-clock tail.  Posting the LDL from the A wave (one lane's 14 mailbox stores) instead
+// costs its chain ~200 clocks a round.  Not used by the engine.
+// The w1 factor with its inverse work moved to a second wave on another SIMD: in w1 the R work
+// of the 8 rounds costs ~2.9k of the ~8.2k clocks (tools/ubench_w1.hip, "A wave alone").
+// The A wave runs only the elimination chain (publish the pivot rows, 4x4 LDL^T, own-row
+// substitution, rank-4 MFMA update of A).  Round K's pivot rows go to their own LDS panel
+// Pn + 128 K; lane 0 posts the round's LDL^T (1/d, L, d) to the mailbox mb + 16 K and then raises
+// *flag to base + K + 1 (the DS operations of one wave are processed in issue order, so the
+// mailbox and panel writes land before the flag).  The R wave spins on the flag, reads the
+// mailbox and its own rows of the panel, forms W_R and applies R -= W_R R[P, :] with the same
+// instructions as w1; a third wave (S) turns the posted pivots into L_ii, 1/L_ii and the first bad
+// pivot, and the R wave scales its rows by them on the way out: D = L^{-1}, L_ii and *bad as
+// tile_potrf_inv_w1_wave writes them (identical bits).
+// Pn: 8 x 128 doubles of LDS that may alias X (the A wave reads X before it first writes Pn;
+// the R wave never reads X).  mb: 8 x 16 doubles, sc: 32 doubles of LDS; flag, sflag: LDS ints,
+// monotonic across calls (call c uses base = 8 c).
+struct S2Ldl {
+    double i0, i1, i2, i3, L10, L20, L30, L21, L31, L32, d0, d1, d2, d3;
+};
+
+__device__ __forceinline__ S2Ldl s2_ldl(const double* __restrict__ P, int K) {
+    const f64x2* Pm = reinterpret_cast<const f64x2*>(P + 16 * K);
+    const f64x2 c0a = Pm[0], c0b = Pm[1], c1a = Pm[2], c1b = Pm[3], c2b = Pm[5], c3b = Pm[7];
+    S2Ldl s;
+    const double m00 = c0a.x, m10 = c0a.y, m20 = c0b.x, m30 = c0b.y;
+    const double m11 = c1a.y, m21 = c1b.x, m31 = c1b.y, m22 = c2b.x, m32 = c2b.y, m33 = c3b.y;
+    s.d0 = m00;
+    s.i0 = rcp_nr1(m00);
+    s.L10 = m10 * s.i0; s.L20 = m20 * s.i0; s.L30 = m30 * s.i0;
+    s.d1 = fma(-s.L10, m10, m11);
+    s.i1 = rcp_nr1(s.d1);
+    const double e21 = fma(-s.L20, m10, m21), e31 = fma(-s.L30, m10, m31);
+    s.L21 = e21 * s.i1; s.L31 = e31 * s.i1;
+    s.d2 = fma(-s.L21, e21, fma(-s.L20, m20, m22));
+    s.i2 = rcp_nr1(s.d2);
+    const double e32 = fma(-s.L31, e21, fma(-s.L30, m20, m32));
+    s.L32 = e32 * s.i2;
+    s.d3 = fma(-s.L32, e32, fma(-s.L31, e31, fma(-s.L30, m30, m33)));
+    s.i3 = rcp_nr1(s.d3);
+    return s;
+}
+
+// y = C L_M^{-T} for the row held in (ua, ub)
+__device__ __forceinline__ void s2_y(const S2Ldl& s, f64x2 ua, f64x2 ub, double y[4]) {
+    y[0] = ua.x;
+    y[1] = fma(-s.L10, y[0], ua.y);
+    y[2] = fma(-s.L21, y[1], fma(-s.L20, y[0], ub.x));
+    y[3] = fma(-s.L32, y[2], fma(-s.L31, y[1], fma(-s.L30, y[0], ub.y)));
+}
+
+template <int K>
+__device__ __forceinline__ void s2_round_a(double* __restrict__ Pn, int* flag, int base,
+                                           f64x4& a00, f64x4& a01, f64x4& a11, int l, long long* tr) {
+    if constexpr (K < 8) {
+        constexpr int bk = K >> 2, kq = K & 3;
+        const int lc = l & 15, kk = l >> 4;
+        double* P = Pn + 128 * K;
+        if constexpr (bk == 0) P[lc * 4 + kk] = a00[kq];
+        P[(16 + lc) * 4 + kk] = (bk == 0) ? a01[kq] : a11[kq];
+        asm volatile("" ::: "memory");
+        const f64x2* Pr = reinterpret_cast<const f64x2*>(P);
+        f64x2 u0a = {0.0, 0.0}, u0b = {0.0, 0.0};
+        if constexpr (bk == 0) { u0a = Pr[2 * lc]; u0b = Pr[2 * lc + 1]; }
+        const f64x2 u1a = Pr[2 * (16 + lc)], u1b = Pr[2 * (16 + lc) + 1];
+        const S2Ldl s = s2_ldl(P, K);
+        __builtin_amdgcn_sched_barrier(0);
+        // the LDL^T consumed the panel reads, so the panel writes have landed too
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (l == 0) {
+            __hip_atomic_store(flag, base + K + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (tr) tr[K] = __builtin_amdgcn_s_memtime();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (K < 7) {   // the last round's pivots leave nothing below them to update
+            double zA[2], yB[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                if (h < bk) { zA[h] = 0.0; yB[h] = 0.0; continue; }
+                const bool below = (h > bk) || ((lc >> 2) > kq);
+                double y[4];
+                s2_y(s, h ? u1a : u0a, h ? u1b : u0b, y);
+                const double z = sel4(kk, y[0] * s.i0, y[1] * s.i1, y[2] * s.i2, y[3] * s.i3);
+                zA[h] = below ? z : 0.0;
+                yB[h] = sel4(kk, y[0], y[1], y[2], y[3]);
+            }
+            if constexpr (bk == 0) {
+                if constexpr (K < 3) {
+                    a00 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[0], yB[0], a00, 0, 0, 0);
+                    a01 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[0], yB[1], a01, 0, 0, 0);
+                }
+                a11 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[1], yB[1], a11, 0, 0, 0);
+            } else {
+                a11 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[1], yB[1], a11, 0, 0, 0);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        s2_round_a<K + 1>(Pn, flag, base, a00, a01, a11, l, tr);
+    }
+}
+
+template <int K>
+__device__ __forceinline__ void s2_round_r(const double* __restrict__ Pn, const double* __restrict__ mb,
+                                           const int* flag, int base, f64x4& r00, f64x4& r10, f64x4& r11,
+                                           int l, long long* tr) {
+    if constexpr (K < 8) {
+        constexpr int bk = K >> 2, kq = K & 3;
+        const int lc = l & 15, kk = l >> 4, p = lc & 3;
+        while (__builtin_amdgcn_readfirstlane(
+                   __hip_atomic_load(const_cast<int*>(flag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) <
+               base + K + 1) {
+            // the A wave's panel round trips queue behind a tight poll: sleep except for the last
+            // round, when the A wave has no LDS traffic left
+            if constexpr (K < 7) __builtin_amdgcn_s_sleep(1);
+        }
+        if (tr && l == 0) tr[8 + K] = __builtin_amdgcn_s_memtime();
+        asm volatile("" ::: "memory");
+        const f64x2* m = reinterpret_cast<const f64x2*>(mb + 16 * K);
+        const f64x2 m0 = m[0], m1 = m[1], m2 = m[2], m3 = m[3], m4 = m[4], m5 = m[5], m6 = m[6];
+        const f64x2* Pr = reinterpret_cast<const f64x2*>(Pn + 128 * K);
+        f64x2 u0a = {0.0, 0.0}, u0b = {0.0, 0.0};
+        if constexpr (bk == 0) { u0a = Pr[2 * lc]; u0b = Pr[2 * lc + 1]; }
+        const f64x2 u1a = Pr[2 * (16 + lc)], u1b = Pr[2 * (16 + lc) + 1];
+        S2Ldl s;
+        s.i0 = m0.x; s.i1 = m0.y; s.i2 = m1.x; s.i3 = m1.y; s.L10 = m2.x; s.L20 = m2.y;
+        s.L30 = m3.x; s.L21 = m3.y; s.L31 = m4.x; s.L32 = m4.y; s.d0 = m5.x; s.d1 = m5.y;
+        s.d2 = m6.x; s.d3 = m6.y;
+        double wR[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (h < bk) { wR[h] = 0.0; continue; }
+            const bool piv = (h == bk) && ((lc >> 2) == kq);
+            const bool below = (h > bk) || ((lc >> 2) > kq);
+            double y[4], v[4];
+            s2_y(s, h ? u1a : u0a, h ? u1b : u0b, y);
+            v[0] = y[0] * s.i0; v[1] = y[1] * s.i1; v[2] = y[2] * s.i2; v[3] = y[3] * s.i3;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v[c] = piv ? (p == c ? 1.0 : 0.0) : v[c];
+            const double x3 = v[3];
+            const double x2 = fma(-s.L32, x3, v[2]);
+            const double x1 = fma(-s.L31, x3, fma(-s.L21, x2, v[1]));
+            const double x0 = fma(-s.L30, x3, fma(-s.L20, x2, fma(-s.L10, x1, v[0])));
+            const double xk = sel4(kk, x0, x1, x2, x3);
+            wR[h] = below ? xk : piv ? ((p == kk ? 1.0 : 0.0) - xk) : 0.0;
+        }
+        if constexpr (bk == 0) {
+            const double pR0 = r00[kq];
+            r00 = __builtin_amdgcn_mfma_f64_16x16x4f64(-wR[0], pR0, r00, 0, 0, 0);
+            r10 = __builtin_amdgcn_mfma_f64_16x16x4f64(-wR[1], pR0, r10, 0, 0, 0);
+        } else {
+            const double pR0 = r10[kq], pR1 = r11[kq];
+            r10 = __builtin_amdgcn_mfma_f64_16x16x4f64(-wR[1], pR0, r10, 0, 0, 0);
+            r11 = __builtin_amdgcn_mfma_f64_16x16x4f64(-wR[1], pR1, r11, 0, 0, 0);
+        }
+        if (tr && l == 0) tr[16 + K] = __builtin_amdgcn_s_memtime();
+        s2_round_r<K + 1>(Pn, mb, flag, base, r00, r10, r11, l, tr);
+    }
+}
+
+// A wave: X (lower triangle, stride ldx) -> elimination; returns when its last panel is out.
+__device__ __forceinline__ void tile_potrf_inv_s2_a(const double* __restrict__ X, int ldx, double* __restrict__ Pn,
+                                                    int* flag, int base,
+                                                    long long* tr = nullptr) {
+    const int l = threadIdx.x & 63, lc = l & 15, lr = l >> 4;
+    f64x4 a00, a01, a11;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int r = lr + 4 * q;
+        const int hi = r > lc ? r : lc, lo = r > lc ? lc : r;
+        a00[q] = X[hi * ldx + lo];
+        a11[q] = X[(16 + hi) * ldx + 16 + lo];
+        a01[q] = X[(16 + lc) * ldx + r];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // X fully read before Pn (may alias) is written
+    s2_round_a<0>(Pn, flag, base, a00, a01, a11, l, tr);
+}
+
+// L wave: re-derives each round's 4x4 LDL^T from the A wave's panel and posts it to the mailbox
+// (the A wave itself never writes the mailbox: one lane's stores there cost its chain ~200 clocks
+// a round), then raises *lflag to base + K + 1.
+__device__ __forceinline__ void tile_potrf_inv_s2_l(const double* __restrict__ Pn, double* __restrict__ mb,
+                                                    const int* flag, int* lflag, int base) {
+    const int l = threadIdx.x & 63;
+#pragma unroll
+    for (int K = 0; K < 8; ++K) {
+        while (__builtin_amdgcn_readfirstlane(
+                   __hip_atomic_load(const_cast<int*>(flag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) <
+               base + K + 1)
+            __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");
+        const S2Ldl s = s2_ldl(Pn + 128 * K, K);
+        if (l == 0) {
+            double* m = mb + 16 * K;
+            m[0] = s.i0; m[1] = s.i1; m[2] = s.i2; m[3] = s.i3; m[4] = s.L10; m[5] = s.L20; m[6] = s.L30;
+            m[7] = s.L21; m[8] = s.L31; m[9] = s.L32; m[10] = s.d0; m[11] = s.d1; m[12] = s.d2; m[13] = s.d3;
+            asm volatile("" ::: "memory");
+            __hip_atomic_store(lflag, base + K + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+}
+
+// S wave: 1/sqrt(d) of every pivot into sc[0..31], L_ii = sqrt(d) into dg, the first bad pivot
+// into *bad; then raises *sflag to base + 8.  Off both chains: its rounds are a few lanes' work.
+__device__ __forceinline__ void tile_potrf_inv_s2_s(const double* __restrict__ mb, const int* flag, int* sflag,
+                                                    int base, double* __restrict__ sc, double* __restrict__ dg,
+                                                    int* __restrict__ bad) {
+    const int l = threadIdx.x & 63;
+    int first = 0;
+    for (int K = 0; K < 8; ++K) {
+        while (__builtin_amdgcn_readfirstlane(
+                   __hip_atomic_load(const_cast<int*>(flag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) <
+               base + K + 1)
+            __builtin_amdgcn_s_sleep(1);
+        const double d = mb[16 * K + 10 + (l & 3)];
+        const double r = rsq_nr(d);
+        if (l < 4) { sc[4 * K + l] = r; dg[4 * K + l] = d * r; }
+        const unsigned long long m = __ballot(l < 4 && !(d > 0.0 && d < INFINITY));
+        if (first == 0 && m) first = 4 * K + __ffsll((long long)m);
+    }
+    if (l == 0) *bad = first;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (l == 0) __hip_atomic_store(sflag, base + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// R wave: follows the A wave's rounds, builds L^{-1}; with the S wave's scales writes R (stride S).
+__device__ __forceinline__ void tile_potrf_inv_s2_r(const double* __restrict__ Pn, const double* __restrict__ mb,
+                                                    const int* flag, const int* sflag, int base,
+                                                    const double* __restrict__ sc, double* __restrict__ R,
+                                                    long long* tr = nullptr) {
+    constexpr int S = TileCfg<32>::S;
+    const int l = threadIdx.x & 63, lc = l & 15, lr = l >> 4;
+    f64x4 r00, r10 = {0.0, 0.0, 0.0, 0.0}, r11;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        r00[q] = (lr + 4 * q == lc) ? 1.0 : 0.0;
+        r11[q] = r00[q];
+    }
+    s2_round_r<0>(Pn, mb, flag, base, r00, r10, r11, l, tr);
+    while (__builtin_amdgcn_readfirstlane(
+               __hip_atomic_load(const_cast<int*>(sflag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) <
+           base + 8) {}
+    asm volatile("" ::: "memory");
+    double s0[4], s1[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        s0[q] = sc[lr + 4 * q];
+        s1[q] = sc[16 + lr + 4 * q];
+    }
+    // all eight loads in flight at once (a select on a loaded value otherwise becomes a branch
+    // around the load: one LDS round trip per row)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) asm volatile("" :: "v"(s0[q]), "v"(s1[q]));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int r = lr + 4 * q;
+        R[r * S + lc] = (lc <= r) ? r00[q] * s0[q] : 0.0;
+        R[r * S + 16 + lc] = 0.0;
+        R[(16 + r) * S + lc] = r10[q] * s1[q];
+        R[(16 + r) * S + 16 + lc] = (lc <= r) ? r11[q] * s1[q] : 0.0;
+    }
+}
+
 }  // namespace mfgp
