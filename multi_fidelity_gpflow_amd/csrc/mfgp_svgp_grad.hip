@@ -258,113 +258,193 @@ __global__ __launch_bounds__(NTHREADS) void k_gw(const double* r, const double* 
 // For pairs (a in P1 = Z rows, b in P2), weight Wt[a][b] (padded row-major):
 //   gth[q] += sum Wt dk/dtheta_q     (q over [vL, lL(D), vD, lD(D), rho])
 //   gz[a][d] += zf * sum_b Wt dk(a, b)/dz_a[d]
-// One workgroup per (a-tile of 32 rows, b-chunk); thread: row a = t % 32, b stride 8.
-constexpr int KG_ROWS = 32, KG_COLS = 256;
+// With wl = Wt sa sb kL (the LF part of k) the dimension sums expand in moments of the b side:
+//   sum_b wl (za_d - xb_d)^2 = za_d^2 S0 - 2 za_d S1_d + S2_d,   sum_b wl (za_d - xb_d) = za_d S0 - S1_d
+// with [S0 | S1 | S2](a) = sum_b wl(a, b) [1 | xb | xb^2]: a GEMM of the pair weights with the
+// augmented b rows, on the matrix core (v_mfma_f64_16x16x4: lane (i, k) forms the weight of pair
+// (a_i, b_k) straight into its A operand; B = [1 | x | x^2] of b_k).  Likewise T for
+// wd = Wt kD (HF x HF pairs, only when the wave holds one).  Coordinates are taken relative to
+// the block's first Z row, which keeps the expansion's cancellation at the data's spread.
+// The per-pair work left on the VALU is r^2 and one exp (two for HF x HF pairs).
+// Workgroup: 32 a rows x KG_COLS b columns; wave w: rows 16 (w & 1) .., b half w >> 1; the b rows
+// go through LDS KG_CHUNK per half at a time, W is loaded one step ahead.
+constexpr int KG_ROWS = 32, KG_COLS = 256, KG_CHUNK = 32;
+template <int DC>
+constexpr int kg_ncb() { return (2 * DC + 1 + 15) / 16; }
+
 template <int DC>
 __global__ __launch_bounds__(NTHREADS) void k_kgrad(const double* P1, long ld1, int n1, const double* P2, long ld2,
                                                     int n2, const double* Wt, long ldw, long sW, const double* thetas,
                                                     int G, int D, double zf, int nbc, double* gth_part,
                                                     double* gz_part) {
-    __shared__ double wred[NTHREADS / 64][2 * DC + 4];
-    __shared__ double zsw[NTHREADS / 64][KG_ROWS][DC + 1];
-    const int l = blockIdx.z;
+    constexpr int NCB = kg_ncb<DC>(), SC = NCB * 16 + 1, XS = DC + 1;
+    constexpr int SACC = (NTHREADS / 64) * 16 * SC, XST = 2 * KG_CHUNK * XS;
+    __shared__ double il[DC], id[DC], cz[DC];
+    // the b rows of a chunk (centred; column DC holds the fidelity) during the pair loop, the
+    // moment accumulators after it
+    __shared__ double lds_buf[SACC > XST ? SACC : XST];
+    auto sacc = reinterpret_cast<double(*)[16][SC]>(lds_buf);
+    __shared__ double wred[NTHREADS / 64][4];
+    __shared__ double dsum[2][DC];
+    const int lat = blockIdx.z;
     const int at = blockIdx.x / nbc, bc = blockIdx.x % nbc;
-    const int t = threadIdx.x;
-    const int ar = t % KG_ROWS, bs = t / KG_ROWS;   // 8 column lanes per row
-    const int a = at * KG_ROWS + ar;
-    const MFTheta th{thetas + (long)l * G, D};
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    const int li = l & 15, lk = l >> 4;
+    const MFTheta th{thetas + (long)lat * G, D};
     const double vL = th.vL(), vD = th.vD(), rho = th.rho();
-    // inverse lengthscales of the latent in LDS (every thread reads the same word: a broadcast),
-    // which keeps 2 DC doubles out of the register file of the pair loop
-    __shared__ double il[DC], id[DC];
     if (t < DC) {
         il[t] = (t < D) ? 1.0 / th.lL(t) : 0.0;
         id[t] = (t < D) ? 1.0 / th.lD(t) : 0.0;
+        cz[t] = (t < D) ? P1[(long)(at * KG_ROWS) * ld1 + t] : 0.0;
+        dsum[0][t] = 0.0;
+        dsum[1][t] = 0.0;
     }
     __syncthreads();
-    double gl[DC], gd[DC], gz[DC];
+    const int a = at * KG_ROWS + 16 * (w & 1) + li;
+    const double fa = (a < n1) ? P1[(long)a * ld1 + D] : -1.0;
+    const bool La = (fa == 0.0), Ha = (fa == 1.0), aval = La || Ha;
+    double za[DC];
+#pragma unroll
+    for (int d = 0; d < DC; ++d) za[d] = (aval && d < D) ? P1[(long)a * ld1 + d] - cz[d] : 0.0;
+    f64x4 accL[NCB], accD[NCB];
+#pragma unroll
+    for (int c = 0; c < NCB; ++c) { accL[c] = f64x4{0.0, 0.0, 0.0, 0.0}; accD[c] = accL[c]; }
     double gvL = 0.0, gvD = 0.0, grho = 0.0;
+    const double sa = La ? 1.0 : rho;
+    const int half = w >> 1;
+    const int bbase = bc * KG_COLS;
+    const int bend = min(n2, bbase + KG_COLS);
+    const double* wrow = Wt + lat * sW + (long)a * ldw;
+    // b rows are staged KG_CHUNK per half at a time: [half][row][XS]
+    for (int c0 = 0; c0 < KG_COLS / 2; c0 += KG_CHUNK) {
+        __syncthreads();   // the previous chunk is consumed
+        for (int e = t; e < 2 * KG_CHUNK * XS; e += NTHREADS) {
+            const int hf = e / (KG_CHUNK * XS), rem = e % (KG_CHUNK * XS);
+            const int r = rem / XS, d = rem % XS;
+            const int b = bbase + (KG_COLS / 2) * hf + c0 + r;
+            double v = (d == DC) ? -1.0 : 0.0;
+            if (b < bend) {
+                if (d < D) v = P2[(long)b * ld2 + d] - cz[d];
+                else if (d == DC) v = P2[(long)b * ld2 + D];
+            }
+            lds_buf[e] = v;
+        }
+        __syncthreads();
+        const double* xs = lds_buf + half * KG_CHUNK * XS;
+        const int bh0 = bbase + (KG_COLS / 2) * half + c0;
+        // W of the first step; each step loads the next one's before its own work
+        double wnext = 0.0;
+        {
+            const int b = bh0 + lk;
+            if (aval && b < bend) wnext = wrow[b];
+        }
+        for (int s4 = 0; s4 < KG_CHUNK; s4 += 4) {
+            const int r = s4 + lk, b = bh0 + r;
+            double wv = wnext;
+            {
+                const int bn = b + 4;
+                wnext = (aval && s4 + 4 < KG_CHUNK && bn < bend) ? wrow[bn] : 0.0;
+            }
+            const double* xr = xs + r * XS;
+            const double fb = xr[DC];
+            const bool Lb = (fb == 0.0), Hb = (fb == 1.0);
+            if (!(Lb || Hb)) wv = 0.0;
+            double rL = 0.0;
 #pragma unroll
-    for (int d = 0; d < DC; ++d) {
-        gl[d] = 0.0; gd[d] = 0.0; gz[d] = 0.0;
-    }
-    if (a < n1) {
-        const double fa = P1[(long)a * ld1 + D];
-        const bool La = (fa == 0.0), Ha = (fa == 1.0);
-        if (La || Ha) {
-            double za[DC];
-#pragma unroll
-            for (int d = 0; d < DC; ++d) za[d] = (d < D) ? P1[(long)a * ld1 + d] : 0.0;
-            const int b0 = bc * KG_COLS, b1 = min(n2, b0 + KG_COLS);
-            for (int b = b0 + bs; b < b1; b += NTHREADS / KG_ROWS) {
-                const double w = Wt[l * sW + (long)a * ldw + b];
-                if (w == 0.0) continue;
-                const double fb = P2[(long)b * ld2 + D];
-                const bool Lb = (fb == 0.0), Hb = (fb == 1.0);
-                if (!(Lb || Hb)) continue;
-                double rL = 0.0, rD = 0.0, dl[DC];
+            for (int d = 0; d < DC; ++d) {
+                const double xl = (za[d] - xr[d]) * il[d];
+                rL = fma(xl, xl, rL);
+            }
+            const double sb = Lb ? 1.0 : rho;
+            const double kL = vL * exp(-0.5 * rL);
+            const double wl = wv * sa * sb * kL;
+            gvL += wl;
+            grho += wv * ((Ha ? sb : 0.0) + (Hb ? sa : 0.0)) * kL;
+            const bool hh = Ha && Hb && wv != 0.0;
+            const bool anyhh = __ballot(hh) != 0;   // wave-uniform
+            double wd = 0.0;
+            if (anyhh) {
+                double rD = 0.0;
 #pragma unroll
                 for (int d = 0; d < DC; ++d) {
-                    dl[d] = (d < D) ? za[d] - P2[(long)b * ld2 + d] : 0.0;
-                    const double xl = dl[d] * il[d], xd = dl[d] * id[d];
-                    rL += xl * xl;
-                    rD += xd * xd;
+                    const double xd = (za[d] - xr[d]) * id[d];
+                    rD = fma(xd, xd, rD);
                 }
-                const double sa = La ? 1.0 : rho, sb = Lb ? 1.0 : rho;
-                const double kL = vL * exp(-0.5 * rL);
-                const double wl = w * sa * sb * kL;
-                gvL += wl / vL;
-                grho += w * ((Ha ? sb : 0.0) + (Hb ? sa : 0.0)) * kL;
-                const bool hh = Ha && Hb;
-                const double kD = hh ? vD * exp(-0.5 * rD) : 0.0;
-                const double wd = w * kD;
-                if (hh) gvD += wd / vD;
+                wd = hh ? wv * vD * exp(-0.5 * rD) : 0.0;
+                gvD += wd;
+            }
+            // B operand: column j of [1 | x | x^2] of row b_k (rows past the end are zero and
+            // carry zero weight)
 #pragma unroll
-                for (int d = 0; d < DC; ++d) {
-                    const double tl = dl[d] * il[d] * il[d];   // (x_a - x_b) / l^2
-                    gl[d] += wl * tl * dl[d] * il[d];          // dk/dl = k (x_a - x_b)^2 / l^3
-                    gz[d] -= wl * tl;
-                    if (hh) {
-                        const double td = dl[d] * id[d] * id[d];
-                        gd[d] += wd * td * dl[d] * id[d];
-                        gz[d] -= wd * td;
-                    }
+            for (int c = 0; c < NCB; ++c) {
+                const int j = 16 * c + li;
+                double bv = 0.0;
+                if (j == 0) bv = (b < bend) ? 1.0 : 0.0;
+                else if (j <= D) bv = xr[j - 1];
+                else if (j <= 2 * D) {
+                    const double x = xr[j - 1 - D];
+                    bv = x * x;
                 }
+                accL[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(wl, bv, accL[c], 0, 0, 0);
+                if (anyhh) accD[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(wd, bv, accD[c], 0, 0, 0);
             }
         }
     }
-    // theta partials: wave shuffles, one LDS slot per (entry, wave), ONE barrier (a tree
-    // reduction per entry cost 9 barriers x G entries, ten times the pair loop itself)
-    const int lane = t & 63, wv = t >> 6;
-    auto put = [&](double v, int q) {
-        v = wave_sum(v);
-        if (lane == 0) wred[wv][q] = v;
-    };
-    put(gvL, 0);
-#pragma unroll
-    for (int d = 0; d < DC; ++d)
-        if (d < D) put(gl[d], 1 + d);
-    put(gvD, 1 + D);
-#pragma unroll
-    for (int d = 0; d < DC; ++d)
-        if (d < D) put(gd[d], 2 + D + d);
-    put(grho, 2 + 2 * D);
-    // z partials of the tile's rows: the two column lanes of a row that share a wave (lanes
-    // ar and ar + 32) by one shuffle, the four waves through LDS
-#pragma unroll
-    for (int d = 0; d < DC; ++d) {
-        const double v = gz[d] + __shfl_xor(gz[d], 32, 64);
-        if (lane < 32 && d < D) zsw[wv][ar][d] = v;
+    __syncthreads();   // lds_buf becomes the moment buffer
+    // scalar theta partials: one LDS slot per wave
+    {
+        const double r0 = wave_sum(gvL), r1 = wave_sum(gvD), r2 = wave_sum(grho);
+        if (l == 0) { wred[w][0] = r0; wred[w][1] = r1; wred[w][2] = r2; }
     }
-    __syncthreads();
-    for (int q = t; q < G; q += NTHREADS)
-        gth_part[((long)l * gridDim.x + blockIdx.x) * G + q] =
-            (q == G - 1) ? 0.0 : (wred[0][q] + wred[1][q]) + (wred[2][q] + wred[3][q]);   // noise slot: 0
-    for (int e = t; e < KG_ROWS * D; e += NTHREADS) {
-        const int r = e / D, d = e % D;
+    // moments -> dimension sums, LF part (ph = 0) then HF part (ph = 1)
+    double gzv[(KG_ROWS * DC + NTHREADS - 1) / NTHREADS];
+#pragma unroll
+    for (int i = 0; i < (KG_ROWS * DC + NTHREADS - 1) / NTHREADS; ++i) gzv[i] = 0.0;
+#pragma unroll
+    for (int ph = 0; ph < 2; ++ph) {
+#pragma unroll
+        for (int c = 0; c < NCB; ++c)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sacc[w][lk + 4 * r][16 * c + li] = ph ? accD[c][r] : accL[c][r];
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < (KG_ROWS * DC + NTHREADS - 1) / NTHREADS; ++i) {
+            const int e = t + NTHREADS * i;
+            const int r = e & (KG_ROWS - 1), d = e / KG_ROWS;   // a half-wave per dimension
+            double term = 0.0;
+            if (d < D) {
+                const int hw = r >> 4, rr = r & 15;
+                const int ag = at * KG_ROWS + r;
+                auto S = [&](int col) { return sacc[hw][rr][col] + sacc[2 + hw][rr][col]; };
+                const double s0 = S(0), s1 = S(1 + d), s2 = S(1 + D + d);
+                const double z = (ag < n1) ? P1[(long)ag * ld1 + d] - cz[d] : 0.0;
+                const double ic = ph ? id[d] : il[d];
+                const double ic2 = ic * ic;
+                term = (z * z * s0 - 2.0 * z * s1 + s2) * ic2 * ic;   // d k / d l = k (za - xb)^2 / l^3
+                gzv[i] -= (z * s0 - s1) * ic2;
+            }
+            // sum over the 32 rows: the half-wave of this dimension
+#pragma unroll
+            for (int o = 16; o > 0; o >>= 1) term += __shfl_xor(term, o, 64);
+            if (r == 0 && d < D) dsum[ph][d] += term;   // one writer per (ph, d)
+        }
+        __syncthreads();
+    }
+    for (int q = t; q < G; q += NTHREADS) {
+        double v = 0.0;
+        if (q == 0) v = ((wred[0][0] + wred[1][0]) + (wred[2][0] + wred[3][0])) / vL;
+        else if (q <= D) v = dsum[0][q - 1];
+        else if (q == D + 1) v = ((wred[0][1] + wred[1][1]) + (wred[2][1] + wred[3][1])) / vD;
+        else if (q <= 2 * D + 1) v = dsum[1][q - D - 2];
+        else if (q == 2 * D + 2) v = (wred[0][2] + wred[1][2]) + (wred[2][2] + wred[3][2]);
+        gth_part[((long)lat * gridDim.x + blockIdx.x) * G + q] = v;   // noise slot (G - 1): 0
+    }
+#pragma unroll
+    for (int i = 0; i < (KG_ROWS * DC + NTHREADS - 1) / NTHREADS; ++i) {
+        const int e = t + NTHREADS * i;
+        const int r = e & (KG_ROWS - 1), d = e / KG_ROWS;
         const int ag = at * KG_ROWS + r;
-        const double v = (zsw[0][r][d] + zsw[1][r][d]) + (zsw[2][r][d] + zsw[3][r][d]);
-        gz_part[(((long)l * gridDim.x + blockIdx.x) * KG_ROWS + r) * D + d] = (ag < n1) ? zf * v : 0.0;
+        if (d < D) gz_part[(((long)lat * gridDim.x + blockIdx.x) * KG_ROWS + r) * D + d] = (ag < n1) ? zf * gzv[i] : 0.0;
     }
 }
 

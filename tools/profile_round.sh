@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round profile recipe (run on the GPU box from the repo root).  Usage:
-#   bash tools/profile_round.sh OUTDIR CONFIG "BENCH ARGS" "SHORT BENCH ARGS"
+#   bash tools/profile_round.sh OUTDIR CONFIG "BENCH ARGS" "SHORT BENCH ARGS" ["TRACE ARGS"]
 # 1. the bench JSON line;  2. rocprofv3 --kernel-trace --stats of the same command;
 # 3./4. HBM traffic FETCH_SIZE / WRITE_SIZE, 5. MFMA counters -- each in a separate --pmc pass of
 # the short command (MI355X_MICROARCH.md: counters in their own runs, no trace domains with --pmc).
@@ -10,10 +10,11 @@ OUT=${1:-gpurun_out/r02}
 CFG=${2:-goku}
 ARGS=${3:-}
 SHORT=${4:-"--steps 20 --warmup 5 --no-cpu-baseline --no-train-predict"}
+TRACE=${5:-$ARGS}
 mkdir -p "$OUT"
 timeout -k 10 400 python3 bench.py --config "$CFG" $ARGS > "$OUT/bench.json" 2> "$OUT/bench.err"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-    python3 bench.py --config "$CFG" $ARGS > "$OUT/bench_under_rocprof.json" 2> "$OUT/trace.err"
+    python3 bench.py --config "$CFG" $TRACE > "$OUT/bench_under_rocprof.json" 2> "$OUT/trace.err"
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
     python3 bench.py --config "$CFG" $SHORT > "$OUT/pmc_fetch.json" 2> "$OUT/pmc_fetch.err"
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
