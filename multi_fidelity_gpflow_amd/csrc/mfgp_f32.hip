@@ -399,18 +399,15 @@ __global__ __launch_bounds__(GT) void k32_gram(F32Args a) {
 // ---------------------------------------------------------------- K2a: diagonal block factor
 // L_kk = chol(M(k,k)) and D_k = L_kk^-1 of one 128 x 128 block: ONE workgroup of 4 waves, the
 // block and its inverse staged in LDS, blocked by 32:
-//   for s = 0..3:  wave 0 factors the 32 x 32 diagonal sub-block (factor32, below) -> L_ss, D_ss;
-//                  L_is = A_is D_ss^T (i > s) and A_ij -= L_is L_js^T (s < j <= i) on the MFMA
-//                  (v_mfma_f32_32x32x2_f32, one 32 x 32 x 32 product per wave at a time);
+//   for s = 0..3:  wave 0 factors the 32 x 32 diagonal sub-block in fp64 (factor32_w1, below) ->
+//                  D_ss, L_ii;  L_is = A_is D_ss^T (i >= s) and A_ij -= L_is L_js^T (s < j <= i)
+//                  on the MFMA (v_mfma_f32_32x32x2_f32, one 32 x 32 x 32 product per wave at a time);
 //   then the inverse's off-diagonal blocks D_ij = -D_ii sum_{m=j}^{i-1} L_im D_mj, row by row.
-// factor32 keeps the whole 32 x 32 problem in ONE wave's registers: lanes 0-31 hold the columns
-// of the (symmetric, unscaled) Schur complement, lanes 32-63 the columns of the running inverse;
-// pivot j broadcasts column j with v_readlane (scalar registers), so no pivot needs a barrier or
-// an LDS round trip:  A(r,c) -= A(r,j) A(j,c) / d_j  (c > j),  Y(r,c) -= A(r,j) Y(j,c) / d_j
-// (c <= j), rows r > j; the scaling by sqrt(d) is applied once at the end.
 constexpr int DIAG_THREADS = 256;
 constexpr int DLD = TB + 4;   // LDS row stride of the staged block / inverse (floats)
-constexpr size_t DIAG_SMEM = sizeof(float) * (2 * (size_t)TB * DLD + 3 * 32 * 33 + TB) + 16;
+constexpr int DIAG_R64 = 32 * TileCfg<32>::S;   // fp64 inverse of a 32 x 32 sub-block (w1 layout)
+constexpr size_t DIAG_SMEM = sizeof(float) * (2 * (size_t)TB * DLD + 3 * 32 * 33 + TB) + 16 +
+                             sizeof(double) * (DIAG_R64 + 32);
 
 // acc += A[0:32, 0:32] B[0:32, 0:32]^T (row-major LDS tiles, ld multiple of 4)
 __device__ __forceinline__ void mma32_nt(f32x16& acc, const float* A, int lda, const float* B, int ldb) {
@@ -446,44 +443,30 @@ __device__ __forceinline__ void acc32_load(f32x16& acc, const float* C, int ldc)
     for (int r = 0; r < 16; ++r) acc[r] = C[((r & 3) + 8 * (r >> 2) + 4 * (l >> 5)) * ldc + (l & 31)];
 }
 
-// One wave: L = chol(A_ss), D = L^-1 of the 32 x 32 sub-block at (S, S) of As / Ds; pivots
-// (non-positive ones replaced by 1, *bad = first such row + 1) into piv[S..S+31].
-__device__ __forceinline__ void factor32(float* As, float* Ds, int S, float* piv, int* bad) {
-    const int l = threadIdx.x & 63, c = l & 31;
-    const bool isA = l < 32;
-    float v[32];
+// One wave: the 32 x 32 sub-block at (S, S) through the fp64 single-wave factor of the fp64 path
+// (tile_potrf_inv_w1_wave, mfgp_device.h: 4 pivots a round on v_mfma_f64_16x16x4): the
+// lower triangle widened into X (fp64, stride 33; also its panel scratch), D = L^-1 rounded into
+// Ds, L_ii straight to ldiag.  (An fp32 one-wave factor that broadcast every pivot row with
+// v_readlane took ~10 us a sub-block: tools/ubench_f32diag.hip.)  L_ss itself is formed by the
+// panel step as A_ss D_ss^T.
+__device__ __forceinline__ void factor32_w1(float* As, float* Ds, int S, double* X, double* R, double* dg, int* badw,
+                                            int* bad, double* ldiag) {
+    const int l = threadIdx.x & 63;
 #pragma unroll
-    for (int r = 0; r < 32; ++r) {
-        const float a = (r >= c) ? As[(S + r) * DLD + S + c] : As[(S + c) * DLD + S + r];   // symmetric column
-        v[r] = isA ? a : (r == c ? 1.0f : 0.0f);
+    for (int q = 0; q < 16; ++q) {
+        const int e = l + 64 * q, r = e >> 5, c = e & 31;
+        X[r * 33 + c] = (double)As[(S + r) * DLD + S + c];
     }
-    float dpiv = 1.0f;
-    int b = 0;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    tile_potrf_inv_w1_wave(X, 33, X, R, dg, badw);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-    for (int j = 0; j < 32; ++j) {
-        float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v[j]), j));   // A(j, j)
-        if (!(d > 0.0f)) { if (b == 0) b = j + 1; d = 1.0f; }
-        if (isA && c == j) dpiv = d;
-        const float invd = 1.0f / d;
-        const float own = v[j];   // A(j, c) (A lanes, by symmetry) or Y(j, c) (inverse lanes)
-        const float m = (isA ? (c > j) : (c <= j)) ? own * invd : 0.0f;
-#pragma unroll
-        for (int r = j + 1; r < 32; ++r) {
-            const float sr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v[r]), j));   // A(r, j)
-            v[r] = fmaf(-sr, m, v[r]);
-        }
+    for (int q = 0; q < 16; ++q) {
+        const int e = l + 64 * q, r = e >> 5, c = e & 31;
+        Ds[(S + r) * DLD + S + c] = (float)R[r * TileCfg<32>::S + c];   // w1 writes zeros above
     }
-    if (isA) piv[S + c] = dpiv;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the pivots are in LDS for the inverse lanes
-    if (isA) {
-        const float rs = rsqrtf(dpiv);
-#pragma unroll
-        for (int r = 0; r < 32; ++r) As[(S + r) * DLD + S + c] = (r >= c) ? v[r] * rs : 0.0f;
-    } else {
-#pragma unroll
-        for (int r = 0; r < 32; ++r) Ds[(S + r) * DLD + S + c] = (r >= c) ? v[r] * rsqrtf(piv[S + r]) : 0.0f;
-    }
-    if (b && *bad == 0) *bad = S + b;
+    if (l < 32) ldiag[S + l] = dg[l];
+    if (l == 0 && *badw && *bad == 0) *bad = S + *badw;
 }
 
 __global__ __launch_bounds__(DIAG_THREADS) void k32_diag(F32Args a, int k) {
@@ -493,21 +476,37 @@ __global__ __launch_bounds__(DIAG_THREADS) void k32_diag(F32Args a, int k) {
     float* Ts = Ds + TB * DLD;        // 3 x [32][33] scratch for the inverse
     float* piv = Ts + 3 * 32 * 33;    // [128]
     int* bad = reinterpret_cast<int*>(piv + TB);
+    int* badw = bad + 1;
+    double* R64 = reinterpret_cast<double*>(smem + 2 * TB * DLD + 3 * 32 * 33 + TB + 4);   // 16-B aligned
+    double* dg64 = R64 + DIAG_R64;
+    double* X64 = reinterpret_cast<double*>(Ts);   // the inverse's scratch, free until the inverse
     const int w = threadIdx.x >> 6;
     float* Mkk = a.M + row_off(a, k) + (long)k * TB;
-    for (int e = threadIdx.x; e < TB * TB / 4; e += DIAG_THREADS) {
-        const int r = e / (TB / 4), c4 = (e % (TB / 4)) * 4;
-        *reinterpret_cast<f32x4*>(As + r * DLD + c4) = *reinterpret_cast<const f32x4*>(Mkk + (long)r * a.ld + c4);
-        *reinterpret_cast<f32x4*>(Ds + r * DLD + c4) = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    {
+        // all 16 loads of a thread in flight before the first LDS store (one memory round trip)
+        constexpr int NQ = TB * TB / 4 / DIAG_THREADS;
+        f32x4 v[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int e = threadIdx.x + q * DIAG_THREADS, r = e / (TB / 4), c4 = (e % (TB / 4)) * 4;
+            v[q] = *reinterpret_cast<const f32x4*>(Mkk + (long)r * a.ld + c4);
+        }
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int e = threadIdx.x + q * DIAG_THREADS, r = e / (TB / 4), c4 = (e % (TB / 4)) * 4;
+            *reinterpret_cast<f32x4*>(As + r * DLD + c4) = v[q];
+            *reinterpret_cast<f32x4*>(Ds + r * DLD + c4) = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        }
     }
     if (threadIdx.x == 0) *bad = 0;
     __syncthreads();
     auto T32 = [&](float* base, int i, int j) { return base + 32 * i * DLD + 32 * j; };
     for (int s = 0; s < 4; ++s) {
-        if (w == 0) factor32(As, Ds, 32 * s, piv, bad);
+        if (w == 0) factor32_w1(As, Ds, 32 * s, X64, R64, dg64, badw, bad, a.ldiag + k * TB);
         __syncthreads();
-        // panel: L_is = A_is D_ss^T, one sub-block per wave
-        for (int i = s + 1 + w; i < 4; i += 4) {
+        // panel: L_is = A_is D_ss^T (i >= s: the diagonal sub-block's L too, from the full
+        // symmetric A_ss), one sub-block per wave
+        for (int i = s + w; i < 4; i += 4) {
             f32x16 acc = {};
             mma32_nt(acc, T32(As, i, s), DLD, T32(Ds, s, s), DLD);
             acc32_store(T32(As, i, s), DLD, acc, 1.0f);   // the wave read its whole input first
@@ -554,7 +553,6 @@ __global__ __launch_bounds__(DIAG_THREADS) void k32_diag(F32Args a, int k) {
             if (c4 + q <= r) dst[q] = lv[q];
         *reinterpret_cast<f32x4*>(Dk + r * TB + c4) = *reinterpret_cast<const f32x4*>(Ds + r * DLD + c4);
     }
-    for (int r = threadIdx.x; r < TB; r += DIAG_THREADS) a.ldiag[k * TB + r] = (double)sqrtf(piv[r]);
     if (threadIdx.x == 0 && *bad && k * TB + *bad - 1 < a.n && *a.info == 0) *a.info = k * TB + *bad;
 }
 
