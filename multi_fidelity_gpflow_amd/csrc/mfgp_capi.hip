@@ -20,6 +20,7 @@ struct mfgp_handle_s {
     int grad_chunk;
     int flow_wgs;   // k_chol_flow grid (one workgroup per CU); 0: launch-per-step Cholesky
     int ncu;        // compute units of the device
+    int gram_wgs;   // k_gram tile workgroups, LML layout (0: one per CU; < 0: one per tile; MFGP_GRAM_WGS)
     int flow_trace; // k_chol_flow writes its diagnostic timeline into the workspace
     long long flow_timeout;   // k_chol_flow hand-off wait bound (100 MHz ticks)
     int f32_panel;  // fp32 path: 128-wide tile columns per outer panel (trailing-update K = 128 * f32_panel)
@@ -110,6 +111,16 @@ static GprLayout gpr_layout(int nb, int n, int p, int d, void* ws, int grad_chun
 
 static inline hipError_t last() { return hipGetLastError(); }
 
+// k_gram (LML layout) with more lower tiles than CUs: one workgroup per CU, tile (0,0) and its
+// fused factor alone on workgroup 0 (beside two other tile workgroups it took ~2x as long, and
+// it is the launch's tail), the rest looping over the other tiles.  0: one tile per workgroup.
+static int gram_tile_wgs(mfgp_handle_t h, int T, int extra) {
+    const int nt = T * (T + 1) / 2;
+    if (h->gram_wgs < 0) return 0;
+    const int wgs = (h->gram_wgs > 0 ? h->gram_wgs : h->ncu) - extra;
+    return (wgs > 1 && nt > wgs) ? wgs : 0;
+}
+
 template <int NB>
 static void gram_lml_and_factor(hipStream_t s, const GprLayout& L, int n, int p, int d, const double* X, int ldx,
                                 const double* Y, int ldy, const double* theta, int* info, int nlf = 0) {
@@ -163,7 +174,9 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
         if (order) { g.gorder = L.gorder; g.gT = L.T; g.gchunk = h->grad_chunk; g.gTp = L.Tp; }
         if (L.flow_wgs) { g.fown = L.own; g.fW = FLOW_WAVES * (L.flow_wgs - 1); g.fflags = L.flags; g.nfflags = L.nflags; g.fpub = L.pub; g.npub = L.npub; }
         if (L.flow_wgs && h->flow_trace) g.dbg = L.trace + L.ntrace - 3 * 2048;   // k_gram timeline (diagnostic)
-        launch_gram<NB>(g, L.T * (L.T + 1) / 2 + (order ? 1 : 0) + (L.flow_wgs ? 1 : 0), 1, s);
+        const int extra = (order ? 1 : 0) + (L.flow_wgs ? 1 : 0);
+        g.tile_wgs = gram_tile_wgs(h, L.T, extra);
+        launch_gram<NB>(g, (g.tile_wgs ? g.tile_wgs : L.T * (L.T + 1) / 2) + extra, 1, s);
     }
     if (pm) pm->mark(s);
     if (L.flow_wgs) {
@@ -536,6 +549,8 @@ int mfgp_create(int device, mfgp_handle_t* out) {
     h->f32_panel = 6;
     h->f32_lookahead = 1;
     h->f32_reserve = 32;
+    h->gram_wgs = 0;
+    if (const char* gv = getenv("MFGP_GRAM_WGS")) h->gram_wgs = atoi(gv);
     if (const char* rv = getenv("MFGP_F32_RESERVE")) h->f32_reserve = std::max(0, atoi(rv));
     if (const char* la = getenv("MFGP_F32_LOOKAHEAD")) h->f32_lookahead = atoi(la) != 0;
     {

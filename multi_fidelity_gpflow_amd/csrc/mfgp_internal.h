@@ -31,6 +31,9 @@ struct GramArgs {
     int* fown; int fW; int* fflags; int nfflags;
     double* fpub; long npub;
     long long* dbg;               // diagnostic per-workgroup timeline (nullptr: off)
+    // LML layout: > 0 -> that many tile workgroups, workgroup 0 takes tile (0,0) (and its fused
+    // factor) alone on its CU, the others loop over the remaining tiles; 0 -> one tile each
+    int tile_wgs;
 };
 
 // k_chol_flow (mfgp_flow.hip): persistent dataflow Cholesky + L^{-1} + Z + alpha, NB = 32, batch 1

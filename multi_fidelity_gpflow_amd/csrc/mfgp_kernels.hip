@@ -176,7 +176,7 @@ template <int NB>
 __device__ __forceinline__ void gram_copy_y(const GramArgs& a) {
     if (a.R == nullptr) return;
     const int T = a.npad / NB;
-    const long nt = (long)T * (T + 1) / 2;
+    const long nt = a.tile_wgs > 1 ? a.tile_wgs : (long)T * (T + 1) / 2;   // tile workgroups
     const long ne = (long)a.npad * a.ppad;
     const int b = blockIdx.z;
     const double* Yb = a.Y + b * a.sY;
@@ -224,17 +224,6 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
     }
     if (a.cnt && blockIdx.x == 0 && b == 0)
         for (int e = threadIdx.x; e < a.ncnt; e += NTHREADS) a.cnt[e] = 0;
-    int ti, tj;
-    if (a.padded) {   // lower tiles: t -> (ti, tj), ti >= tj
-        const int t = blockIdx.x;
-        ti = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-        while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
-        while (ti * (ti + 1) / 2 > t) --ti;
-        tj = t - ti * (ti + 1) / 2;
-    } else {
-        ti = blockIdx.x / a.tiles_c;
-        tj = blockIdx.x % a.tiles_c;
-    }
     const MFTheta th{a.theta + b * a.stheta, a.D};
     MFScal sc{0.0, 0.0, 0.0};
     double noise = 0.0;
@@ -246,9 +235,32 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
     } else if (a.add_noise) {
         noise = a.theta[b * a.stheta + kernel_theta_size(a.nlf, a.D) - 1];
     }
+    (void)th;
     const GraphTheta gth{a.theta + b * a.stheta, a.D, a.nlf};
     const double* X1 = a.X1 + b * a.sx1;
     const double* X2 = a.X2 + b * a.sx2;
+    // tiles of this workgroup: one (tile_wgs == 0, or the dense layout); with tile_wgs > 0
+    // workgroup 0 takes tile (0,0) alone -- the first diagonal factor runs on a CU of its own
+    // instead of beside two other tile workgroups -- and workgroups 1.. stride over the rest
+    const int Tl = a.npad / NB;
+    const int ntl = a.padded ? Tl * (Tl + 1) / 2 : 0;
+    int t0 = blockIdx.x, tstep = 1 << 30;
+    if (a.padded && a.tile_wgs > 1) {
+        if (blockIdx.x == 0) tstep = 1 << 30;
+        else tstep = a.tile_wgs - 1;
+    }
+    for (int t = t0; t < (a.padded ? ntl : t0 + 1); t += tstep) {
+    int ti, tj;
+    if (a.padded) {   // lower tiles: t -> (ti, tj), ti >= tj
+        ti = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+        while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+        while (ti * (ti + 1) / 2 > t) --ti;
+        tj = t - ti * (ti + 1) / 2;
+    } else {
+        ti = blockIdx.x / a.tiles_c;
+        tj = blockIdx.x % a.tiles_c;
+    }
+    if (t != t0) __syncthreads();   // the previous tile's LDS is consumed
     if (a.nlf) {   // graph kernel: raw rows + source index (f1/f2 hold the source as a double)
         for (int e = threadIdx.x; e < NB * (a.D + 1); e += NTHREADS) {
             const int r = e / (a.D + 1), d = e % (a.D + 1);
@@ -306,6 +318,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
         for (int r = threadIdx.x; r < NB; r += NTHREADS) a.ldiag[b * a.sL + r] = dg[r];
         if (threadIdx.x == 0) a.info[b] = bad;   // first writer of info in the sequence: initialises it
     }
+    }   // tiles of this workgroup
     gram_copy_y<NB>(a);
     gram_fill_pub(a);
     if (a.dbg && threadIdx.x == 0) a.dbg[3 * blockIdx.x + 2] = __builtin_amdgcn_s_memrealtime() - dbg_t0;
