@@ -174,6 +174,23 @@ def test_latent_elbo_grad_vs_autograd(hbs, kl_mult):
     _check_grads(gd, ga, 1e-6)
 
 
+@pytest.mark.parametrize("d", [3, 14, 20])
+def test_latent_elbo_grad_dimension_bounds(d):
+    """The kernel-derivative sums (k_kgrad, moment form on the MFMA) are instantiated per
+    dimension bound 4 / 8 / 12 / 16 / 32: HBS (d = 5) and Goku (d = 10) exercise 8 and 12, these
+    synthetic sets the other three.  Against torch autograd through the oracle."""
+    from multi_fidelity_gpflow_amd.data import synthetic_multifidelity
+    X, Y, _, _ = synthetic_multifidelity(150, 40, d, 6, 8, seed=40 + d)
+    m = M.LatentMFCoregionalizationSVGP(X, Y, M.SquaredExponential(lengthscales=np.ones(d)),
+                                        M.SquaredExponential(lengthscales=np.ones(d)), num_latents=3,
+                                        num_inducing=40, num_outputs=6, w_type='diagonal')
+    _randomize(m, 50 + d)
+    e, gd = m.elbo_and_grad((X, Y))
+    eo, ga = _autograd_grads(m, X, Y, m.kernel.W.numpy(), num_data=X.shape[0])
+    assert abs(e - eo) < 1e-7 * abs(eo)
+    _check_grads(gd, ga, 1e-6)
+
+
 def test_singlebin_training_kat(hbs, kats):
     """notebooks/demo matter power single bin.ipynb:156-159: -ELBO after Adam steps 0/10/20/30
     (M=50, initial_lr=0.1, 2000-step CosineDecay), run as the reference's optimize loop."""
