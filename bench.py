@@ -253,11 +253,11 @@ def bench_svgp(args):
     import multi_fidelity_gpflow_amd as M
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = dist_device_index()
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        init_dist(device)
     X, Y, Xt, Yt = broadcast_inputs(rank, world, device)
     n, d, P = X.shape[0], X.shape[1] - 1, Y.shape[1]
     from multi_fidelity_gpflow_amd.distributed import bin_block
@@ -332,6 +332,24 @@ def bench_svgp(args):
     return 0
 
 
+def dist_device_index() -> int:
+    """LOCAL_RANK's GPU.  With fewer visible GPUs than ranks (a rehearsal of the N > 1 path on a
+    one-GPU box) ranks share devices round-robin."""
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    return local % ndev if ndev > 0 else local
+
+
+def init_dist(device):
+    """RCCL ("nccl") process group; MFGP_DIST_BACKEND=gloo for a rehearsal with several ranks on
+    one GPU (RCCL wants one rank per device)."""
+    backend = os.environ.get("MFGP_DIST_BACKEND", "nccl")
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=device)
+    else:
+        dist.init_process_group(backend)
+
+
 def spawn_ranks(n: int) -> int:
     """python -m torch.distributed.run --nproc-per-node n bench.py <same args>, as a child."""
     import socket
@@ -373,11 +391,11 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = dist_device_index()
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        init_dist(device)
 
     from multi_fidelity_gpflow_amd.engine import Engine
     eng = Engine.get(device)
