@@ -5,13 +5,7 @@
 #include "../multi_fidelity_gpflow_amd/csrc/mfgp_device.h"
 using namespace mfgp;
 
-__device__ __forceinline__ double rcp_nr(double a) {
-    double r = __builtin_amdgcn_rcp(a);
-    double e = fma(-a, r, 1.0);
-    r = fma(r, e, r);
-    e = fma(-a, r, 1.0);
-    return fma(r, e, r);
-}
+// rcp_nr: v_rcp_f64 + two Newton steps (mfgp_device.h)
 
 template <int V>
 __device__ void fac(double* __restrict__ A, double* __restrict__ R, double* __restrict__ dg) {
