@@ -19,6 +19,8 @@ Behavioural quirks of the reference that are reproduced:
 """
 from __future__ import annotations
 
+import gc
+
 import numpy as np
 import torch
 
@@ -349,9 +351,18 @@ class _StepRunner:
         g = self.graphs.get(n)
         if g is None:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                for _ in range(n):
-                    self.step()
+            # No cyclic GC while capturing: a collection in the middle of a capture can destroy an
+            # earlier session's graph (hipGraphExecDestroy / pool release), which is illegal on a
+            # capturing stream and aborts the process.  torch.cuda.graph collects on entry.
+            was_enabled = gc.isenabled()
+            gc.disable()
+            try:
+                with torch.cuda.graph(g):
+                    for _ in range(n):
+                        self.step()
+            finally:
+                if was_enabled:
+                    gc.enable()
             self.graphs[n] = g
         return g
 
