@@ -26,33 +26,6 @@ constexpr int XS = MAXD + 1;   // LDS row stride of staged inputs: odd, so a wav
 
 __device__ void build_grad_order(int T, int chunk, int Tp, int* order, int* hist);
 
-template <int NB>
-__device__ __forceinline__ void stage_rows(double* aL, double* aD, double* nL, double* nD, double* f,
-                                           const double* X, long ldx, int n, int r0, int D,
-                                           const MFTheta& th, int rbf_only) {
-    // aL[r*XS + d] = X[r][d] / lL[d] ; nL[r] = sum aL^2 (GPflow square_distance)
-    for (int e = threadIdx.x; e < NB * D; e += NTHREADS) {
-        const int r = e / D, d = e % D;
-        const int gr = r0 + r;
-        const double x = (gr < n) ? X[(long)gr * ldx + d] : 0.0;
-        aL[r * XS + d] = x / th.lL(d);
-        if (!rbf_only) aD[r * XS + d] = x / th.lD(d);
-    }
-    __syncthreads();
-    for (int r = threadIdx.x; r < NB; r += NTHREADS) {
-        double sL = 0.0, sD = 0.0;
-        for (int d = 0; d < D; ++d) {
-            const double a = aL[r * XS + d];
-            sL += a * a;
-            if (!rbf_only) { const double b = aD[r * XS + d]; sD += b * b; }
-        }
-        nL[r] = sL;
-        nD[r] = sD;
-        const int gr = r0 + r;
-        f[r] = (gr < n) ? (rbf_only ? 0.0 : X[(long)gr * ldx + D]) : -1.0;
-    }
-}
-
 // one Gram entry from staged rows (GPflow: dist = -2 a.b + (|a|^2 + |b|^2); k = v exp(-dist/2))
 // kernel scalars held in registers (one load each per workgroup, issued with the row loads)
 struct MFScal {
@@ -64,61 +37,97 @@ struct MFScal {
 
 // Both row blocks of a tile in ONE memory round trip: every X element, fidelity flag and
 // lengthscale a thread needs is loaded before any is used (the two-pass stage_rows took ~4
-// dependent global-load latencies).  Then aL = X / lL (GPflow divides; here X * rcp(lL), within
-// an ulp), squared norms and flags into LDS.
+// dependent global-load latencies).  Split in two so a workgroup that loops over several tiles
+// issues the next tile's loads before it computes the current one (the per-tile round trip was
+// ~3 us of the ~5.5 us a tile took): stage_pair_load fills registers, stage_pair_commit turns
+// them into aL = X / lL (GPflow divides; here X * rcp(lL), within an ulp), squared norms and
+// flags in LDS.
+__device__ __forceinline__ int pad4(int D) { return (D + 3) & ~3; }
+
+// sum_d a[d] b[d] over d < D4 (a multiple of 4; slots past D hold 0.0): the same sequential
+// accumulation as a d < D loop, bit for bit, with the 8 LDS reads of a step issued together (a
+// runtime-D loop waited on each read: ~2/3 of a tile's time in k_gram)
+__device__ __forceinline__ double dot4(const double* a, const double* b, int D4) {
+    double dot = 0.0;
+    for (int d = 0; d < D4; d += 4) {
+        const double a0 = a[d], a1 = a[d + 1], a2 = a[d + 2], a3 = a[d + 3];
+        const double b0 = b[d], b1 = b[d + 1], b2 = b[d + 2], b3 = b[d + 3];
+        dot += a0 * b0;
+        dot += a1 * b1;
+        dot += a2 * b2;
+        dot += a3 * b3;
+    }
+    return dot;
+}
+
 template <int NB>
-__device__ __forceinline__ void stage_pair(double* aL1, double* aD1, double* nL1, double* nD1, double* f1,
-                                           double* aL2, double* aD2, double* nL2, double* nD2, double* f2,
-                                           const double* X1, long ldx1, int n1, int r01,
-                                           const double* X2, long ldx2, int n2, int r02,
-                                           int D, const double* theta, int rbf_only) {
-    constexpr int PER = (NB * MAXD + NTHREADS - 1) / NTHREADS;
+struct StageRegs {
+    static constexpr int PER = (NB * MAXD + NTHREADS - 1) / NTHREADS;
     double x1[PER], x2[PER], lL[PER], lD[PER];
+    double fv;
+};
+
+template <int NB>
+__device__ __forceinline__ void stage_pair_load(StageRegs<NB>& g, const double* X1, long ldx1, int n1, int r01,
+                                                const double* X2, long ldx2, int n2, int r02,
+                                                int D, const double* theta, int rbf_only) {
+    constexpr int PER = StageRegs<NB>::PER;
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const int e = threadIdx.x + q * NTHREADS;
         if (e < NB * D) {
             const int r = e / D, d = e % D;
-            x1[q] = (r01 + r < n1) ? X1[(long)(r01 + r) * ldx1 + d] : 0.0;
-            x2[q] = (r02 + r < n2) ? X2[(long)(r02 + r) * ldx2 + d] : 0.0;
-            lL[q] = theta[1 + d];
-            lD[q] = rbf_only ? 1.0 : theta[2 + D + d];
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-        if (threadIdx.x + q * NTHREADS < NB * D) {
-            lL[q] = rcp_nr(lL[q]);   // 1/l to <= 1 ulp: x * (1/l) for the IEEE division's ~30-op sequence
-            lD[q] = rcp_nr(lD[q]);
+            g.x1[q] = (r01 + r < n1) ? X1[(long)(r01 + r) * ldx1 + d] : 0.0;
+            g.x2[q] = (r02 + r < n2) ? X2[(long)(r02 + r) * ldx2 + d] : 0.0;
+            g.lL[q] = theta[1 + d];
+            g.lD[q] = rbf_only ? 1.0 : theta[2 + D + d];
         }
     }
     const int t = threadIdx.x;
-    double fv = -1.0;
-    if (t < NB) fv = (r01 + t < n1) ? (rbf_only ? 0.0 : X1[(long)(r01 + t) * ldx1 + D]) : -1.0;
-    else if (t < 2 * NB) fv = (r02 + t - NB < n2) ? (rbf_only ? 0.0 : X2[(long)(r02 + t - NB) * ldx2 + D]) : -1.0;
+    g.fv = -1.0;
+    if (t < NB) g.fv = (r01 + t < n1) ? (rbf_only ? 0.0 : X1[(long)(r01 + t) * ldx1 + D]) : -1.0;
+    else if (t < 2 * NB) g.fv = (r02 + t - NB < n2) ? (rbf_only ? 0.0 : X2[(long)(r02 + t - NB) * ldx2 + D]) : -1.0;
+}
+
+template <int NB>
+__device__ __forceinline__ void stage_pair_commit(StageRegs<NB>& g, double* aL1, double* aD1, double* nL1,
+                                                  double* nD1, double* f1, double* aL2, double* aD2, double* nL2,
+                                                  double* nD2, double* f2, int D, int rbf_only) {
+    constexpr int PER = StageRegs<NB>::PER;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        if (threadIdx.x + q * NTHREADS < NB * D) {
+            g.lL[q] = rcp_nr(g.lL[q]);   // 1/l to <= 1 ulp: x * (1/l) for the IEEE division's ~30-op sequence
+            g.lD[q] = rcp_nr(g.lD[q]);
+        }
+    }
+    const int t = threadIdx.x;
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const int e = threadIdx.x + q * NTHREADS;
         if (e < NB * D) {
             const int r = e / D, d = e % D;
-            aL1[r * XS + d] = x1[q] * lL[q];
-            aL2[r * XS + d] = x2[q] * lL[q];
-            if (!rbf_only) { aD1[r * XS + d] = x1[q] * lD[q]; aD2[r * XS + d] = x2[q] * lD[q]; }
+            aL1[r * XS + d] = g.x1[q] * g.lL[q];
+            aL2[r * XS + d] = g.x2[q] * g.lL[q];
+            if (!rbf_only) { aD1[r * XS + d] = g.x1[q] * g.lD[q]; aD2[r * XS + d] = g.x2[q] * g.lD[q]; }
         }
     }
-    if (t < NB) f1[t] = fv;
-    else if (t < 2 * NB) f2[t - NB] = fv;
+    if (t < NB) f1[t] = g.fv;
+    else if (t < 2 * NB) f2[t - NB] = g.fv;
+    const int D4 = pad4(D), np4 = D4 - D;
+    if (np4 && t < NB * np4) {   // zero slots D..D4-1: the dots run 4 dimensions per step
+        const int r = t / np4, d = D + t % np4;
+        aL1[r * XS + d] = 0.0;
+        aL2[r * XS + d] = 0.0;
+        if (!rbf_only) { aD1[r * XS + d] = 0.0; aD2[r * XS + d] = 0.0; }
+    }
     __syncthreads();
     if (t < 2 * NB) {
         const int r = t & (NB - 1);
         const double* aL = (t < NB ? aL1 : aL2) + r * XS;
         const double* aD = (t < NB ? aD1 : aD2) + r * XS;
-        double sL = 0.0, sD = 0.0;
-        for (int d = 0; d < D; ++d) {
-            const double a = aL[d];
-            sL += a * a;
-            if (!rbf_only) { const double b = aD[d]; sD += b * b; }
-        }
+        const double sL = dot4(aL, aL, D4);
+        const double sD = rbf_only ? 0.0 : dot4(aD, aD, D4);
         if (t < NB) { nL1[r] = sL; nD1[r] = sD; }
         else { nL2[r] = sL; nD2[r] = sD; }
     }
@@ -128,23 +137,21 @@ template <class TH>
 __device__ __forceinline__ double gram_entry(const double* aL1, const double* aD1, double nL1, double nD1, double f1,
                                              const double* aL2, const double* aD2, double nL2, double nD2, double f2,
                                              int D, const TH& th, int rbf_only) {
+    const int D4 = pad4(D);
     if (rbf_only) {
         if (f1 < 0.0 || f2 < 0.0) return 0.0;
-        double dot = 0.0;
-        for (int d = 0; d < D; ++d) dot += aL1[d] * aL2[d];
+        const double dot = dot4(aL1, aL2, D4);
         const double r2 = -2.0 * dot + (nL1 + nL2);
         return th.vL() * exp(-0.5 * r2);
     }
     const bool L1 = (f1 == 0.0), H1 = (f1 == 1.0), L2 = (f2 == 0.0), H2 = (f2 == 1.0);
     if (!(L1 || H1) || !(L2 || H2)) return 0.0;        // linear.py:67-70 exact masks
-    double dot = 0.0;
-    for (int d = 0; d < D; ++d) dot += aL1[d] * aL2[d];
+    const double dot = dot4(aL1, aL2, D4);
     const double kL = th.vL() * exp(-0.5 * (-2.0 * dot + (nL1 + nL2)));
     const double rho = th.rho();
     if (L1 && L2) return kL;                           // K_LL
     if (!(H1 && H2)) return kL * rho;                  // K_LH, K_HL
-    double dotD = 0.0;
-    for (int d = 0; d < D; ++d) dotD += aD1[d] * aD2[d];
+    const double dotD = dot4(aD1, aD2, D4);
     const double kD = th.vD() * exp(-0.5 * (-2.0 * dotD + (nD1 + nD2)));
     return kL * (rho * rho) + kD;                      // K_HH (linear.py:96)
 }
@@ -185,6 +192,19 @@ __device__ __forceinline__ void gram_copy_y(const GramArgs& a) {
         const int r = (int)(e / a.ppad), c = (int)(e % a.ppad);
         Rb[(long)r * a.ldr + a.npad + c] = (r < a.n1 && c < a.p) ? Yb[(long)r * a.ldy + c] : 0.0;
     }
+}
+
+// Fused factor of the first diagonal tile (step "-1" of the tile Cholesky), run by one workgroup
+// of k_gram.  Not inlined: inlined, its register demand set the whole kernel's allocation (222
+// SGPR spills to VGPR lanes that every tile loop reloaded).
+template <int NB>
+__device__ __attribute__((noinline)) void gram_first_factor(double* tile, double* rtile, double* dg, int* bad,
+                                                            double* Dd, double* ldiag, int* info) {
+    __syncthreads();
+    tile_potrf_inv<NB>(tile, rtile, dg, bad);
+    tile_store<NB>(Dd, NB, rtile);
+    for (int r = threadIdx.x; r < NB; r += NTHREADS) ldiag[r] = dg[r];
+    if (threadIdx.x == 0) *info = *bad;   // first writer of info in the sequence: initialises it
 }
 
 template <int NB>
@@ -249,17 +269,28 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
         if (blockIdx.x == 0) tstep = 1 << 30;
         else tstep = a.tile_wgs - 1;
     }
-    for (int t = t0; t < (a.padded ? ntl : t0 + 1); t += tstep) {
-    int ti, tj;
-    if (a.padded) {   // lower tiles: t -> (ti, tj), ti >= tj
-        ti = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-        while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
-        while (ti * (ti + 1) / 2 > t) --ti;
-        tj = t - ti * (ti + 1) / 2;
-    } else {
-        ti = blockIdx.x / a.tiles_c;
-        tj = blockIdx.x % a.tiles_c;
+    auto decode = [&](int t, int& ti, int& tj) {
+        if (a.padded) {   // lower tiles: t -> (ti, tj), ti >= tj
+            ti = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+            while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+            while (ti * (ti + 1) / 2 > t) --ti;
+            tj = t - ti * (ti + 1) / 2;
+        } else {
+            ti = blockIdx.x / a.tiles_c;
+            tj = blockIdx.x % a.tiles_c;
+        }
+    };
+    const int tend = a.padded ? ntl : t0 + 1;
+    StageRegs<NB> sr;   // the row loads of the tile this workgroup computes next
+    if (!a.nlf && t0 < tend) {
+        int ti, tj;
+        decode(t0, ti, tj);
+        stage_pair_load<NB>(sr, X1, a.ldx1, a.n1, ti * NB, X2, a.ldx2, a.n2, tj * NB, a.D, a.theta + b * a.stheta,
+                            a.rbf_only);
     }
+    for (int t = t0; t < tend; t += tstep) {
+    int ti, tj;
+    decode(t, ti, tj);
     if (t != t0) __syncthreads();   // the previous tile's LDS is consumed
     if (a.nlf) {   // graph kernel: raw rows + source index (f1/f2 hold the source as a double)
         for (int e = threadIdx.x; e < NB * (a.D + 1); e += NTHREADS) {
@@ -274,10 +305,15 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
             }
         }
     } else {
-        stage_pair<NB>(aL1, aD1, nL1, nD1, f1, aL2, aD2, nL2, nD2, f2, X1, a.ldx1, a.n1, ti * NB,
-                       X2, a.ldx2, a.n2, tj * NB, a.D, a.theta + b * a.stheta, a.rbf_only);
+        stage_pair_commit<NB>(sr, aL1, aD1, nL1, nD1, f1, aL2, aD2, nL2, nD2, f2, a.D, a.rbf_only);
     }
     __syncthreads();
+    if (!a.nlf && t + tstep < tend) {   // next tile's rows: in flight while this one is computed
+        int ni, nj;
+        decode(t + tstep, ni, nj);
+        stage_pair_load<NB>(sr, X1, a.ldx1, a.n1, ni * NB, X2, a.ldx2, a.n2, nj * NB, a.D,
+                            a.theta + b * a.stheta, a.rbf_only);
+    }
     if (a.dbg && threadIdx.x == 0) a.dbg[3 * blockIdx.x] = __builtin_amdgcn_s_memrealtime() - dbg_t0;   // stage time (ticks)
 
     double* out = a.out + b * a.so;
@@ -310,14 +346,8 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
     __syncthreads();
     if (a.dbg && threadIdx.x == 0) a.dbg[3 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - dbg_t0;
     tile_store<NB>(out + (long)ti * NB * a.ldo + tj * NB, a.ldo, tile);
-    if (a.Dd != nullptr && ti == 0 && tj == 0) {
-        // fused factor of the first diagonal tile (step "-1" of the tile Cholesky)
-        __syncthreads();
-        tile_potrf_inv<NB>(tile, rtile, dg, &bad);
-        tile_store<NB>(a.Dd + b * a.sD, NB, rtile);
-        for (int r = threadIdx.x; r < NB; r += NTHREADS) a.ldiag[b * a.sL + r] = dg[r];
-        if (threadIdx.x == 0) a.info[b] = bad;   // first writer of info in the sequence: initialises it
-    }
+    if (a.Dd != nullptr && ti == 0 && tj == 0)
+        gram_first_factor<NB>(tile, rtile, dg, &bad, a.Dd + b * a.sD, a.ldiag + b * a.sL, a.info + b);
     }   // tiles of this workgroup
     gram_copy_y<NB>(a);
     gram_fill_pub(a);
