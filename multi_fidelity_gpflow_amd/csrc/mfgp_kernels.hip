@@ -317,6 +317,45 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
     if (a.dbg && threadIdx.x == 0) a.dbg[3 * blockIdx.x] = __builtin_amdgcn_s_memrealtime() - dbg_t0;   // stage time (ticks)
 
     double* out = a.out + b * a.so;
+    if (a.padded && !a.nlf) {
+        // the NB*NB/256 entries of a thread side by side (one wave per SIMD: a lone entry's LDS
+        // reads -> dot -> exp chain was latency-bound); same arithmetic as gram_entry, bit for bit
+        constexpr int PT = NB * NB / NTHREADS;
+        static_assert(NB * NB % NTHREADS == 0, "entries per thread");
+        const int D4 = pad4(a.D);
+        double kl[PT];
+#pragma unroll
+        for (int k = 0; k < PT; ++k) {
+            const int e = threadIdx.x + k * NTHREADS;
+            const int r = e / NB, c = e % NB;
+            const double dot = dot4(aL1 + r * XS, aL2 + c * XS, D4);
+            kl[k] = sc.vL() * exp(-0.5 * (-2.0 * dot + (nL1[r] + nL2[c])));
+        }
+#pragma unroll
+        for (int k = 0; k < PT; ++k) {
+            const int e = threadIdx.x + k * NTHREADS;
+            const int r = e / NB, c = e % NB;
+            const int gi = ti * NB + r, gj = tj * NB + c;
+            const double fa = f1[r], fb = f2[c];
+            double v;
+            if (a.rbf_only) {
+                v = (fa < 0.0 || fb < 0.0) ? 0.0 : kl[k];
+            } else {
+                const bool L1 = (fa == 0.0), H1 = (fa == 1.0), L2 = (fb == 0.0), H2 = (fb == 1.0);
+                const double rho = sc.rho();
+                double kD = 0.0;
+                if (H1 && H2) {   // K_HH (linear.py:96): rare, a branch of its own
+                    const double dotD = dot4(aD1 + r * XS, aD2 + c * XS, D4);
+                    kD = sc.vD() * exp(-0.5 * (-2.0 * dotD + (nD1[r] + nD2[c])));
+                }
+                const double vhh = kl[k] * (rho * rho) + kD;
+                v = (L1 && L2) ? kl[k] : (!(H1 && H2) ? kl[k] * rho : vhh);
+                if (!(L1 || H1) || !(L2 || H2)) v = 0.0;    // linear.py:67-70 exact masks
+            }
+            if (gi == gj) v = (gi < a.n1) ? v + noise + a.diag_add : 1.0;   // identity padding
+            tile[r * S + c] = v;
+        }
+    } else
     for (int e = threadIdx.x; e < NB * NB; e += NTHREADS) {
         const int r = e / NB, c = e % NB;
         const int gi = ti * NB + r, gj = tj * NB + c;
