@@ -6,9 +6,11 @@ fallback — on a machine without a GPU every compute call raises.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 
 import numpy as np
+
 import torch
 
 from . import _lib
@@ -61,6 +63,7 @@ class Engine:
         self.device = device
         self.index = device.index if device.index is not None else torch.cuda.current_device()
         self._ws: dict = {}
+        self._last_ordered = None
         self.lib = _lib.load()
 
     @classmethod
@@ -74,6 +77,24 @@ class Engine:
             eng = cls(torch.device("cuda", key))
             cls._engines[key] = eng
         return eng
+
+    # ------------------------------------------------------------ session ordering
+    @contextlib.contextmanager
+    def ordered(self, stream: torch.cuda.Stream):
+        """Work enqueued on `stream` inside the block starts after the previous ordered block on
+        this device ended, whatever its stream.  Training sessions run on streams of their own,
+        and two persistent k_chol_flow launches must never share the device: each needs every CU
+        resident, and one that cannot get them stalls until its hand-off bound expires (a lost
+        step).  Device-side ordering only: no host synchronisation."""
+        prev = self._last_ordered
+        if prev is not None:
+            stream.wait_event(prev)
+        try:
+            yield
+        finally:
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            self._last_ordered = ev
 
     # ------------------------------------------------------------ plumbing
     @property

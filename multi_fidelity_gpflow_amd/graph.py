@@ -212,7 +212,7 @@ class _GraphAdamSession:
         self.max_iters = max(int(max_iters), 1)
         self.stream = torch.cuda.Stream(dev)
         f64 = dict(dtype=torch.float64, device=dev)
-        with torch.cuda.stream(self.stream):
+        with torch.cuda.stream(self.stream), self.eng.ordered(self.stream):
             self.theta = torch.tensor(c, **f64)
             self.u = torch.tensor(u, **f64)
             self.mo = torch.zeros(G, **f64)
@@ -244,7 +244,7 @@ class _GraphAdamSession:
     def run(self, n):
         if self.done + n > self.max_iters:
             raise ValueError("optimize: more iterations than max_iters")
-        with torch.cuda.stream(self.stream):
+        with torch.cuda.stream(self.stream), self.eng.ordered(self.stream):
             self.runner.run(n)
         self.done += n
 

@@ -290,7 +290,7 @@ class AdamSession:
         # every buffer the recorded graphs point at is allocated on the session's stream and
         # owned by the session for its lifetime (no shared grow-only workspace under a graph)
         self.stream.wait_stream(torch.cuda.current_stream(self.eng.device))
-        with torch.cuda.stream(self.stream):
+        with torch.cuda.stream(self.stream), self.eng.ordered(self.stream):
             self.st = AdamState(self.eng.device, self.tm.u(), self.tm.trainable(), self.tm.tie(), lr)
             self.hist = torch.zeros((self.max_iters,), dtype=torch.float64, device=self.eng.device)
             self.out = torch.empty((1 + theta_size(self.tm.d),), dtype=torch.float64, device=self.eng.device)
@@ -308,7 +308,7 @@ class AdamSession:
     def run(self, n: int):
         if self.done + n > self.max_iters:
             raise ValueError("AdamSession: more iterations than max_iters")
-        with torch.cuda.stream(self.stream):
+        with torch.cuda.stream(self.stream), self.eng.ordered(self.stream):
             self.runner.run(n)
         self.done += n
 
@@ -330,6 +330,12 @@ class AdamSession:
         self.model.loss_history = [np.float64(v) for v in h]
         self.tm.set_u(self.st.u.cpu().numpy())
         v = int(self.info.item())
+        steps = int(self.st.step.item())
+        if v == 0 and steps != self.done and np.all(np.isfinite(h)):
+            # a failed step leaves the step counter behind and the next one retries it, so a
+            # failure followed by good steps shows only here (trailing loss entries never written)
+            raise MFGPError(f"optimize: {self.done - steps} of {self.done} steps failed (Cholesky or flow "
+                            f"hand-off) and were retried; the trajectory is incomplete")
         if v != 0 or not np.all(np.isfinite(h)):
             bad = int(np.argmax(~np.isfinite(h))) if not np.all(np.isfinite(h)) else len(h) - 1
             self.model.loss_history = self.model.loss_history[:bad + 1]
