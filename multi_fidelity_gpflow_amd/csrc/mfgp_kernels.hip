@@ -63,14 +63,14 @@ __device__ __forceinline__ double dot4(const double* a, const double* b, int D4)
 template <int NB>
 struct StageRegs {
     static constexpr int PER = (NB * MAXD + NTHREADS - 1) / NTHREADS;
-    double x1[PER], x2[PER], lL[PER], lD[PER];
+    double x1[PER], x2[PER];
     double fv;
 };
 
 template <int NB>
 __device__ __forceinline__ void stage_pair_load(StageRegs<NB>& g, const double* X1, long ldx1, int n1, int r01,
                                                 const double* X2, long ldx2, int n2, int r02,
-                                                int D, const double* theta, int rbf_only) {
+                                                int D, int rbf_only) {
     constexpr int PER = StageRegs<NB>::PER;
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
@@ -79,8 +79,6 @@ __device__ __forceinline__ void stage_pair_load(StageRegs<NB>& g, const double* 
             const int r = e / D, d = e % D;
             g.x1[q] = (r01 + r < n1) ? X1[(long)(r01 + r) * ldx1 + d] : 0.0;
             g.x2[q] = (r02 + r < n2) ? X2[(long)(r02 + r) * ldx2 + d] : 0.0;
-            g.lL[q] = theta[1 + d];
-            g.lD[q] = rbf_only ? 1.0 : theta[2 + D + d];
         }
     }
     const int t = threadIdx.x;
@@ -89,27 +87,26 @@ __device__ __forceinline__ void stage_pair_load(StageRegs<NB>& g, const double* 
     else if (t < 2 * NB) g.fv = (r02 + t - NB < n2) ? (rbf_only ? 0.0 : X2[(long)(r02 + t - NB) * ldx2 + D]) : -1.0;
 }
 
+// il: LDS [1/lL(0..MAXD) | 1/lD(0..MAXD)], staged once per workgroup (stage_inv_lengthscales)
 template <int NB>
-__device__ __forceinline__ void stage_pair_commit(StageRegs<NB>& g, double* aL1, double* aD1, double* nL1,
-                                                  double* nD1, double* f1, double* aL2, double* aD2, double* nL2,
-                                                  double* nD2, double* f2, int D, int rbf_only) {
+__device__ __forceinline__ void stage_pair_commit(StageRegs<NB>& g, const double* il, double* aL1, double* aD1,
+                                                  double* nL1, double* nD1, double* f1, double* aL2, double* aD2,
+                                                  double* nL2, double* nD2, double* f2, int D, int rbf_only) {
     constexpr int PER = StageRegs<NB>::PER;
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-        if (threadIdx.x + q * NTHREADS < NB * D) {
-            g.lL[q] = rcp_nr(g.lL[q]);   // 1/l to <= 1 ulp: x * (1/l) for the IEEE division's ~30-op sequence
-            g.lD[q] = rcp_nr(g.lD[q]);
-        }
-    }
     const int t = threadIdx.x;
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const int e = threadIdx.x + q * NTHREADS;
         if (e < NB * D) {
             const int r = e / D, d = e % D;
-            aL1[r * XS + d] = g.x1[q] * g.lL[q];
-            aL2[r * XS + d] = g.x2[q] * g.lL[q];
-            if (!rbf_only) { aD1[r * XS + d] = g.x1[q] * g.lD[q]; aD2[r * XS + d] = g.x2[q] * g.lD[q]; }
+            const double lL = il[d];
+            aL1[r * XS + d] = g.x1[q] * lL;
+            aL2[r * XS + d] = g.x2[q] * lL;
+            if (!rbf_only) {
+                const double lD = il[MAXD + d];
+                aD1[r * XS + d] = g.x1[q] * lD;
+                aD2[r * XS + d] = g.x2[q] * lD;
+            }
         }
     }
     if (t < NB) f1[t] = g.fv;
@@ -226,6 +223,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
     double* dg = rtile + TileCfg<NB>::ELEMS;   // NB
     int& bad = *reinterpret_cast<int*>(dg + NB);   // keep ALL LDS dynamic: a static __shared__
                                                    // would shift the dynamic base off 16 B (G17)
+    double* il = dg + NB + 2;                  // 2 x MAXD inverse lengthscales
 
     const int b = blockIdx.z;
     const long long dbg_t0 = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -285,8 +283,15 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
     if (!a.nlf && t0 < tend) {
         int ti, tj;
         decode(t0, ti, tj);
-        stage_pair_load<NB>(sr, X1, a.ldx1, a.n1, ti * NB, X2, a.ldx2, a.n2, tj * NB, a.D, a.theta + b * a.stheta,
-                            a.rbf_only);
+        stage_pair_load<NB>(sr, X1, a.ldx1, a.n1, ti * NB, X2, a.ldx2, a.n2, tj * NB, a.D, a.rbf_only);
+        // 1/l once per workgroup (was: every thread, every tile: 2 loads + 2 Newton reciprocals per
+        // staged element); rcp_nr is 1/l to <= 1 ulp, x * (1/l) for the IEEE division's ~30 ops
+        const double* tp = a.theta + b * a.stheta;
+        if (threadIdx.x < a.D) {
+            il[threadIdx.x] = rcp_nr(tp[1 + threadIdx.x]);
+            il[MAXD + threadIdx.x] = a.rbf_only ? 1.0 : rcp_nr(tp[2 + a.D + threadIdx.x]);
+        }
+        __syncthreads();
     }
     for (int t = t0; t < tend; t += tstep) {
     int ti, tj;
@@ -305,14 +310,13 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
             }
         }
     } else {
-        stage_pair_commit<NB>(sr, aL1, aD1, nL1, nD1, f1, aL2, aD2, nL2, nD2, f2, a.D, a.rbf_only);
+        stage_pair_commit<NB>(sr, il, aL1, aD1, nL1, nD1, f1, aL2, aD2, nL2, nD2, f2, a.D, a.rbf_only);
     }
     __syncthreads();
     if (!a.nlf && t + tstep < tend) {   // next tile's rows: in flight while this one is computed
         int ni, nj;
         decode(t + tstep, ni, nj);
-        stage_pair_load<NB>(sr, X1, a.ldx1, a.n1, ni * NB, X2, a.ldx2, a.n2, nj * NB, a.D,
-                            a.theta + b * a.stheta, a.rbf_only);
+        stage_pair_load<NB>(sr, X1, a.ldx1, a.n1, ni * NB, X2, a.ldx2, a.n2, nj * NB, a.D, a.rbf_only);
     }
     if (a.dbg && threadIdx.x == 0) a.dbg[3 * blockIdx.x] = __builtin_amdgcn_s_memrealtime() - dbg_t0;   // stage time (ticks)
 
@@ -395,7 +399,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
 
 size_t gram_smem_bytes(int nb) {
     const size_t tile = (size_t)nb * (nb + 2);
-    return sizeof(double) * (4 * (size_t)nb * XS + 6 * (size_t)nb + 2 * tile + nb + 2);
+    return sizeof(double) * (4 * (size_t)nb * XS + 6 * (size_t)nb + 2 * tile + nb + 2 + 2 * MAXD);
 }
 
 // ============================================================ K2: tile Cholesky step
