@@ -369,13 +369,14 @@ static int predict_impl(mfgp_handle_t h, int n, int p, int d, int nstar, const d
     hipStream_t s = h->stream;
     const GprLayout& L = P.g;
     gram_lml_and_factor<NB>(s, L, n, p, d, X, ldx, Y, ldy, theta, info, nlf);
-    (void)hipMemsetAsync(P.Kmn, 0, sizeof(double) * (size_t)L.npad * P.nspad, s);
+    if (nlf) (void)hipMemsetAsync(P.Kmn, 0, sizeof(double) * (size_t)L.npad * P.nspad, s);
     GramArgs g{};
     g.X1 = X; g.ldx1 = ldx; g.n1 = n;
     g.X2 = Xs; g.ldx2 = ldxs; g.n2 = nstar;
     g.theta = theta; g.D = d; g.rbf_only = 0;
     g.out = P.Kmn; g.ldo = P.nspad; g.padded = 0; g.tiles_c = P.Ts; g.diag_add = 0.0; g.nlf = nlf;
-    launch_gram<NB>(g, L.T * P.Ts, 1, s);
+    if (nlf) launch_gram<NB>(g, L.T * P.Ts, 1, s);
+    else launch_gram_dense(g, 1, L.npad, P.nspad, s);   // zero padding written by the kernel
     hipLaunchKernelGGL(k_kdiag, dim3(ceil_div(nstar, 256)), dim3(256), 0, s, Xs, (long)ldxs, nstar, d, theta,
                        P.kdiag, nlf);
     const long ldr = L.npad + L.ppad;
@@ -384,14 +385,15 @@ static int predict_impl(mfgp_handle_t h, int n, int p, int d, int nstar, const d
     launch_pred<NB>(pa, po, L.T, s);
     if (cov) {
         // base_conditional(full_cov=True): Kss - A^T A with A = L^{-1} Kmn (padded rows of A are 0)
-        (void)hipMemsetAsync(P.Kss, 0, sizeof(double) * (size_t)P.nspad * P.nspad, s);
+        if (nlf) (void)hipMemsetAsync(P.Kss, 0, sizeof(double) * (size_t)P.nspad * P.nspad, s);
         GramArgs gs{};
         gs.X1 = Xs; gs.ldx1 = ldxs; gs.n1 = nstar;
         gs.X2 = Xs; gs.ldx2 = ldxs; gs.n2 = nstar;
         gs.theta = theta; gs.D = d; gs.rbf_only = 0;
         gs.out = P.Kss; gs.ldo = P.nspad; gs.padded = 0; gs.tiles_c = P.Ts; gs.nlf = nlf;
         gs.diag_add = nlf ? GRAPH_JITTER : 0.0;   // graph.py:96 adds the jitter inside K(X*, X*) too
-        launch_gram<NB>(gs, P.Ts * P.Ts, 1, s);
+        if (nlf) launch_gram<NB>(gs, P.Ts * P.Ts, 1, s);
+        else launch_gram_dense(gs, 1, P.nspad, P.nspad, s);
         BgemmArgs b{};
         b.A = P.Am; b.lda = P.nspad;
         b.B = P.Am; b.ldb = P.nspad;

@@ -714,12 +714,13 @@ __global__ __launch_bounds__(GT, 2) void k32_grad(F32Args a) {
             s2 = fmaf(df2[d], il[d], s2);
             s2d = fmaf(df2[d], ild[d], s2d);
         }
-        const float kL = vL * __expf(-0.5f * s2);
-        const float kD = (H1 && H2) ? vD * __expf(-0.5f * s2d) : 0.0f;
+        const float eL = __expf(-0.5f * s2);   // dk/dv in TF's autodiff form (finite at v = 0)
+        const float eD = (H1 && H2) ? __expf(-0.5f * s2d) : 0.0f;
+        const float kL = vL * eL, kD = vD * eD;
         const float si = L1 ? 1.0f : rho, hi = H1 ? 1.0f : 0.0f;
         const float cL = w * si * sj * kL, cD = w * hi * hj * kD;
-        gvL += cL;
-        gvD += cD;
+        gvL += w * si * sj * eL;
+        gvD += w * hi * hj * eD;
         grho += w * (hi * sj + si * hj) * kL;
         if (I == J && r == c && I * TB + r < a.n) gno += w;
 #pragma unroll
@@ -748,10 +749,7 @@ __global__ __launch_bounds__(GT, 2) void k32_grad(F32Args a) {
     __syncthreads();
     for (int q = threadIdx.x; q < G; q += GT) {
         double v = (red[q * 4] + red[q * 4 + 1]) + (red[q * 4 + 2] + red[q * 4 + 3]);
-        if (q == 0) v /= a.theta[0];
-        else if (q <= D) { const double l = a.theta[q]; v /= l * l * l; }
-        else if (q == 1 + D) v /= a.theta[1 + D];
-        else if (q <= 1 + 2 * D) { const double l = a.theta[q]; v /= l * l * l; }
+        if ((q >= 1 && q <= D) || (q >= 2 + D && q <= 1 + 2 * D)) { const double l = a.theta[q]; v /= l * l * l; }
         a.gpart[(long)q * gridDim.x + task] = v;
     }
 }

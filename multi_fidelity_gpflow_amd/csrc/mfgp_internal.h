@@ -222,7 +222,10 @@ int flow_nflags(int T, int Tp);
 long flow_npub(int T, int Tp);
 void launch_chol_flow(const FlowArgs& a, int nwg, hipStream_t s);
 
+// LML layout (padded) or graph kernel: k_gram; dense layout of the linear MF / RBF kernel: k_gram_dense
 template <int NB> void launch_gram(const GramArgs& g, int nblocks, int batch, hipStream_t s);
+// dense layout, write extents wr1 x wr2 (>= n1 x n2; the excess is written 0.0)
+void launch_gram_dense(const GramArgs& g, int batch, int wr1, int wr2, hipStream_t s);
 template <int NB> void launch_chol_steps(CholArgs c, int batch, hipStream_t s);
 template <int NB> void launch_grad(const GradArgs& g, hipStream_t s);
 template <int NB> void launch_pred(const PredAArgs& pa, const PredOutArgs& po, int T, hipStream_t s);

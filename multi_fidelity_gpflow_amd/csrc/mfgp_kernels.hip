@@ -42,7 +42,7 @@ struct MFScal {
 // ~3 us of the ~5.5 us a tile took): stage_pair_load fills registers, stage_pair_commit turns
 // them into aL = X / lL (GPflow divides; here X * rcp(lL), within an ulp), squared norms and
 // flags in LDS.
-__device__ __forceinline__ int pad4(int D) { return (D + 3) & ~3; }
+__host__ __device__ __forceinline__ int pad4(int D) { return (D + 3) & ~3; }
 
 // sum_d a[d] b[d] over d < D4 (a multiple of 4; slots past D hold 0.0): the same sequential
 // accumulation as a d < D loop, bit for bit, with the 8 LDS reads of a step issued together (a
@@ -400,6 +400,131 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
 size_t gram_smem_bytes(int nb) {
     const size_t tile = (size_t)nb * (nb + 2);
     return sizeof(double) * (4 * (size_t)nb * XS + 6 * (size_t)nb + 2 * tile + nb + 2 + 2 * MAXD);
+}
+
+// ------------------------------------------------------------ K1 dense (rectangular) layout
+// K(X1, X2) written row-major (Kuf, K(X, X*), K(X*, X*), the mfgp_*_gram entry points).  A lean
+// kernel of its own: k_gram carries the fused diagonal factor and the flow set-up, whose register
+// demand (256 VGPRs, one wave per SIMD) starved these launches of thousands of small tiles (the
+// Goku SingleBinSVGP Kuf: 64 latents x 300 x 1164).  64 x 64 entries per 256-thread workgroup:
+// lane = column (coalesced 512-B row stores), wave w = rows w, w+4, .., w+60; the column's scaled
+// row lives in registers (D4 = dimensions padded to 4, a template parameter), the row side is
+// read from LDS as a wave-wide broadcast.  Same arithmetic as gram_entry, bit for bit (same
+// scaling x * rcp_nr(l), same dot4 accumulation order, same expressions).
+// Entries with gi < wr1, gj < wr2 outside n1 x n2 are written 0.0 (the padded Kuf / Kmn buffers
+// need no memset).
+constexpr int GD_T = 64;
+
+template <int D4>
+__device__ __forceinline__ double dot_rl(const double* a, const double (&b)[D4]) {
+    double dot = 0.0;
+#pragma unroll
+    for (int d = 0; d < D4; d += 4) {
+        const double a0 = a[d], a1 = a[d + 1], a2 = a[d + 2], a3 = a[d + 3];
+        dot += a0 * b[d];
+        dot += a1 * b[d + 1];
+        dot += a2 * b[d + 2];
+        dot += a3 * b[d + 3];
+    }
+    return dot;
+}
+
+template <int D4>
+__global__ __launch_bounds__(NTHREADS) void k_gram_dense(GramArgs a, int wr1, int wr2, int tc) {
+    __shared__ __attribute__((aligned(16))) double sL1[GD_T * D4];
+    __shared__ __attribute__((aligned(16))) double sD1[GD_T * D4];
+    __shared__ __attribute__((aligned(16))) double sD2[GD_T * D4];
+    __shared__ double nL1[GD_T], nD1[GD_T], f1[GD_T];
+    __shared__ double il[2 * MAXD];
+    const int b = blockIdx.z, t = threadIdx.x;
+    const int ti = blockIdx.x / tc, tj = blockIdx.x % tc;
+    const int r0 = ti * GD_T, c0 = tj * GD_T;
+    const int D = a.D;
+    const double* tp = a.theta + b * a.stheta;
+    const double* X1 = a.X1 + b * a.sx1;
+    const double* X2 = a.X2 + b * a.sx2;
+    if (t < D) {
+        il[t] = rcp_nr(tp[1 + t]);
+        il[MAXD + t] = a.rbf_only ? 1.0 : rcp_nr(tp[2 + D + t]);
+    }
+    const double vL = tp[0];
+    const double vD = a.rbf_only ? 0.0 : tp[1 + D];
+    const double rho = a.rbf_only ? 0.0 : tp[2 + 2 * D];
+    __syncthreads();
+    // stage the row side (X1) and the column side's delta rows (X2, for K_HH pairs)
+    for (int e = t; e < GD_T * D4; e += NTHREADS) {
+        const int r = e / D4, d = e % D4;
+        const bool in = d < D;
+        const double x1 = (in && r0 + r < a.n1) ? X1[(long)(r0 + r) * a.ldx1 + d] : 0.0;
+        sL1[e] = in ? x1 * il[d] : 0.0;
+        if (!a.rbf_only) {
+            const double x2 = (in && c0 + r < a.n2) ? X2[(long)(c0 + r) * a.ldx2 + d] : 0.0;
+            sD1[e] = in ? x1 * il[MAXD + d] : 0.0;
+            sD2[e] = in ? x2 * il[MAXD + d] : 0.0;
+        }
+    }
+    if (t < GD_T) f1[t] = (r0 + t < a.n1) ? (a.rbf_only ? 0.0 : X1[(long)(r0 + t) * a.ldx1 + D]) : -1.0;
+    // the column's LF-scaled row in registers
+    const int c = t & 63, gj = c0 + c;
+    double bl[D4];
+#pragma unroll
+    for (int d = 0; d < D4; ++d)
+        bl[d] = (d < D && gj < a.n2) ? X2[(long)gj * a.ldx2 + d] * il[d] : 0.0;
+    const double f2 = (gj < a.n2) ? (a.rbf_only ? 0.0 : X2[(long)gj * a.ldx2 + D]) : -1.0;
+    __syncthreads();
+    if (t < GD_T) {
+        nL1[t] = dot4(sL1 + t * D4, sL1 + t * D4, D4);
+        nD1[t] = a.rbf_only ? 0.0 : dot4(sD1 + t * D4, sD1 + t * D4, D4);
+    }
+    const double nL2 = dot_rl<D4>(bl, bl);
+    const double nD2 = a.rbf_only ? 0.0 : dot4(sD2 + c * D4, sD2 + c * D4, D4);
+    __syncthreads();
+    double* out = a.out + b * a.so;
+    const bool L2 = (f2 == 0.0), H2 = (f2 == 1.0);
+    for (int rr = t >> 6; rr < GD_T; rr += NTHREADS / 64) {
+        const int gi = r0 + rr;
+        if (gi >= wr1) break;
+        if (gj >= wr2) continue;
+        double v = 0.0;
+        if (gi < a.n1 && gj < a.n2) {
+            const double fa = f1[rr];
+            const double dot = dot_rl<D4>(sL1 + rr * D4, bl);
+            const double kl = vL * exp(-0.5 * (-2.0 * dot + (nL1[rr] + nL2)));
+            if (a.rbf_only) {
+                v = (fa < 0.0 || f2 < 0.0) ? 0.0 : kl;
+            } else {
+                const bool L1 = (fa == 0.0), H1 = (fa == 1.0);
+                double kD = 0.0;
+                if (H1 && H2) {   // K_HH (linear.py:96)
+                    const double dotD = dot4(sD1 + rr * D4, sD2 + c * D4, D4);
+                    kD = vD * exp(-0.5 * (-2.0 * dotD + (nD1[rr] + nD2)));
+                }
+                const double vhh = kl * (rho * rho) + kD;
+                v = (L1 && L2) ? kl : (!(H1 && H2) ? kl * rho : vhh);
+                if (!(L1 || H1) || !(L2 || H2)) v = 0.0;   // linear.py:67-70 exact masks
+            }
+            if (gi == gj) v += a.diag_add;
+        }
+        out[(long)gi * a.ldo + gj] = v;
+    }
+}
+
+// dense-layout Gram of a (batch of) rectangular blocks; write extents wr1 >= n1, wr2 >= n2
+void launch_gram_dense(const GramArgs& g, int batch, int wr1, int wr2, hipStream_t s) {
+    wr1 = wr1 > g.n1 ? wr1 : g.n1;
+    wr2 = wr2 > g.n2 ? wr2 : g.n2;
+    const int tr = (wr1 + GD_T - 1) / GD_T, tc = (wr2 + GD_T - 1) / GD_T;
+    const dim3 grid(tr * tc, 1, batch);
+    switch (pad4(g.D)) {
+        case 4: hipLaunchKernelGGL(k_gram_dense<4>, grid, dim3(NTHREADS), 0, s, g, wr1, wr2, tc); break;
+        case 8: hipLaunchKernelGGL(k_gram_dense<8>, grid, dim3(NTHREADS), 0, s, g, wr1, wr2, tc); break;
+        case 12: hipLaunchKernelGGL(k_gram_dense<12>, grid, dim3(NTHREADS), 0, s, g, wr1, wr2, tc); break;
+        case 16: hipLaunchKernelGGL(k_gram_dense<16>, grid, dim3(NTHREADS), 0, s, g, wr1, wr2, tc); break;
+        case 20: hipLaunchKernelGGL(k_gram_dense<20>, grid, dim3(NTHREADS), 0, s, g, wr1, wr2, tc); break;
+        case 24: hipLaunchKernelGGL(k_gram_dense<24>, grid, dim3(NTHREADS), 0, s, g, wr1, wr2, tc); break;
+        case 28: hipLaunchKernelGGL(k_gram_dense<28>, grid, dim3(NTHREADS), 0, s, g, wr1, wr2, tc); break;
+        default: hipLaunchKernelGGL(k_gram_dense<32>, grid, dim3(NTHREADS), 0, s, g, wr1, wr2, tc); break;
+    }
 }
 
 // ============================================================ K2: tile Cholesky step
@@ -950,15 +1075,19 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
             const int e = q * 4 + r;
             const double w = acc.v[q][r] * wscale;
             const bool live = (L1[e] || H1[e]) && (L2[e] || H2[e]);
-            const double kL = live ? th.vL() * exp(-0.5 * s2[e]) : 0.0;
-            double kD = 0.0;
-            if (anyHH && H1[e] && H2[e]) kD = th.vD() * exp(-0.5 * s2d[e]);
+            // dK/dv = exp(-r2/2), TF's autodiff of v * exp(-r2/2): finite where v underflows to 0
+            // (the division form K / v gave 0/0 at L-BFGS line-search points)
+            const double eL = live ? exp(-0.5 * s2[e]) : 0.0;
+            const double kL = th.vL() * eL;
+            double eD = 0.0;
+            if (anyHH && H1[e] && H2[e]) eD = exp(-0.5 * s2d[e]);
+            const double kD = th.vD() * eD;
             const double si = L1[e] ? 1.0 : (H1[e] ? rho : 0.0), sj = L2[e] ? 1.0 : (H2[e] ? rho : 0.0);
             const double hi = H1[e] ? 1.0 : 0.0, hj = H2[e] ? 1.0 : 0.0;
             cL[e] = w * si * sj * kL;
             cD[e] = w * hi * hj * kD;
-            gvL += cL[e];
-            gvD += cD[e];
+            gvL += w * si * sj * eL;
+            gvD += w * hi * hj * eD;
             grho += w * (hi * sj + si * hj) * kL;
             if (i == j && ri[e] == cj[e] && i * NB + ri[e] < a.n) gnoise += w;
         }
@@ -979,10 +1108,8 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
     }
     __syncthreads();
     reduce_entries([&](int qx, double v) {   // gpart [quantity][task]: coalesced reduction
-        if (qx == 0) v /= th.vL();
-        else if (qx <= a.D) { const double l = th.lL(qx - 1); v /= l * l * l; }
-        else if (qx == 1 + a.D) v /= th.vD();
-        else if (qx <= 1 + 2 * a.D) { const double l = th.lD(qx - 2 - a.D); v /= l * l * l; }
+        if (qx >= 1 && qx <= a.D) { const double l = th.lL(qx - 1); v /= l * l * l; }
+        else if (qx >= 2 + a.D && qx <= 1 + 2 * a.D) { const double l = th.lD(qx - 2 - a.D); v /= l * l * l; }
         return v;
     });
 }
@@ -1191,6 +1318,7 @@ __global__ void k_selftest_mfma(double* out /* 16x16 */) {
 // ============================================================ launch helpers
 template <int NB>
 void launch_gram(const GramArgs& g, int nblocks, int batch, hipStream_t s) {
+    if (!g.padded && !g.nlf) { launch_gram_dense(g, batch, 0, 0, s); return; }
     hipLaunchKernelGGL(k_gram<NB>, dim3(nblocks, 1, batch), dim3(NTHREADS), gram_smem_bytes(NB), s, g);
 }
 template <int NB>

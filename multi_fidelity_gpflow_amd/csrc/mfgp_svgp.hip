@@ -337,14 +337,13 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
     }
     // Kuf_l = K_l(Z, X), zero padded to Mpad x Npad
     {
-        (void)hipMemsetAsync(S.Kuf, 0, sizeof(double) * (size_t)S.mpad * S.npad * L, s);
         GramArgs g{};
         g.X1 = Z; g.ldx1 = ldz; g.sx1 = 0; g.n1 = m;
         g.X2 = X; g.ldx2 = ldx; g.sx2 = 0; g.n2 = n;
         g.theta = thetas; g.stheta = S.G; g.D = d; g.rbf_only = 0;
         g.out = S.Kuf; g.ldo = S.npad; g.so = (long)S.mpad * S.npad;
         g.padded = 0; g.tiles_c = S.Tn; g.diag_add = 0.0;
-        launch_gram<NB>(g, S.Tm * S.Tn, L, s);
+        launch_gram_dense(g, L, S.mpad, S.npad, s);   // zero padding written by the kernel
     }
     hipLaunchKernelGGL(k_svgp_cond<NB>, dim3(S.Tm * S.Tn, 1, L), dim3(NTHREADS),
                        sizeof(double) * (3 * NB * (NB + 2) + 12 * NB), s, S.Xo, S.C, S.Kuf, q_mu, L, m, S.Tm,

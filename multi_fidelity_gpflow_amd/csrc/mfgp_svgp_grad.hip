@@ -356,9 +356,10 @@ __global__ __launch_bounds__(NTHREADS) void k_kgrad(const double* P1, long ld1, 
                 rL = fma(xl, xl, rL);
             }
             const double sb = Lb ? 1.0 : rho;
-            const double kL = vL * exp(-0.5 * rL);
+            const double eL = exp(-0.5 * rL);   // dk/dvL (TF form: finite where vL underflows)
+            const double kL = vL * eL;
             const double wl = wv * sa * sb * kL;
-            gvL += wl;
+            gvL += wv * sa * sb * eL;
             grho += wv * ((Ha ? sb : 0.0) + (Hb ? sa : 0.0)) * kL;
             const bool hh = Ha && Hb && wv != 0.0;
             const bool anyhh = __ballot(hh) != 0;   // wave-uniform
@@ -370,8 +371,9 @@ __global__ __launch_bounds__(NTHREADS) void k_kgrad(const double* P1, long ld1, 
                     const double xd = (za[d] - xr[d]) * id[d];
                     rD = fma(xd, xd, rD);
                 }
-                wd = hh ? wv * vD * exp(-0.5 * rD) : 0.0;
-                gvD += wd;
+                const double we = hh ? wv * exp(-0.5 * rD) : 0.0;
+                wd = we * vD;
+                gvD += we;
             }
             // B operand: column j of [1 | x | x^2] of row b_k (rows past the end are zero and
             // carry zero weight)
@@ -432,9 +434,9 @@ __global__ __launch_bounds__(NTHREADS) void k_kgrad(const double* P1, long ld1, 
     }
     for (int q = t; q < G; q += NTHREADS) {
         double v = 0.0;
-        if (q == 0) v = ((wred[0][0] + wred[1][0]) + (wred[2][0] + wred[3][0])) / vL;
+        if (q == 0) v = (wred[0][0] + wred[1][0]) + (wred[2][0] + wred[3][0]);
         else if (q <= D) v = dsum[0][q - 1];
-        else if (q == D + 1) v = ((wred[0][1] + wred[1][1]) + (wred[2][1] + wred[3][1])) / vD;
+        else if (q == D + 1) v = (wred[0][1] + wred[1][1]) + (wred[2][1] + wred[3][1]);
         else if (q <= 2 * D + 1) v = dsum[1][q - D - 2];
         else if (q == 2 * D + 2) v = (wred[0][2] + wred[1][2]) + (wred[2][2] + wred[3][2]);
         gth_part[((long)lat * gridDim.x + blockIdx.x) * G + q] = v;   // noise slot (G - 1): 0

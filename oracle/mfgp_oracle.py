@@ -202,8 +202,12 @@ def gpr_lml_and_grad(X, Y, p: MFParams):
     HH = np.outer(h, h)
     SH = np.outer(h, s) + np.outer(s, h)
     g = {}
-    g["vL"] = 0.5 * np.sum(W * SS * kL) / p.vL
-    g["vD"] = 0.5 * np.sum(W * HH * kD) / p.vD
+    # dK/dv = exp(-r2/2): TF's autodiff of v * exp(-r2/2) (GPflow SquaredExponential.K), finite
+    # where v underflows to 0 (the division form K / v gave 0/0 at L-BFGS line-search points)
+    eL = rbf_K(Xc, Xc, 1.0, p.lL)
+    eD = rbf_K(Xc, Xc, 1.0, p.lD)
+    g["vL"] = 0.5 * np.sum(W * SS * eL)
+    g["vD"] = 0.5 * np.sum(W * HH * eD)
     g["rho0"] = 0.5 * np.sum(W * SH * kL)
     D = Xc.shape[1]
     gl, gd = np.zeros(D), np.zeros(D)

@@ -30,15 +30,17 @@ def _rbf(Xs: torch.Tensor, var: float, ls: torch.Tensor) -> torch.Tensor:
     return var * torch.exp(-0.5 * r2)
 
 
-def _blocks(X: torch.Tensor, vL, lL, vD, lD, rho0):
+def _blocks(X: torch.Tensor, vL, lL, vD, lD, rho0, unit=False):
     f = X[:, -1]
     isL = (f == 0).to(X.dtype)
     isH = (f == 1).to(X.dtype)
     s = isL + rho0 * isH
     Xc = X[:, :-1]
-    kL = _rbf(Xc, vL, lL)
-    kD = _rbf(Xc, vD, lD)
-    return s, isH, Xc, kL, kD
+    eL = _rbf(Xc, 1.0, lL)
+    eD = _rbf(Xc, 1.0, lD)
+    if unit:   # exp(-r2/2) too: dK/dv in TF's autodiff form
+        return s, isH, Xc, vL * eL, vD * eD, eL, eD
+    return s, isH, Xc, vL * eL, vD * eD
 
 
 def lml(X: torch.Tensor, Y: torch.Tensor, vL, lL, vD, lD, rho0, noise) -> float:
@@ -53,7 +55,7 @@ def lml(X: torch.Tensor, Y: torch.Tensor, vL, lL, vD, lD, rho0, noise) -> float:
 
 def lml_and_grad(X: torch.Tensor, Y: torch.Tensor, vL, lL, vD, lD, rho0, noise):
     """(LML, dLML/d[vL, lL(D), vD, lD(D), rho0, noise]) — constrained parameters, fp64."""
-    s, h, Xc, kL, kD = _blocks(X, vL, lL, vD, lD, rho0)
+    s, h, Xc, kL, kD, eL, eD = _blocks(X, vL, lL, vD, lD, rho0, unit=True)
     SS = s[:, None] * s[None, :]
     HH = h[:, None] * h[None, :]
     K = SS * kL + HH * kD
@@ -73,9 +75,9 @@ def lml_and_grad(X: torch.Tensor, Y: torch.Tensor, vL, lL, vD, lD, rho0, noise):
         return 2.0 * (r @ (Xc * Xc)) - 2.0 * ((M @ Xc) * Xc).sum(0)
 
     g = torch.cat([
-        (0.5 * ML.sum() / vL).reshape(1),
+        (0.5 * (W * SS * eL).sum()).reshape(1),
         0.5 * ls_grad(ML) / lL ** 3,
-        (0.5 * MD.sum() / vD).reshape(1),
+        (0.5 * (W * HH * eD).sum()).reshape(1),
         0.5 * ls_grad(MD) / lD ** 3,
         (0.5 * (W * SH * kL).sum()).reshape(1),
         (0.5 * W.diagonal().sum()).reshape(1),
