@@ -209,6 +209,26 @@ def _median_rate(fn, min_evals=20, budget_s=6.0):
     return 1.0 / float(np.median(ts)), len(ts)
 
 
+def host_cpus():
+    """(cores this process may run on, how that was found): the CPU affinity mask, capped by the
+    cgroup CPU quota when one is set (a container's share of a large host)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    src = f"sched_getaffinity {aff}"
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            q = max(1, int(int(quota) // int(period)))
+            src += f", cgroup cpu.max quota {q}"
+            aff = min(aff, q)
+    except (OSError, ValueError):
+        pass
+    return aff, src
+
+
 def cpu_baseline(X, Y):
     """fp64 torch-CPU restatement of the reference path (oracle/torch_oracle.py, checked against
     the KAT-pinned oracle/mfgp_oracle.py) on this host: all threads and 1 thread, value-only and
@@ -217,7 +237,8 @@ def cpu_baseline(X, Y):
     Xt = torch.as_tensor(X, dtype=torch.float64)
     Yt = torch.as_tensor(Y, dtype=torch.float64)
     args = TO.initial_args(X.shape[1] - 1)
-    nthreads = torch.get_num_threads()
+    torch_threads = torch.get_num_threads()
+    nthreads, cores_src = host_cpus()
     legs = {}
     for label, threads in (("all", nthreads), ("one", 1)):
         torch.set_num_threads(threads)
@@ -225,17 +246,19 @@ def cpu_baseline(X, Y):
             vg, nvg = _median_rate(lambda: TO.lml_and_grad(Xt, Yt, *args))
             v, nv = _median_rate(lambda: TO.lml(Xt, Yt, *args))
         finally:
-            torch.set_num_threads(nthreads)
+            torch.set_num_threads(torch_threads)
         legs[label] = {"threads": threads, "value_grad_evals_s": round(vg, 3), "value_evals_s": round(v, 3),
                        "samples": [nvg, nv]}
     return {"value": legs["all"]["value_grad_evals_s"], "unit": "LML value+grad evals/s",
-            "cores": nthreads, "kind": "port", "nproc": os.cpu_count(),
+            "cores": nthreads, "kind": "port", "nproc": os.cpu_count(), "cores_source": cores_src,
+            "torch_default_threads": torch_threads,
             "value_only_evals_s": legs["all"]["value_evals_s"],
             "one_core": legs["one"],
             "train_1000_adam_s_est": round(1000.0 / legs["all"]["value_grad_evals_s"], 2),
             "sample": (f"Goku (N={X.shape[0]}, P={Y.shape[1]}) fp64 LML value+grad and value-only evaluations at "
                        f"the initial theta, oracle/torch_oracle.py (MKL Cholesky/TRSM/GEMM), median of >=20 "
-                       f"after warm-up (fewer if a leg exceeds ~6 s), torch threads {nthreads} and 1; "
+                       f"after warm-up (fewer if a leg exceeds ~6 s), torch threads {nthreads} (the cores available: "
+                       f"{cores_src}) and 1; "
                        f"train_1000_adam_s_est = 1000 / value")}
 
 
@@ -244,28 +267,18 @@ def svgp_elbo_flops(n, m, L, p, d):
     return L * ((m * (m + 1) / 2 + m * n) * (3 * d + 6) + m ** 3 / 3 + 2 * m * m * n) + 4 * n * L * p
 
 
-def bench_svgp(args):
+def svgp_leg(X, Yr, Xt, steps, warmup, world=1, device=None, train_predict=True, latent=True):
     """BASELINE configs[3]: the Goku SVGP models of notebooks/demo: goku power spectra.ipynb --
     SingleBinSVGP (M=300 KMeans centres, L=P=64; cell 10, 1000 iterations, published 2237.47 s on
     the M1) and LatentMFCoregionalizationSVGP (L=15, M=300; published 1020.22 s for 2000).  A step
     is one optimize() iteration: ELBO + analytic gradient + Keras Adam with the CosineDecay
     schedule, replayed from hipGraphs (graphs captured in warm-up).  N > 1: each rank trains the
-    single-bin model of its own bin block (per-shard Z / noise, no collective)."""
+    single-bin model of its own bin block (per-shard Z / noise, no collective).  Returns the
+    per-rank times and the line's fields."""
     import multi_fidelity_gpflow_amd as M
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = dist_device_index()
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
-    if world > 1:
-        init_dist(device)
-    X, Y, Xt, Yt = broadcast_inputs(rank, world, device)
-    n, d, P = X.shape[0], X.shape[1] - 1, Y.shape[1]
-    from multi_fidelity_gpflow_amd.distributed import bin_block
-    b0, b1 = bin_block(P, rank, world)
-    Yr = np.ascontiguousarray(Y[:, b0:b1])
+    n, d = X.shape[0], X.shape[1] - 1
     pr = Yr.shape[1]
-    K, W = args.steps, args.warmup
+    K, W = steps, warmup
     kern = lambda: M.SquaredExponential(lengthscales=np.ones(d))
 
     def timed(model, max_iters):
@@ -286,16 +299,19 @@ def bench_svgp(args):
             t = torch.tensor([dt], dtype=torch.float64, device=device)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
-        return dt, tr
+        tr.close()
+        return dt
 
     sb = M.SingleBinSVGP(X, Yr, kern(), kern(), pr, Z=np.zeros((300, d + 1)))
-    dt_sb, _ = timed(sb, K + W)
-    lat = M.LatentMFCoregionalizationSVGP(X, Yr, kern(), kern(), num_latents=min(15, pr), num_inducing=300,
-                                          num_outputs=pr, w_type="diagonal", window_fraction=0.4, scale=0.2)
-    dt_lat, _ = timed(lat, max(K + W, 2000))
+    dt_sb = timed(sb, K + W)
+    dt_lat = None
+    if latent:
+        lat = M.LatentMFCoregionalizationSVGP(X, Yr, kern(), kern(), num_latents=min(15, pr), num_inducing=300,
+                                              num_outputs=pr, w_type="diagonal", window_fraction=0.4, scale=0.2)
+        dt_lat = timed(lat, max(K + W, 2000))
     # notebook protocol for the single-bin model: a fresh model, optimize(max_iters=1000, initial_lr=0.1)
     train_s = None
-    if not args.no_train_predict:
+    if train_predict:
         m2 = M.SingleBinSVGP(X, Yr, kern(), kern(), pr, Z=np.zeros((300, d + 1)))
         torch.cuda.synchronize()
         t1 = time.perf_counter()
@@ -303,34 +319,147 @@ def bench_svgp(args):
         m2.predict_f(Xt)
         torch.cuda.synchronize()
         train_s = time.perf_counter() - t1
+    fl = svgp_elbo_flops(n, 300, pr, pr, d)
+    achieved = fl * K / dt_sb / 1e12
+    return {
+        "steps": K, "warmup": W,
+        "ms_per_step": round(dt_sb / K * 1e3, 4),
+        "iters_per_s": round(world * K / dt_sb, 3),
+        "config": {"workload": "goku_singlebin_svgp_step", "n": n, "d": d, "m": 300, "latents": pr,
+                   "bins_per_rank": pr},
+        "latent_l15": None if dt_lat is None else {
+            "latents": min(15, pr), "ms_per_step": round(dt_lat / K * 1e3, 4),
+            "iters_per_s": round(world * K / dt_lat, 3), "published_m1_s_per_iter": round(1020.22 / 2000, 4)},
+        "train_1000_predict_s": None if train_s is None else round(train_s, 3),
+        "published_m1": {"train_1000_s": 2237.47, "source": "notebooks/demo: goku power spectra.ipynb:451"},
+        "roofline": {"kernel": "whole optimize() iteration (SURVEY §8(d) ELBO-value flops only; the gradient's "
+                               "reverse pass is not counted, so this is a lower bound)",
+                     "bound": "mfma", "achieved": round(achieved, 4), "peak": FP64_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 5), "traffic": None,
+                     "flop_per_step": fl},
+    }
+
+
+def bench_svgp(args):
+    """--config goku_svgp: the SVGP leg as the headline line."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = dist_device_index()
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        init_dist(device)
+    X, Y, Xt, Yt = broadcast_inputs(rank, world, device)
+    from multi_fidelity_gpflow_amd.distributed import bin_block
+    b0, b1 = bin_block(Y.shape[1], rank, world)
+    Yr = np.ascontiguousarray(Y[:, b0:b1])
+    leg = svgp_leg(X, Yr, Xt, args.steps, args.warmup, world, device, train_predict=not args.no_train_predict)
     if rank == 0:
-        value = world * K / dt_sb
-        fl = svgp_elbo_flops(n, 300, pr, pr, d)
-        achieved = fl * K / dt_sb / 1e12
+        cfg = dict(leg.pop("config"), parallelism=f"bins{world}" if world > 1 else "single")
         line = {
             "metric": "SVGP optimize iterations/s (Goku SingleBinSVGP M=300, L=P=64: ELBO + gradient + Adam)",
-            "value": round(value, 3), "unit": "iters/s", "n_gpus": world, "steps": K, "warmup": W,
-            "ms_per_step": round(dt_sb / K * 1e3, 4), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f64",
+            "value": leg.pop("iters_per_s"), "unit": "iters/s", "n_gpus": world, "steps": leg.pop("steps"),
+            "warmup": leg.pop("warmup"), "ms_per_step": leg.pop("ms_per_step"), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "Goku z=0 P(k) (reference data files, tests/golden/data), RCCL-broadcast from rank 0",
-            "config": {"workload": "goku_singlebin_svgp_step", "n": n, "d": d, "m": 300, "latents": pr,
-                       "bins_per_rank": pr, "parallelism": f"bins{world}" if world > 1 else "single"},
-            "latent_l15": {"latents": min(15, pr), "ms_per_step": round(dt_lat / K * 1e3, 4),
-                           "iters_per_s": round(world * K / dt_lat, 3),
-                           "published_m1_s_per_iter": round(1020.22 / 2000, 4)},
-            "train_1000_predict_s": None if train_s is None else round(train_s, 3),
-            "published_m1": {"train_1000_s": 2237.47, "source": "notebooks/demo: goku power spectra.ipynb:451"},
-            "roofline": {"kernel": "whole optimize() iteration (SURVEY §8(d) ELBO-value flops only; the gradient's "
-                                   "reverse pass is not counted, so this is a lower bound)",
-                         "bound": "mfma", "achieved": round(achieved, 4), "peak": FP64_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 5), "traffic": None,
-                         "flop_per_step": fl},
-            "cpu_baseline": None,
+            "config": cfg,
         }
+        line.update(leg)
+        line["cpu_baseline"] = None
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
     return 0
+
+
+HBS = os.path.join(ROOT, "tests", "golden", "data", "50_LR_3_HR")
+
+
+def hbs_leg(steps=200, warmup=20):
+    """BASELINE configs[1] (Ho-Bird-Shelton 50LF/3HF, D=5, P=49, fp64): pure latency, so the
+    figure is wall-clock.  train_predict_s = the reference's test protocol
+    (tests/test_ho2021_multibin.py:20-43: a fresh MultiFidelityGPModel, optimize(max_iters=100,
+    use_adam=True, learning_rate=0.1, unfix_noise_after=50), then predict_f on the 10 test
+    inputs), after one untimed run of the same protocol (per-process kernel loading and graph
+    set-up); ms_per_step = replayed Adam steps of a session, like the Goku line."""
+    from multi_fidelity_gpflow_amd.data import PowerSpecs, multifidelity_training_set
+    ps = PowerSpecs()
+    ps.read_from_txt(HBS)
+    X, Y, Xt, _ = multifidelity_training_set(ps)
+    n, d, P = X.shape[0], X.shape[1] - 1, Y.shape[1]
+
+    def protocol():
+        m = make_model(X, Y)
+        m.optimize(max_iters=100, learning_rate=0.1, use_adam=True, unfix_noise_after=50, verbose=False)
+        mean, var = m.predict_f(Xt)
+        torch.cuda.synchronize()
+        return m
+
+    protocol()
+    ts = []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        protocol()
+        ts.append(time.perf_counter() - t0)
+    model = make_model(X, Y)
+    sess = model.adam_session(0.1, steps + warmup, graph=True, graph_chunk=50)
+    sess.run(warmup)
+    sess.prepare(steps)
+    sess.sync()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sess.run(steps)
+    sess.sync()
+    dt = time.perf_counter() - t0
+    sess.finish()
+    roof = roofline(model, n, P, d, pmc=False)
+    roof["bound"] = "latency"
+    return {
+        "config": {"workload": "hbs_multibin_adam_step", "n_lf": int((X[:, -1] == 0).sum()),
+                   "n_hf": int((X[:, -1] == 1).sum()), "d": d, "p": P},
+        "dtype": "f64",
+        "train_predict_s": round(float(np.median(ts)), 5),
+        "train_predict_s_runs": [round(t, 5) for t in ts],
+        "protocol": "tests/test_ho2021_multibin.py:20-43 (optimize 100 Adam steps, lr 0.1, then predict_f(X_test))",
+        "steps": steps, "warmup": warmup,
+        "ms_per_step": round(dt / steps * 1e3, 4),
+        "evals_per_s": round(steps / dt, 2),
+        "roofline": roof,
+    }
+
+
+def synth_leg(steps=3, warmup=2):
+    """BASELINE configs[4] (synthetic N_L=16384, N_H=2048, D=10, P=512, fp32), 1 GPU: replayed
+    value+grad+Adam steps (graphs of 2 steps captured in warm-up), roofline of k32_update."""
+    from multi_fidelity_gpflow_amd.data import synthetic_multifidelity
+    X, Y, Xt, Yt = synthetic_multifidelity()
+    n, d, P = X.shape[0], X.shape[1] - 1, Y.shape[1]
+    model = make_model(X, Y, "float32")
+    sess = model.adam_session(0.1, steps + warmup, graph=True, graph_chunk=2)
+    sess.run(warmup)
+    sess.prepare(steps)
+    sess.sync()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sess.run(steps)
+    sess.sync()
+    dt = time.perf_counter() - t0
+    sess.finish()
+    roof = roofline_f32(model, reps=1)
+    out = {
+        "config": {"workload": "synth_multibin_adam_step", "n_lf": int((X[:, -1] == 0).sum()),
+                   "n_hf": int((X[:, -1] == 1).sum()), "d": d, "p": P},
+        "dtype": "f32",
+        "steps": steps, "warmup": warmup,
+        "ms_per_step": round(dt / steps * 1e3, 3),
+        "evals_per_s": round(steps / dt, 3),
+        "step_tflops": round(step_flops(n, P, d) * steps / dt / 1e12, 2),
+        "roofline": roof,
+    }
+    del sess, model
+    torch.cuda.empty_cache()
+    return out
 
 
 def dist_device_index() -> int:
@@ -371,6 +500,8 @@ def main():
     ap.add_argument("--tile", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-train-predict", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the hbs / synth / goku_svgp sub-objects of the default (Goku, N=1) line")
     ap.add_argument("--mode", choices=["shard", "shared"], default="shard",
                     help="shard: per-shard-theta bin blocks (no inner-loop collective); shared: one model, "
                          "one all-reduce of 1+G doubles per step (reference-parity mode, SURVEY 8(e))")
@@ -392,6 +523,13 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if world > max(torch.cuda.device_count(), 1):
+        # ranks share a device (a rehearsal on fewer GPUs): persistent flows of different
+        # processes cannot all be resident (the library's fence is per process), so use the
+        # launch-per-step Cholesky
+        os.environ["MFGP_FLOW"] = "0"
+        if rank == 0:
+            print("bench.py: more ranks than GPUs, persistent Cholesky disabled (MFGP_FLOW=0)", file=sys.stderr)
     local = dist_device_index()
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
@@ -499,6 +637,11 @@ def main():
             "published_m1_cpu": None if synth else {"train_1000_adam_s": 142.36, "evals_per_s": 7.02,
                                                     "source": "notebooks/demo: goku power spectra.ipynb:120"},
         }
+        if world == 1 and args.config == "goku" and not args.no_extras:
+            # every other BASELINE config, measured in this process after the headline timing
+            line["hbs"] = hbs_leg()
+            line["goku_svgp"] = svgp_leg(X, Yr, Xt, 20, 5)
+            line["synth"] = synth_leg()
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()

@@ -67,6 +67,16 @@ int mfgp_get_flow(mfgp_handle_t h);
  * failure (not every workgroup resident, e.g. another kernel holding CUs), not a numerical one.
  * 0 makes any wait that polls 8 times give up (diagnostic: exercises the abort path). */
 int mfgp_set_flow_timeout_us(mfgp_handle_t h, long long us);
+/* Device-wide ordering of the persistent flow (k_chol_flow needs every CU; two flows launched
+ * on two streams at once would each stall waiting for workgroups the other keeps off the CUs).
+ * The library fences every flow it launches outside a stream capture: the launch waits for the
+ * previous flow on the device (any handle, stream or host thread of the process) and becomes the
+ * last one.  A captured graph's flows are not fenced at capture: before replaying such a graph
+ * call mfgp_flow_fence(h, MFGP_FENCE_WAIT) on the replay stream, and after enqueueing the replay
+ * mfgp_flow_fence(h, MFGP_FENCE_RECORD).  Stream-ordered only (no host synchronisation). */
+#define MFGP_FENCE_WAIT 0
+#define MFGP_FENCE_RECORD 1
+int mfgp_flow_fence(mfgp_handle_t h, int op);
 /* Where the flow timeline sits inside an mfgp_gpr_* workspace (diagnostic): `count` int64
  * ticks of the 100 MHz device clock from byte `offset`: per step k the diag workgroup's step
  * start [k], A' ready [T+k], factor start [2T+k], D_k published [3T+k], owner hand-offs of
@@ -208,6 +218,15 @@ int mfgp_adam_packed(mfgp_handle_t h, int n, double* u, double* c, const double*
                      int* step,
                      const double* lr_sched, double beta1, double beta2, double eps, const double* out,
                      double kl_mult, double* loss_hist, double* kl_hist);
+/* mfgp_adam_packed gated on the evaluation's info words (info[0..ninfo), e.g. the per-latent
+ * Cholesky info of mfgp_svgp_elbo_grad or the info of mfgp_gpr_lml): if any is nonzero the step
+ * leaves u / c / m / v and the step counter unchanged (loss_hist[step] still records the loss),
+ * like the fused step of mfgp_gpr_adam_step: a session can tell lost steps by the counter. */
+int mfgp_adam_packed_ex(mfgp_handle_t h, int n, double* u, double* c, const double* g, double* m, double* v,
+                        const unsigned char* trainable, const unsigned char* transform, const unsigned char* span,
+                        int* step, const double* lr_sched, double beta1, double beta2, double eps,
+                        const double* out, double kl_mult, double* loss_hist, double* kl_hist, const int* info,
+                        int ninfo);
 
 /* SVGP.predict_f(Xnew, full_cov=False) of the same models (GPflow posteriors with
  * mix_latent_gp): latent moments g_mu / g_var [L][nstar] and mixed f_mu / f_var

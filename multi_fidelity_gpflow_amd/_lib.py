@@ -31,6 +31,7 @@ SIGNATURES = {
     "mfgp_set_flow": [_p, _i],
     "mfgp_get_flow": [_p],
     "mfgp_set_flow_timeout_us": [_p, C.c_longlong],
+    "mfgp_flow_fence": [_p, _i],
     "mfgp_gpr_flow_trace": [_p, _i, _i, _i, C.POINTER(C.c_size_t), C.POINTER(_i)],
     "mfgp_rbf_gram": [_p, _i, _i, _i, _p, _i, _p, _i, _p, _p, _i],
     "mfgp_mf_gram": [_p, _i, _i, _i, _p, _i, _p, _i, _p, _d, _p, _i],
@@ -56,6 +57,7 @@ SIGNATURES = {
     "mfgp_svgp_elbo_grad": [_p, _i, _i, _i, _i, _i, _p, _i, _p, _i, _p, _i, _p, _p, _p, _p, _p, _d, _d, _d, _p,
                             _sz, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
     "mfgp_adam_packed": [_p, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _d, _d, _d, _p, _d, _p, _p],
+    "mfgp_adam_packed_ex": [_p, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _d, _d, _d, _p, _d, _p, _p, _p, _i],
     "mfgp_gmf_gram": [_p, _i, _i, _i, _i, _p, _i, _p, _i, _p, _d, _p, _i],
     "mfgp_gmf_kdiag": [_p, _i, _i, _i, _p, _i, _p, _p],
     "mfgp_gmf_gpr_workspace_size": [_p, _i, _i, _i, _i, C.POINTER(_sz)],
@@ -91,6 +93,8 @@ class MFGPError(RuntimeError):
 
 
 MFGP_FLOW_TIMEOUT = -100   # include/mfgp.h: info written when a k_chol_flow hand-off stalled
+MFGP_FENCE_WAIT = 0        # include/mfgp.h mfgp_flow_fence ops
+MFGP_FENCE_RECORD = 1
 
 
 class FlowTimeoutError(MFGPError):

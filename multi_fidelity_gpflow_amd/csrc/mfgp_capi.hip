@@ -8,6 +8,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
+
 #include "../../include/mfgp.h"
 #include "mfgp_device.h"
 #include "mfgp_internal.h"
@@ -111,6 +113,49 @@ static GprLayout gpr_layout(int nb, int n, int p, int d, void* ws, int grad_chun
 
 static inline hipError_t last() { return hipGetLastError(); }
 
+// ---------------------------------------------------------------- device-wide flow fence
+// k_chol_flow needs every CU: two flows whose workgroups interleave (launched on two streams
+// at once) each wait for workgroups the other keeps off the CUs, and stall to the hand-off bound.
+// One fence per device for the whole process (every handle, every stream, every host thread):
+// each flow launch waits for the previous one and becomes the new last one.  Stream-ordered
+// (hipStreamWaitEvent), never a host synchronisation.  Inside a stream capture the wait / record
+// are skipped (an event recorded outside a capture cannot be waited on inside it): the caller
+// orders the replay of such a graph with mfgp_flow_fence (the Python sessions do).
+struct FlowFence {
+    std::mutex mu;
+    hipEvent_t ev = nullptr;
+    bool armed = false;
+};
+constexpr int FENCE_MAX_DEVICES = 64;
+static FlowFence g_fence[FENCE_MAX_DEVICES];
+
+static bool stream_capturing(hipStream_t s) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
+}
+
+static void fence_wait(int dev, hipStream_t s) {
+    if (dev < 0 || dev >= FENCE_MAX_DEVICES || stream_capturing(s)) return;
+    FlowFence& f = g_fence[dev];
+    std::lock_guard<std::mutex> lk(f.mu);
+    if (f.armed) (void)hipStreamWaitEvent(s, f.ev, 0);
+}
+
+static void fence_record(int dev, hipStream_t s) {
+    if (dev < 0 || dev >= FENCE_MAX_DEVICES || stream_capturing(s)) return;
+    FlowFence& f = g_fence[dev];
+    std::lock_guard<std::mutex> lk(f.mu);
+    if (!f.ev) {
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (cur != dev) (void)hipSetDevice(dev);
+        if (hipEventCreateWithFlags(&f.ev, hipEventDisableTiming) != hipSuccess) f.ev = nullptr;
+        if (cur >= 0 && cur != dev) (void)hipSetDevice(cur);
+        if (!f.ev) return;
+    }
+    if (hipEventRecord(f.ev, s) == hipSuccess) f.armed = true;
+}
+
 // k_gram (LML layout) with more lower tiles than CUs: one workgroup per CU, tile (0,0) and its
 // fused factor alone on workgroup 0 (beside two other tile workgroups it took ~2x as long, and
 // it is the launch's tail), the rest looping over the other tiles.  0: one tile per workgroup.
@@ -156,6 +201,7 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
                           const FinArgs* adam, PhaseMarks* pm = nullptr, int nlf = 0) {
     const GprLayout L = gpr_layout(NB, n, p, d, ws, h->grad_chunk, nlf, h->flow_wgs);
     if (ws_bytes < L.bytes) return MFGP_ERR_WORKSPACE;
+    if (L.G > FIN_MAXG) return MFGP_ERR_ARG;   // finalize_body stages theta in LDS
     hipStream_t s = h->stream;
     const long ldr = L.npad + L.ppad;
     if (pm) pm->mark(s);
@@ -191,7 +237,9 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
         fa.trace = h->flow_trace ? L.trace : nullptr;
         fa.nwaves = FLOW_WAVES * (L.flow_wgs - 1);
         fa.timeout = h->flow_timeout;
+        fence_wait(h->device, s);
         launch_chol_flow(fa, L.flow_wgs, s);
+        fence_record(h->device, s);
     } else {
         CholArgs c{};
         c.A = L.A; c.lda = L.npad; c.sA = 0;
@@ -423,7 +471,7 @@ int svgp_grad_impl(hipStream_t s, int nb, int n, int m, int l, int p, int d, con
 int adam_packed_impl(hipStream_t st, int n, double* u, double* c, const double* g, double* m, double* v,
                      const unsigned char* trainable, const unsigned char* transform, const unsigned char* span,
                      int* step, const double* lr_sched, double b1, double b2, double eps, const double* out,
-                     double klm, double* loss_hist, double* kl_hist);
+                     double klm, double* loss_hist, double* kl_hist, const int* info, int ninfo);
 
 int svgp_predict_impl(hipStream_t s, int nb, int n, int m, int l, int p, int d, const double* Xs, int ldx,
                       const double* Z, int ldz, const double* thetas, const double* q_mu, const double* q_sqrt,
@@ -627,6 +675,14 @@ int mfgp_set_flow_timeout_us(mfgp_handle_t h, long long us) {
 }
 
 int mfgp_get_flow(mfgp_handle_t h) { return h ? (h->flow_wgs > 0 ? 1 : 0) : MFGP_ERR_ARG; }
+
+int mfgp_flow_fence(mfgp_handle_t h, int op) {
+    CHECK_H(h);
+    if (op == MFGP_FENCE_WAIT) fence_wait(h->device, h->stream);
+    else if (op == MFGP_FENCE_RECORD) fence_record(h->device, h->stream);
+    else return MFGP_ERR_ARG;
+    return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;
+}
 
 static int gram_common(mfgp_handle_t h, int n1, int n2, int d, const double* X1, int ldx1, const double* X2,
                        int ldx2, const double* params, double diag_add, double* K, int ldk, int rbf, int nlf = 0) {
@@ -917,7 +973,20 @@ int mfgp_adam_packed(mfgp_handle_t h, int n, double* u, double* c, const double*
     if (n < 1 || !u || !c || !g || !m || !v || !trainable || !transform || !step || !lr_sched || !out)
         return MFGP_ERR_ARG;
     return adam_packed_impl(h->stream, n, u, c, g, m, v, trainable, transform, span, step, lr_sched, beta1, beta2, eps,
-                            out, kl_mult, loss_hist, kl_hist);
+                            out, kl_mult, loss_hist, kl_hist, nullptr, 0);
+}
+
+int mfgp_adam_packed_ex(mfgp_handle_t h, int n, double* u, double* c, const double* g, double* m, double* v,
+                        const unsigned char* trainable, const unsigned char* transform, const unsigned char* span,
+                        int* step, const double* lr_sched, double beta1, double beta2, double eps,
+                        const double* out, double kl_mult, double* loss_hist, double* kl_hist, const int* info,
+                        int ninfo) {
+    CHECK_H(h);
+    if (n < 1 || !u || !c || !g || !m || !v || !trainable || !transform || !step || !lr_sched || !out || ninfo < 0 ||
+        (ninfo > 0 && !info))
+        return MFGP_ERR_ARG;
+    return adam_packed_impl(h->stream, n, u, c, g, m, v, trainable, transform, span, step, lr_sched, beta1, beta2, eps,
+                            out, kl_mult, loss_hist, kl_hist, info, ninfo);
 }
 
 int mfgp_svgp_predict(mfgp_handle_t h, int nstar, int m, int l, int p, int d, const double* Xs, int ldxs,

@@ -91,6 +91,7 @@ struct GradArgs {
     const int* order;                     // workgroup -> task (nullptr: identity), see grad_order
 };
 
+constexpr int FIN_MAXG = 254;   // theta entries finalize_body stages in LDS (graph kernel: <= 186)
 struct FinArgs {
     const double* zpart; int nz;
     const double* ldiag; int n;

@@ -1126,7 +1126,8 @@ size_t grad_smem_bytes(int nb, int G, int nil2) {
 // Stage 2: LML, gradient output and the optional Keras-Adam step; run by the last
 // item workgroup of k_reduce_items to arrive.
 __device__ void adam_body(const FinArgs& a, int G, int s, const double* gsh, const int* tsh);
-constexpr int FIN_MAXG = 254;   // theta entries staged in LDS (graph kernel: <= 186)
+static_assert(FIN_MAXG >= kernel_theta_size(MFGP_MAX_LF, MAXD) && FIN_MAXG >= kernel_theta_size(0, MAXD),
+              "finalize_body stages every theta entry in LDS");
 __device__ void finalize_body(const FinArgs& a) {
     const int G = a.G ? a.G : theta_size(a.D);
     const double LOG2PI = 1.8378770664093453;

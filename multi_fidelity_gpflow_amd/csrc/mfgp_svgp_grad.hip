@@ -707,7 +707,9 @@ int svgp_grad_impl(hipStream_t s, int nb, int n, int m, int l, int p, int d, con
 __global__ void k_adam_packed(int n, double* u, double* c, const double* g, double* m, double* v,
                               const unsigned char* trainable, const unsigned char* transform,
                               const unsigned char* span, const int* step, const double* lr_sched, double b1,
-                              double b2, double eps) {
+                              double b2, double eps, const int* info, int ninfo) {
+    for (int i = 0; i < ninfo; ++i)
+        if (info[i] != 0) return;   // failed evaluation: no update (the step counter stays)
     const int s = *step;
     const double t = (double)(s + 1);
     const double alpha = lr_sched[s] * sqrt(1.0 - pow(b2, t)) / (1.0 - pow(b1, t));
@@ -739,21 +741,26 @@ __global__ void k_adam_packed(int n, double* u, double* c, const double* g, doub
 }
 
 // loss_hist[step] = -out[0] + (klm - 1) out[1] (the optimised objective), kl_hist[step] = out[1]; ++step
-__global__ void k_step_record(const double* out, double klm, double* loss_hist, double* kl_hist, int* step) {
+// (info gate: with a nonzero info word the counter stays, so the next step rewrites this entry)
+__global__ void k_step_record(const double* out, double klm, double* loss_hist, double* kl_hist, int* step,
+                              const int* info, int ninfo) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     const int s = *step;
     if (loss_hist) loss_hist[s] = -out[0] + (klm - 1.0) * out[1];
     if (kl_hist) kl_hist[s] = out[1];
-    *step = s + 1;
+    bool ok = true;
+    for (int i = 0; i < ninfo; ++i) ok = ok && info[i] == 0;
+    if (ok) *step = s + 1;
 }
 
 int adam_packed_impl(hipStream_t st, int n, double* u, double* c, const double* g, double* m, double* v,
                      const unsigned char* trainable, const unsigned char* transform, const unsigned char* span,
                      int* step, const double* lr_sched, double b1, double b2, double eps, const double* out,
-                     double klm, double* loss_hist, double* kl_hist) {
+                     double klm, double* loss_hist, double* kl_hist, const int* info, int ninfo) {
+    if (!info) ninfo = 0;
     hipLaunchKernelGGL(k_adam_packed, dim3(std::min(cdv(n, 256), 1024)), dim3(256), 0, st, n, u, c, g, m, v, trainable,
-                       transform, span, step, lr_sched, b1, b2, eps);
-    hipLaunchKernelGGL(k_step_record, dim3(1), dim3(64), 0, st, out, klm, loss_hist, kl_hist, step);
+                       transform, span, step, lr_sched, b1, b2, eps, info, ninfo);
+    hipLaunchKernelGGL(k_step_record, dim3(1), dim3(64), 0, st, out, klm, loss_hist, kl_hist, step, info, ninfo);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

@@ -134,10 +134,15 @@ class SharedThetaTrainer:
                 self.info.copy_(info)
                 return self.out
 
+            self.bad = torch.zeros((1,), dtype=torch.int32, device=dev)
+
             def _adam(out):
+                # the reduced LML is NaN on every rank when any rank's evaluation failed (its
+                # finalize writes NaN): all ranks then skip the update and keep the step counter
+                self.bad.copy_(torch.isnan(out[:1]))
                 eng.adam_packed(self.u, self.theta, out[1:], self.m, self.v, self.trainable, self.transform,
                                 self.span, self.step_t, self.lr, self.b1, self.b2, 1e-7, out, 1.0, self.hist_t,
-                                None)
+                                None, info=self.bad)
             self.lml_grad, self.adam = _lml_grad, _adam
         else:
             self.lml_grad, self.adam = lml_grad, adam
@@ -158,7 +163,7 @@ class SharedThetaTrainer:
 
     def finish(self):
         """Write theta back into the model (device path) and its loss_history."""
-        from ._lib import MFGP_FLOW_TIMEOUT, info_error
+        from ._lib import MFGP_FLOW_TIMEOUT, MFGPError, info_error
         from .models import CholeskyError
         if not hasattr(self, "u"):
             return
@@ -167,7 +172,11 @@ class SharedThetaTrainer:
         h = self.hist_t[:self.done].cpu().numpy()
         self.model.loss_history = [np.float64(v) for v in h]
         v = int(self.info.item())
+        steps = int(self.step_t.item())
         if v == MFGP_FLOW_TIMEOUT:
             raise info_error(v, "shared-theta optimize")
+        if v == 0 and steps != self.done and np.all(np.isfinite(h)):
+            raise MFGPError(f"shared-theta optimize: {self.done - steps} of {self.done} steps failed on some rank "
+                            f"and were retried; the trajectory is incomplete")
         if v != 0 or not np.all(np.isfinite(h)):
             raise CholeskyError("shared-theta optimize: Cholesky failed")

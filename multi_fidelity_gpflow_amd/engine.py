@@ -63,7 +63,6 @@ class Engine:
         self.device = device
         self.index = device.index if device.index is not None else torch.cuda.current_device()
         self._ws: dict = {}
-        self._last_ordered = None
         self.lib = _lib.load()
 
     @classmethod
@@ -81,20 +80,21 @@ class Engine:
     # ------------------------------------------------------------ session ordering
     @contextlib.contextmanager
     def ordered(self, stream: torch.cuda.Stream):
-        """Work enqueued on `stream` inside the block starts after the previous ordered block on
-        this device ended, whatever its stream.  Training sessions run on streams of their own,
-        and two persistent k_chol_flow launches must never share the device: each needs every CU
-        resident, and one that cannot get them stalls until its hand-off bound expires (a lost
-        step).  Device-side ordering only: no host synchronisation."""
-        prev = self._last_ordered
-        if prev is not None:
-            stream.wait_event(prev)
+        """Work enqueued on `stream` inside the block starts after the previous flow-bearing work
+        on this device ended (whatever its stream, handle or host thread), and the block's end
+        becomes the new last one: the library's device-wide flow fence (include/mfgp.h
+        mfgp_flow_fence).  Two persistent k_chol_flow launches must never share the device: each
+        needs every CU resident, and one that cannot get them stalls until its hand-off bound
+        expires (a lost step).  The library fences every eager flow launch itself; this block is
+        for graph replays, whose flows were captured unfenced.  Device-side ordering only: no host
+        synchronisation."""
+        with torch.cuda.stream(stream):
+            check(self.lib.mfgp_flow_fence(self.h, _lib.MFGP_FENCE_WAIT), "mfgp_flow_fence")
         try:
             yield
         finally:
-            ev = torch.cuda.Event()
-            ev.record(stream)
-            self._last_ordered = ev
+            with torch.cuda.stream(stream):
+                check(self.lib.mfgp_flow_fence(self.h, _lib.MFGP_FENCE_RECORD), "mfgp_flow_fence")
 
     # ------------------------------------------------------------ plumbing
     @property
@@ -351,11 +351,14 @@ class Engine:
                                            ptr(gnoise), ptr(info)), "mfgp_svgp_elbo_grad")
 
     def adam_packed(self, u, c, g, m, v, trainable, transform, span, step, lr_sched, b1, b2, eps, out, kl_mult,
-                    loss_hist, kl_hist):
-        check(self.lib.mfgp_adam_packed(self.h, u.numel(), ptr(u), ptr(c), ptr(g), ptr(m), ptr(v), ptr(trainable),
-                                        ptr(transform), ptr(span), ptr(step), ptr(lr_sched), float(b1), float(b2),
-                                        float(eps), ptr(out), float(kl_mult), ptr(loss_hist), ptr(kl_hist)),
-              "mfgp_adam_packed")
+                    loss_hist, kl_hist, info=None):
+        """One packed Keras-Adam step; with `info` (the evaluation's int32 info words) a failed
+        evaluation leaves the parameters and the step counter unchanged (mfgp_adam_packed_ex)."""
+        check(self.lib.mfgp_adam_packed_ex(self.h, u.numel(), ptr(u), ptr(c), ptr(g), ptr(m), ptr(v), ptr(trainable),
+                                           ptr(transform), ptr(span), ptr(step), ptr(lr_sched), float(b1), float(b2),
+                                           float(eps), ptr(out), float(kl_mult), ptr(loss_hist), ptr(kl_hist),
+                                           ptr(info), 0 if info is None else info.numel()),
+              "mfgp_adam_packed_ex")
 
     def svgp_predict(self, Xs, Z, thetas, q_mu, q_sqrt, W, p, jitter=1e-6):
         ns, dp1 = Xs.shape

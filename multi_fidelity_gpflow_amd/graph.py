@@ -18,7 +18,7 @@ import torch
 
 from .engine import Engine, to_dev
 from .kernels import GraphMultiFidelityKernel
-from ._lib import MFGP_FLOW_TIMEOUT, info_error
+from ._lib import MFGP_FLOW_TIMEOUT, MFGPError, info_error
 from .models import CholeskyError, Gaussian, _StepRunner
 from .params import Module, Sigmoid, Softplus, as_result, set_trainable
 
@@ -239,7 +239,8 @@ class _GraphAdamSession:
     def _step(self):
         self._lml()
         self.eng.adam_packed(self.u, self.theta, self.out[1:], self.mo, self.vo, self.trainable, self.transform,
-                             self.span, self.step, self.lr, self.b1, self.b2, 1e-7, self.out, 1.0, self.hist, None)
+                             self.span, self.step, self.lr, self.b1, self.b2, 1e-7, self.out, 1.0, self.hist, None,
+                             info=self.info)
 
     def run(self, n):
         if self.done + n > self.max_iters:
@@ -248,8 +249,13 @@ class _GraphAdamSession:
             self.runner.run(n)
         self.done += n
 
+    def close(self):
+        """Release the recorded step graphs now (a later run re-captures)."""
+        self.runner.close()
+
     def finish(self):
         self.stream.synchronize()
+        self.close()
         u = self.u.cpu().numpy()
         for (prm, idx), uq in zip(self.ents, u):
             if idx is None:
@@ -261,7 +267,11 @@ class _GraphAdamSession:
         h = self.hist[:self.done].cpu().numpy()
         self.model.loss_history = [np.float64(v) for v in h]
         v = int(self.info.item())
+        steps = int(self.step.item())
         if v == MFGP_FLOW_TIMEOUT:
             raise info_error(v, "optimize")
+        if v == 0 and steps != self.done and np.all(np.isfinite(h)):
+            raise MFGPError(f"optimize: {self.done - steps} of {self.done} steps failed and were retried; "
+                            f"the trajectory is incomplete")
         if v != 0 or not np.all(np.isfinite(h)):
             raise CholeskyError("optimize: Cholesky failed")

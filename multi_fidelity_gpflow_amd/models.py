@@ -19,7 +19,7 @@ Behavioural quirks of the reference that are reproduced:
 """
 from __future__ import annotations
 
-import gc
+import weakref
 
 import numpy as np
 import torch
@@ -324,8 +324,19 @@ class AdamSession:
         self.sync()
         return float(self.hist[i].item())
 
+    def close(self):
+        """Release the recorded step graphs now (a later run re-captures)."""
+        self.runner.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
     def finish(self):
         self.sync()
+        self.close()
         h = self.hist[:self.done].cpu().numpy()
         self.model.loss_history = [np.float64(v) for v in h]
         self.tm.set_u(self.st.u.cpu().numpy())
@@ -346,29 +357,36 @@ class AdamSession:
 
 class _StepRunner:
     """Runs a step function n times: eagerly, or replaying a hipGraph of `chunk`
-    captured steps (torch.cuda.CUDAGraph is the HIP graph API on ROCm)."""
+    captured steps (torch.cuda.CUDAGraph is the HIP graph API on ROCm).
+
+    Graph lifetime is deterministic: the runner holds its session's step method weakly (no
+    session <-> runner reference cycle), so a session and its hipGraphExecs are freed by
+    reference counting the moment the last reference goes, or at close() -- never by a cyclic
+    collection that could run in the middle of another session's capture (destroying a graph
+    while a stream captures is illegal and aborts the process)."""
 
     def __init__(self, step, chunk: int):
-        self.step = step
+        self._step = weakref.WeakMethod(step) if hasattr(step, "__self__") else (lambda f=step: f)
         self.chunk = chunk
         self.graphs = {}
+
+    def step(self):
+        fn = self._step()
+        if fn is None:
+            raise MFGPError("the training session of this step runner was released")
+        fn()
+
+    def close(self):
+        """Destroy the captured graphs now (outside any capture)."""
+        self.graphs.clear()
 
     def _graph(self, n):
         g = self.graphs.get(n)
         if g is None:
             g = torch.cuda.CUDAGraph()
-            # No cyclic GC while capturing: a collection in the middle of a capture can destroy an
-            # earlier session's graph (hipGraphExecDestroy / pool release), which is illegal on a
-            # capturing stream and aborts the process.  torch.cuda.graph collects on entry.
-            was_enabled = gc.isenabled()
-            gc.disable()
-            try:
-                with torch.cuda.graph(g):
-                    for _ in range(n):
-                        self.step()
-            finally:
-                if was_enabled:
-                    gc.enable()
+            with torch.cuda.graph(g):
+                for _ in range(n):
+                    self.step()
             self.graphs[n] = g
         return g
 

@@ -22,6 +22,7 @@ import torch
 
 from .engine import Engine, theta_size, to_dev
 from .kernels import LinearCoregionalization, LinearMultiFidelityKernel, SeparateIndependent
+from ._lib import MFGPError
 from .models import CholeskyError, Gaussian, _StepRunner
 from .params import Module, Parameter, Softplus, as_result, parameter_dict, multiple_assign
 
@@ -330,7 +331,7 @@ class _SVGPTrainer:
         self._grad()
         self.eng.adam_packed(self.u, self.c, self.g, self.mo, self.vo, self.trainable, self.transform, self.span,
                              self.step_t, self.lr, self.b1, self.b2, 1e-7, self.out, self.klm, self.loss_hist,
-                             self.kl_hist)
+                             self.kl_hist, info=self.info)
 
     def run(self, n):
         if self.done + n > self.max_iters:
@@ -359,8 +360,13 @@ class _SVGPTrainer:
         self.sync()
         return float(self.loss_hist[i].item())
 
+    def close(self):
+        """Release the recorded step graphs now (a later run re-captures)."""
+        self.runner.close()
+
     def finish(self, reset_history=True):
         self.sync()
+        self.close()
         model = self.model
         u = self.u.cpu().numpy()
 
@@ -391,8 +397,12 @@ class _SVGPTrainer:
         model.loss_history.extend(np.float64(v) for v in h)
         if hasattr(model, "kl_history"):
             model.kl_history.extend(np.float64(v) for v in k)
+        steps = int(self.step_t.item())
         if int(self.info.max().item()) != 0 or not np.all(np.isfinite(h)):
             raise CholeskyError("SVGP optimize: Cholesky of K_uu failed")
+        if steps != self.done:
+            raise MFGPError(f"SVGP optimize: {self.done - steps} of {self.done} steps failed (Cholesky of K_uu) "
+                            f"and were retried; the trajectory is incomplete")
 
 
 class LatentMFCoregionalizationSVGP(_SVGPBase):

@@ -156,3 +156,80 @@ def test_prepared_run_matches(hbs, eng):
     s1.finish()
     m2.optimize(max_iters=80, learning_rate=0.1, verbose=False, graph=False)
     np.testing.assert_array_equal(np.array(m1.loss_history), np.array(m2.loss_history))
+
+
+def test_eager_lml_during_async_session_is_fenced(goku, eng):
+    """An eager log_marginal_likelihood() issued while an AdamSession's graph replays are still in
+    flight on the session's stream: the library's device-wide flow fence orders the eager flow
+    after them (no co-resident flows, no FlowTimeoutError) and the value is exact."""
+    eng.set_flow(True)
+    m, other = _model(goku), _model(goku)
+    ref = other.log_marginal_likelihood_and_grad()
+    solo = _model(goku)
+    solo.optimize(max_iters=150, learning_rate=0.1, verbose=False)
+    sess = m.adam_session(0.1, 150, graph_chunk=50)
+    sess.prepare(150)
+    sess.run(150)                       # ~40 ms of replays queued on the session's stream
+    got = other.log_marginal_likelihood_and_grad()   # default stream, eager, while they run
+    sess.finish()
+    assert got[0] == ref[0]
+    np.testing.assert_array_equal(got[1], ref[1])
+    np.testing.assert_array_equal(np.array(m.loss_history), np.array(solo.loss_history))
+
+
+def test_eager_flows_on_two_streams_are_fenced(goku, eng):
+    """Two eager value+grad calls enqueued back to back on two non-blocking streams (two flows
+    that would otherwise interleave their workgroups) both return the exact value."""
+    eng.set_flow(True)
+    m = _model(goku)
+    ref = m.log_marginal_likelihood_and_grad()
+    eng_, X, Y = m._device_data()
+    theta = torch.tensor(m._theta_map().theta(), dtype=torch.float64, device=eng.device)
+    s1, s2 = torch.cuda.Stream(eng.device), torch.cuda.Stream(eng.device)
+    for s in (s1, s2):
+        s.wait_stream(torch.cuda.current_stream(eng.device))
+    outs = []
+    for _ in range(3):
+        for s in (s1, s2):
+            with torch.cuda.stream(s):
+                ws = eng.private_workspace(eng.gpr_workspace_bytes(X.shape[0], Y.shape[1], X.shape[1] - 1))
+                outs.append(eng.gpr_lml(X, Y, theta, want_grad=True, ws=ws))
+    torch.cuda.synchronize()
+    for out, info in outs:
+        assert int(info.item()) == 0
+        o = out.cpu().numpy()
+        assert o[0] == ref[0]
+        np.testing.assert_array_equal(o[1:], ref[1])
+
+
+def test_session_graph_lifetime_is_deterministic(hbs, eng):
+    """A session and its hipGraphs are freed by reference counting when dropped (no session <->
+    runner cycle left for a cyclic collection to reap mid-capture), and a forced collection inside
+    another session's capture is harmless."""
+    import gc
+    import weakref
+    m = _model(hbs)
+    sa = m.adam_session(0.1, 60, graph_chunk=20)
+    sa.run(40)
+    sa.sync()
+    ref_a = weakref.ref(sa)
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        del sa
+        assert ref_a() is None, "session kept alive by a reference cycle"
+    finally:
+        if was:
+            gc.enable()
+    m2, m3 = _model(hbs), _model(hbs)
+    sb = m2.adam_session(0.1, 60, graph_chunk=20)
+    step = sb._step
+
+    def step_with_collect():
+        gc.collect()
+        step()
+    sb.runner = M.models._StepRunner(step_with_collect, 20)   # collects inside the capture
+    sb.run(60)
+    sb.finish()
+    m3.optimize(max_iters=60, learning_rate=0.1, verbose=False, graph=False)
+    np.testing.assert_array_equal(np.array(m2.loss_history), np.array(m3.loss_history))
