@@ -228,6 +228,22 @@ int mfgp_adam_packed_ex(mfgp_handle_t h, int n, double* u, double* c, const doub
                         const double* out, double kl_mult, double* loss_hist, double* kl_hist, const int* info,
                         int ninfo);
 
+/* SVGP.predict_f(Xnew, full_cov, full_output_cov) covariance forms (GPflow base_conditional_with_lm
+ * full_cov branch per latent, G_l = Knn_l - A^T A + (Lq^T A)^T Lq^T A, then mix_latent_gp):
+ *   mode 1 (full_cov)            f_cov [P][nstar][nstar]     = sum_l W_pl^2 G_l
+ *   mode 2 (full_output_cov)     f_cov [nstar][P][P]         = sum_l W_pl W_ql g_var_l
+ *   mode 3 (both)                f_cov [nstar][P][nstar][P]  = sum_l W_pl W_ql G_l
+ * W == NULL: independent outputs (SeparateIndependent, P == l).  Also writes the diagonal outputs
+ * of mfgp_svgp_predict (g_mu, g_var, f_mu, f_var).
+ * Workspace: mfgp_svgp_predict_cov_workspace_size(h, nstar, m, l, p, d).
+ * Replaces: gpflow SVGP.predict_f(full_cov / full_output_cov) inherited by
+ * mfgpflow/linear_svgp.py:64 and singlebin_svgp.py:13. */
+int mfgp_svgp_predict_cov_workspace_size(mfgp_handle_t h, int nstar, int m, int l, int p, int d, size_t* bytes);
+int mfgp_svgp_predict_cov(mfgp_handle_t h, int mode, int nstar, int m, int l, int p, int d, const double* Xs,
+                          int ldxs, const double* Z, int ldz, const double* thetas, const double* q_mu,
+                          const double* q_sqrt, const double* W, double jitter, void* ws, size_t ws_bytes,
+                          double* g_mu, double* g_var, double* f_mu, double* f_var, double* f_cov, int* info);
+
 /* SVGP.predict_f(Xnew, full_cov=False) of the same models (GPflow posteriors with
  * mix_latent_gp): latent moments g_mu / g_var [L][nstar] and mixed f_mu / f_var
  * [nstar][P].  Workspace: mfgp_svgp_workspace_size(h, nstar, m, l, p, d). */

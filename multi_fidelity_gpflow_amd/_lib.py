@@ -53,6 +53,9 @@ SIGNATURES = {
                        _p, _p, _p],
     "mfgp_svgp_predict": [_p, _i, _i, _i, _i, _i, _p, _i, _p, _i, _p, _p, _p, _p, _d, _p, _sz, _p, _p, _p, _p,
                           _p],
+    "mfgp_svgp_predict_cov_workspace_size": [_p, _i, _i, _i, _i, _i, C.POINTER(_sz)],
+    "mfgp_svgp_predict_cov": [_p, _i, _i, _i, _i, _i, _i, _p, _i, _p, _i, _p, _p, _p, _p, _d, _p, _sz, _p, _p, _p,
+                              _p, _p, _p],
     "mfgp_svgp_grad_workspace_size": [_p, _i, _i, _i, _i, _i, C.POINTER(_sz)],
     "mfgp_svgp_elbo_grad": [_p, _i, _i, _i, _i, _i, _p, _i, _p, _i, _p, _i, _p, _p, _p, _p, _p, _d, _d, _d, _p,
                             _sz, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
@@ -128,7 +131,10 @@ def load(path: str = None):
                     f"libmfgp.so not found at {path}: build it with "
                     "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950)")
             lib = C.CDLL(path)
+            variant = path != LIB_PATH   # an older diagnostic build may predate newer entry points
             for name, args in SIGNATURES.items():
+                if variant and not hasattr(lib, name):
+                    continue
                 fn = getattr(lib, name)
                 fn.argtypes = args
                 fn.restype = C.c_char_p if name == "mfgp_error_string" else C.c_int

@@ -473,6 +473,11 @@ int adam_packed_impl(hipStream_t st, int n, double* u, double* c, const double* 
                      int* step, const double* lr_sched, double b1, double b2, double eps, const double* out,
                      double klm, double* loss_hist, double* kl_hist, const int* info, int ninfo);
 
+size_t svgp_predict_cov_workspace_bytes(int nb, int ns, int m, int l, int p, int d);
+int svgp_predict_cov_impl(hipStream_t s, int nb, int mode, int ns, int m, int l, int p, int d, const double* Xs,
+                          int ldx, const double* Z, int ldz, const double* thetas, const double* q_mu,
+                          const double* q_sqrt, const double* W, double jitter, void* ws, size_t ws_bytes,
+                          double* g_mu, double* g_var, double* f_mu, double* f_var, double* f_cov, int* info);
 int svgp_predict_impl(hipStream_t s, int nb, int n, int m, int l, int p, int d, const double* Xs, int ldx,
                       const double* Z, int ldz, const double* thetas, const double* q_mu, const double* q_sqrt,
                       const double* W, double jitter, void* ws, size_t ws_bytes, double* g_mu, double* g_var,
@@ -1001,6 +1006,29 @@ int mfgp_svgp_predict(mfgp_handle_t h, int nstar, int m, int l, int p, int d, co
     if (!W && l != p) return MFGP_ERR_ARG;
     return svgp_predict_impl(h->stream, h->nb, nstar, m, l, p, d, Xs, ldxs, Z, ldz, thetas, q_mu, q_sqrt, W, jitter,
                              ws, ws_bytes, g_mu, g_var, f_mu, f_var, info);
+}
+
+int mfgp_svgp_predict_cov_workspace_size(mfgp_handle_t h, int nstar, int m, int l, int p, int d, size_t* bytes) {
+    CHECK_H(h);
+    CHECK_D(d);
+    if (nstar < 1 || m < 1 || l < 1 || p < 1 || !bytes) return MFGP_ERR_ARG;
+    *bytes = svgp_predict_cov_workspace_bytes(h->nb, nstar, m, l, p, d);
+    return MFGP_OK;
+}
+
+int mfgp_svgp_predict_cov(mfgp_handle_t h, int mode, int nstar, int m, int l, int p, int d, const double* Xs,
+                          int ldxs, const double* Z, int ldz, const double* thetas, const double* q_mu,
+                          const double* q_sqrt, const double* W, double jitter, void* ws, size_t ws_bytes,
+                          double* g_mu, double* g_var, double* f_mu, double* f_var, double* f_cov, int* info) {
+    CHECK_H(h);
+    CHECK_D(d);
+    if (mode < 1 || mode > 3 || nstar < 1 || m < 1 || l < 1 || p < 1 || !Xs || !Z || !thetas || !q_mu || !q_sqrt ||
+        !ws || !g_mu || !g_var || !f_mu || !f_var || !f_cov || !info)
+        return MFGP_ERR_ARG;
+    if (!W && l != p) return MFGP_ERR_ARG;
+    const int rc = svgp_predict_cov_impl(h->stream, h->nb, mode, nstar, m, l, p, d, Xs, ldxs, Z, ldz, thetas, q_mu,
+                                         q_sqrt, W, jitter, ws, ws_bytes, g_mu, g_var, f_mu, f_var, f_cov, info);
+    return rc == -2 ? MFGP_ERR_WORKSPACE : (rc ? MFGP_ERR_LAUNCH : MFGP_OK);
 }
 
 int mfgp_selftest_mfma(mfgp_handle_t h, double* out) {

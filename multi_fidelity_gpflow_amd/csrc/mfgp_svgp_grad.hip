@@ -576,6 +576,10 @@ int svgp_elbo_impl(hipStream_t s, int nb, int n, int m, int l, int p, int d, con
                    const double* Y, int ldy, const double* Z, int ldz, const double* thetas, const double* q_mu,
                    const double* q_sqrt, const double* W, double noise, double scale, double jitter, void* ws,
                    size_t ws_bytes, double* out, double* g_mu, double* g_var, int* info, const double* noise_dev);
+int svgp_predict_impl(hipStream_t s, int nb, int n, int m, int l, int p, int d, const double* Xs, int ldx,
+                      const double* Z, int ldz, const double* thetas, const double* q_mu, const double* q_sqrt,
+                      const double* W, double jitter, void* ws, size_t ws_bytes, double* g_mu, double* g_var,
+                      double* f_mu, double* f_var, int* info);
 // forward intermediates of svgp_run (mfgp_svgp.hip)
 void svgp_forward_buffers(int nb, int n, int m, int l, int p, int d, void* ws, double** Xo, double** C, double** Kuf,
                           double** Lq, int* mpad, int* npad);
@@ -697,6 +701,129 @@ int svgp_grad_impl(hipStream_t s, int nb, int n, int m, int l, int p, int d, con
     return svgp_grad_run<32>(s, n, m, l, p, d, X, ldx, Y, ldy, Z, ldz, thetas, q_mu, q_sqrt, W, noise_dev, scale,
                              jitter, ws, ws_bytes, out, g_mu, g_var, gZ, gtheta, gq_mu, gq_sqrt, gW, gnoise, info,
                              noise_host, kl_mult);
+}
+
+// ---------------------------------------------------------------- predict with covariances
+// GPflow SVGP.predict_f(Xnew, full_cov, full_output_cov) beyond the diagonal
+// (posteriors.IndependentPosteriorMultiOutput -> base_conditional_with_lm(full_cov=True, white)
+// per latent, then mix_latent_gp): G_l = Knn_l - A^T A + (Lq^T A)^T (Lq^T A), A = Li Kuf,
+// written as G_l = Knn_l + Kuf^T F Kuf with F = C^T C - Li^T Li (C = Lq^T Li) -- the same F the
+// ELBO gradient forms.  Mixing (W = NULL: independent outputs, P = L):
+//   mode 1 full_cov            f_cov[p][a][b]    = sum_l W_pl^2 G_l[a][b]
+//   mode 2 full_output_cov     f_cov[a][p][q]    = sum_l W_pl W_ql g_var[l][a]
+//   mode 3 both                f_cov[a][p][b][q] = sum_l W_pl W_ql G_l[a][b]
+__global__ void k_svgp_mix_cov(int mode, int ns, int p, int L, const double* W, const double* g_var, const double* G,
+                               long ldg, long sG, double* out) {
+    const long nn = (long)ns * ns, pp2 = (long)p * p;
+    const long tot = mode == 1 ? p * nn : (mode == 2 ? ns * pp2 : nn * pp2);
+    for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < tot; e += (long)gridDim.x * blockDim.x) {
+        int a, b, pa, qa;
+        if (mode == 1) {
+            pa = (int)(e / nn);
+            const long r = e % nn;
+            a = (int)(r / ns); b = (int)(r % ns); qa = pa;
+        } else if (mode == 2) {
+            a = (int)(e / pp2);
+            const long r = e % pp2;
+            pa = (int)(r / p); qa = (int)(r % p); b = a;
+        } else {   // [a][pa][b][qa]
+            long r = e;
+            qa = (int)(r % p); r /= p;
+            b = (int)(r % ns); r /= ns;
+            pa = (int)(r % p); a = (int)(r / p);
+        }
+        double v = 0.0;
+        if (!W) {
+            if (pa == qa) v = (mode == 2) ? g_var[(long)pa * ns + a] : G[pa * sG + a * ldg + b];
+        } else {
+            for (int l = 0; l < L; ++l) {
+                const double w = W[(long)pa * L + l] * W[(long)qa * L + l];
+                v = fma(w, (mode == 2) ? g_var[(long)l * ns + a] : G[l * sG + a * ldg + b], v);
+            }
+        }
+        out[e] = v;
+    }
+}
+
+static size_t pcov_extra(int nb, int ns, int m, int L) {
+    const size_t mpad = (size_t)cdv(m, nb) * nb, npad = (size_t)cdv(ns, nb) * nb;
+    return sizeof(double) * L * (2 * mpad * mpad + mpad * npad + 2 * npad * npad) + 5 * 256;
+}
+
+size_t svgp_predict_cov_workspace_bytes(int nb, int ns, int m, int l, int p, int d) {
+    return svgp_workspace_bytes(nb, ns, m, l, p, d) + pcov_extra(nb, ns, m, l) + 256;
+}
+
+template <int NB>
+static int svgp_predict_cov_run(hipStream_t s, int mode, int ns, int m, int L, int p, int d, const double* Xs,
+                                int ldx, const double* Z, int ldz, const double* thetas, const double* q_mu,
+                                const double* q_sqrt, const double* W, double jitter, void* ws, size_t ws_bytes,
+                                double* g_mu, double* g_var, double* f_mu, double* f_var, double* f_cov, int* info) {
+    if (ws_bytes < svgp_predict_cov_workspace_bytes(NB, ns, m, L, p, d)) return -2;
+    int rc = svgp_predict_impl(s, NB, ns, m, L, p, d, Xs, ldx, Z, ldz, thetas, q_mu, q_sqrt, W, jitter, ws, ws_bytes,
+                               g_mu, g_var, f_mu, f_var, info);
+    if (rc) return rc;
+    double *Li, *C, *Kuf, *Lq;
+    int mpad, npad;
+    svgp_forward_buffers(NB, ns, m, L, p, d, ws, &Li, &C, &Kuf, &Lq, &mpad, &npad);
+    const int Tm = mpad / NB, Tn = npad / NB;
+    const long mm = (long)mpad * mpad, mn = (long)mpad * npad, nn = (long)npad * npad;
+    size_t off = (svgp_workspace_bytes(NB, ns, m, L, p, d) + 255) & ~(size_t)255;
+    auto take = [&](size_t count) {
+        off = (off + 255) & ~(size_t)255;
+        double* q = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + off);
+        off += count * sizeof(double);
+        return q;
+    };
+    double* F1 = take((size_t)L * mm);
+    double* F = take((size_t)L * mm);
+    double* Tk = take((size_t)L * mn);
+    double* Knn = take((size_t)L * nn);
+    double* G = take((size_t)L * nn);
+    if (mode != 2) {
+        sq<NB>(s, Tm, L, mm, mpad, 1, C, 0, C, F1);                   // C^T C
+        sq<NB>(s, Tm, L, mm, mpad, 1, Li, 0, Li, F, -1.0, F1, 1.0);   // F = C^T C - Li^T Li
+        {
+            BgemmArgs a{};
+            a.A = F; a.lda = mpad; a.sA = mm;
+            a.B = Kuf; a.ldb = npad; a.sB = mn;
+            a.D = Tk; a.ldd = npad; a.sD = mn;
+            a.alpha = 1.0;
+            a.Mt = Tm; a.Nt = Tn; a.Kt = Tm;
+            bgemm<NB>(s, 0, 0, a, L);                                 // F Kuf
+        }
+        GramArgs g{};
+        g.X1 = Xs; g.ldx1 = ldx; g.sx1 = 0; g.n1 = ns;
+        g.X2 = Xs; g.ldx2 = ldx; g.sx2 = 0; g.n2 = ns;
+        g.theta = thetas; g.stheta = theta_size(d); g.D = d; g.rbf_only = 0;
+        g.out = Knn; g.ldo = npad; g.so = nn; g.padded = 0; g.diag_add = 0.0;
+        launch_gram_dense(g, L, npad, npad, s);                       // Knn_l (GPflow adds no jitter)
+        {
+            BgemmArgs a{};
+            a.A = Kuf; a.lda = npad; a.sA = mn;
+            a.B = Tk; a.ldb = npad; a.sB = mn;
+            a.Cin = Knn; a.ldc = npad; a.sC = nn; a.beta = 1.0;
+            a.D = G; a.ldd = npad; a.sD = nn;
+            a.alpha = 1.0;
+            a.Mt = Tn; a.Nt = Tn; a.Kt = Tm;
+            bgemm<NB>(s, 1, 0, a, L);                                 // G = Knn + Kuf^T F Kuf
+        }
+    }
+    const long tot = mode == 1 ? (long)p * ns * ns : (mode == 2 ? (long)ns * p * p : (long)ns * ns * p * p);
+    hipLaunchKernelGGL(k_svgp_mix_cov, dim3((unsigned)std::min<long>(cdv((int)std::min<long>(tot, 1L << 30), 256), 4096)),
+                       dim3(256), 0, s, mode, ns, p, L, W, g_var, G, (long)npad, nn, f_cov);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+int svgp_predict_cov_impl(hipStream_t s, int nb, int mode, int ns, int m, int l, int p, int d, const double* Xs,
+                          int ldx, const double* Z, int ldz, const double* thetas, const double* q_mu,
+                          const double* q_sqrt, const double* W, double jitter, void* ws, size_t ws_bytes,
+                          double* g_mu, double* g_var, double* f_mu, double* f_var, double* f_cov, int* info) {
+    if (nb == 64)
+        return svgp_predict_cov_run<64>(s, mode, ns, m, l, p, d, Xs, ldx, Z, ldz, thetas, q_mu, q_sqrt, W, jitter, ws,
+                                        ws_bytes, g_mu, g_var, f_mu, f_var, f_cov, info);
+    return svgp_predict_cov_run<32>(s, mode, ns, m, l, p, d, Xs, ldx, Z, ldz, thetas, q_mu, q_sqrt, W, jitter, ws,
+                                    ws_bytes, g_mu, g_var, f_mu, f_var, f_cov, info);
 }
 
 // ---------------------------------------------------------------- packed Adam (training step)

@@ -378,6 +378,27 @@ class Engine:
               "mfgp_svgp_predict")
         return f_mu, f_var, g_mu, g_var, info
 
+    def svgp_predict_cov(self, mode, Xs, Z, thetas, q_mu, q_sqrt, W, p, jitter=1e-6):
+        """SVGP predict_f covariance forms (include/mfgp.h mfgp_svgp_predict_cov): mode 1 full_cov
+        -> f_cov [p, ns, ns]; 2 full_output_cov -> [ns, p, p]; 3 both -> [ns, p, ns, p]."""
+        ns, dp1 = Xs.shape
+        d = dp1 - 1
+        m = Z.shape[0]
+        L = thetas.shape[0]
+        nbytes = self._size(self.lib.mfgp_svgp_predict_cov_workspace_size, ns, m, L, p, d)
+        ws = self.workspace("svgp_pred_cov", nbytes)
+        f64 = dict(dtype=torch.float64, device=self.device)
+        g_mu, g_var = torch.empty((L, ns), **f64), torch.empty((L, ns), **f64)
+        f_mu, f_var = torch.empty((ns, p), **f64), torch.empty((ns, p), **f64)
+        shape = {1: (p, ns, ns), 2: (ns, p, p), 3: (ns, p, ns, p)}[mode]
+        f_cov = torch.empty(shape, **f64)
+        info = torch.empty((L,), dtype=torch.int32, device=self.device)
+        check(self.lib.mfgp_svgp_predict_cov(self.h, mode, ns, m, L, p, d, ptr(Xs), dp1, ptr(Z), Z.shape[1],
+                                             ptr(thetas), ptr(q_mu), ptr(q_sqrt), ptr(W), float(jitter), ptr(ws),
+                                             ws.numel(), ptr(g_mu), ptr(g_var), ptr(f_mu), ptr(f_var), ptr(f_cov),
+                                             ptr(info)), "mfgp_svgp_predict_cov")
+        return f_mu, f_cov, info
+
     def selftest_mfma(self) -> np.ndarray:
         out = torch.zeros((16, 16), dtype=torch.float64, device=self.device)
         check(self.lib.mfgp_selftest_mfma(self.h, ptr(out)), "mfgp_selftest_mfma")

@@ -116,17 +116,30 @@ class _SVGPBase(Module):
         return 0.5 * (np.sum(q * q) - M * Lat + np.sum(L * L) - np.sum(np.log(d * d)))
 
     def predict_f(self, Xnew, full_cov=False, full_output_cov=False):
-        if full_cov or full_output_cov:
-            raise NotImplementedError("SVGP predict_f(full_cov=True) is not provided by the MI355X engine yet")
+        """GPflow SVGP.predict_f (IndependentPosteriorMultiOutput + mix_latent_gp): mean [N*, P];
+        var [N*, P], or with full_cov [P, N*, N*], with full_output_cov [N*, P, P], with both
+        [N*, P, N*, P] (linear_svgp.py:64 / singlebin_svgp.py:13 inherit it)."""
         eng, Z, thetas, q_mu, q_sqrt, W = self._dev_state()
         Xs = to_dev(Xnew, eng.device)
+        if full_cov or full_output_cov:
+            mode = 3 if (full_cov and full_output_cov) else (1 if full_cov else 2)
+            f_mu, f_cov, info = eng.svgp_predict_cov(mode, Xs, Z, thetas, q_mu, q_sqrt, W, self.num_outputs,
+                                                     DEFAULT_JITTER)
+            if int(info.max().item()) != 0:
+                raise CholeskyError("predict_f: Cholesky of K_uu was not successful")
+            return as_result(f_mu), as_result(f_cov)
         f_mu, f_var, _, _, info = eng.svgp_predict(Xs, Z, thetas, q_mu, q_sqrt, W, self.num_outputs, DEFAULT_JITTER)
         if int(info.max().item()) != 0:
             raise CholeskyError("predict_f: Cholesky of K_uu was not successful")
         return as_result(f_mu), as_result(f_var)
 
     def predict_y(self, Xnew, full_cov=False, full_output_cov=False):
-        mean, var = self.predict_f(Xnew, full_cov, full_output_cov)
+        """GPflow GPModel.predict_y: predict_f plus the Gaussian noise variance."""
+        if full_cov or full_output_cov:
+            # GPflow 2.9 GPModel.predict_y (gpflow issue 1461): only the marginal form is supported
+            raise NotImplementedError("The predict_y method currently supports only the argument values "
+                                      "full_cov=False and full_output_cov=False")
+        mean, var = self.predict_f(Xnew)
         return mean, as_result(var + float(self.likelihood.variance.numpy()))
 
     def elbo_and_grad(self, data, kl_multiplier=1.0):

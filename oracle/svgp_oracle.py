@@ -78,6 +78,35 @@ def latent_moments(X, Z, kps, q_mu, q_sqrt):
     return torch.stack(gm, 1), torch.stack(gv, 1)
 
 
+def latent_cov(X, Z, kps, q_mu, q_sqrt):
+    """GPflow base_conditional_with_lm(full_cov=True, white=True) per latent:
+    g_mu [N, L], g_cov [L, N, N] = Knn - A^T A + (Lq^T A)^T (Lq^T A), A = Lm^{-1} Kuf (no jitter on Knn)."""
+    gm, gc = [], []
+    M = Z.shape[0]
+    for l, kp in enumerate(kps):
+        Kuu = mf_K_t(Z, Z, kp) + JITTER * torch.eye(M, dtype=torch.float64)
+        Kuf = mf_K_t(Z, X, kp)
+        Knn = mf_K_t(X, X, kp)
+        Lm = torch.linalg.cholesky(Kuu)
+        A = torch.linalg.solve_triangular(Lm, Kuf, upper=False)
+        LTA = torch.tril(q_sqrt[l]).T @ A
+        gm.append(A.T @ q_mu[:, l])
+        gc.append(Knn - A.T @ A + LTA.T @ LTA)
+    return torch.stack(gm, 1), torch.stack(gc, 0)
+
+
+def mix_cov(g_cov, g_var, W, full_cov, full_output_cov):
+    """GPflow mix_latent_gp covariance branches (W None: independent outputs, P = L):
+    full_cov only -> [P, N, N]; full_output_cov only -> [N, P, P]; both -> [N, P, N, P]."""
+    L = g_cov.shape[0]
+    Wm = torch.eye(L, dtype=torch.float64) if W is None else W
+    if full_cov and full_output_cov:
+        return torch.einsum("pl,ql,lab->apbq", Wm, Wm, g_cov)
+    if full_cov:
+        return torch.einsum("pl,lab->pab", Wm * Wm, g_cov)
+    return torch.einsum("pl,ql,al->apq", Wm, Wm, g_var)
+
+
 def elbo_t(X, Y, Z, kps, q_mu, q_sqrt, W, noise, num_data=None):
     """GPflow SVGP.elbo (Gaussian likelihood, whiten=True). W=None -> SeparateIndependent."""
     gm, gv = latent_moments(X, Z, kps, q_mu, q_sqrt)

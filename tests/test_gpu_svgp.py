@@ -281,3 +281,46 @@ def test_latent_training_matches_oracle(hbs):
     ref = S.LatentTrainer(X, Y, kw, lr=0.05, max_iters=20)
     oh = [ref.step() for _ in range(20)]
     np.testing.assert_allclose(hist, oh, rtol=1e-6)
+
+
+@pytest.mark.parametrize("which", ["singlebin", "latent"])
+def test_predict_f_covariance_forms(hbs, which):
+    """SVGP.predict_f(full_cov / full_output_cov) (GPflow base_conditional_with_lm full_cov branch +
+    mix_latent_gp) against the torch oracle, on the HBS test inputs with randomized parameters:
+    shapes [P, N*, N*], [N*, P, P], [N*, P, N*, P]; the diagonals equal the full_cov=False
+    variances; predict_y raises for the covariance forms like GPflow 2.9."""
+    X, Y = hbs["X"], hbs["Y"]
+    D, P = X.shape[1] - 1, Y.shape[1]
+    if which == "singlebin":
+        m = M.SingleBinSVGP(X, Y, M.SquaredExponential(lengthscales=np.ones(D)),
+                            M.SquaredExponential(lengthscales=np.ones(D)), P, Z=np.zeros((50, D + 1)))
+        _randomize(m, 21)
+        Wm = None
+    else:
+        m = M.LatentMFCoregionalizationSVGP(X, Y, M.SquaredExponential(lengthscales=np.ones(D)),
+                                            M.SquaredExponential(lengthscales=np.ones(D)), num_latents=5,
+                                            num_inducing=30, num_outputs=P, w_type='diagonal')
+        _randomize(m, 22)
+        Wm = m.kernel.W.numpy()
+    Xs = hbs["Xtest"]
+    ns = Xs.shape[0]
+    Z, kps, q_mu, q_sqrt, W, noise = _oracle_state(m, Wm)
+    gm, gc = S.latent_cov(torch.tensor(Xs), Z, kps, q_mu, q_sqrt)
+    gv = torch.diagonal(gc, dim1=-2, dim2=-1).T.contiguous()   # [N*, L]
+    mean0, var0 = m.predict_f(Xs)
+    for fc, foc, shape in ((True, False, (P, ns, ns)), (False, True, (ns, P, P)), (True, True, (ns, P, ns, P))):
+        mean, cov = m.predict_f(Xs, full_cov=fc, full_output_cov=foc)
+        assert tuple(cov.shape) == shape
+        ref = S.mix_cov(gc, gv, W, fc, foc).numpy()
+        np.testing.assert_allclose(cov.numpy(), ref, rtol=0, atol=1e-8 * max(1.0, np.abs(ref).max()))
+        np.testing.assert_array_equal(mean.numpy(), mean0.numpy())
+        c = cov.numpy()
+        if fc and not foc:
+            diag = np.diagonal(c, axis1=1, axis2=2).T
+        elif foc and not fc:
+            diag = np.diagonal(c, axis1=1, axis2=2)
+        else:
+            diag = np.stack([c[a, :, a, :].diagonal() for a in range(ns)])
+        np.testing.assert_allclose(diag, var0.numpy(), rtol=0, atol=1e-9)
+        with pytest.raises(NotImplementedError):
+            m.predict_y(Xs, full_cov=fc, full_output_cov=foc)
