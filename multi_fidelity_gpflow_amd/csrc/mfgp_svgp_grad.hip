@@ -476,39 +476,45 @@ __global__ __launch_bounds__(NTHREADS) void k_kff_grad(const double* X, long ldx
     }
 }
 
-// Final reductions: gtheta[l][q] (kff + Kuu + Kuf partials), gZ[m][D+1] (sum over latents;
-// fidelity column 0), gnoise = sum of partials.
+// Final reductions: gtheta[l][q] (kff + Kuu + Kuf partials), gZ[m][D+1] (sum over latents and
+// column blocks; fidelity column 0), gnoise.  GR_LANES lanes per output, lane j summing the
+// partials b = j mod GR_LANES, combined by a fixed xor tree (a thread per output walking its
+// partials in one dependent chain took 93 us at L = 64: 19 workgroups of 448-load chains).
+constexpr int GR_LANES = 8;
 __global__ void k_grad_reduce(const double* gth_uu, int nb_uu, const double* gth_uf, int nb_uf, const double* gth_kff,
                               const double* gz_uu, const double* gz_uf, int n_at, int nbc_uu, int nbc_uf, int L,
                               int G, int D, int m, const double* gnoise_part, int nnoise, double* gtheta, double* gZ,
                               double* gnoise) {
-    const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const long gt = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    const int tid = (int)(gt / GR_LANES), j = (int)(gt % GR_LANES);
     const int nth = L * G;
+    double s = 0.0;
     if (tid < nth) {
         const int l = tid / G, q = tid % G;
-        double s = gth_kff[(long)l * G + q];
-        for (int bk = 0; bk < nb_uu; ++bk) s += gth_uu[((long)l * nb_uu + bk) * G + q];
-        for (int bk = 0; bk < nb_uf; ++bk) s += gth_uf[((long)l * nb_uf + bk) * G + q];
-        gtheta[tid] = s;
+        const double* pu = gth_uu + (long)l * nb_uu * G + q;
+        const double* pf = gth_uf + (long)l * nb_uf * G + q;
+        for (int b = j; b < nb_uu + nb_uf; b += GR_LANES) s += (b < nb_uu) ? pu[(long)b * G] : pf[(long)(b - nb_uu) * G];
     } else if (tid < nth + m * (D + 1)) {
         const int e = tid - nth;
         const int a = e / (D + 1), d = e % (D + 1);
-        double s = 0.0;
         if (d < D) {
             const int at = a / KG_ROWS, r = a % KG_ROWS;
-            for (int l = 0; l < L; ++l) {
-                for (int bc = 0; bc < nbc_uu; ++bc)
-                    s += gz_uu[(((long)l * nb_uu + at * nbc_uu + bc) * KG_ROWS + r) * D + d];
-                for (int bc = 0; bc < nbc_uf; ++bc)
-                    s += gz_uf[(((long)l * nb_uf + at * nbc_uf + bc) * KG_ROWS + r) * D + d];
+            const int per = nbc_uu + nbc_uf;            // partials per latent
+            for (int b = j; b < L * per; b += GR_LANES) {
+                const int l = b / per, bc = b % per;
+                s += (bc < nbc_uu) ? gz_uu[(((long)l * nb_uu + at * nbc_uu + bc) * KG_ROWS + r) * D + d]
+                                   : gz_uf[(((long)l * nb_uf + at * nbc_uf + (bc - nbc_uu)) * KG_ROWS + r) * D + d];
             }
         }
-        gZ[e] = s;
     } else if (tid == nth + m * (D + 1)) {
-        double s = 0.0;
-        for (int i = 0; i < nnoise; ++i) s += gnoise_part[i];
-        gnoise[0] = s;
+        for (int i = j; i < nnoise; i += GR_LANES) s += gnoise_part[i];
     }
+#pragma unroll
+    for (int o = 1; o < GR_LANES; o <<= 1) s += __shfl_xor(s, o, 64);
+    if (j != 0) return;
+    if (tid < nth) gtheta[tid] = s + gth_kff[tid];
+    else if (tid < nth + m * (D + 1)) gZ[tid - nth] = s;
+    else if (tid == nth + m * (D + 1)) gnoise[0] = s;
     (void)n_at;
 }
 
@@ -683,7 +689,7 @@ static int svgp_grad_run(hipStream_t s, int n, int m, int L, int p, int d, const
     hipLaunchKernelGGL(k_kff_grad, dim3(L), dim3(NTHREADS), 0, s, X, (long)ldx, n, g.beta, npad, thetas, G, d,
                        g.gth_kff);
     const int tot = L * G + m * (d + 1) + 1;
-    hipLaunchKernelGGL(k_grad_reduce, dim3(cdv(tot, 256)), dim3(256), 0, s, g.gth_uu, g.nb_uu, g.gth_uf, g.nb_uf,
+    hipLaunchKernelGGL(k_grad_reduce, dim3(cdv(tot * GR_LANES, 256)), dim3(256), 0, s, g.gth_uu, g.nb_uu, g.gth_uf, g.nb_uf,
                        g.gth_kff, g.gz_uu, g.gz_uf, g.n_at, g.nbc_uu, g.nbc_uf, L, G, d, m, g.gnp, g.nnoise, gtheta,
                        gZ, gnoise);
     return hipGetLastError() == hipSuccess ? 0 : -3;

@@ -280,18 +280,22 @@ def test_graph_and_eager_agree(hbs, eng):
 
 
 def test_lbfgs_forrester_kat(kats, eng):
-    """L-BFGS on this objective is degenerate once the noise reaches its 1e-6 floor:
-    1-ulp changes move the stopping point along a flat valley (the bit-identical host
-    driver fed by the fp64 oracle stops at rho 1.9998815, 5.6e-5 from the recorded
-    1.99976989).  The KAT is therefore checked at 1e-4, the noise floor exactly, and
-    the GPU objective along the first L-BFGS evaluations against the oracle driver."""
+    """notebooks/demo.ipynb:233,257: rho 1.99976989, noise 1e-06 after GPflow's two L-BFGS
+    passes.  With the variance gradients in TF's autodiff form (dK/dv = exp(-r2/2), finite
+    where the line search drives v to 0; the division form K / v gave NaN there) the device
+    stops at rho 1.999768564 (6.6e-7 from the recorded value, round 3; it was 5.6e-5 off
+    before).  Checked at 2e-6, the noise floor, and the GPU objective along the first
+    L-BFGS evaluations against the oracle driver."""
     from conftest import forrester_demo_data
     X, Y = forrester_demo_data()
     m = M.MultiFidelityGPModel(X, Y, M.SquaredExponential(), M.SquaredExponential())
     m.optimize(max_iters=1000, learning_rate=0.01, use_adam=False, unfix_noise_after=500, verbose=False)
     rho = float(m.kernel.rho.numpy()[0, 0])
-    assert abs(rho - kats["forrester_lbfgs"]["rho"]) < 1e-4 * kats["forrester_lbfgs"]["rho"]
-    assert float(m.likelihood.variance.numpy()) == pytest.approx(kats["forrester_lbfgs"]["noise"], rel=1e-3)
+    print(f"L-BFGS Forrester rho {rho:.9f} vs recorded {kats['forrester_lbfgs']['rho']} "
+          f"(rel {abs(rho - kats['forrester_lbfgs']['rho']) / kats['forrester_lbfgs']['rho']:.1e}), "
+          f"noise {float(m.likelihood.variance.numpy()):.9e}")
+    assert abs(rho - kats["forrester_lbfgs"]["rho"]) < 2e-6 * kats["forrester_lbfgs"]["rho"]
+    assert float(m.likelihood.variance.numpy()) == pytest.approx(kats["forrester_lbfgs"]["noise"], rel=1e-6)
     _, trace = O.lbfgs_train(X, Y, O.MFParams.initial(1, 1), max_iters=1000, return_trace=True)
     np.testing.assert_allclose(m.loss_history[:8], trace[:8], rtol=1e-9)
 

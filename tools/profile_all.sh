@@ -1,8 +1,8 @@
 #!/bin/bash
 # All configs of a round's profile (GPU box, repo root): Goku (BASELINE metric), Synth fp32, Goku SVGP.
 set -e
-R=${1:-r02}
-bash tools/profile_round.sh gpurun_out/$R/goku goku "" "--steps 20 --warmup 5 --no-cpu-baseline --no-train-predict"
+R=${1:-r03}
+bash tools/profile_round.sh gpurun_out/$R/goku goku "--no-extras" "--steps 20 --warmup 5 --no-cpu-baseline --no-train-predict --no-extras"
 echo GOKU_DONE
 bash tools/profile_round.sh gpurun_out/$R/synth synth "--steps 6 --warmup 2" "--steps 2 --warmup 1"
 echo SYNTH_DONE
