@@ -142,6 +142,10 @@ struct BgemmArgs {
     double* D; long ldd; long sD;
     double alpha;
     int Mt, Nt, Kt, tril;
+    // known-zero triangles of the operands, so their k-tiles are skipped (never read):
+    // amask 1: op(A) lower (k-tile <= row tile), 2: op(A) upper (k-tile >= row tile);
+    // bmask 1: op(B) lower (k-tile >= column tile), 2: op(B) upper (k-tile <= column tile)
+    int amask, bmask;
 };
 void launch_bgemm(int nb, hipStream_t st, int ta, int tb, const BgemmArgs& a, int batch);
 

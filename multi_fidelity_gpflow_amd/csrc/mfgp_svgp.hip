@@ -74,6 +74,16 @@ void svgp_forward_buffers(int nb, int n, int m, int l, int p, int d, void* ws, d
     *npad = S.npad;
 }
 
+// Zeros in the strictly-upper tiles of L^{-1} (the step sequence writes only tiles (i, c <= i)):
+// the matvecs and the E = Lq C - Li input read whole rows of it
+__global__ void k_zero_upper_tiles(double* Xo, int nb, int mpad, long mm) {
+    const int l = blockIdx.z;
+    for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < mm; e += (long)gridDim.x * blockDim.x) {
+        const int r = (int)(e / mpad), c = (int)(e % mpad);
+        if (r / nb < c / nb) Xo[l * mm + e] = 0.0;
+    }
+}
+
 // tril(q_sqrt_l) into a zero-padded Mpad x Mpad buffer
 __global__ void k_lq_pad(const double* q_sqrt, int m, int mpad, double* Lq) {
     const int l = blockIdx.z;
@@ -346,6 +356,7 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
         c.Dd = S.Dd; c.sD = (long)S.Tm * NB * NB; c.ldiag = S.ldiag; c.sL = S.mpad; c.info = info;
         c.T = S.Tm; c.Tp = 0; c.k = 0;
         launch_chol_steps<NB>(c, L, s);
+        hipLaunchKernelGGL(k_zero_upper_tiles, dim3(blocks, 1, L), dim3(256), 0, s, S.Xo, NB, S.mpad, mm);
         hipLaunchKernelGGL(k_lq_pad, dim3(blocks, 1, L), dim3(256), 0, s, q_sqrt, m, S.mpad, S.Lq);
         hipLaunchKernelGGL(k_lqt_linv<NB>, dim3(S.Tm * S.Tm, 1, L), dim3(NTHREADS),
                            2 * sizeof(double) * NB * (NB + 2), s, S.Lq, S.Xo, S.C, S.Tm);

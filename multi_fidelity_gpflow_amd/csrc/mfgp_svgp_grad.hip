@@ -49,7 +49,12 @@ __global__ __launch_bounds__(NTHREADS) void k_bgemm(BgemmArgs a) {
     const double* s = a.s ? a.s + b * a.ss : nullptr;
     Acc<NB> acc;
     acc_zero(acc);
-    for (int kt = 0; kt < a.Kt; ++kt) {
+    int k0 = 0, k1 = a.Kt;
+    if (a.amask == 1) k1 = min(k1, ti + 1);
+    else if (a.amask == 2) k0 = max(k0, ti);
+    if (a.bmask == 1) k0 = max(k0, tj);
+    else if (a.bmask == 2) k1 = min(k1, tj + 1);
+    for (int kt = k0; kt < k1; ++kt) {
         tile_load<NB>(As, TA ? A + (long)kt * NB * a.lda + (long)ti * NB : A + (long)ti * NB * a.lda + (long)kt * NB,
                       a.lda);
         tile_load<NB>(Bs, TB ? B + (long)tj * NB * a.ldb + (long)kt * NB : B + (long)kt * NB * a.ldb + (long)tj * NB,
@@ -101,8 +106,9 @@ void launch_bgemm(int nb, hipStream_t st, int ta, int tb, const BgemmArgs& a, in
 template <int NB>
 static void sq(hipStream_t st, int Tm, int L, long mm, long ld, int ta, const double* A, int tb, const double* B,
                double* D, double alpha = 1.0, const double* Cin = nullptr, double beta = 0.0, int tril = 0,
-               const double* x = nullptr, const double* y = nullptr, long sxy = 0) {
+               const double* x = nullptr, const double* y = nullptr, long sxy = 0, int amask = 0, int bmask = 0) {
     BgemmArgs a{};
+    a.amask = amask; a.bmask = bmask;
     a.A = A; a.lda = ld; a.sA = mm;
     a.B = B; a.ldb = ld; a.sB = mm;
     a.Cin = Cin; a.ldc = ld; a.sC = mm; a.beta = beta;
@@ -644,16 +650,16 @@ static int svgp_grad_run(hipStream_t s, int n, int m, int L, int p, int d, const
                        g.u, (long)mpad, mpad, mpad, 1.0, g.qm, (long)mpad, -kl_mult, g.gqm, (long)mpad);
     hipLaunchKernelGGL(k_qmu_unpad, dim3(cdv(m, 256), 1, L), dim3(256), 0, s, g.gqm, m, L, mpad, gq_mu);
     // 4. E = Lq C - Li ; Gb = tril(2 E Q + m u^T)
-    sq<NB>(s, Tm, L, mm, mpad, 0, Lq, 0, C, g.E, 1.0, Li, -1.0);
+    sq<NB>(s, Tm, L, mm, mpad, 0, Lq, 0, C, g.E, 1.0, Li, -1.0, 0, nullptr, nullptr, 0, 1, 0);   // Lq lower
     sq<NB>(s, Tm, L, mm, mpad, 0, g.E, 0, g.Q, g.Gb, 2.0, nullptr, 0.0, 1, g.qm, g.u, mpad);
     // 5. Sigma_bar = -Li^T Psi(Gb Li^T) Li
-    sq<NB>(s, Tm, L, mm, mpad, 0, g.Gb, 1, Li, g.H);
+    sq<NB>(s, Tm, L, mm, mpad, 0, g.Gb, 1, Li, g.H, 1.0, nullptr, 0.0, 0, nullptr, nullptr, 0, 1, 2);   // Gb lower, Li^T upper
     hipLaunchKernelGGL(k_psi, dim3(std::min<long>(cdv((int)mm, 256), 1024), 1, L), dim3(256), 0, s, g.H, g.P, mpad, mm);
-    sq<NB>(s, Tm, L, mm, mpad, 0, g.P, 0, Li, g.T1);
-    sq<NB>(s, Tm, L, mm, mpad, 1, Li, 0, g.T1, g.Sig, -1.0);
+    sq<NB>(s, Tm, L, mm, mpad, 0, g.P, 0, Li, g.T1, 1.0, nullptr, 0.0, 0, nullptr, nullptr, 0, 0, 1);   // Li lower
+    sq<NB>(s, Tm, L, mm, mpad, 1, Li, 0, g.T1, g.Sig, -1.0, nullptr, 0.0, 0, nullptr, nullptr, 0, 2, 0);   // Li^T upper
     // 6. F = C^T C - Li^T Li ; Kbar = 2 F Kuf diag(beta) + (Li^T m) alpha^T
     sq<NB>(s, Tm, L, mm, mpad, 1, C, 0, C, g.T1);
-    sq<NB>(s, Tm, L, mm, mpad, 1, Li, 0, Li, g.F, -1.0, g.T1, 1.0);
+    sq<NB>(s, Tm, L, mm, mpad, 1, Li, 0, Li, g.F, -1.0, g.T1, 1.0, 0, nullptr, nullptr, 0, 2, 1);   // Li^T upper, Li lower
     hipLaunchKernelGGL(k_bmatvec, dim3(cdv(mpad, NTHREADS / 64), 1, L), dim3(NTHREADS), 0, s, Li, (long)mpad, mm, 1,
                        g.qm, (long)mpad, mpad, mpad, 1.0, (const double*)nullptr, 0L, 0.0, g.vli, (long)mpad);
     {
@@ -668,7 +674,7 @@ static int svgp_grad_run(hipStream_t s, int n, int m, int L, int p, int d, const
         bgemm<NB>(s, 0, 0, a, L);
     }
     // 7. dE/dLq = tril(2 Li Q C^T) - Lq + diag(1/Lq_ii)
-    sq<NB>(s, Tm, L, mm, mpad, 0, Li, 0, g.Q, g.T1);
+    sq<NB>(s, Tm, L, mm, mpad, 0, Li, 0, g.Q, g.T1, 1.0, nullptr, 0.0, 0, nullptr, nullptr, 0, 1, 0);   // Li lower
     sq<NB>(s, Tm, L, mm, mpad, 0, g.T1, 1, C, g.gLq, 2.0, nullptr, 0.0, 1);
     hipLaunchKernelGGL(k_glq_final, dim3(std::min(cdv(m * m, 256), 1024), 1, L), dim3(256), 0, s, g.gLq, Lq, m, mpad,
                        mm, kl_mult, gq_sqrt);
@@ -788,7 +794,7 @@ static int svgp_predict_cov_run(hipStream_t s, int mode, int ns, int m, int L, i
     double* G = take((size_t)L * nn);
     if (mode != 2) {
         sq<NB>(s, Tm, L, mm, mpad, 1, C, 0, C, F1);                   // C^T C
-        sq<NB>(s, Tm, L, mm, mpad, 1, Li, 0, Li, F, -1.0, F1, 1.0);   // F = C^T C - Li^T Li
+        sq<NB>(s, Tm, L, mm, mpad, 1, Li, 0, Li, F, -1.0, F1, 1.0, 0, nullptr, nullptr, 0, 2, 1);   // F = C^T C - Li^T Li
         {
             BgemmArgs a{};
             a.A = F; a.lda = mpad; a.sA = mm;

@@ -324,3 +324,26 @@ def test_predict_f_covariance_forms(hbs, which):
         np.testing.assert_allclose(diag, var0.numpy(), rtol=0, atol=1e-9)
         with pytest.raises(NotImplementedError):
             m.predict_y(Xs, full_cov=fc, full_output_cov=foc)
+
+
+def test_gradients_independent_of_workspace_contents(hbs):
+    """Every workspace byte the SVGP gradient reads is written first in the same call: with the
+    workspaces pre-filled with NaN bytes (0xFF) the gradients still match autograd (L^{-1}'s
+    strictly-upper tiles are zeroed explicitly; the products skip the known-zero triangles)."""
+    from multi_fidelity_gpflow_amd.engine import Engine
+    X, Y = hbs["X"], hbs["Y"]
+    D, P = X.shape[1] - 1, Y.shape[1]
+    m = M.LatentMFCoregionalizationSVGP(X, Y, M.SquaredExponential(lengthscales=np.ones(D)),
+                                        M.SquaredExponential(lengthscales=np.ones(D)), num_latents=4,
+                                        num_inducing=40, num_outputs=P, w_type='diagonal')
+    _randomize(m, 41)
+    eng = Engine.get()
+    orig = eng.private_workspace
+    eng.private_workspace = lambda nbytes: torch.full((int(nbytes),), 255, dtype=torch.uint8, device=eng.device)
+    try:
+        e, gd = m.elbo_and_grad((X, Y))
+    finally:
+        eng.private_workspace = orig
+    eo, ga = _autograd_grads(m, X, Y, m.kernel.W.numpy(), num_data=X.shape[0])
+    assert abs(e - eo) < 1e-7 * abs(eo)
+    _check_grads(gd, ga, 1e-6)
