@@ -291,6 +291,14 @@ int mfgp_gpr_predict_workspace_size_ex(mfgp_handle_t h, int dtype, int n, int p,
 int mfgp_gpr_predict_ex(mfgp_handle_t h, int dtype, int n, int p, int d, int nstar, const void* X, int ldx,
                         const void* Y, int ldy, const void* Xs, int ldxs, const double* theta, void* ws,
                         size_t ws_bytes, void* mean, int ldm, void* var, int* info);
+/* predict_f(full_cov=True) in either dtype: mfgp_gpr_predict_cov for MFGP_F64 (any nlf);
+ * MFGP_F32 (nlf = 0): cov [nstar x nstar] (ldc) = K(X*, X*) - A^T A computed in fp32 from the
+ * same factor sweep as mfgp_gpr_predict_ex.  Workspace: mfgp_gpr_predict_cov_workspace_size_ex. */
+int mfgp_gpr_predict_cov_workspace_size_ex(mfgp_handle_t h, int dtype, int nlf, int n, int p, int d, int nstar,
+                                           size_t* bytes);
+int mfgp_gpr_predict_cov_ex(mfgp_handle_t h, int dtype, int nlf, int n, int p, int d, int nstar, const void* X,
+                            int ldx, const void* Y, int ldy, const void* Xs, int ldxs, const double* theta, void* ws,
+                            size_t ws_bytes, void* mean, int ldm, void* var, void* cov, int ldc, int* info);
 /* Diagnostic: one LML value+grad evaluation with hipEvents around its launches; synchronises.
  * Per phase (HOST arrays of nphase entries): ms, flops performed (fp32 only) and launch count.
  * fp32 phases: [gram, diag factors, panels, in-panel updates, trailing updates, alpha, gradient,

@@ -81,6 +81,9 @@ SIGNATURES = {
                                 C.POINTER(_d), C.POINTER(_i), _i],
     "mfgp_gpr_predict_workspace_size_ex": [_p, _i, _i, _i, _i, _i, C.POINTER(_sz)],
     "mfgp_gpr_predict_ex": [_p, _i, _i, _i, _i, _i, _p, _i, _p, _i, _p, _i, _p, _p, _sz, _p, _i, _p, _p],
+    "mfgp_gpr_predict_cov_workspace_size_ex": [_p, _i, _i, _i, _i, _i, _i, C.POINTER(_sz)],
+    "mfgp_gpr_predict_cov_ex": [_p, _i, _i, _i, _i, _i, _i, _p, _i, _p, _i, _p, _i, _p, _p, _sz, _p, _i, _p, _p, _i,
+                                _p],
 }
 
 MFGP_F64 = 0

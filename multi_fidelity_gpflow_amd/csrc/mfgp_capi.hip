@@ -552,7 +552,7 @@ static int f32_value_grad(mfgp_handle_t h, int n, int p, int d, const float* X, 
 
 static int f32_predict(mfgp_handle_t h, int n, int p, int d, int ns, const float* X, int ldx, const float* Y, int ldy,
                        const float* Xs, int ldxs, const double* theta, void* ws, size_t ws_bytes, float* mean, int ldm,
-                       float* var, int* info) {
+                       float* var, int* info, float* cov = nullptr, int ldc = 0) {
     F32Layout L = f32_layout(n, p, d, ns, 0, h->f32_panel, ws);
     if (ws_bytes < L.bytes) return MFGP_ERR_WORKSPACE;
     F32Args& a = L.a;
@@ -561,6 +561,7 @@ static int f32_predict(mfgp_handle_t h, int n, int p, int d, int ns, const float
     if (h->f32_lookahead) launch_f32_sweep(a, h->stream, nullptr, h->side, h->ev_fork, h->ev_join);
     else launch_f32_sweep(a, h->stream);
     launch_f32_predict(a, mean, ldm, var, h->stream);
+    if (cov) launch_f32_predict_cov(a, cov, ldc, h->stream);
     return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;
 }
 
@@ -1178,6 +1179,33 @@ int mfgp_gpr_predict_ex(mfgp_handle_t h, int dtype, int n, int p, int d, int nst
     if (!Xs || !mean || !var || ldx < d + 1 || ldy < p || ldxs < d + 1 || ldm < p) return MFGP_ERR_ARG;
     return f32_predict(h, n, p, d, nstar, (const float*)X, ldx, (const float*)Y, ldy, (const float*)Xs, ldxs, theta,
                        ws, ws_bytes, (float*)mean, ldm, (float*)var, info);
+}
+
+int mfgp_gpr_predict_cov_workspace_size_ex(mfgp_handle_t h, int dtype, int nlf, int n, int p, int d, int nstar,
+                                           size_t* bytes) {
+    CHECK_H(h);
+    CHECK_DT(dtype);
+    if (dtype == MFGP_F64) return mfgp_gpr_predict_cov_workspace_size(h, nlf, n, p, d, nstar, bytes);
+    if (nlf != 0) return MFGP_ERR_ARG;   // the fp32 path runs the linear multi-fidelity kernel
+    return mfgp_gpr_predict_workspace_size_ex(h, dtype, n, p, d, nstar, bytes);
+}
+
+int mfgp_gpr_predict_cov_ex(mfgp_handle_t h, int dtype, int nlf, int n, int p, int d, int nstar, const void* X,
+                            int ldx, const void* Y, int ldy, const void* Xs, int ldxs, const double* theta, void* ws,
+                            size_t ws_bytes, void* mean, int ldm, void* var, void* cov, int ldc, int* info) {
+    CHECK_H(h);
+    CHECK_D(d);
+    CHECK_DT(dtype);
+    if (dtype == MFGP_F64)
+        return mfgp_gpr_predict_cov(h, nlf, n, p, d, nstar, (const double*)X, ldx, (const double*)Y, ldy,
+                                    (const double*)Xs, ldxs, theta, ws, ws_bytes, (double*)mean, ldm, (double*)var,
+                                    (double*)cov, ldc, info);
+    if (nlf != 0 || n < 1 || p < 1 || nstar < 0 || !X || !Y || !theta || !ws || !info) return MFGP_ERR_ARG;
+    if (nstar == 0) return MFGP_OK;
+    if (!Xs || !mean || !var || !cov || ldx < d + 1 || ldy < p || ldxs < d + 1 || ldm < p || ldc < nstar)
+        return MFGP_ERR_ARG;
+    return f32_predict(h, n, p, d, nstar, (const float*)X, ldx, (const float*)Y, ldy, (const float*)Xs, ldxs, theta,
+                       ws, ws_bytes, (float*)mean, ldm, (float*)var, info, (float*)cov, ldc);
 }
 
 }  // extern "C"

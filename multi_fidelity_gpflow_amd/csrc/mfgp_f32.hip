@@ -795,6 +795,26 @@ __global__ __launch_bounds__(GT, 2) void k32_pred_mean(F32Args a, float* mean, l
             }
 }
 
+// full_cov: cov[s][s'] -= sum_i A[i][s] A[i][s'] on top of K(X*, X*) already in cov (GPflow
+// base_conditional(full_cov=True): Knn - A^T A); both operands are rows of the A^T region of M
+__global__ __launch_bounds__(GT, 2) void k32_pred_cov(F32Args a, float* cov, long ldc) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int st = blockIdx.x / a.Ts, st2 = blockIdx.x % a.Ts;
+    Acc acc;
+    acc_zero(acc);
+    gemm_nt(acc, a.M + row_off(a, a.T + a.Tp + st), a.ld, a.M + row_off(a, a.T + a.Tp + st2), a.ld,
+            a.T * (TB / BK), smem);
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int gs = st * TB + acc_row(m, r), gs2 = st2 * TB + acc_col(n);
+                if (gs < a.ns && gs2 < a.ns) cov[(long)gs * ldc + gs2] -= acc.c[m][n][r];
+            }
+}
+
 // var[s] = K_diag(x*_s) - sum_i A[i][s]^2 (linear.py:106-136 for K_diag); one wave per row
 __global__ __launch_bounds__(GT) void k32_pred_var(F32Args a, float* var) {
     const int s = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -973,6 +993,11 @@ void launch_f32_zsum(const F32Args& a, hipStream_t s) {
 void launch_f32_predict(const F32Args& a, float* mean, long ldm, float* var, hipStream_t s) {
     hipLaunchKernelGGL(k32_pred_mean, dim3(a.Ts * a.Tp), dim3(GT), GEMM_SMEM, s, a, mean, ldm);
     hipLaunchKernelGGL(k32_pred_var, dim3((a.ns + 3) / 4), dim3(GT), 0, s, a, var);
+}
+
+void launch_f32_predict_cov(const F32Args& a, float* cov, long ldc, hipStream_t s) {
+    launch_f32_gram_dense(a.Xs, a.ldxs, a.ns, a.Xs, a.ldxs, a.ns, a.D, a.theta, 0.0f, cov, ldc, s);
+    hipLaunchKernelGGL(k32_pred_cov, dim3(a.Ts * a.Ts), dim3(GT), GEMM_SMEM, s, a, cov, ldc);
 }
 
 void launch_f32_gram_dense(const float* X1, long ldx1, int n1, const float* X2, long ldx2, int n2, int D,

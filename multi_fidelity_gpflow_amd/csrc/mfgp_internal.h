@@ -213,6 +213,7 @@ void launch_f32_sweep(const F32Args& a, hipStream_t s, F32Marks* mk = nullptr, h
 void launch_f32_grad(const F32Args& a, hipStream_t s, F32Marks* mk = nullptr);
 void launch_f32_zsum(const F32Args& a, hipStream_t s);
 void launch_f32_predict(const F32Args& a, float* mean, long ldm, float* var, hipStream_t s);
+void launch_f32_predict_cov(const F32Args& a, float* cov, long ldc, hipStream_t s);
 void launch_f32_gram_dense(const float* X1, long ldx1, int n1, const float* X2, long ldx2, int n2, int D,
                            const double* theta, float diag_add, float* K, long ldk, hipStream_t s);
 

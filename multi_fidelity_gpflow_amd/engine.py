@@ -226,20 +226,22 @@ class Engine:
         return mean, var, info
 
     def gpr_predict_cov(self, nlf, X, Y, Xs, theta):
-        """predict_f(full_cov=True): mean [ns, p], var [ns], cov [ns, ns] (nlf 0: linear MF kernel)."""
+        """predict_f(full_cov=True): mean [ns, p], var [ns], cov [ns, ns] in X's dtype (nlf 0: linear
+        MF kernel; float32 only for nlf 0)."""
         n, dp1 = X.shape
         p = Y.shape[1]
         d = dp1 - 1
         ns = Xs.shape[0]
-        nbytes = self._size(self.lib.mfgp_gpr_predict_cov_workspace_size, nlf, n, p, d, ns)
-        ws = self.workspace("pred_cov", nbytes)
-        mean = torch.empty((ns, p), dtype=torch.float64, device=self.device)
-        var = torch.empty((ns,), dtype=torch.float64, device=self.device)
-        cov = torch.empty((ns, ns), dtype=torch.float64, device=self.device)
+        dt = dtype_code(X)
+        nbytes = self._size(self.lib.mfgp_gpr_predict_cov_workspace_size_ex, dt, nlf, n, p, d, ns)
+        ws = self.workspace("pred_cov" if X.dtype == torch.float64 else "pred_cov32", nbytes)
+        mean = torch.empty((ns, p), dtype=X.dtype, device=self.device)
+        var = torch.empty((ns,), dtype=X.dtype, device=self.device)
+        cov = torch.empty((ns, ns), dtype=X.dtype, device=self.device)
         info = torch.empty((1,), dtype=torch.int32, device=self.device)
-        check(self.lib.mfgp_gpr_predict_cov(self.h, nlf, n, p, d, ns, ptr(X), dp1, ptr(Y), p, ptr(Xs), Xs.shape[1],
-                                            ptr(theta), ptr(ws), ws.numel(), ptr(mean), p, ptr(var), ptr(cov), ns,
-                                            ptr(info)), "mfgp_gpr_predict_cov")
+        check(self.lib.mfgp_gpr_predict_cov_ex(self.h, dt, nlf, n, p, d, ns, ptr(X), dp1, ptr(Y), p, ptr(Xs),
+                                               Xs.shape[1], ptr(theta), ptr(ws), ws.numel(), ptr(mean), p, ptr(var),
+                                               ptr(cov), ns, ptr(info)), "mfgp_gpr_predict_cov_ex")
         return mean, var, cov, info
 
     # ---- GraphMultiFidelityKernel (graph.py) with nlf LF sources

@@ -172,8 +172,6 @@ class MultiFidelityGPModel(Module):
         eng, X, Y = self._device_data()
         Xs = to_dev(Xnew, eng.device, self.dtype)
         theta = torch.tensor(self._theta_map().theta(), dtype=torch.float64, device=eng.device)
-        if full_cov and self.dtype != torch.float64:
-            raise NotImplementedError("predict_f(full_cov=True) runs on the fp64 path only (dtype=None)")
         if full_cov:
             mean, _, cov, info = eng.gpr_predict_cov(0, X, Y, Xs, theta)
             self._raise_info(info, "predict_f")

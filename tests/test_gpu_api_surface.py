@@ -235,3 +235,29 @@ def test_session_graph_lifetime_is_deterministic(hbs, eng):
     sb.finish()
     m3.optimize(max_iters=60, learning_rate=0.1, verbose=False, graph=False)
     np.testing.assert_array_equal(np.array(m2.loss_history), np.array(m3.loss_history))
+
+
+@pytest.mark.parametrize("flow", [True, False])
+def test_gpr_independent_of_workspace_contents(goku, eng, flow):
+    """Every workspace byte the GPR LML / gradient / predict read is written first in the same
+    call: with the shared workspaces pre-filled with NaN bytes (0xFF) the results are bitwise the
+    clean ones, for the persistent-flow and the launch-per-step Cholesky."""
+    eng.set_flow(flow)
+    try:
+        m = _model(goku, theta_seed=5)
+        eng._ws.clear()
+        ref = m.log_marginal_likelihood_and_grad()
+        mref, vref = m.predict_f(goku["Xtest"])
+        eng._ws.clear()
+        n, p, d = goku["X"].shape[0], goku["Y"].shape[1], goku["X"].shape[1] - 1
+        for key, nbytes in (("gpr", eng.gpr_workspace_bytes(n, p, d)), ("pred", 256 << 20)):
+            eng._ws[key] = torch.full((int(nbytes),), 255, dtype=torch.uint8, device=eng.device)
+        got = m.log_marginal_likelihood_and_grad()
+        mg, vg = m.predict_f(goku["Xtest"])
+    finally:
+        eng.set_flow(True)
+        eng._ws.clear()
+    assert got[0] == ref[0]
+    np.testing.assert_array_equal(got[1], ref[1])
+    np.testing.assert_array_equal(mg.numpy(), mref.numpy())
+    np.testing.assert_array_equal(vg.numpy(), vref.numpy())

@@ -145,3 +145,18 @@ def test_f32_synth_full_size_vs_f64_path(eng, synth):
           f"var maxabs {np.max(np.abs(v32 - v64)):.2e}")
     assert np.max(np.abs(mu32 - mu64)) / np.max(np.abs(mu64)) < 3e-2
     assert np.max(np.abs(v32 - v64)) < 5e-4
+
+
+def test_f32_predict_full_cov(eng):
+    """predict_f(full_cov=True) on the fp32 path: K(X*, X*) - A^T A from the same factor sweep
+    (GPflow base_conditional full_cov branch), [P, N*, N*], against the fp64 oracle; its
+    diagonal is the full_cov=False variance."""
+    X, Y, Xt, _ = synthetic_multifidelity(500, 100, 10, 6, 150, seed=7)
+    m = _model(X, Y)
+    mean, cov = m.predict_f(Xt, full_cov=True)
+    assert cov.dtype == torch.float32 and tuple(cov.shape) == (6, 150, 150)
+    mo, co = O.gpr_predict_f_full_cov(X, Y, Xt, O.MFParams.initial(10, 6))
+    assert np.max(np.abs(mean.numpy() - mo)) / np.max(np.abs(mo)) < 1e-2
+    assert np.max(np.abs(cov.numpy() - co)) < 1e-4
+    _, var = m.predict_f(Xt)
+    np.testing.assert_allclose(np.diagonal(cov.numpy()[0]), var.numpy()[:, 0], rtol=0, atol=2e-6)
