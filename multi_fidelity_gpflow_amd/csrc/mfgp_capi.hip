@@ -23,6 +23,8 @@ struct mfgp_handle_s {
     int flow_wgs;   // k_chol_flow grid (one workgroup per CU); 0: launch-per-step Cholesky
     int ncu;        // compute units of the device
     int gram_wgs;   // k_gram tile workgroups, LML layout (0: one per CU; < 0: one per tile; MFGP_GRAM_WGS)
+    int gram_legacy;   // flow path: the looping k_gram instead of k_gram_flow (MFGP_GRAM_LEGACY, A/B only)
+    int flow_d0;       // flow path: the chain factors D_0 (no factor workgroup in k_gram_flow; MFGP_FLOW_D0)
     int flow_trace; // k_chol_flow writes its diagnostic timeline into the workspace
     long long flow_timeout;   // k_chol_flow hand-off wait bound (100 MHz ticks)
     int f32_panel;  // fp32 path: 128-wide tile columns per outer panel (trailing-update K = 128 * f32_panel)
@@ -221,8 +223,14 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
         if (L.flow_wgs) { g.fown = L.own; g.fW = FLOW_WAVES * (L.flow_wgs - 1); g.fflags = L.flags; g.nfflags = L.nflags; g.fpub = L.pub; g.npub = L.npub; }
         if (L.flow_wgs && h->flow_trace) g.dbg = L.trace + L.ntrace - 3 * 2048;   // k_gram timeline (diagnostic)
         const int extra = (order ? 1 : 0) + (L.flow_wgs ? 1 : 0);
-        g.tile_wgs = gram_tile_wgs(h, L.T, extra);
-        launch_gram<NB>(g, (g.tile_wgs ? g.tile_wgs : L.T * (L.T + 1) / 2) + extra, 1, s);
+        if (NB == 32 && L.flow_wgs && !nlf && !h->gram_legacy) {
+            if (h->flow_d0) g.Dd = nullptr;
+            if (h->flow_trace) if (const char* ge = getenv("MFGP_GRAM_EXPERIMENT")) g.tiles_c = atoi(ge);   // diagnostic ablations
+            launch_gram_flow(g, extra, s);
+        } else {
+            g.tile_wgs = gram_tile_wgs(h, L.T, extra);
+            launch_gram<NB>(g, (g.tile_wgs ? g.tile_wgs : L.T * (L.T + 1) / 2) + extra, 1, s);
+        }
     }
     if (pm) pm->mark(s);
     if (L.flow_wgs) {
@@ -237,6 +245,7 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
         fa.trace = h->flow_trace ? L.trace : nullptr;
         fa.nwaves = FLOW_WAVES * (L.flow_wgs - 1);
         fa.timeout = h->flow_timeout;
+        fa.d0 = (NB == 32 && !nlf && !h->gram_legacy && h->flow_d0) ? 1 : 0;
         fence_wait(h->device, s);
         launch_chol_flow(fa, L.flow_wgs, s);
         fence_record(h->device, s);
@@ -607,6 +616,10 @@ int mfgp_create(int device, mfgp_handle_t* out) {
     h->f32_reserve = 32;
     h->gram_wgs = 0;
     if (const char* gv = getenv("MFGP_GRAM_WGS")) h->gram_wgs = atoi(gv);
+    h->gram_legacy = 0;
+    if (const char* gl = getenv("MFGP_GRAM_LEGACY")) h->gram_legacy = atoi(gl) != 0;
+    h->flow_d0 = 0;
+    if (const char* d0 = getenv("MFGP_FLOW_D0")) h->flow_d0 = atoi(d0) != 0;
     if (const char* rv = getenv("MFGP_F32_RESERVE")) h->f32_reserve = std::max(0, atoi(rv));
     if (const char* la = getenv("MFGP_F32_LOOKAHEAD")) h->f32_lookahead = atoi(la) != 0;
     {

@@ -742,6 +742,12 @@ __device__ __forceinline__ void diag_chain(FlowCtx& C, const DiagLds& B) {
     const int T = a.T;
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     int epoch = 0;
+    if (a.d0 && w == 0) {   // D_0 from k_gram's A(0,0)
+        for (int e = l; e < 32 * 32; e += 64) B.fsc()[(e >> 5) * 33 + (e & 31)] = a.A[(long)(e >> 5) * a.lda + (e & 31)];
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        tile_potrf_inv_w1_wave(B.fsc(), 33, B.fsc(), B.Db(0), B.dg(0), &B.bad()[0]);
+        if (l == 0) lds_put(&B.w()[DW_D], 0);
+    }
     for (int k = 1; k < T; ++k) {
         const int pk = k & 1;
         if (a.trace && threadIdx.x == 0) a.trace[k] = flow_clock() - C.t0;
@@ -789,6 +795,7 @@ __device__ __forceinline__ void diag_publisher(FlowCtx& C, const DiagLds& B) {
     const int l = threadIdx.x & 63;
     for (int k = 0; k < T; ++k) {
         const int pk = k & 1;
+        if (k == 0 && a.d0) lds_wait_ge(&B.w()[DW_D], 0);
         if (k > 0) {
             lds_wait_ge(&B.w()[DW_LS], k);
             double* dst = C.P.L(k, k - 1);
@@ -820,7 +827,7 @@ __device__ __forceinline__ void diag_publisher(FlowCtx& C, const DiagLds& B) {
             st_coherent(xt + c * 32 + r, v);             // X^T(k,k) = D_k^T
             xo[(long)r * a.ldx + c] = v;
         }
-        if (k > 0) {
+        if (k > 0 || a.d0) {
             if (l < 32) a.ldiag[k * 32 + l] = B.dg(pk)[l];
             if (l == 0 && B.bad()[pk] && a.info[0] == 0) a.info[0] = k * 32 + B.bad()[pk];
         }
@@ -928,9 +935,10 @@ __device__ __forceinline__ void diag_prefetch(FlowCtx& C, const DiagLds& B, bool
 __device__ __forceinline__ void flow_diag(FlowCtx& C, double* smem) {
     DiagLds B;
     B.base = smem;
-    if (threadIdx.x < DW_N) B.w()[threadIdx.x] = (threadIdx.x == DW_LPUB || threadIdx.x == DW_DPUB) ? -1 : 0;
+    if (threadIdx.x < DW_N)
+        B.w()[threadIdx.x] = (threadIdx.x == DW_LPUB || threadIdx.x == DW_DPUB || (threadIdx.x == DW_D && C.a.d0)) ? -1 : 0;
     if (threadIdx.x < 2) B.bad()[threadIdx.x] = 0;
-    tile_load<32>(B.Db(0), C.a.Dd, 32);   // D_0: k_gram's fused factor (previous launch)
+    if (!C.a.d0) tile_load<32>(B.Db(0), C.a.Dd, 32);   // D_0: k_gram's fused factor (previous launch)
     __syncthreads();
     const int w = threadIdx.x >> 6;
     if (w < 4) diag_chain(C, B);

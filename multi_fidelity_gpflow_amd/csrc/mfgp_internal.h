@@ -60,6 +60,7 @@ struct FlowArgs {
     long long* trace;             // diagnostic timeline (nullptr: off), flow_trace_count entries
     int nwaves;                   // worker waves (trace layout)
     long long timeout;            // bound of every hand-off wait, 100 MHz ticks (FLOW_TIMEOUT_TICKS)
+    int d0;                       // 1: the chain factors D_0 from A(0,0) (else D_0 is read from Dd)
 };
 constexpr long long FLOW_TIMEOUT_TICKS = 5000000;   // 50 ms (s_memrealtime is 100 MHz)
 int flow_trace_count(int T, int nwg);
@@ -232,6 +233,7 @@ void launch_chol_flow(const FlowArgs& a, int nwg, hipStream_t s);
 template <int NB> void launch_gram(const GramArgs& g, int nblocks, int batch, hipStream_t s);
 // dense layout, write extents wr1 x wr2 (>= n1 x n2; the excess is written 0.0)
 void launch_gram_dense(const GramArgs& g, int batch, int wr1, int wr2, hipStream_t s);
+void launch_gram_flow(const GramArgs& g, int extra, hipStream_t s);   // set-up launch of k_chol_flow
 template <int NB> void launch_chol_steps(CholArgs c, int batch, hipStream_t s);
 template <int NB> void launch_grad(const GradArgs& g, hipStream_t s);
 template <int NB> void launch_pred(const PredAArgs& pa, const PredOutArgs& po, int T, hipStream_t s);

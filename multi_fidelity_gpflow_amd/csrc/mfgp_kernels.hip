@@ -527,6 +527,258 @@ void launch_gram_dense(const GramArgs& g, int batch, int wr1, int wr2, hipStream
     }
 }
 
+// exp of four independent arguments, stage by stage across the four (the compiler lays out
+// four exp() calls as four back-to-back dependent chains, which a wave issues in order).  The
+// same operations and constants as the device library's exp (range reduction by ln 2, degree-11
+// polynomial, ldexp, overflow / underflow selects), so each result is bitwise the library's.
+__device__ __forceinline__ double dbits(unsigned long long u) { return __longlong_as_double((long long)u); }
+#define MFGP_PIN4(v) asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]))
+__device__ __forceinline__ void exp4(double (&x)[4]) {
+    const double C[10] = {dbits(0x3e928af3fca7ab0cull), dbits(0x3ec71dee623fde64ull), dbits(0x3efa01997c89e6b0ull),
+                          dbits(0x3f2a01a014761f6eull), dbits(0x3f56c16c1852b7b0ull), dbits(0x3f81111111122322ull),
+                          dbits(0x3fa55555555502a1ull), dbits(0x3fc5555555555511ull), dbits(0x3fe000000000000bull), 1.0};
+    double n[4], r[4], p[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) n[u] = __builtin_rint(x[u] * dbits(0x3ff71547652b82feull));
+    MFGP_PIN4(n);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) r[u] = fma(dbits(0xbfe62e42fefa39efull), n[u], x[u]);
+    MFGP_PIN4(r);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) r[u] = fma(dbits(0xbc7abc9e3b39803full), n[u], r[u]);
+    MFGP_PIN4(r);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) p[u] = fma(dbits(0x3e5ade156a5dcb37ull), r[u], C[0]);
+    MFGP_PIN4(p);
+#pragma unroll
+    for (int k = 1; k < 10; ++k) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) p[u] = fma(r[u], p[u], C[k]);
+        MFGP_PIN4(p);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) p[u] = fma(r[u], p[u], 1.0);
+    MFGP_PIN4(p);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const double e = __builtin_ldexp(p[u], (int)n[u]);
+        x[u] = x[u] > 1024.0 ? __builtin_inf() : (x[u] < -1075.0 ? 0.0 : e);
+    }
+}
+
+// ------------------------------------------------------------ K1 flow set-up (LML layout, NB = 32)
+// The Gram launch in front of k_chol_flow, in the k_gram_dense form: workgroup b < nblk computes
+// lower 64 x 64 block b of the padded K + s2 I (row-major, ld = npad; identity on the padded
+// diagonal, zero elsewhere in the padding; the upper 32-tile of a diagonal block is skipped, and
+// tile (0,0) is left to the factor workgroup).  Workgroup nblk computes tile (0,0) into LDS and
+// runs the fused first diagonal factor (D_0, diag(L) 0..31, info); the set-up workgroups after it
+// build the flow owner table and the k_grad task order.  Every workgroup fills its share of the
+// publication area with the sentinel; the block workgroups copy the Y block of R.
+// It replaces k_gram's looping tile workgroups for this path: ~3 tiles each, one global round trip
+// per tile, and the fused factor's 256-VGPR allocation on every one (~18 us at Goku).
+// Entries: the same arithmetic as gram_entry (see k_gram_dense), K_ii = (k_ii + s2) + diag_add.
+// dbg (diagnostic): per workgroup [start, entries written / factor / table done, end], absolute
+// s_memrealtime ticks.
+template <int D4>
+__global__ __launch_bounds__(NTHREADS) void k_gram_flow(GramArgs a, int nblk) {
+    constexpr int S = TileCfg<32>::S;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    double* sL1 = smem;                 // 64 x D4  row side, LF-scaled
+    double* sD1 = sL1 + GD_T * D4;      // 64 x D4  row side, HF-scaled
+    double* sD2 = sD1 + GD_T * D4;      // 64 x D4  column side, HF-scaled (K_HH pairs)
+    double* nL1 = sD2 + GD_T * D4;      // 64
+    double* nD1 = nL1 + GD_T;           // 64
+    double* f1 = nD1 + GD_T;            // 64 row fidelity flags (-1: padding)
+    double* il = f1 + GD_T;             // 2 x MAXD inverse lengthscales
+    double* ftile = il + 2 * MAXD;      // 32 x S  tile (0,0)       (factor workgroup)
+    double* frt = ftile + 32 * S;       // 32 x S  factor scratch   (factor workgroup)
+    double* fdg = frt + 32 * S;         // 32 pivots + the bad word
+    const int t = threadIdx.x, bx = blockIdx.x;
+    const int nfac = a.Dd ? 1 : 0;   // Dd == nullptr: k_chol_flow factors D_0 itself
+    const long long t0 = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+    if (bx >= nblk + nfac) {   // set-up workgroups (LDS as int scratch)
+        int* sh = reinterpret_cast<int*>(smem);
+        if (a.gorder && bx == (int)gridDim.x - 1) build_grad_order(a.gT, a.gchunk, a.gTp, a.gorder, sh);
+        else if (a.fown) build_flow_owner(a.npad / 32, a.ppad / 32, a.fW, a.fown, a.fflags, a.nfflags, sh);
+        if (a.dbg && t == 0) { a.dbg[3 * bx] = t0; a.dbg[3 * bx + 1] = __builtin_amdgcn_s_memrealtime(); }
+        gram_fill_pub(a);
+        if (a.dbg && t == 0) a.dbg[3 * bx + 2] = __builtin_amdgcn_s_memrealtime();
+        return;
+    }
+    // workgroup 0: the factor workgroup (dispatched first: it is the launch's longest path)
+    const bool fac = nfac && bx == 0;
+    const int blk = bx - nfac;   // block index (block workgroups)
+    if (!nfac && bx == 0 && t == 0 && a.info) *a.info = 0;   // first writer of info in the sequence
+    int bi = 0, bj = 0;
+    if (!fac) flow_tri(blk, bi, bj);
+    const int r0 = bi * GD_T, c0 = bj * GD_T, nr = fac ? 32 : GD_T;
+    const int D = a.D, n = a.n1;
+    const double* tp = a.theta;
+    const double* X = a.X1;
+    if (t < D) {
+        il[t] = rcp_nr(tp[1 + t]);
+        il[MAXD + t] = a.rbf_only ? 1.0 : rcp_nr(tp[2 + D + t]);
+    }
+    const double vL = tp[0];
+    const double vD = a.rbf_only ? 0.0 : tp[1 + D];
+    const double rho = a.rbf_only ? 0.0 : tp[2 + 2 * D];
+    const double noise = a.add_noise ? tp[kernel_theta_size(0, D) - 1] : 0.0;
+    if (a.cnt && bx == 0)
+        for (int e = t; e < a.ncnt; e += NTHREADS) a.cnt[e] = 0;
+    __syncthreads();
+    for (int e = t; e < nr * D4; e += NTHREADS) {
+        const int r = e / D4, d = e % D4;
+        const bool in = d < D;
+        const double x1 = (in && r0 + r < n) ? X[(long)(r0 + r) * a.ldx1 + d] : 0.0;
+        sL1[e] = in ? x1 * il[d] : 0.0;
+        if (!a.rbf_only) {
+            const double x2 = (in && c0 + r < n) ? X[(long)(c0 + r) * a.ldx1 + d] : 0.0;
+            sD1[e] = in ? x1 * il[MAXD + d] : 0.0;
+            sD2[e] = in ? x2 * il[MAXD + d] : 0.0;
+        }
+    }
+    if (t < nr) f1[t] = (r0 + t < n) ? (a.rbf_only ? 0.0 : X[(long)(r0 + t) * a.ldx1 + D]) : -1.0;
+    // lane -> column c (blocks: 64 columns, one row a wave step; factor tile: 32 columns, lanes
+    // 32-63 take the odd row of each pair, so all 64 lanes work)
+    const int c = fac ? (t & 31) : (t & 63), gj = c0 + c;
+    const int half = fac ? ((t >> 5) & 1) : 0, rstep = fac ? 2 : 1;
+    double bl[D4];
+#pragma unroll
+    for (int d = 0; d < D4; ++d) bl[d] = (d < D && gj < n) ? X[(long)gj * a.ldx1 + d] * il[d] : 0.0;
+    const double f2 = (gj < n) ? (a.rbf_only ? 0.0 : X[(long)gj * a.ldx1 + D]) : -1.0;
+    __syncthreads();
+    if (t < nr) {
+        nL1[t] = dot4(sL1 + t * D4, sL1 + t * D4, D4);
+        nD1[t] = a.rbf_only ? 0.0 : dot4(sD1 + t * D4, sD1 + t * D4, D4);
+    }
+    const double nL2 = dot_rl<D4>(bl, bl);
+    const double nD2 = a.rbf_only ? 0.0 : dot4(sD2 + c * D4, sD2 + c * D4, D4);
+    __syncthreads();
+    if (a.dbg && t == 0) { a.dbg[3 * bx] = t0; a.dbg[3072 + 2 * bx + 1] = __builtin_amdgcn_s_memrealtime(); }
+    const bool L2 = (f2 == 0.0), H2 = (f2 == 1.0);
+    const bool col_ok = fac || gj < a.npad;
+    const int w = t >> 6;
+    // rows w + 4 (rstep q + half), q < nr / (4 rstep): four at a time, stage by stage
+    for (int q0 = 0; q0 < nr / (4 * rstep); q0 += 4) {
+        int rr[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) rr[u] = w + 4 * (rstep * (q0 + u) + half);
+        double kl[4] = {0.0, 0.0, 0.0, 0.0};
+        double ra[4][D4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int d = 0; d < D4; ++d) ra[u][d] = sL1[rr[u] * D4 + d];
+#pragma unroll
+        for (int d = 0; d < D4; ++d) {   // dot4 / dot_rl order per entry
+#pragma unroll
+            for (int u = 0; u < 4; ++u) kl[u] += ra[u][d] * bl[d];
+            MFGP_PIN4(kl);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) kl[u] = -0.5 * (-2.0 * kl[u] + (nL1[rr[u]] + nL2));
+        if (!(a.tiles_c & 2)) exp4(kl);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) kl[u] = vL * kl[u];
+        MFGP_PIN4(kl);   // keep the four chains in one basic block (else each sinks into the branch below)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int gi = r0 + rr[u];
+            double v;
+            if (gi < n && gj < n) {
+                const double fa = f1[rr[u]];
+                if (a.rbf_only) {
+                    v = (fa < 0.0 || f2 < 0.0) ? 0.0 : kl[u];
+                } else {
+                    const bool L1 = (fa == 0.0), H1 = (fa == 1.0);
+                    double kD = 0.0;
+                    if (H1 && H2) {   // K_HH (linear.py:96)
+                        const double dotD = dot4(sD1 + rr[u] * D4, sD2 + c * D4, D4);
+                        kD = vD * exp(-0.5 * (-2.0 * dotD + (nD1[rr[u]] + nD2)));
+                    }
+                    const double vhh = kl[u] * (rho * rho) + kD;
+                    v = (L1 && L2) ? kl[u] : (!(H1 && H2) ? kl[u] * rho : vhh);
+                    if (!(L1 || H1) || !(L2 || H2)) v = 0.0;   // linear.py:67-70 exact masks
+                }
+                if (gi == gj) v = v + noise + a.diag_add;
+            } else {
+                v = (gi == gj) ? 1.0 : 0.0;                   // identity padding
+            }
+            if (fac) {
+                ftile[rr[u] * S + c] = v;
+            } else {
+                // skipped: rows past npad, the upper tile of a diagonal block, tile (0,0) (the
+                // factor workgroup's, when there is one)
+                const bool keep = gi < a.npad && col_ok && (gi >> 5) >= (gj >> 5) && (!nfac || gi >= 32 || gj >= 32);
+                if (keep && !(a.tiles_c & 1)) a.out[(long)gi * a.ldo + gj] = v;
+            }
+        }
+    }
+    if (a.dbg && t == 0) a.dbg[3 * bx + 1] = __builtin_amdgcn_s_memrealtime();
+    if (fac) {
+        __syncthreads();
+        tile_store<32>(a.out, a.ldo, ftile);
+        gram_first_factor<32>(ftile, frt, fdg, reinterpret_cast<int*>(fdg + 32), a.Dd, a.ldiag, a.info);
+        if (a.dbg && t == 0) a.dbg[3 * bx + 1] = __builtin_amdgcn_s_memrealtime();
+    } else if (a.R != nullptr && !(a.tiles_c & 8)) {   // Y block of R (rows < n, columns < p; zero padding), shared by the blocks
+        const long ne = (long)a.npad * a.ppad, st = (long)nblk * NTHREADS;
+        const long e0 = blk * (long)NTHREADS + t;
+        double yv[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {   // loads first, then the stores (one round trip)
+            const long e = e0 + k * st;
+            const int r = (int)(e / a.ppad), cc = (int)(e % a.ppad);
+            yv[k] = (e < ne && r < n && cc < a.p) ? a.Y[(long)r * a.ldy + cc] : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const long e = e0 + k * st;
+            if (e < ne) a.R[(long)(e / a.ppad) * a.ldr + a.npad + e % a.ppad] = yv[k];
+        }
+        for (long e = e0 + 2 * st; e < ne; e += st) {
+            const int r = (int)(e / a.ppad), cc = (int)(e % a.ppad);
+            a.R[(long)r * a.ldr + a.npad + cc] = (r < n && cc < a.p) ? a.Y[(long)r * a.ldy + cc] : 0.0;
+        }
+    }
+    if (!(a.tiles_c & 4)) gram_fill_pub(a);
+    if (a.dbg && t == 0) a.dbg[3 * bx + 2] = __builtin_amdgcn_s_memrealtime();
+}
+
+static size_t gram_flow_smem_bytes(int D4) {
+    return sizeof(double) * (3 * (size_t)GD_T * D4 + 3 * GD_T + 2 * MAXD + 2 * 32 * TileCfg<32>::S + 32 + 2);
+}
+
+template <int D4>
+static void launch_gram_flow_d4(const GramArgs& g, int nblk, int grid, hipStream_t s) {
+    static bool attr = false;
+    const size_t lds = gram_flow_smem_bytes(D4);
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gram_flow<D4>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_gram_flow<D4>, dim3(grid), dim3(NTHREADS), lds, s, g, nblk);
+}
+
+// g: the LML-layout GramArgs of gpr_value_grad (batch 1, nlf = 0, NB = 32); extra: set-up
+// workgroups (flow owner table, k_grad order); g.Dd == nullptr: no factor workgroup (the flow
+// factors D_0 itself).
+void launch_gram_flow(const GramArgs& g, int extra, hipStream_t s) {
+    const int nb = (g.npad + GD_T - 1) / GD_T;
+    const int nblk = nb * (nb + 1) / 2;
+    const int grid = nblk + (g.Dd ? 1 : 0) + extra;
+    switch (pad4(g.D)) {
+        case 4: launch_gram_flow_d4<4>(g, nblk, grid, s); break;
+        case 8: launch_gram_flow_d4<8>(g, nblk, grid, s); break;
+        case 12: launch_gram_flow_d4<12>(g, nblk, grid, s); break;
+        case 16: launch_gram_flow_d4<16>(g, nblk, grid, s); break;
+        case 20: launch_gram_flow_d4<20>(g, nblk, grid, s); break;
+        case 24: launch_gram_flow_d4<24>(g, nblk, grid, s); break;
+        case 28: launch_gram_flow_d4<28>(g, nblk, grid, s); break;
+        default: launch_gram_flow_d4<32>(g, nblk, grid, s); break;
+    }
+}
+
 // ============================================================ K2: tile Cholesky step
 
 __device__ __forceinline__ void tri_decode(int t, int& i, int& j) {

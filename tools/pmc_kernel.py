@@ -20,6 +20,10 @@ GROUPS = [
     ["SQ_WAIT_INST_LDS", "SQ_WAIT_INST_ANY", "SQ_WAVE_CYCLES"],
     ["TCC_HIT_sum", "TCC_MISS_sum"],
     ["SQ_INSTS_VALU", "SQ_INSTS_VMEM_RD", "SQ_INSTS_SALU"],
+    ["SQ_WAIT_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_VMEM", "SQ_ACTIVE_INST_SCA",
+     "SQ_IFETCH", "SQ_INST_CYCLES_VMEM_WR", "SQ_ACTIVE_INST_ANY"],
+    ["SQ_VMEM_WR_TA_DATA_FIFO_FULL", "SQ_VMEM_TA_ADDR_FIFO_FULL", "SQ_VMEM_TA_CMD_FIFO_FULL", "SQ_INSTS_VMEM_WR",
+     "SQ_INSTS_SMEM", "SQ_INST_CYCLES_SMEM", "SQ_LDS_DATA_FIFO_FULL", "SQ_LDS_CMD_FIFO_FULL"],
 ]
 
 
