@@ -225,7 +225,7 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
         const int extra = (order ? 1 : 0) + (L.flow_wgs ? 1 : 0);
         if (NB == 32 && L.flow_wgs && !nlf && !h->gram_legacy) {
             if (h->flow_d0) g.Dd = nullptr;
-            if (h->flow_trace) if (const char* ge = getenv("MFGP_GRAM_EXPERIMENT")) g.tiles_c = atoi(ge);   // diagnostic ablations
+            if (h->flow_trace) if (const char* ge = getenv("MFGP_GRAM_EXPERIMENT")) g.exper = atoi(ge);   // diagnostic ablations
             launch_gram_flow(g, extra, s);
         } else {
             g.tile_wgs = gram_tile_wgs(h, L.T, extra);

@@ -34,6 +34,7 @@ struct GramArgs {
     // LML layout: > 0 -> that many tile workgroups, workgroup 0 takes tile (0,0) (and its fused
     // factor) alone on its CU, the others loop over the remaining tiles; 0 -> one tile each
     int tile_wgs;
+    int exper;                    // k_gram_flow diagnostic ablations (0: none; MFGP_GRAM_EXPERIMENT)
 };
 
 // k_chol_flow (mfgp_flow.hip): persistent dataflow Cholesky + L^{-1} + Z + alpha, NB = 32, batch 1

@@ -626,26 +626,44 @@ __global__ __launch_bounds__(NTHREADS) void k_gram_flow(GramArgs a, int nblk) {
     if (a.cnt && bx == 0)
         for (int e = t; e < a.ncnt; e += NTHREADS) a.cnt[e] = 0;
     __syncthreads();
-    for (int e = t; e < nr * D4; e += NTHREADS) {
-        const int r = e / D4, d = e % D4;
-        const bool in = d < D;
-        const double x1 = (in && r0 + r < n) ? X[(long)(r0 + r) * a.ldx1 + d] : 0.0;
-        sL1[e] = in ? x1 * il[d] : 0.0;
-        if (!a.rbf_only) {
-            const double x2 = (in && c0 + r < n) ? X[(long)(c0 + r) * a.ldx1 + d] : 0.0;
-            sD1[e] = in ? x1 * il[MAXD + d] : 0.0;
-            sD2[e] = in ? x2 * il[MAXD + d] : 0.0;
+    // every global load issued before any is used (clamped, in-bounds addresses; the selects come
+    // after): a conditional load per element compiled to one memory round trip each
+    constexpr int SPT = (GD_T * D4 + NTHREADS - 1) / NTHREADS;   // staged elements per thread
+    const int c = fac ? (t & 31) : (t & 63), gj = c0 + c;
+    double x1v[SPT], x2v[SPT], xb[D4];
+#pragma unroll
+    for (int k = 0; k < SPT; ++k) {
+        const int e = t + k * NTHREADS, r = min(e / D4, nr - 1), d = min(e % D4, D - 1);
+        x1v[k] = X[(long)min(r0 + r, n - 1) * a.ldx1 + d];
+        x2v[k] = X[(long)min(c0 + r, n - 1) * a.ldx1 + d];
+    }
+#pragma unroll
+    for (int d = 0; d < D4; ++d) xb[d] = X[(long)min(gj, n - 1) * a.ldx1 + min(d, D - 1)];
+    const double fr = X[(long)min(r0 + min(t, nr - 1), n - 1) * a.ldx1 + D];   // fidelity flags
+    const double fc = X[(long)min(gj, n - 1) * a.ldx1 + D];
+#pragma unroll
+    for (int k = 0; k < SPT; ++k) {
+        const int e = t + k * NTHREADS;
+        if (e < nr * D4) {
+            const int r = e / D4, d = e % D4;
+            const bool in = d < D;
+            const double x1 = (in && r0 + r < n) ? x1v[k] : 0.0;
+            sL1[e] = in ? x1 * il[d] : 0.0;
+            if (!a.rbf_only) {
+                const double x2 = (in && c0 + r < n) ? x2v[k] : 0.0;
+                sD1[e] = in ? x1 * il[MAXD + d] : 0.0;
+                sD2[e] = in ? x2 * il[MAXD + d] : 0.0;
+            }
         }
     }
-    if (t < nr) f1[t] = (r0 + t < n) ? (a.rbf_only ? 0.0 : X[(long)(r0 + t) * a.ldx1 + D]) : -1.0;
+    if (t < nr) f1[t] = (r0 + t < n) ? (a.rbf_only ? 0.0 : fr) : -1.0;
     // lane -> column c (blocks: 64 columns, one row a wave step; factor tile: 32 columns, lanes
     // 32-63 take the odd row of each pair, so all 64 lanes work)
-    const int c = fac ? (t & 31) : (t & 63), gj = c0 + c;
     const int half = fac ? ((t >> 5) & 1) : 0, rstep = fac ? 2 : 1;
     double bl[D4];
 #pragma unroll
-    for (int d = 0; d < D4; ++d) bl[d] = (d < D && gj < n) ? X[(long)gj * a.ldx1 + d] * il[d] : 0.0;
-    const double f2 = (gj < n) ? (a.rbf_only ? 0.0 : X[(long)gj * a.ldx1 + D]) : -1.0;
+    for (int d = 0; d < D4; ++d) bl[d] = (d < D && gj < n) ? xb[d] * il[d] : 0.0;
+    const double f2 = (gj < n) ? (a.rbf_only ? 0.0 : fc) : -1.0;
     __syncthreads();
     if (t < nr) {
         nL1[t] = dot4(sL1 + t * D4, sL1 + t * D4, D4);
@@ -677,7 +695,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram_flow(GramArgs a, int nblk) {
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) kl[u] = -0.5 * (-2.0 * kl[u] + (nL1[rr[u]] + nL2));
-        if (!(a.tiles_c & 2)) exp4(kl);
+        if (!(a.exper & 2)) exp4(kl);
 #pragma unroll
         for (int u = 0; u < 4; ++u) kl[u] = vL * kl[u];
         MFGP_PIN4(kl);   // keep the four chains in one basic block (else each sinks into the branch below)
@@ -710,7 +728,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram_flow(GramArgs a, int nblk) {
                 // skipped: rows past npad, the upper tile of a diagonal block, tile (0,0) (the
                 // factor workgroup's, when there is one)
                 const bool keep = gi < a.npad && col_ok && (gi >> 5) >= (gj >> 5) && (!nfac || gi >= 32 || gj >= 32);
-                if (keep && !(a.tiles_c & 1)) a.out[(long)gi * a.ldo + gj] = v;
+                if (keep && !(a.exper & 1)) a.out[(long)gi * a.ldo + gj] = v;
             }
         }
     }
@@ -720,7 +738,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram_flow(GramArgs a, int nblk) {
         tile_store<32>(a.out, a.ldo, ftile);
         gram_first_factor<32>(ftile, frt, fdg, reinterpret_cast<int*>(fdg + 32), a.Dd, a.ldiag, a.info);
         if (a.dbg && t == 0) a.dbg[3 * bx + 1] = __builtin_amdgcn_s_memrealtime();
-    } else if (a.R != nullptr && !(a.tiles_c & 8)) {   // Y block of R (rows < n, columns < p; zero padding), shared by the blocks
+    } else if (a.R != nullptr && !(a.exper & 8)) {   // Y block of R (rows < n, columns < p; zero padding), shared by the blocks
         const long ne = (long)a.npad * a.ppad, st = (long)nblk * NTHREADS;
         const long e0 = blk * (long)NTHREADS + t;
         double yv[2];
@@ -740,7 +758,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram_flow(GramArgs a, int nblk) {
             a.R[(long)r * a.ldr + a.npad + cc] = (r < n && cc < a.p) ? a.Y[(long)r * a.ldy + cc] : 0.0;
         }
     }
-    if (!(a.tiles_c & 4)) gram_fill_pub(a);
+    if (!(a.exper & 4)) gram_fill_pub(a);
     if (a.dbg && t == 0) a.dbg[3 * bx + 2] = __builtin_amdgcn_s_memrealtime();
 }
 
