@@ -30,6 +30,7 @@ struct mfgp_handle_s {
     int f32_panel;  // fp32 path: 128-wide tile columns per outer panel (trailing-update K = 128 * f32_panel)
     int f32_lookahead;          // fp32 sweep: factor the next panel beside the trailing update
     int f32_reserve;            // CUs the capped trailing update leaves to the side stream
+    int f32_refine;             // fp32 value-only LML / predict mean: one fp64 refinement step (mfgp_set_f32_refine)
     hipStream_t side;           // its high-priority side stream + fork / join events (created with the handle)
     hipEvent_t ev_fork, ev_join;
 };
@@ -495,13 +496,15 @@ int svgp_predict_impl(hipStream_t s, int nb, int n, int m, int l, int p, int d, 
 // ---------------------------------------------------------------- fp32 path (mfgp_f32.hip)
 struct F32Layout {
     F32Args a;
+    F32Refine r;
     double* items;
     int ntask, G;
     size_t bytes;
 };
 
-// ns > 0: predict rows; want_grad: identity rows + alpha + gradient partials
-static F32Layout f32_layout(int n, int p, int d, int ns, int want_grad, int panel, void* ws) {
+// ns > 0: predict rows; want_grad: identity rows + alpha + gradient partials; refine (value-only /
+// predict): L^T tiles, fp32 work rows, fp64 alpha and residual (mfgp_set_f32_refine)
+static F32Layout f32_layout(int n, int p, int d, int ns, int want_grad, int panel, void* ws, int refine = 0) {
     F32Layout L{};
     F32Args& a = L.a;
     const int TB = F32_TILE;
@@ -525,6 +528,13 @@ static F32Layout f32_layout(int n, int p, int d, int ns, int want_grad, int pane
     a.gpart = c.take<double>(want_grad ? (size_t)L.G * L.ntask : 0);
     L.items = c.take<double>((size_t)L.G + 8);
     a.cnt = c.take<int>(1);
+    if (refine && !want_grad) {
+        a.LT = c.take<float>((size_t)a.T * TB * a.ld);
+        L.r.XB = c.take<float>((size_t)a.Tp * TB * a.ld);
+        L.r.ld64 = (long)ceil_div(a.Tp * TB, 256) * 256;   // k64_kmat reads 256-column blocks
+        L.r.A64 = c.take<double>((size_t)a.ld * L.r.ld64);
+        L.r.R64 = c.take<double>((size_t)a.ld * L.r.ld64);
+    }
     L.bytes = c.off + 256;
     return L;
 }
@@ -532,7 +542,8 @@ static F32Layout f32_layout(int n, int p, int d, int ns, int want_grad, int pane
 static int f32_value_grad(mfgp_handle_t h, int n, int p, int d, const float* X, int ldx, const float* Y, int ldy,
                           double* theta, int want_grad, void* ws, size_t ws_bytes, double* out, int* info,
                           const FinArgs* adam, F32Marks* mk = nullptr) {
-    F32Layout L = f32_layout(n, p, d, 0, want_grad, h->f32_panel, ws);
+    const int refine = h->f32_refine && !want_grad && !adam && !mk;
+    F32Layout L = f32_layout(n, p, d, 0, want_grad, h->f32_panel, ws, refine);
     if (ws_bytes < L.bytes) return MFGP_ERR_WORKSPACE;
     hipStream_t s = h->stream;
     F32Args& a = L.a;
@@ -542,7 +553,8 @@ static int f32_value_grad(mfgp_handle_t h, int n, int p, int d, const float* X, 
     else launch_f32_sweep(a, s, mk);
     if (want_grad) launch_f32_grad(a, s, mk);
     if (mk) mk->begin(s, F32_FIN);
-    launch_f32_zsum(a, s);
+    if (refine) launch_f32_refine_lml(a, L.r, s);   // q = Y.a0 + a0.R + |L~^-1 R|^2 partials into zpart
+    else launch_f32_zsum(a, s);
     FinArgs f{};
     if (adam) f = *adam;
     f.zpart = a.zpart; f.nz = a.nz;
@@ -562,14 +574,15 @@ static int f32_value_grad(mfgp_handle_t h, int n, int p, int d, const float* X, 
 static int f32_predict(mfgp_handle_t h, int n, int p, int d, int ns, const float* X, int ldx, const float* Y, int ldy,
                        const float* Xs, int ldxs, const double* theta, void* ws, size_t ws_bytes, float* mean, int ldm,
                        float* var, int* info, float* cov = nullptr, int ldc = 0) {
-    F32Layout L = f32_layout(n, p, d, ns, 0, h->f32_panel, ws);
+    F32Layout L = f32_layout(n, p, d, ns, 0, h->f32_panel, ws, h->f32_refine);
     if (ws_bytes < L.bytes) return MFGP_ERR_WORKSPACE;
     F32Args& a = L.a;
     a.info = info; a.X = X; a.ldx = ldx; a.Y = Y; a.ldy = ldy; a.Xs = Xs; a.ldxs = ldxs; a.theta = theta;
     a.upd_slots = (h->f32_reserve > 0 && h->ncu > h->f32_reserve) ? 2 * (h->ncu - h->f32_reserve) : 0;
     if (h->f32_lookahead) launch_f32_sweep(a, h->stream, nullptr, h->side, h->ev_fork, h->ev_join);
     else launch_f32_sweep(a, h->stream);
-    launch_f32_predict(a, mean, ldm, var, h->stream);
+    launch_f32_predict(a, mean, ldm, var, h->stream);   // variance (and the unrefined mean)
+    if (h->f32_refine) launch_f32_refine_mean(a, L.r, mean, ldm, h->stream);
     if (cov) launch_f32_predict_cov(a, cov, ldc, h->stream);
     return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;
 }
@@ -622,6 +635,8 @@ int mfgp_create(int device, mfgp_handle_t* out) {
     if (const char* d0 = getenv("MFGP_FLOW_D0")) h->flow_d0 = atoi(d0) != 0;
     if (const char* rv = getenv("MFGP_F32_RESERVE")) h->f32_reserve = std::max(0, atoi(rv));
     if (const char* la = getenv("MFGP_F32_LOOKAHEAD")) h->f32_lookahead = atoi(la) != 0;
+    h->f32_refine = 1;
+    if (const char* rf = getenv("MFGP_F32_REFINE")) h->f32_refine = atoi(rf) != 0;
     {
         int lo = 0, hi = 0;
         int cur = -1;
@@ -666,6 +681,13 @@ int mfgp_set_tile(mfgp_handle_t h, int nb) {
 }
 
 int mfgp_get_tile(mfgp_handle_t h) { return h ? h->nb : MFGP_ERR_ARG; }
+
+int mfgp_set_f32_refine(mfgp_handle_t h, int enable) {
+    CHECK_H(h);
+    if (enable < 0 || enable > 1) return MFGP_ERR_ARG;
+    h->f32_refine = enable;
+    return MFGP_OK;
+}
 
 int mfgp_set_flow(mfgp_handle_t h, int enable) {
     CHECK_H(h);
@@ -1098,6 +1120,7 @@ int mfgp_gpr_workspace_size_ex(mfgp_handle_t h, int dtype, int n, int p, int d, 
     if (dtype == MFGP_F64) return mfgp_gpr_workspace_size(h, n, p, d, bytes);
     if (n < 1 || p < 1 || !bytes) return MFGP_ERR_ARG;
     *bytes = f32_layout(n, p, d, 0, 1, h->f32_panel, nullptr).bytes;
+    if (h->f32_refine) *bytes = std::max(*bytes, f32_layout(n, p, d, 0, 0, h->f32_panel, nullptr, 1).bytes);
     return MFGP_OK;
 }
 
@@ -1174,7 +1197,7 @@ int mfgp_gpr_predict_workspace_size_ex(mfgp_handle_t h, int dtype, int n, int p,
     CHECK_DT(dtype);
     if (dtype == MFGP_F64) return mfgp_gpr_predict_workspace_size(h, n, p, d, nstar, bytes);
     if (n < 1 || p < 1 || nstar < 0 || !bytes) return MFGP_ERR_ARG;
-    *bytes = f32_layout(n, p, d, nstar > 0 ? nstar : 1, 0, h->f32_panel, nullptr).bytes;
+    *bytes = f32_layout(n, p, d, nstar > 0 ? nstar : 1, 0, h->f32_panel, nullptr, h->f32_refine).bytes;
     return MFGP_OK;
 }
 

@@ -553,6 +553,13 @@ __global__ __launch_bounds__(DIAG_THREADS) void k32_diag(F32Args a, int k) {
             if (c4 + q <= r) dst[q] = lv[q];
         *reinterpret_cast<f32x4*>(Dk + r * TB + c4) = *reinterpret_cast<const f32x4*>(Ds + r * DLD + c4);
     }
+    if (a.LT) {   // refinement: D_k^T as tile (k, k) of L^T
+        float* lt = a.LT + row_off(a, k) + (long)k * TB;
+        for (int e = threadIdx.x; e < TB * TB; e += DIAG_THREADS) {
+            const int r = e / TB, c = e % TB;   // lt row r = column r of D_k
+            lt[(long)r * a.ld + c] = Ds[c * DLD + r];
+        }
+    }
     if (threadIdx.x == 0 && *bad && k * TB + *bad - 1 < a.n && *a.info == 0) *a.info = k * TB + *bad;
 }
 
@@ -568,6 +575,15 @@ __global__ __launch_bounds__(GT, 2) void k32_panel(F32Args a, int k) {
     acc_zero(acc);
     gemm_nt(acc, Mr, a.ld, a.Dd + (long)k * TB * TB, TB, TB / BK, smem);
     acc_store(acc, Mr, a.ld);
+    if (a.LT && rt < a.T) {   // refinement: L(rt,k)^T as tile (k, rt) of L^T
+        float* lt = a.LT + row_off(a, k) + (long)rt * TB;
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) lt[(long)acc_col(n) * a.ld + acc_row(m, r)] = acc.c[m][n][r];
+    }
 }
 
 // ---------------------------------------------------------------- K2c: update
@@ -855,6 +871,270 @@ __global__ __launch_bounds__(GT) void k32_gram_dense(const float* X1, long ldx1,
         }
 }
 
+// ---------------------------------------------------------------- fp64 refinement of the solve
+// One step of iterative refinement with the residual in fp64 (value-only LML, predict mean):
+//   alpha0 = L~^-T L~^-1 Y (fp32 factor), R = Y - K alpha0 (fp64, K recomputed in fp64),
+//   W = L~^-1 R;  LML quad term q = Y.alpha0 + alpha0.R + |W|^2  (exact identity
+//   Y^T K^-1 Y = Y^T a0 + a0^T R + R^T K^-1 R, with K^-1 ~ K~^-1 only in the second-order term);
+//   predict: alpha1 = alpha0 + L~^-T W, mean = K(X*, X) alpha1 (fp64).
+// The triangular solves run on rows [P x Npad] (right solves X L^T = B and X L = B) with the NT
+// GEMM core: the forward solve reads L's rows, the backward one the rows of L^T (stored by the
+// sweep's panel / diagonal kernels when a.LT is set).
+
+// B(pt, k) <- B(pt, k) Dop^T (in place; Dop row-major, ld ldd)
+__global__ __launch_bounds__(GT, 2) void k32_sdiag(float* B, long ldb, int k, const float* Dop, long ldd) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* Bt = B + (long)blockIdx.x * TB * ldb + (long)k * TB;
+    Acc acc;
+    acc_zero(acc);
+    gemm_nt(acc, Bt, ldb, Dop, ldd, TB / BK, smem);
+    acc_store(acc, Bt, ldb);
+}
+
+// B(pt, j) -= sum_{kk in [k0, k1)} B(pt, kk) Lr(j, kk)^T for j in [jb, je) (tile t: pt = t % np)
+__global__ __launch_bounds__(GT, 2) void k32_supd(float* B, long ldb, int np, int k0, int k1, int jb,
+                                                  const float* Lr, long ldl) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int pt = blockIdx.x % np, j = jb + blockIdx.x / np;
+    float* Brow = B + (long)pt * TB * ldb;
+    Acc acc;
+    acc_zero(acc);
+    gemm_nt(acc, Brow + (long)k0 * TB, ldb, Lr + (long)j * TB * ldl + (long)k0 * TB, ldl, (k1 - k0) * (TB / BK), smem);
+    acc_sub_into(acc, Brow + (long)j * TB, ldb);
+}
+
+// One column step of a right-looking solve (one launch per tile column): for j in [jb, jb + nj),
+// B(pt, j) -= B(pt, k) Lr(j, k)^T; the tile of column jf (the next diagonal) is then finalised in
+// the same workgroup, B(pt, jf) <- B(pt, jf) Dop^T (its only writer: the update went through
+// global memory, read back by the same workgroup after a barrier).
+__global__ __launch_bounds__(GT, 2) void k32_sstep(float* B, long ldb, int np, int k, int jb, const float* Lr,
+                                                   long ldl, int jf, const float* Dop, long ldd) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int pt = blockIdx.x % np, j = jb + blockIdx.x / np;
+    float* Brow = B + (long)pt * TB * ldb;
+    Acc acc;
+    acc_zero(acc);
+    gemm_nt(acc, Brow + (long)k * TB, ldb, Lr + (long)j * TB * ldl + (long)k * TB, ldl, TB / BK, smem);
+    acc_sub_into(acc, Brow + (long)j * TB, ldb);
+    if (j != jf) return;
+    __threadfence_block();
+    __syncthreads();
+    acc_zero(acc);
+    gemm_nt(acc, Brow + (long)j * TB, ldb, Dop, ldd, TB / BK, smem);
+    acc_store(acc, Brow + (long)j * TB, ldb);
+}
+
+// out[i][q] = (Y ? Y[i][q] - (K C)[i][q] : (K C)[i][q]), fp64.  K entries recomputed in fp64 from
+// the fp32 inputs, in GPflow's expanded form with the exact fidelity masks (the fp64 path's
+// gram_entry, mfgp_kernels.hip; linear.py:55-104), plus s2 on i == j when add_noise
+// (K(X, X) + s2 I).  64 rows x 256 columns a workgroup (K recomputed once per 256 columns of C),
+// 16 columns of K a step: the K tile (64 x 16) and the C slab (16 x 256) through LDS, the next
+// step's inputs prefetched into registers during this step's products; v_mfma_f64_16x16x4,
+// a wave 16 rows x 256 columns (16 accumulators).  C must have >= ceil16(n2) readable rows and
+// tq * 256 readable columns (the refinement's fp64 buffers: Npad x Ppad, zero padded).
+struct KmatArgs {
+    const float* X1; long ldx1; int n1;
+    const float* X2; long ldx2; int n2;
+    int D; const double* theta; int add_noise;
+    const double* C; long ldc;
+    const float* Y; long ldy;
+    double* out; long ldo; float* out32; long ldo32; int p;
+    int tq;   // column blocks of 256
+};
+constexpr int KM_R = 64, KM_Q = 256, KM_J = 16, KM_XS = MAXD_HOST + 1, KM_CS = KM_Q + 2;
+constexpr size_t KMAT_SMEM = sizeof(double) * (KM_R * KM_XS + KM_R + 2 * KM_J * KM_XS + 3 * KM_J +
+                                               KM_R * (KM_J + 1) + KM_J * KM_CS + 2 * MAXD_HOST);
+
+template <int D4>
+__global__ __launch_bounds__(256, 2) void k64_kmat(KmatArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double sm64[];
+    double* rD = sm64;                       // [64][XS] row side, HF-scaled (K_HH pairs)
+    double* rnd = rD + KM_R * KM_XS;         // [64] |rD|^2
+    double* cL = rnd + KM_R;                 // [16][D4] column side, LF-scaled (zero padded)
+    double* cD = cL + KM_J * KM_XS;          // [16][XS] column side, HF-scaled
+    double* cn = cD + KM_J * KM_XS;
+    double* cnd = cn + KM_J;
+    double* cf = cnd + KM_J;
+    double* Ks = cf + KM_J;                  // [64][17]
+    double* Cs = Ks + KM_R * (KM_J + 1);     // [16][KM_CS]
+    double* il = Cs + KM_J * KM_CS;          // [2][MAXD]
+    const int t = threadIdx.x, D = a.D;
+    const int i0 = (blockIdx.x / a.tq) * KM_R, q0 = (blockIdx.x % a.tq) * KM_Q;
+    const double vL = a.theta[0], vD = a.theta[1 + D], rho = a.theta[2 + 2 * D];
+    const double s2 = a.add_noise ? a.theta[3 + 2 * D] : 0.0;
+    if (t < D) {
+        il[t] = 1.0 / a.theta[1 + t];
+        il[MAXD_HOST + t] = 1.0 / a.theta[2 + D + t];
+    }
+    __syncthreads();
+    // row side in registers: thread t's row r = t / 4 for the whole launch (the LF-scaled row, its
+    // norm and flag; the HF-scaled row in LDS for the rare K_HH pairs)
+    const int r = t >> 2, gi = i0 + r;
+    const bool rin = gi < a.n1;
+    double ra[D4], rn, rf;
+    {
+        float xr[D4 + 1];
+        const int gc = min(gi, a.n1 - 1);
+#pragma unroll
+        for (int d = 0; d < D4 + 1; ++d) xr[d] = a.X1[(long)gc * a.ldx1 + min(d, D)];   // unconditional
+        double sl = 0.0, sd = 0.0;
+#pragma unroll
+        for (int d = 0; d < D4; ++d) {
+            const double x = (rin && d < D) ? (double)xr[d] : 0.0;
+            ra[d] = d < D ? x * il[d] : 0.0;
+            sl += ra[d] * ra[d];
+            if ((t & 3) == 0 && d < D) {
+                const double h = x * il[MAXD_HOST + d];
+                rD[r * KM_XS + d] = h;
+                sd += h * h;
+            }
+        }
+        rn = sl;
+        rf = rin ? (double)xr[D] : -1.0;   // xr[D]: the flag column (min(d, D) at d = D)
+        if ((t & 3) == 0) rnd[r] = sd;
+        if (D4 == D) rf = rin ? (double)a.X1[(long)gc * a.ldx1 + D] : -1.0;
+    }
+    // column-side prefetch: thread t < 16 loads row j0 + t of X2; every thread 16 C values
+    float xc[D4 + 1];
+    double cv[KM_J];
+    auto prefetch = [&](int j0) {
+        if (t < KM_J) {
+            const int gj = min(j0 + t, a.n2 - 1);
+#pragma unroll
+            for (int d = 0; d < D4 + 1; ++d) xc[d] = a.X2[(long)gj * a.ldx2 + min(d, D)];
+        }
+#pragma unroll
+        for (int u = 0; u < KM_J; ++u) cv[u] = a.C[(long)(j0 + u) * a.ldc + q0 + t];
+    };
+    const int lane = t & 63, w = t >> 6, li = lane & 15, lk = lane >> 4;
+    f64x4 acc[KM_Q / 16];
+#pragma unroll
+    for (int b = 0; b < KM_Q / 16; ++b) acc[b] = f64x4{0.0, 0.0, 0.0, 0.0};
+    prefetch(0);
+    for (int j0 = 0; j0 < a.n2; j0 += KM_J) {
+        // commit the prefetched step
+        if (t < KM_J) {
+            const bool in = j0 + t < a.n2;
+            double sl = 0.0, sd = 0.0;
+#pragma unroll
+            for (int d = 0; d < D4; ++d) {
+                const double x = (in && d < D) ? (double)xc[d] : 0.0;
+                const double l = x * (d < D ? il[d] : 0.0), h = x * (d < D ? il[MAXD_HOST + d] : 0.0);
+                cL[t * D4 + d] = l;
+                cD[t * KM_XS + d] = h;
+                sl += l * l;
+                sd += h * h;
+            }
+            cn[t] = sl;
+            cnd[t] = sd;
+            cf[t] = in ? (double)(D4 == D ? a.X2[(long)min(j0 + t, a.n2 - 1) * a.ldx2 + D] : xc[D]) : -1.0;
+        }
+#pragma unroll
+        for (int u = 0; u < KM_J; ++u) Cs[u * KM_CS + t] = cv[u];
+        __syncthreads();
+        if (j0 + KM_J < a.n2) prefetch(j0 + KM_J);
+        // 4 entries a thread: row r, columns 4 (t % 4) + u, side by side (dot4 order per entry)
+        double kl[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int d = 0; d < D4; ++d) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) kl[u] += ra[d] * cL[(4 * (t & 3) + u) * D4 + d];
+            MFGP_PIN4(kl);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) kl[u] = -0.5 * (-2.0 * kl[u] + (rn + cn[4 * (t & 3) + u]));
+        exp4(kl);
+        MFGP_PIN4(kl);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int c = 4 * (t & 3) + u, gj = j0 + c;
+            const double f2 = cf[c];
+            double v = 0.0;
+            if (rin && gj < a.n2) {
+                const double kL = vL * kl[u];
+                const bool L1 = rf == 0.0, H1 = rf == 1.0, L2 = f2 == 0.0, H2 = f2 == 1.0;
+                if (!(L1 || H1) || !(L2 || H2)) v = 0.0;   // linear.py:67-70 exact masks
+                else if (L1 && L2) v = kL;
+                else if (!(H1 && H2)) v = kL * rho;
+                else {   // K_HH (linear.py:96)
+                    double dd = 0.0;
+                    for (int d = 0; d < D; ++d) dd += rD[r * KM_XS + d] * cD[c * KM_XS + d];
+                    v = kL * (rho * rho) + vD * exp(-0.5 * (-2.0 * dd + (rnd[r] + cnd[c])));
+                }
+                if (gi == gj) v += s2;
+            }
+            Ks[r * (KM_J + 1) + c] = v;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int ks = 0; ks < KM_J / 4; ++ks) {
+            const double av = Ks[(16 * w + li) * (KM_J + 1) + 4 * ks + lk];
+#pragma unroll
+            for (int b = 0; b < KM_Q / 16; ++b) {
+                const double bv = Cs[(4 * ks + lk) * KM_CS + 16 * b + li];
+                acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[b], 0, 0, 0);
+            }
+        }
+        __syncthreads();   // K / C slabs consumed before the next commit
+    }
+#pragma unroll
+    for (int b = 0; b < KM_Q / 16; ++b)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int gi2 = i0 + 16 * w + lk + 4 * rr, gq = q0 + 16 * b + li;
+            if (gi2 >= a.n1 || gq >= a.p) continue;
+            const double v = a.Y ? (double)a.Y[(long)gi2 * a.ldy + gq] - acc[b][rr] : acc[b][rr];
+            if (a.out) a.out[(long)gi2 * a.ldo + gq] = v;
+            if (a.out32) a.out32[(long)gi2 * a.ldo32 + gq] = (float)v;
+        }
+}
+
+// fp32 rows [P][N] (ld ldr) <-> fp64 [N][P] (ld ld64); zero outside n x p.  mode 0: to64 (out = rows^T),
+// 1: to32 (rows = in^T), 2: add (out += rows^T).  32 x 32 tiles through LDS.
+__global__ __launch_bounds__(256) void k_tr3264(float* rows, long ldr, double* m64, long ld64, int n, int p,
+                                               int npad, int ppad, int mode) {
+    __shared__ double tl[32][33];
+    const int tn = npad / 32;
+    const int bi = blockIdx.x % tn, bq = blockIdx.x / tn;   // tile: i in 32 bi.., q in 32 bq..
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    for (int yy = ty; yy < 32; yy += 8) {
+        const int i = 32 * bi + yy, q = 32 * bq + tx;   // read m64 coalesced along q, rows along i
+        if (mode == 1) tl[yy][tx] = (i < n && q < p) ? m64[(long)i * ld64 + q] : 0.0;
+        else tl[yy][tx] = (double)rows[(long)(32 * bq + yy) * ldr + 32 * bi + tx];   // rows: q row, i col
+    }
+    __syncthreads();
+    for (int yy = ty; yy < 32; yy += 8) {
+        if (mode == 1) {
+            const int q = 32 * bq + yy, i = 32 * bi + tx;
+            rows[(long)q * ldr + i] = (float)tl[tx][yy];
+        } else {
+            const int i = 32 * bi + yy, q = 32 * bq + tx;
+            const double v = (i < n && q < p) ? tl[tx][yy] : 0.0;
+            if (mode == 0) m64[(long)i * ld64 + q] = v;
+            else if (i < n && q < p) m64[(long)i * ld64 + q] += v;
+        }
+    }
+}
+
+// q partials: sum_{i<n, q<p} (Y a0 + a0 R)[i][q] + sum W^2 over the fp32 rows (P x Npad)
+__global__ __launch_bounds__(256) void k_refine_q(const float* Y, long ldy, const double* A64, const double* R64,
+                                                 long ld64, const float* Wr, long ldw, int n, int p, double* part) {
+    __shared__ double red[4];
+    double s = 0.0;
+    const long tot = (long)n * p;
+    for (long e = blockIdx.x * 256L + threadIdx.x; e < tot; e += (long)gridDim.x * 256) {
+        const int i = (int)(e / p), q = (int)(e % p);
+        const double a = A64[(long)i * ld64 + q];
+        s += ((double)Y[(long)i * ldy + q] + R64[(long)i * ld64 + q]) * a;
+        const double wv = (double)Wr[(long)q * ldw + i];
+        s += wv * wv;
+    }
+    s = wave_sum_d(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
 }  // namespace f32
 
 // ---------------------------------------------------------------- host launchers
@@ -877,6 +1157,7 @@ static void f32_lds_attributes() {
                               (int)DIAG_SMEM);
     const void* gemms[] = {reinterpret_cast<const void*>(&k32_panel), reinterpret_cast<const void*>(&k32_update),
                            reinterpret_cast<const void*>(&k32_alpha), reinterpret_cast<const void*>(&k32_pred_mean),
+                           reinterpret_cast<const void*>(&k32_pred_cov),
                            reinterpret_cast<const void*>(&k32_grad<4>), reinterpret_cast<const void*>(&k32_grad<8>),
                            reinterpret_cast<const void*>(&k32_grad<12>), reinterpret_cast<const void*>(&k32_grad<16>),
                            reinterpret_cast<const void*>(&k32_grad<32>)};
@@ -998,6 +1279,87 @@ void launch_f32_predict(const F32Args& a, float* mean, long ldm, float* var, hip
 void launch_f32_predict_cov(const F32Args& a, float* cov, long ldc, hipStream_t s) {
     launch_f32_gram_dense(a.Xs, a.ldxs, a.ns, a.Xs, a.ldxs, a.ns, a.D, a.theta, 0.0f, cov, ldc, s);
     hipLaunchKernelGGL(k32_pred_cov, dim3(a.Ts * a.Ts), dim3(GT), GEMM_SMEM, s, a, cov, ldc);
+}
+
+// ---- refinement (see k32_sdiag .. k_refine_q)
+// rows B [np x 128 tiles][Npad]: X L~^T = B  (forward: X = B L~^-T, i.e. (L~^-1 B^T)^T); one launch
+// per tile column (k32_sstep), K = 128 each
+static void f32_fsolve(const F32Args& a, float* B, long ldb, int np, hipStream_t s) {
+    hipLaunchKernelGGL(k32_sdiag, dim3(np), dim3(GT), GEMM_SMEM, s, B, ldb, 0, (const float*)a.Dd, (long)TB);
+    for (int k = 0; k + 1 < a.T; ++k)
+        hipLaunchKernelGGL(k32_sstep, dim3(np * (a.T - k - 1)), dim3(GT), GEMM_SMEM, s, B, ldb, np, k, k + 1,
+                           (const float*)a.M, a.ld, k + 1, (const float*)(a.Dd + (long)(k + 1) * TB * TB), (long)TB);
+}
+// X L~ = B  (backward: X = B L~^-1, i.e. (L~^-T B^T)^T), with the L^T tiles
+static void f32_bsolve(const F32Args& a, float* B, long ldb, int np, hipStream_t s) {
+    auto dT = [&](int k) { return (const float*)(a.LT + row_off(a, k) + (long)k * TB); };
+    hipLaunchKernelGGL(k32_sdiag, dim3(np), dim3(GT), GEMM_SMEM, s, B, ldb, a.T - 1, dT(a.T - 1), a.ld);
+    for (int k = a.T - 1; k > 0; --k)
+        hipLaunchKernelGGL(k32_sstep, dim3(np * k), dim3(GT), GEMM_SMEM, s, B, ldb, np, k, 0, (const float*)a.LT,
+                           a.ld, k - 1, dT(k - 1), a.ld);
+}
+
+static void refine_lds_attributes() {
+    static bool done = false;
+    if (done) return;
+    done = true;
+    for (const void* f : {reinterpret_cast<const void*>(&k32_sdiag), reinterpret_cast<const void*>(&k32_supd),
+                          reinterpret_cast<const void*>(&k32_sstep)})
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    for (const void* f : {reinterpret_cast<const void*>(&k64_kmat<4>), reinterpret_cast<const void*>(&k64_kmat<8>),
+                          reinterpret_cast<const void*>(&k64_kmat<12>), reinterpret_cast<const void*>(&k64_kmat<16>),
+                          reinterpret_cast<const void*>(&k64_kmat<20>), reinterpret_cast<const void*>(&k64_kmat<24>),
+                          reinterpret_cast<const void*>(&k64_kmat<28>), reinterpret_cast<const void*>(&k64_kmat<32>)})
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)KMAT_SMEM);
+}
+
+static void kmat(const float* X1, long ldx1, int n1, const float* X2, long ldx2, int n2, int D, const double* theta,
+                 int add_noise, const double* C, long ldc, const float* Y, long ldy, double* out, long ldo,
+                 float* out32, long ldo32, int p, hipStream_t s) {
+    KmatArgs k{X1, ldx1, n1, X2, ldx2, n2, D, theta, add_noise, C, ldc, Y, ldy, out, ldo, out32, ldo32, p,
+               (p + KM_Q - 1) / KM_Q};
+    const dim3 g(((n1 + KM_R - 1) / KM_R) * k.tq);
+    switch ((D + 3) & ~3) {
+        case 4: hipLaunchKernelGGL(k64_kmat<4>, g, dim3(256), KMAT_SMEM, s, k); break;
+        case 8: hipLaunchKernelGGL(k64_kmat<8>, g, dim3(256), KMAT_SMEM, s, k); break;
+        case 12: hipLaunchKernelGGL(k64_kmat<12>, g, dim3(256), KMAT_SMEM, s, k); break;
+        case 16: hipLaunchKernelGGL(k64_kmat<16>, g, dim3(256), KMAT_SMEM, s, k); break;
+        case 20: hipLaunchKernelGGL(k64_kmat<20>, g, dim3(256), KMAT_SMEM, s, k); break;
+        case 24: hipLaunchKernelGGL(k64_kmat<24>, g, dim3(256), KMAT_SMEM, s, k); break;
+        case 28: hipLaunchKernelGGL(k64_kmat<28>, g, dim3(256), KMAT_SMEM, s, k); break;
+        default: hipLaunchKernelGGL(k64_kmat<32>, g, dim3(256), KMAT_SMEM, s, k); break;
+    }
+}
+
+// after the sweep with a.LT set: alpha0 (r.A64), R (r.R64), W^T rows (r.XB) and the q partials
+// (a.zpart, a.nz workgroups); the Z^T rows of M become alpha0^T
+static void f32_refine_core(const F32Args& a, const F32Refine& r, hipStream_t s) {
+    refine_lds_attributes();
+    const int npad = a.T * TB, ppad = a.Tp * TB;
+    float* Zr = a.M + row_off(a, a.T);
+    f32_bsolve(a, Zr, a.ld, a.Tp, s);                                                  // alpha0^T
+    const dim3 tg((npad / 32) * (ppad / 32));
+    hipLaunchKernelGGL(k_tr3264, tg, dim3(256), 0, s, Zr, a.ld, r.A64, r.ld64, a.n, a.p, npad, ppad, 0);
+    kmat(a.X, a.ldx, a.n, a.X, a.ldx, a.n, a.D, a.theta, 1, r.A64, r.ld64, a.Y, a.ldy, r.R64, r.ld64, nullptr, 0,
+         a.p, s);                                                                          // R = Y - K alpha0
+    hipLaunchKernelGGL(k_tr3264, tg, dim3(256), 0, s, r.XB, a.ld, r.R64, r.ld64, a.n, a.p, npad, ppad, 1);
+    f32_fsolve(a, r.XB, a.ld, a.Tp, s);                                                  // W^T = (L~^-1 R)^T
+}
+
+void launch_f32_refine_lml(const F32Args& a, const F32Refine& r, hipStream_t s) {
+    f32_refine_core(a, r, s);
+    hipLaunchKernelGGL(k_refine_q, dim3(a.nz), dim3(256), 0, s, a.Y, a.ldy, (const double*)r.A64,
+                       (const double*)r.R64, r.ld64, (const float*)r.XB, a.ld, a.n, a.p, a.zpart);
+}
+
+void launch_f32_refine_mean(const F32Args& a, const F32Refine& r, float* mean, long ldm, hipStream_t s) {
+    f32_refine_core(a, r, s);
+    const int npad = a.T * TB, ppad = a.Tp * TB;
+    f32_bsolve(a, r.XB, a.ld, a.Tp, s);                                                  // delta^T = (L~^-T W)^T
+    hipLaunchKernelGGL(k_tr3264, dim3((npad / 32) * (ppad / 32)), dim3(256), 0, s, r.XB, a.ld, r.A64, r.ld64, a.n,
+                       a.p, npad, ppad, 2);                                                // alpha1 = alpha0 + delta
+    kmat(a.Xs, a.ldxs, a.ns, a.X, a.ldx, a.n, a.D, a.theta, 0, r.A64, r.ld64, nullptr, 0, nullptr, 0, mean, ldm,
+         a.p, s);                                                                          // mean = K(X*, X) alpha1
 }
 
 void launch_f32_gram_dense(const float* X1, long ldx1, int n1, const float* X2, long ldx2, int n2, int D,

@@ -172,6 +172,14 @@ struct F32Args {
     double* gpart;                        // [G][T(T+1)/2] gradient partials
     int* cnt;                             // k_reduce_items arrival counter, zeroed by k32_gram
     int upd_slots;                        // lookahead: cap on resident trailing-update workgroups (0: none)
+    float* LT;                            // refinement: L^T tiles (L(r,k)^T at tile (k,r), D_k^T at (k,k)), or nullptr
+};
+// fp64 refinement of the fp32 solve (value-only LML and predict mean, mfgp_set_f32_refine)
+struct F32Refine {
+    double* A64;                          // alpha (Npad x Ppad, fp64)
+    double* R64;                          // R = Y - K alpha (Npad x Ppad, fp64)
+    long ld64;                            // = Ppad
+    float* XB;                            // work rows (Ppad x Npad, fp32, ld = Npad)
 };
 size_t f32_gemm_smem();
 // Diagnostic timing of the fp32 launches (never on the hot path): events around every launch,
@@ -218,6 +226,8 @@ void launch_f32_predict(const F32Args& a, float* mean, long ldm, float* var, hip
 void launch_f32_predict_cov(const F32Args& a, float* cov, long ldc, hipStream_t s);
 void launch_f32_gram_dense(const float* X1, long ldx1, int n1, const float* X2, long ldx2, int n2, int D,
                            const double* theta, float diag_add, float* K, long ldk, hipStream_t s);
+void launch_f32_refine_lml(const F32Args& a, const F32Refine& r, hipStream_t s);
+void launch_f32_refine_mean(const F32Args& a, const F32Refine& r, float* mean, long ldm, hipStream_t s);
 
 size_t gram_smem_bytes(int nb);
 size_t chol_smem_bytes(int nb);

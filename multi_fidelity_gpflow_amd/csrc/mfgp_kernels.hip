@@ -527,45 +527,6 @@ void launch_gram_dense(const GramArgs& g, int batch, int wr1, int wr2, hipStream
     }
 }
 
-// exp of four independent arguments, stage by stage across the four (the compiler lays out
-// four exp() calls as four back-to-back dependent chains, which a wave issues in order).  The
-// same operations and constants as the device library's exp (range reduction by ln 2, degree-11
-// polynomial, ldexp, overflow / underflow selects), so each result is bitwise the library's.
-__device__ __forceinline__ double dbits(unsigned long long u) { return __longlong_as_double((long long)u); }
-#define MFGP_PIN4(v) asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]))
-__device__ __forceinline__ void exp4(double (&x)[4]) {
-    const double C[10] = {dbits(0x3e928af3fca7ab0cull), dbits(0x3ec71dee623fde64ull), dbits(0x3efa01997c89e6b0ull),
-                          dbits(0x3f2a01a014761f6eull), dbits(0x3f56c16c1852b7b0ull), dbits(0x3f81111111122322ull),
-                          dbits(0x3fa55555555502a1ull), dbits(0x3fc5555555555511ull), dbits(0x3fe000000000000bull), 1.0};
-    double n[4], r[4], p[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) n[u] = __builtin_rint(x[u] * dbits(0x3ff71547652b82feull));
-    MFGP_PIN4(n);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) r[u] = fma(dbits(0xbfe62e42fefa39efull), n[u], x[u]);
-    MFGP_PIN4(r);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) r[u] = fma(dbits(0xbc7abc9e3b39803full), n[u], r[u]);
-    MFGP_PIN4(r);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) p[u] = fma(dbits(0x3e5ade156a5dcb37ull), r[u], C[0]);
-    MFGP_PIN4(p);
-#pragma unroll
-    for (int k = 1; k < 10; ++k) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) p[u] = fma(r[u], p[u], C[k]);
-        MFGP_PIN4(p);
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) p[u] = fma(r[u], p[u], 1.0);
-    MFGP_PIN4(p);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const double e = __builtin_ldexp(p[u], (int)n[u]);
-        x[u] = x[u] > 1024.0 ? __builtin_inf() : (x[u] < -1075.0 ? 0.0 : e);
-    }
-}
-
 // ------------------------------------------------------------ K1 flow set-up (LML layout, NB = 32)
 // The Gram launch in front of k_chol_flow, in the k_gram_dense form: workgroup b < nblk computes
 // lower 64 x 64 block b of the padded K + s2 I (row-major, ld = npad; identity on the padded

@@ -161,6 +161,11 @@ class Engine:
         """fp32 path: 128-wide tile columns per outer Cholesky panel (trailing-update K = 128 * tiles)."""
         check(self.lib.mfgp_set_f32_panel(self.h, int(tiles)), "mfgp_set_f32_panel")
 
+    def set_f32_refine(self, enable: bool):
+        """fp32 path: one fp64 refinement step for the value-only LML and the predictive mean
+        (default on; gradients and Adam steps are never refined).  mfgp_set_f32_refine."""
+        check(self.lib.mfgp_set_f32_refine(self.h, 1 if enable else 0), "mfgp_set_f32_refine")
+
     def set_f32_lookahead(self, enable: bool):
         """fp32 path: factor the next panel on a side stream beside the trailing update (default on)."""
         check(self.lib.mfgp_set_f32_lookahead(self.h, 1 if enable else 0), "mfgp_set_f32_lookahead")

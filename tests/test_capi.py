@@ -56,8 +56,14 @@ def test_host_only_entry_points(lib):
     assert lib.mfgp_gpr_workspace_size_ex(h, 0, 1164, 64, 10, C.byref(s64)) == 0
     assert lib.mfgp_gpr_workspace_size(h, 1164, 64, 10, C.byref(sz)) == 0 and s64.value == sz.value
     assert lib.mfgp_gpr_workspace_size_ex(h, 1, 18432, 512, 10, C.byref(s32)) == 0
-    # M = (T + Tp + T) x 128 rows of Npad floats (K, Y^T, identity rows) = 2.76 GB at the Synth config
+    # the value-only refinement layout (default on): M = (T + Tp) x 128 rows + the L^T tiles + fp64
+    # alpha / residual = 2.95 GB at the Synth config; without it, the gradient layout M = (T + Tp + T)
+    # x 128 rows of Npad floats (K, Y^T, identity rows) = 2.76 GB
+    assert 2.9e9 < s32.value < 3.0e9
+    assert lib.mfgp_set_f32_refine(h, 2) == -1 and lib.mfgp_set_f32_refine(h, 0) == 0
+    assert lib.mfgp_gpr_workspace_size_ex(h, 1, 18432, 512, 10, C.byref(s32)) == 0
     assert 2.7e9 < s32.value < 2.9e9
+    assert lib.mfgp_set_f32_refine(h, 1) == 0
     assert lib.mfgp_gpr_workspace_size_ex(h, 2, 1164, 64, 10, C.byref(sz)) == -1     # unknown dtype
     assert lib.mfgp_gpr_lml_ex(h, 1, 0, 1, 1, None, 2, None, 1, None, 0, None, 0, None, None) == -1
     assert lib.mfgp_set_f32_panel(h, 0) == -1 and lib.mfgp_set_f32_panel(h, 6) == 0
