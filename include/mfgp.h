@@ -61,11 +61,11 @@ int mfgp_get_tile(mfgp_handle_t h);
  * (k_chol_flow, default when the device reports its CU count), 0 = one launch per tile step.
  * Results agree to rounding; a workspace must be sized under the setting it is used with. */
 int mfgp_set_flow(mfgp_handle_t h, int enable);   /* 2: flow + diagnostic timeline */
-/* fp32 path (dtype MFGP_F32): one step of iterative refinement with an fp64 residual for the
- * value-only LML (want_grad = 0) and the predictive mean (default 1; 0: plain fp32 solve).  The
- * gradient / Adam calls are never refined.  Workspace sizes follow the setting (size after
+/* fp32 path (dtype MFGP_F32): iterative refinement with an fp64 residual for the value-only LML
+ * (want_grad = 0; one step whenever steps >= 1) and the predictive mean (`steps` steps, 0..2;
+ * default 2; 0: plain fp32 solve).  The gradient / Adam calls are never refined.  Workspace sizes follow the setting (size after
  * setting it).  Replaces nothing in the reference (it computes in fp64: linear.py:63-64). */
-int mfgp_set_f32_refine(mfgp_handle_t h, int enable);
+int mfgp_set_f32_refine(mfgp_handle_t h, int steps);
 int mfgp_get_flow(mfgp_handle_t h);
 /* Bound of every k_chol_flow hand-off wait, in microseconds from the start of that wait
  * (default 50000).  On expiry the launch drains and info = MFGP_FLOW_TIMEOUT: a scheduling

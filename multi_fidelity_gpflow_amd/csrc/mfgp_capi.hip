@@ -30,7 +30,7 @@ struct mfgp_handle_s {
     int f32_panel;  // fp32 path: 128-wide tile columns per outer panel (trailing-update K = 128 * f32_panel)
     int f32_lookahead;          // fp32 sweep: factor the next panel beside the trailing update
     int f32_reserve;            // CUs the capped trailing update leaves to the side stream
-    int f32_refine;             // fp32 value-only LML / predict mean: one fp64 refinement step (mfgp_set_f32_refine)
+    int f32_refine;             // fp32 value-only LML (one step) / predict mean (this many steps): fp64 refinement (mfgp_set_f32_refine)
     hipStream_t side;           // its high-priority side stream + fork / join events (created with the handle)
     hipEvent_t ev_fork, ev_join;
 };
@@ -582,7 +582,7 @@ static int f32_predict(mfgp_handle_t h, int n, int p, int d, int ns, const float
     if (h->f32_lookahead) launch_f32_sweep(a, h->stream, nullptr, h->side, h->ev_fork, h->ev_join);
     else launch_f32_sweep(a, h->stream);
     launch_f32_predict(a, mean, ldm, var, h->stream);   // variance (and the unrefined mean)
-    if (h->f32_refine) launch_f32_refine_mean(a, L.r, mean, ldm, h->stream);
+    if (h->f32_refine) launch_f32_refine_mean(a, L.r, mean, ldm, h->f32_refine, h->stream);
     if (cov) launch_f32_predict_cov(a, cov, ldc, h->stream);
     return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;
 }
@@ -635,8 +635,8 @@ int mfgp_create(int device, mfgp_handle_t* out) {
     if (const char* d0 = getenv("MFGP_FLOW_D0")) h->flow_d0 = atoi(d0) != 0;
     if (const char* rv = getenv("MFGP_F32_RESERVE")) h->f32_reserve = std::max(0, atoi(rv));
     if (const char* la = getenv("MFGP_F32_LOOKAHEAD")) h->f32_lookahead = atoi(la) != 0;
-    h->f32_refine = 1;
-    if (const char* rf = getenv("MFGP_F32_REFINE")) h->f32_refine = atoi(rf) != 0;
+    h->f32_refine = 2;
+    if (const char* rf = getenv("MFGP_F32_REFINE")) h->f32_refine = std::min(2, std::max(0, atoi(rf)));
     {
         int lo = 0, hi = 0;
         int cur = -1;
@@ -684,7 +684,7 @@ int mfgp_get_tile(mfgp_handle_t h) { return h ? h->nb : MFGP_ERR_ARG; }
 
 int mfgp_set_f32_refine(mfgp_handle_t h, int enable) {
     CHECK_H(h);
-    if (enable < 0 || enable > 1) return MFGP_ERR_ARG;
+    if (enable < 0 || enable > 2) return MFGP_ERR_ARG;
     h->f32_refine = enable;
     return MFGP_OK;
 }

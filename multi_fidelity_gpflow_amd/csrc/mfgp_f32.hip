@@ -1352,12 +1352,21 @@ void launch_f32_refine_lml(const F32Args& a, const F32Refine& r, hipStream_t s) 
                        (const double*)r.R64, r.ld64, (const float*)r.XB, a.ld, a.n, a.p, a.zpart);
 }
 
-void launch_f32_refine_mean(const F32Args& a, const F32Refine& r, float* mean, long ldm, hipStream_t s) {
+void launch_f32_refine_mean(const F32Args& a, const F32Refine& r, float* mean, long ldm, int steps, hipStream_t s) {
     f32_refine_core(a, r, s);
     const int npad = a.T * TB, ppad = a.Tp * TB;
-    f32_bsolve(a, r.XB, a.ld, a.Tp, s);                                                  // delta^T = (L~^-T W)^T
-    hipLaunchKernelGGL(k_tr3264, dim3((npad / 32) * (ppad / 32)), dim3(256), 0, s, r.XB, a.ld, r.A64, r.ld64, a.n,
-                       a.p, npad, ppad, 2);                                                // alpha1 = alpha0 + delta
+    const dim3 tg((npad / 32) * (ppad / 32));
+    for (int it = 0;; ++it) {
+        f32_bsolve(a, r.XB, a.ld, a.Tp, s);                                              // delta^T = (L~^-T W)^T
+        hipLaunchKernelGGL(k_tr3264, tg, dim3(256), 0, s, r.XB, a.ld, r.A64, r.ld64, a.n, a.p, npad, ppad,
+                           2);                                                             // alpha += delta
+        if (it + 1 >= steps) break;
+        // the next step: R = Y - K alpha (fp64), W^T = (L~^-1 R)^T
+        kmat(a.X, a.ldx, a.n, a.X, a.ldx, a.n, a.D, a.theta, 1, r.A64, r.ld64, a.Y, a.ldy, r.R64, r.ld64, nullptr, 0,
+             a.p, s);
+        hipLaunchKernelGGL(k_tr3264, tg, dim3(256), 0, s, r.XB, a.ld, r.R64, r.ld64, a.n, a.p, npad, ppad, 1);
+        f32_fsolve(a, r.XB, a.ld, a.Tp, s);
+    }
     kmat(a.Xs, a.ldxs, a.ns, a.X, a.ldx, a.n, a.D, a.theta, 0, r.A64, r.ld64, nullptr, 0, nullptr, 0, mean, ldm,
          a.p, s);                                                                          // mean = K(X*, X) alpha1
 }

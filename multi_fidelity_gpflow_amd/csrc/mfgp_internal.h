@@ -227,7 +227,7 @@ void launch_f32_predict_cov(const F32Args& a, float* cov, long ldc, hipStream_t 
 void launch_f32_gram_dense(const float* X1, long ldx1, int n1, const float* X2, long ldx2, int n2, int D,
                            const double* theta, float diag_add, float* K, long ldk, hipStream_t s);
 void launch_f32_refine_lml(const F32Args& a, const F32Refine& r, hipStream_t s);
-void launch_f32_refine_mean(const F32Args& a, const F32Refine& r, float* mean, long ldm, hipStream_t s);
+void launch_f32_refine_mean(const F32Args& a, const F32Refine& r, float* mean, long ldm, int steps, hipStream_t s);
 
 size_t gram_smem_bytes(int nb);
 size_t chol_smem_bytes(int nb);

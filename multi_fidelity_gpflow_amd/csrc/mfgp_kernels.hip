@@ -977,6 +977,9 @@ __global__ void k_rhs_init(double* R, long ldr, long sR, int npad, int ppad, con
 // NB = 64 tiles are 33 KB each, so one).
 // After the loop the region is reused: raw rows xi, xj, flags fi, fj, then the
 // per-quad gradient partials R [G][GRAD_RLD] and the inverse squared lengthscales.
+#ifndef GRAD_ABL
+#define GRAD_ABL 0   // diagnostic ablation: 1 no epilogue, 2 no MFMA (tools/grad_variants.py)
+#endif
 template <int NB>
 constexpr int GRAD_NBUF = (NB == 32) ? 2 : 1;
 constexpr int GRAD_RLD = 65;   // 64 quad partials per gradient entry, +1 against bank conflicts
@@ -1112,7 +1115,9 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
             if (nq > 2) MFGP_GRAD_FETCH(ra0, rb0, 2);
             __syncthreads();
             for (int q = 0; q < nq; q += 2) {
+#if GRAD_ABL != 2
                 tile_mma<NB, true, false>(acc, A0, B0, 1.0);
+#endif
                 if (q + 1 < nq) {
                     tile_put<NB>(A1, ra1);
                     tile_put<NB>(B1, rb1);
@@ -1120,7 +1125,9 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
                 }
                 __syncthreads();
                 if (q + 1 < nq) {
+#if GRAD_ABL != 2
                     tile_mma<NB, true, false>(acc, A1, B1, 1.0);
+#endif
                     if (q + 2 < nq) {
                         tile_put<NB>(A0, ra0);
                         tile_put<NB>(B0, rb0);
@@ -1144,6 +1151,10 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
 #undef MFGP_GRAD_FETCH
     }
 
+#if GRAD_ABL == 1   // (NB = 32: the one accumulator block stays live, so no MFMA is dropped)
+    if (threadIdx.x < G) a.gpart[(long)threadIdx.x * gridDim.x + task] = acc.v[0][0];
+    return;
+#endif
     // stage the raw inputs of the two row tiles (operand buffers are free now)
     for (int e = threadIdx.x; e < NB * (a.D + 1); e += NTHREADS) {
         const int r = e / (a.D + 1), d = e % (a.D + 1);

@@ -161,10 +161,12 @@ class Engine:
         """fp32 path: 128-wide tile columns per outer Cholesky panel (trailing-update K = 128 * tiles)."""
         check(self.lib.mfgp_set_f32_panel(self.h, int(tiles)), "mfgp_set_f32_panel")
 
-    def set_f32_refine(self, enable: bool):
-        """fp32 path: one fp64 refinement step for the value-only LML and the predictive mean
-        (default on; gradients and Adam steps are never refined).  mfgp_set_f32_refine."""
-        check(self.lib.mfgp_set_f32_refine(self.h, 1 if enable else 0), "mfgp_set_f32_refine")
+    def set_f32_refine(self, steps):
+        """fp32 path: fp64 iterative refinement of the value-only LML (one step) and the predictive
+        mean (`steps` steps: True / 2 = the default two, 1, False / 0 = off); gradients and Adam
+        steps are never refined.  mfgp_set_f32_refine."""
+        steps = 2 if steps is True else 0 if steps is False else int(steps)
+        check(self.lib.mfgp_set_f32_refine(self.h, steps), "mfgp_set_f32_refine")
 
     def set_f32_lookahead(self, enable: bool):
         """fp32 path: factor the next panel on a side stream beside the trailing update (default on)."""

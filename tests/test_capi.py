@@ -60,7 +60,7 @@ def test_host_only_entry_points(lib):
     # alpha / residual = 2.95 GB at the Synth config; without it, the gradient layout M = (T + Tp + T)
     # x 128 rows of Npad floats (K, Y^T, identity rows) = 2.76 GB
     assert 2.9e9 < s32.value < 3.0e9
-    assert lib.mfgp_set_f32_refine(h, 2) == -1 and lib.mfgp_set_f32_refine(h, 0) == 0
+    assert lib.mfgp_set_f32_refine(h, 3) == -1 and lib.mfgp_set_f32_refine(h, 0) == 0
     assert lib.mfgp_gpr_workspace_size_ex(h, 1, 18432, 512, 10, C.byref(s32)) == 0
     assert 2.7e9 < s32.value < 2.9e9
     assert lib.mfgp_set_f32_refine(h, 1) == 0

@@ -11,9 +11,11 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 sys.path.insert(0, ROOT)
-VDIR = os.path.join(HERE, "variants")
+VDIR = os.path.join(ROOT, "multi_fidelity_gpflow_amd", "variants")   # travels to the GPU box
 VARIANTS = {
     "cur": [],
+    "noepi": ["-DGRAD_ABL=1"],
+    "nomfma": ["-DGRAD_ABL=2"],
 }
 
 
