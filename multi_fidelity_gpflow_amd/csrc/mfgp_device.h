@@ -104,6 +104,27 @@ __device__ __forceinline__ void acc_to_lds(const Acc<NB>& a, double* __restrict_
         for (int r = 0; r < 4; ++r) s[acc_row<NB>(q, r) * S + acc_col<NB>(q)] = a.v[q][r];
 }
 
+// ---------------------------------------------------------------- XCD-aware block order
+// Workgroups are dealt round-robin over the 8 XCDs (8 private L2s), so the tiles of one batch entry
+// (one SVGP latent: its K_uf, L^{-1}, C, ... shared by all its output tiles) land on every XCD and
+// every L2 fetches them.  This remap hands each XCD a contiguous chunk of the logical (x, z) grid
+// (cdna_hip_programming.md T1): dispatch slot b -> logical (b % 8) * cpx + b / 8 for the first
+// 8 * cpx slots (cpx = nwg / 8), the remainder unchanged (a bijection for any grid).  Placement
+// only: every logical block computes the same thing wherever it runs.
+__device__ __forceinline__ void xcd_swizzle(int& x, int& z) {
+    const int gx = gridDim.x;
+    const int nwg = gx * gridDim.z;
+    const int b = blockIdx.x + gx * blockIdx.z;
+    const int cpx = nwg >> 3;
+#ifdef MFGP_NO_XCD_SWIZZLE   // A/B builds only
+    const int s = b;
+#else
+    const int s = b < 8 * cpx ? (b & 7) * cpx + (b >> 3) : b;
+#endif
+    x = s % gx;
+    z = s / gx;
+}
+
 // ---------------------------------------------------------------- tile moves
 // LDS tile (row-major, stride S) <- global tile (row-major, ld).  16-byte moves.
 template <int NB>

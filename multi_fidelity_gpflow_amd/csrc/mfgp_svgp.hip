@@ -101,8 +101,9 @@ __global__ __launch_bounds__(NTHREADS) void k_lqt_linv(const double* Lq, const d
     extern __shared__ __attribute__((aligned(16))) double smem[];
     double* As = smem;
     double* Bs = As + E;
-    const int l = blockIdx.z;
-    const int i = blockIdx.x / Tm, j = blockIdx.x % Tm;
+    int bx, l;
+    xcd_swizzle(bx, l);
+    const int i = bx / Tm, j = bx % Tm;
     const long mp = (long)Tm * NB, mm = mp * mp;
     const double* lq = Lq + l * mm;
     const double* xo = Xo + l * mm;
@@ -130,9 +131,10 @@ __global__ __launch_bounds__(NTHREADS) void k_svgp_cond(const double* Xo, const 
     double* Ks = Ls + E;
     double* As = Ks + E;
     double* red = As + E;   // 3 x 4 x NB
-    const int l = blockIdx.z;
+    int bx, l;
+    xcd_swizzle(bx, l);
     const int Tn = npad / NB;
-    const int i = blockIdx.x / Tn, tn = blockIdx.x % Tn;
+    const int i = bx / Tn, tn = bx % Tn;
     const long mp = (long)Tm * NB, mm = mp * mp;
     const double* xo = Xo + l * mm;
     const double* cc = C + l * mm;

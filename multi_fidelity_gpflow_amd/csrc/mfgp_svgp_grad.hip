@@ -36,8 +36,9 @@ __global__ __launch_bounds__(NTHREADS) void k_bgemm(BgemmArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     double* As = smem;
     double* Bs = As + E;
-    const int b = blockIdx.z;
-    const int ti = blockIdx.x / a.Nt, tj = blockIdx.x % a.Nt;
+    int bx, b;
+    xcd_swizzle(bx, b);
+    const int ti = bx / a.Nt, tj = bx % a.Nt;
     if (a.tril && tj > ti) {   // strictly-upper output tile of a lower-masked product: zeros
         Acc<NB> z;
         acc_zero(z);
@@ -292,8 +293,9 @@ __global__ __launch_bounds__(NTHREADS) void k_kgrad(const double* P1, long ld1, 
     auto sacc = reinterpret_cast<double(*)[16][SC]>(lds_buf);
     __shared__ double wred[NTHREADS / 64][4];
     __shared__ double dsum[2][DC];
-    const int lat = blockIdx.z;
-    const int at = blockIdx.x / nbc, bc = blockIdx.x % nbc;
+    int bx, lat;
+    xcd_swizzle(bx, lat);
+    const int at = bx / nbc, bc = bx % nbc;
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
     const int li = l & 15, lk = l >> 4;
     const MFTheta th{thetas + (long)lat * G, D};
@@ -445,14 +447,14 @@ __global__ __launch_bounds__(NTHREADS) void k_kgrad(const double* P1, long ld1, 
         else if (q == D + 1) v = (wred[0][1] + wred[1][1]) + (wred[2][1] + wred[3][1]);
         else if (q <= 2 * D + 1) v = dsum[1][q - D - 2];
         else if (q == 2 * D + 2) v = (wred[0][2] + wred[1][2]) + (wred[2][2] + wred[3][2]);
-        gth_part[((long)lat * gridDim.x + blockIdx.x) * G + q] = v;   // noise slot (G - 1): 0
+        gth_part[((long)lat * gridDim.x + bx) * G + q] = v;   // noise slot (G - 1): 0
     }
 #pragma unroll
     for (int i = 0; i < (KG_ROWS * DC + NTHREADS - 1) / NTHREADS; ++i) {
         const int e = t + NTHREADS * i;
         const int r = e & (KG_ROWS - 1), d = e / KG_ROWS;
         const int ag = at * KG_ROWS + r;
-        if (d < D) gz_part[(((long)lat * gridDim.x + blockIdx.x) * KG_ROWS + r) * D + d] = (ag < n1) ? zf * gzv[i] : 0.0;
+        if (d < D) gz_part[(((long)lat * gridDim.x + bx) * KG_ROWS + r) * D + d] = (ag < n1) ? zf * gzv[i] : 0.0;
     }
 }
 
