@@ -797,7 +797,8 @@ __global__ __launch_bounds__(NTHREADS) void k_chol_step(CholArgs a) {
     double* dg = Pj + E;         // NB
     int& bad = *reinterpret_cast<int*>(dg + NB);
 
-    const int b = blockIdx.z;
+    int t, b;   // task t of system b (XCD-aware order: a run of systems per XCD, mfgp_device.h)
+    xcd_swizzle(t, b);
     const int k = a.k, T = a.T, Tp = a.Tp;
     double* A = a.A + b * a.sA;
     double* R = a.R + b * a.sR;
@@ -811,7 +812,6 @@ __global__ __launch_bounds__(NTHREADS) void k_chol_step(CholArgs a) {
     const int nA = rem * (rem + 1) / 2;
     const int ncol = k + 1 + Tp;               // active RHS column tiles
     const int nR = rem * ncol;
-    int t = blockIdx.x;
 
     tile_load<NB>(Ds, a.Dd + b * a.sD + (long)k * NB * NB, NB);
 
