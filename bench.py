@@ -76,6 +76,14 @@ def load_goku():
     return multifidelity_training_set(ps)
 
 
+def bcast_label(world):
+    """How the inputs reached this rank (the `data` field of the JSON line)."""
+    if world == 1:
+        return "read on the one rank"
+    backend = os.environ.get("MFGP_DIST_BACKEND", "nccl")
+    return ("RCCL" if backend == "nccl" else backend) + "-broadcast from rank 0"
+
+
 def broadcast_inputs(rank, world, device):
     """Rank 0 reads the txt files; one RCCL broadcast of the packed inputs."""
     from multi_fidelity_gpflow_amd.distributed import broadcast_arrays
@@ -361,7 +369,7 @@ def bench_svgp(args):
             "value": leg.pop("iters_per_s"), "unit": "iters/s", "n_gpus": world, "steps": leg.pop("steps"),
             "warmup": leg.pop("warmup"), "ms_per_step": leg.pop("ms_per_step"), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "Goku z=0 P(k) (reference data files, tests/golden/data), RCCL-broadcast from rank 0",
+            "data": "Goku z=0 P(k) (reference data files, tests/golden/data), " + bcast_label(world),
             "config": cfg,
         }
         line.update(leg)
@@ -623,7 +631,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32" if synth else "f64",
             "data": ("synthetic (SURVEY §8(d) recipe, seed 20251015), built on every rank" if synth else
-                     "Goku z=0 P(k) (reference data files, tests/golden/data), RCCL-broadcast from rank 0"),
+                     "Goku z=0 P(k) (reference data files, tests/golden/data), " + bcast_label(world)),
             "config": {"workload": "synth_multibin_adam_step" if synth else "goku_multibin_adam_step",
                        "n_lf": int((X[:, -1] == 0).sum()), "n_hf": int((X[:, -1] == 1).sum()), "d": d, "p": P,
                        "bins_per_rank": Yr.shape[1], "tile": eng.tile(),
