@@ -124,7 +124,7 @@ def roofline(model, n, p, d, reps=10, pmc=True):
         "chol_steps": n ** 3 / 3 + n ** 3 / 3 + n * n * p + n * n * p,
         "grad": n ** 3 / 3 + n * n * p + n * (n + 1) / 2 * (4 * d + 10),
     }
-    flow = eng.flow() and nb == 32    # one persistent k_chol_flow launch, else T k_chol_step launches
+    flow = eng.flow_runs(n)    # one persistent k_chol_flow launch, else T k_chol_step launches
     launches = {"gram": 1, "chol_steps": 1 if flow else T, "grad": 1}
     dom = max(flops, key=lambda k: ms[names.index(k)])
     t_ms = ms[names.index(dom)]

@@ -58,9 +58,11 @@ int mfgp_set_stream(mfgp_handle_t h, void* hip_stream);
 int mfgp_set_tile(mfgp_handle_t h, int nb);
 int mfgp_get_tile(mfgp_handle_t h);
 /* Cholesky schedule of the LML path (tile 32): 1 = one persistent dataflow launch
- * (k_chol_flow, default when the device reports its CU count), 0 = one launch per tile step.
+ * (k_chol_flow, default when the device reports its CU count) for factorizations of 8 or more
+ * 32-tiles (smaller ones are faster as step launches), 3 = the flow at every size, 0 = one launch
+ * per tile step.  mfgp_get_flow returns the mode (0, 1 or 3).
  * Results agree to rounding; a workspace must be sized under the setting it is used with. */
-int mfgp_set_flow(mfgp_handle_t h, int enable);   /* 2: flow + diagnostic timeline */
+int mfgp_set_flow(mfgp_handle_t h, int enable);   /* 2: flow + diagnostic timeline; 3: flow at every size */
 /* fp32 path (dtype MFGP_F32): iterative refinement with an fp64 residual for the value-only LML
  * (want_grad = 0; one step whenever steps >= 1) and the predictive mean (`steps` steps, 0..2;
  * default 2; 0: plain fp32 solve).  The gradient / Adam calls are never refined.  Workspace sizes follow the setting (size after

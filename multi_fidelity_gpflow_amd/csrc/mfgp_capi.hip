@@ -21,6 +21,7 @@ struct mfgp_handle_s {
     int nb;
     int grad_chunk;
     int flow_wgs;   // k_chol_flow grid (one workgroup per CU); 0: launch-per-step Cholesky
+    int flow_min_t; // fewest 32-tiles a factorization needs to take the flow (below: the step launches)
     int ncu;        // compute units of the device
     int gram_wgs;   // k_gram tile workgroups, LML layout (0: one per CU; < 0: one per tile; MFGP_GRAM_WGS)
     int gram_legacy;   // flow path: the looping k_gram instead of k_gram_flow (MFGP_GRAM_LEGACY, A/B only)
@@ -72,13 +73,14 @@ struct GprLayout {
 
 // The persistent Cholesky needs every workgroup resident (one per CU) and the owner table
 // to hold every tile; otherwise the launch-per-step sequence runs.
-static int flow_grid(int nb, int T, int Tp, int flow_wgs) {
-    if (nb != 32 || flow_wgs < 2 || T > 255) return 0;
+static int flow_grid(int nb, int T, int Tp, int flow_wgs, int min_t) {
+    if (nb != 32 || flow_wgs < 2 || T > 255 || T < min_t) return 0;
     if (flow_ntiles(T, Tp) > FLOW_WAVES * (flow_wgs - 1) * FLOW_MAXOWN) return 0;
     return flow_wgs;
 }
 
-static GprLayout gpr_layout(int nb, int n, int p, int d, void* ws, int grad_chunk, int nlf = 0, int flow_wgs = 0) {
+static GprLayout gpr_layout(int nb, int n, int p, int d, void* ws, int grad_chunk, int nlf = 0, int flow_wgs = 0,
+                            int flow_min_t = 0) {
     GprLayout L;
     L.nb = nb;
     L.T = ceil_div(n, nb);
@@ -102,7 +104,7 @@ static GprLayout gpr_layout(int nb, int n, int p, int d, void* ws, int grad_chun
     L.ncnt = 1;
     L.cnt = c.take<int>((size_t)L.ncnt);
     L.gorder = c.take<int>((size_t)L.ng + SCHED_KEY);
-    L.flow_wgs = flow_grid(nb, L.T, L.Tp, flow_wgs);
+    L.flow_wgs = flow_grid(nb, L.T, L.Tp, flow_wgs, flow_min_t);
     L.nflags = L.flow_wgs ? flow_nflags(L.T, L.Tp) : 0;
     L.flags = c.take<int>((size_t)L.nflags * FLOW_FSTRIDE);
     L.npub = L.flow_wgs ? flow_npub(L.T, L.Tp) : 0;
@@ -115,6 +117,12 @@ static GprLayout gpr_layout(int nb, int n, int p, int d, void* ws, int grad_chun
 }
 
 static inline hipError_t last() { return hipGetLastError(); }
+
+// Below this many 32-tiles the launch-per-step Cholesky is faster than the persistent flow (one
+// 256-workgroup launch costs more than a few short step launches): fp64 value+grad evaluation,
+// flow vs steps (tools/flow_threshold.py): T = 2: 67.5 vs 56.8 us, T = 5: 83.2 vs 79.7, T = 7:
+// 95.3 vs 96.2, T = 9: 106.2 vs 110.6, T = 24: 195.9 vs 247.1.
+constexpr int FLOW_MIN_TILES = 8;
 
 // ---------------------------------------------------------------- device-wide flow fence
 // k_chol_flow needs every CU: two flows whose workgroups interleave (launched on two streams
@@ -202,7 +210,7 @@ template <int NB>
 static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X, int ldx, const double* Y, int ldy,
                           double* theta, int want_grad, void* ws, size_t ws_bytes, double* out, int* info,
                           const FinArgs* adam, PhaseMarks* pm = nullptr, int nlf = 0) {
-    const GprLayout L = gpr_layout(NB, n, p, d, ws, h->grad_chunk, nlf, h->flow_wgs);
+    const GprLayout L = gpr_layout(NB, n, p, d, ws, h->grad_chunk, nlf, h->flow_wgs, h->flow_min_t);
     if (ws_bytes < L.bytes) return MFGP_ERR_WORKSPACE;
     if (L.G > FIN_MAXG) return MFGP_ERR_ARG;   // finalize_body stages theta in LDS
     hipStream_t s = h->stream;
@@ -623,6 +631,7 @@ int mfgp_create(int device, mfgp_handle_t* out) {
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 0;
     h->ncu = ncu;
     h->flow_wgs = ncu;
+    h->flow_min_t = FLOW_MIN_TILES;
     h->flow_timeout = FLOW_TIMEOUT_TICKS;
     h->f32_panel = 6;
     h->f32_lookahead = 1;
@@ -691,9 +700,10 @@ int mfgp_set_f32_refine(mfgp_handle_t h, int enable) {
 
 int mfgp_set_flow(mfgp_handle_t h, int enable) {
     CHECK_H(h);
-    if (enable < 0 || enable > 2) return MFGP_ERR_ARG;
+    if (enable < 0 || enable > 3) return MFGP_ERR_ARG;
     h->flow_wgs = enable ? h->ncu : 0;
     h->flow_trace = enable == 2;
+    h->flow_min_t = enable == 3 ? 0 : FLOW_MIN_TILES;
     return MFGP_OK;
 }
 
@@ -702,7 +712,7 @@ int mfgp_gpr_flow_trace(mfgp_handle_t h, int n, int p, int d, size_t* offset, in
     CHECK_D(d);
     if (n < 1 || p < 1 || !offset || !count) return MFGP_ERR_ARG;
     char* const base = reinterpret_cast<char*>((uintptr_t)1 << 20);   // any 256-B aligned stand-in
-    const GprLayout L = gpr_layout(h->nb, n, p, d, base, h->grad_chunk, 0, h->flow_wgs);
+    const GprLayout L = gpr_layout(h->nb, n, p, d, base, h->grad_chunk, 0, h->flow_wgs, h->flow_min_t);
     *offset = (size_t)(reinterpret_cast<char*>(L.trace) - base);
     *count = L.ntrace;
     return MFGP_OK;
@@ -715,7 +725,7 @@ int mfgp_set_flow_timeout_us(mfgp_handle_t h, long long us) {
     return MFGP_OK;
 }
 
-int mfgp_get_flow(mfgp_handle_t h) { return h ? (h->flow_wgs > 0 ? 1 : 0) : MFGP_ERR_ARG; }
+int mfgp_get_flow(mfgp_handle_t h) { return h ? (h->flow_wgs > 0 ? (h->flow_min_t ? 1 : 3) : 0) : MFGP_ERR_ARG; }
 
 int mfgp_flow_fence(mfgp_handle_t h, int op) {
     CHECK_H(h);
@@ -790,7 +800,7 @@ int mfgp_gmf_gpr_workspace_size(mfgp_handle_t h, int nlf, int n, int p, int d, s
     CHECK_D(d);
     CHECK_LF(nlf);
     if (n < 1 || p < 1 || !bytes) return MFGP_ERR_ARG;
-    *bytes = gpr_layout(h->nb, n, p, d, nullptr, h->grad_chunk, nlf, h->flow_wgs).bytes;
+    *bytes = gpr_layout(h->nb, n, p, d, nullptr, h->grad_chunk, nlf, h->flow_wgs, h->flow_min_t).bytes;
     return MFGP_OK;
 }
 
@@ -836,7 +846,7 @@ int mfgp_gpr_workspace_size(mfgp_handle_t h, int n, int p, int d, size_t* bytes)
     CHECK_H(h);
     CHECK_D(d);
     if (n < 1 || p < 1 || !bytes) return MFGP_ERR_ARG;
-    *bytes = gpr_layout(h->nb, n, p, d, nullptr, h->grad_chunk, 0, h->flow_wgs).bytes;
+    *bytes = gpr_layout(h->nb, n, p, d, nullptr, h->grad_chunk, 0, h->flow_wgs, h->flow_min_t).bytes;
     return MFGP_OK;
 }
 

@@ -120,11 +120,19 @@ class Engine:
         check(self.lib.mfgp_set_tile(self.h, nb), "mfgp_set_tile")
 
     def flow(self) -> bool:
-        return self.lib.mfgp_get_flow(self.h) == 1
+        return self.lib.mfgp_get_flow(self.h) in (1, 3)
 
-    def set_flow(self, enable: bool):
-        """Cholesky schedule of the LML path: persistent dataflow launch (True) or one launch per step."""
-        check(self.lib.mfgp_set_flow(self.h, 1 if enable else 0), "mfgp_set_flow")
+    FLOW_MIN_TILES = 8   # mfgp_capi.hip: below this many 32-tiles mode 1 runs the step launches
+
+    def flow_runs(self, n: int) -> bool:
+        """Whether an n-point fp64 factorization takes the persistent flow under the current mode."""
+        mode = self.lib.mfgp_get_flow(self.h)
+        return self.tile() == 32 and (mode == 3 or (mode == 1 and -(-n // 32) >= self.FLOW_MIN_TILES))
+
+    def set_flow(self, enable: bool, any_size: bool = False):
+        """Cholesky schedule of the LML path: persistent dataflow launch (True; for factorizations of
+        8 or more 32-tiles unless any_size) or one launch per step (False)."""
+        check(self.lib.mfgp_set_flow(self.h, (3 if any_size else 1) if enable else 0), "mfgp_set_flow")
 
     def set_flow_timeout_us(self, us: int):
         """Bound of every k_chol_flow hand-off wait (default 50000 us; 0: diagnostic abort path)."""

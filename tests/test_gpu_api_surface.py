@@ -261,3 +261,22 @@ def test_gpr_independent_of_workspace_contents(goku, eng, flow):
     np.testing.assert_array_equal(got[1], ref[1])
     np.testing.assert_array_equal(mg.numpy(), mref.numpy())
     np.testing.assert_array_equal(vg.numpy(), vref.numpy())
+
+
+def test_flow_size_threshold(eng):
+    """mfgp_set_flow(1) (the default) takes the persistent flow only for factorizations of 8 or more
+    32-tiles (smaller ones are faster as step launches, tools/flow_threshold.py); mode 3 takes it at
+    every size.  Observed through the workspace size, which holds the flow's publication area only
+    when the flow runs."""
+    try:
+        sizes = {}
+        for mode, kw in (("steps", dict(enable=False)), ("auto", dict(enable=True)),
+                         ("any", dict(enable=True, any_size=True))):
+            eng.set_flow(**kw)
+            sizes[mode] = (eng.gpr_workspace_bytes(53, 49, 5), eng.gpr_workspace_bytes(1164, 64, 10))
+        assert eng.flow()
+    finally:
+        eng.set_flow(True)
+    small, large = 0, 1
+    assert sizes["auto"][small] == sizes["steps"][small] < sizes["any"][small]   # HBS: T = 2
+    assert sizes["auto"][large] == sizes["any"][large] > sizes["steps"][large]   # Goku: T = 37
