@@ -242,6 +242,8 @@ void launch_chol_flow(const FlowArgs& a, int nwg, hipStream_t s);
 
 // LML layout (padded) or graph kernel: k_gram; dense layout of the linear MF / RBF kernel: k_gram_dense
 template <int NB> void launch_gram(const GramArgs& g, int nblocks, int batch, hipStream_t s);
+template <int NB> void launch_first_factor(const double* A, long lda, long sA, double* Dd, long sD, double* ldiag,
+                                           long sL, int* info, int batch, hipStream_t s);
 // dense layout, write extents wr1 x wr2 (>= n1 x n2; the excess is written 0.0)
 void launch_gram_dense(const GramArgs& g, int batch, int wr1, int wr2, hipStream_t s);
 void launch_gram_flow(const GramArgs& g, int extra, hipStream_t s);   // set-up launch of k_chol_flow

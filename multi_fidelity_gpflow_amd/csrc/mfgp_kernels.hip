@@ -204,7 +204,10 @@ __device__ __attribute__((noinline)) void gram_first_factor(double* tile, double
     if (threadIdx.x == 0) *info = *bad;   // first writer of info in the sequence: initialises it
 }
 
-template <int NB>
+// LEAN: no fused first factor and no set-up workgroups (a.Dd, a.gorder, a.fown unused): the
+// factor call's register demand (noinline, but it still sets the kernel's allocation) is left out,
+// which lifts the occupancy of the many small tile workgroups of the batched SVGP K_uu launch.
+template <int NB, bool LEAN>
 __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
     constexpr int S = TileCfg<NB>::S;
     extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -227,13 +230,13 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
 
     const int b = blockIdx.z;
     const long long dbg_t0 = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
-    if (a.gorder && blockIdx.x == gridDim.x - 1) {   // extra workgroup: k_grad task order
+    if (!LEAN && a.gorder && blockIdx.x == gridDim.x - 1) {   // extra workgroup: k_grad task order
         if (b == 0) build_grad_order(a.gT, a.gchunk, a.gTp, a.gorder, reinterpret_cast<int*>(smem));
         if (a.dbg && threadIdx.x == 0) a.dbg[3 * blockIdx.x + 2] = __builtin_amdgcn_s_memrealtime() - dbg_t0;
         gram_fill_pub(a);
         return;
     }
-    if (a.fown && blockIdx.x == gridDim.x - 1 - (a.gorder ? 1 : 0)) {   // extra: flow owner table
+    if (!LEAN && a.fown && blockIdx.x == gridDim.x - 1 - (a.gorder ? 1 : 0)) {   // extra: flow owner table
         if (b == 0) build_flow_owner(a.npad / NB, a.ppad / NB, a.fW, a.fown, a.fflags, a.nfflags,
                                      reinterpret_cast<int*>(smem));
         if (a.dbg && threadIdx.x == 0) a.dbg[3 * blockIdx.x + 2] = __builtin_amdgcn_s_memrealtime() - dbg_t0;
@@ -389,8 +392,9 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
     __syncthreads();
     if (a.dbg && threadIdx.x == 0) a.dbg[3 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - dbg_t0;
     tile_store<NB>(out + (long)ti * NB * a.ldo + tj * NB, a.ldo, tile);
-    if (a.Dd != nullptr && ti == 0 && tj == 0)
-        gram_first_factor<NB>(tile, rtile, dg, &bad, a.Dd + b * a.sD, a.ldiag + b * a.sL, a.info + b);
+    if constexpr (!LEAN)
+        if (a.Dd != nullptr && ti == 0 && tj == 0)
+            gram_first_factor<NB>(tile, rtile, dg, &bad, a.Dd + b * a.sD, a.ldiag + b * a.sL, a.info + b);
     }   // tiles of this workgroup
     gram_copy_y<NB>(a);
     gram_fill_pub(a);
@@ -1562,7 +1566,31 @@ __global__ void k_selftest_mfma(double* out /* 16x16 */) {
 template <int NB>
 void launch_gram(const GramArgs& g, int nblocks, int batch, hipStream_t s) {
     if (!g.padded && !g.nlf) { launch_gram_dense(g, batch, 0, 0, s); return; }
-    hipLaunchKernelGGL(k_gram<NB>, dim3(nblocks, 1, batch), dim3(NTHREADS), gram_smem_bytes(NB), s, g);
+    if (g.Dd == nullptr && g.gorder == nullptr && g.fown == nullptr)
+        hipLaunchKernelGGL((k_gram<NB, true>), dim3(nblocks, 1, batch), dim3(NTHREADS), gram_smem_bytes(NB), s, g);
+    else
+        hipLaunchKernelGGL((k_gram<NB, false>), dim3(nblocks, 1, batch), dim3(NTHREADS), gram_smem_bytes(NB), s, g);
+}
+// The first diagonal factor of a batch of padded matrices (step "-1" of the tile Cholesky; the
+// lean Gram launch leaves it out): A_b(0,0) -> D_0, diag(L) 0..NB-1, info_b.
+template <int NB>
+__global__ __launch_bounds__(NTHREADS) void k_first_factor(const double* A, long lda, long sA, double* Dd, long sD,
+                                                           double* ldiag, long sL, int* info) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    constexpr int E = TileCfg<NB>::ELEMS;
+    double* tile = smem;
+    double* rtile = tile + E;
+    double* dg = rtile + E;
+    int* bad = reinterpret_cast<int*>(dg + NB);
+    const int b = blockIdx.z;
+    tile_load<NB>(tile, A + b * sA, lda);
+    gram_first_factor<NB>(tile, rtile, dg, bad, Dd + b * sD, ldiag + b * sL, info + b);
+}
+template <int NB>
+void launch_first_factor(const double* A, long lda, long sA, double* Dd, long sD, double* ldiag, long sL, int* info,
+                         int batch, hipStream_t s) {
+    hipLaunchKernelGGL(k_first_factor<NB>, dim3(1, 1, batch), dim3(NTHREADS),
+                       sizeof(double) * (2 * TileCfg<NB>::ELEMS + NB + 2), s, A, lda, sA, Dd, sD, ldiag, sL, info);
 }
 template <int NB>
 void launch_chol_steps(CholArgs c, int batch, hipStream_t s) {
@@ -1590,6 +1618,8 @@ void launch_pred(const PredAArgs& pa, const PredOutArgs& po, int T, hipStream_t 
 }
 
 template void launch_gram<32>(const GramArgs&, int, int, hipStream_t);
+template void launch_first_factor<32>(const double*, long, long, double*, long, double*, long, int*, int, hipStream_t);
+template void launch_first_factor<64>(const double*, long, long, double*, long, double*, long, int*, int, hipStream_t);
 template void launch_gram<64>(const GramArgs&, int, int, hipStream_t);
 template void launch_chol_steps<32>(CholArgs, int, hipStream_t);
 template void launch_chol_steps<64>(CholArgs, int, hipStream_t);
