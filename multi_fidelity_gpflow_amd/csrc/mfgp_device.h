@@ -105,7 +105,7 @@ __device__ __forceinline__ void acc_to_lds(const Acc<NB>& a, double* __restrict_
 }
 
 // ---------------------------------------------------------------- XCD-aware block order
-// Workgroups are dealt round-robin over the 8 XCDs (8 private L2s), so the tiles of one batch entry
+// For (gx, 1, gz) grids.  Workgroups are dealt round-robin over the 8 XCDs (8 private L2s), so the tiles of one batch entry
 // (one SVGP latent: its K_uf, L^{-1}, C, ... shared by all its output tiles) land on every XCD and
 // every L2 fetches them.  This remap hands each XCD a contiguous chunk of the logical (x, z) grid
 // (cdna_hip_programming.md T1): dispatch slot b -> logical (b % 8) * cpx + b / 8 for the first

@@ -1,7 +1,10 @@
 // Diagnostic: the NB = 32 diagonal factor + inverse as two 16 x 16 single-wave factors (w16) and
 // the 16 x 16 products between them (L21 = A21 D11^T, A22 -= L21 L21^T, D21 = -D22 L21 D11), against
 // the library's single-wave 32 x 32 factor (tile_potrf_inv_w1_wave).  Timing (s_memtime clocks) and
-// max error of D = L^{-1} and L_ii against a long-double host factorisation.
+// max error of D = L^{-1} and L_ii against a long-double host factorisation.  Also an 8-pivot-a-round
+// single-wave factor (w8): its elimination (L_ii) is right, its inverse (R work) is not -- it was
+// kept as a timing-only probe once the elimination alone measured slower than the library's
+// whole factor.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
