@@ -3,8 +3,8 @@
 // the library's single-wave 32 x 32 factor (tile_potrf_inv_w1_wave).  Timing (s_memtime clocks) and
 // max error of D = L^{-1} and L_ii against a long-double host factorisation.  Also an 8-pivot-a-round
 // single-wave factor (w8): its elimination (L_ii) is right, its inverse (R work) is not -- it was
-// kept as a timing-only probe once the elimination alone measured slower than the library's
-// whole factor.
+// kept as a timing-only probe once it measured slower (10.5k clocks) than the library's whole
+// 4-pivot factor (8.2k).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
