@@ -80,7 +80,10 @@ int mfgp_set_flow_timeout_us(mfgp_handle_t h, long long us);
  * previous flow on the device (any handle, stream or host thread of the process) and becomes the
  * last one.  A captured graph's flows are not fenced at capture: before replaying such a graph
  * call mfgp_flow_fence(h, MFGP_FENCE_WAIT) on the replay stream, and after enqueueing the replay
- * mfgp_flow_fence(h, MFGP_FENCE_RECORD).  Stream-ordered only (no host synchronisation). */
+ * mfgp_flow_fence(h, MFGP_FENCE_RECORD).  Between the two the calling host thread holds the
+ * fence: a flow launch or fence call from another host thread blocks on the host until the
+ * RECORD (so it cannot land beside the replay's unfenced flows); the holder's own calls pass.
+ * Device ordering is stream-ordered only (no device synchronisation). */
 #define MFGP_FENCE_WAIT 0
 #define MFGP_FENCE_RECORD 1
 int mfgp_flow_fence(mfgp_handle_t h, int op);

@@ -8,7 +8,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <condition_variable>
 #include <mutex>
+#include <thread>
 
 #include "../../include/mfgp.h"
 #include "mfgp_device.h"
@@ -132,10 +134,18 @@ constexpr int FLOW_MIN_TILES = 8;
 // (hipStreamWaitEvent), never a host synchronisation.  Inside a stream capture the wait / record
 // are skipped (an event recorded outside a capture cannot be waited on inside it): the caller
 // orders the replay of such a graph with mfgp_flow_fence (the Python sessions do).
+// mfgp_flow_fence(WAIT) .. (RECORD) brackets such a replay and HOLDS the fence in between: a flow
+// launch from another host thread blocks on the host (a condition variable, no device
+// synchronisation) until the holder records, so it cannot be enqueued beside the replay's
+// unfenced flows.  The holding thread itself passes (its eager calls inside the bracket are
+// ordered by their streams as usual).
 struct FlowFence {
     std::mutex mu;
+    std::condition_variable cv;
     hipEvent_t ev = nullptr;
     bool armed = false;
+    bool held = false;
+    std::thread::id holder;
 };
 constexpr int FENCE_MAX_DEVICES = 64;
 static FlowFence g_fence[FENCE_MAX_DEVICES];
@@ -145,26 +155,42 @@ static bool stream_capturing(hipStream_t s) {
     return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
 }
 
-static void fence_wait(int dev, hipStream_t s) {
-    if (dev < 0 || dev >= FENCE_MAX_DEVICES || stream_capturing(s)) return;
-    FlowFence& f = g_fence[dev];
-    std::lock_guard<std::mutex> lk(f.mu);
-    if (f.armed) (void)hipStreamWaitEvent(s, f.ev, 0);
+// with f.mu locked: wait until no other thread holds the fence
+static void fence_enter(FlowFence& f, std::unique_lock<std::mutex>& lk) {
+    const std::thread::id me = std::this_thread::get_id();
+    f.cv.wait(lk, [&] { return !f.held || f.holder == me; });
 }
 
-static void fence_record(int dev, hipStream_t s) {
+static void fence_wait(int dev, hipStream_t s, bool hold = false) {
     if (dev < 0 || dev >= FENCE_MAX_DEVICES || stream_capturing(s)) return;
     FlowFence& f = g_fence[dev];
-    std::lock_guard<std::mutex> lk(f.mu);
+    std::unique_lock<std::mutex> lk(f.mu);
+    fence_enter(f, lk);
+    if (f.armed) (void)hipStreamWaitEvent(s, f.ev, 0);
+    if (hold) {
+        f.held = true;
+        f.holder = std::this_thread::get_id();
+    }
+}
+
+static void fence_record(int dev, hipStream_t s, bool release = false) {
+    if (dev < 0 || dev >= FENCE_MAX_DEVICES || stream_capturing(s)) return;
+    FlowFence& f = g_fence[dev];
+    std::unique_lock<std::mutex> lk(f.mu);
+    fence_enter(f, lk);
     if (!f.ev) {
         int cur = -1;
         (void)hipGetDevice(&cur);
         if (cur != dev) (void)hipSetDevice(dev);
         if (hipEventCreateWithFlags(&f.ev, hipEventDisableTiming) != hipSuccess) f.ev = nullptr;
         if (cur >= 0 && cur != dev) (void)hipSetDevice(cur);
-        if (!f.ev) return;
     }
-    if (hipEventRecord(f.ev, s) == hipSuccess) f.armed = true;
+    if (f.ev && hipEventRecord(f.ev, s) == hipSuccess) f.armed = true;
+    if (release && f.held) {
+        f.held = false;
+        lk.unlock();
+        f.cv.notify_all();
+    }
 }
 
 // k_gram (LML layout) with more lower tiles than CUs: one workgroup per CU, tile (0,0) and its
@@ -230,7 +256,7 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
         const bool order = want_grad && h->grad_chunk + L.Tp < 2048;   // gram LDS holds the histogram
         if (order) { g.gorder = L.gorder; g.gT = L.T; g.gchunk = h->grad_chunk; g.gTp = L.Tp; }
         if (L.flow_wgs) { g.fown = L.own; g.fW = FLOW_WAVES * (L.flow_wgs - 1); g.fflags = L.flags; g.nfflags = L.nflags; g.fpub = L.pub; g.npub = L.npub; }
-        if (L.flow_wgs && h->flow_trace) g.dbg = L.trace + L.ntrace - 3 * 2048;   // k_gram timeline (diagnostic)
+        if (L.flow_wgs && h->flow_trace) g.dbg = L.trace + L.ntrace - flow_gram_dbg_count(L.T);   // k_gram timeline (diagnostic)
         const int extra = (order ? 1 : 0) + (L.flow_wgs ? 1 : 0);
         if (NB == 32 && L.flow_wgs && !nlf && !h->gram_legacy) {
             if (h->flow_d0) g.Dd = nullptr;
@@ -639,9 +665,13 @@ int mfgp_create(int device, mfgp_handle_t* out) {
     h->gram_wgs = 0;
     if (const char* gv = getenv("MFGP_GRAM_WGS")) h->gram_wgs = atoi(gv);
     h->gram_legacy = 0;
-    if (const char* gl = getenv("MFGP_GRAM_LEGACY")) h->gram_legacy = atoi(gl) != 0;
     h->flow_d0 = 0;
+#ifdef MFGP_AB_KNOBS
+    // A/B diagnostics only (a build with -DMFGP_AB_KNOBS, then tools/ab_env.sh): each switches the
+    // production LML to another numerics path, so the shipped library never reads them
+    if (const char* gl = getenv("MFGP_GRAM_LEGACY")) h->gram_legacy = atoi(gl) != 0;
     if (const char* d0 = getenv("MFGP_FLOW_D0")) h->flow_d0 = atoi(d0) != 0;
+#endif
     if (const char* rv = getenv("MFGP_F32_RESERVE")) h->f32_reserve = std::max(0, atoi(rv));
     if (const char* la = getenv("MFGP_F32_LOOKAHEAD")) h->f32_lookahead = atoi(la) != 0;
     h->f32_refine = 2;
@@ -729,8 +759,8 @@ int mfgp_get_flow(mfgp_handle_t h) { return h ? (h->flow_wgs > 0 ? (h->flow_min_
 
 int mfgp_flow_fence(mfgp_handle_t h, int op) {
     CHECK_H(h);
-    if (op == MFGP_FENCE_WAIT) fence_wait(h->device, h->stream);
-    else if (op == MFGP_FENCE_RECORD) fence_record(h->device, h->stream);
+    if (op == MFGP_FENCE_WAIT) fence_wait(h->device, h->stream, true);
+    else if (op == MFGP_FENCE_RECORD) fence_record(h->device, h->stream, true);
     else return MFGP_ERR_ARG;
     return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;
 }

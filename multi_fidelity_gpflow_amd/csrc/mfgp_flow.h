@@ -6,6 +6,12 @@
 
 namespace mfgp {
 
+// k_gram timeline of a trace-mode call (diagnostic): [3 G] per-workgroup stamps, then [2 G] staging
+// stamps at 3 gridDim.x; G bounds the grid of both set-up Grams (k_gram_flow: nb(nb+1)/2 blocks
+// of 64 + factor + two set-up workgroups; the looping k_gram: at most T(T+1)/2 tiles + two).
+__host__ __device__ inline int flow_gram_dbg_wgs(int T) { return T * (T + 1) / 2 + 4; }
+__host__ __device__ inline int flow_gram_dbg_count(int T) { return 5 * flow_gram_dbg_wgs(T); }
+
 // ---------------------------------------------------------------- tile catalogue
 // code = type << 20 | i << 10 | j ; R tiles use j = column tile c in [0, T + Tp)
 enum : int { FT_A = 0, FT_R = 1, FT_AL = 2, FT_H = 3 };   // FT_H: coupling H_k = D_k L(k,k-1)

@@ -672,10 +672,12 @@ __device__ __forceinline__ void flow_worker(FlowCtx& C, int wid, double* S) {
 // Buffers are double-buffered by step parity.
 struct DiagLds {
     // LDS carve (doubles): Db[2] | Ls[2] | Ap[2] | Cp[2] | L2[2] (NB x S each) | fsc (32 x 33) | dg[2][32]
-    // | bad[2] | words.  Parity-indexed buffers are computed, not held in pointer arrays (a
-    // dynamically indexed pointer array lands in scratch).
+    // | bad[2] | words | pan[2] (8 x 128: the factor's round panels) | dpv[2] (128).  Parity-indexed
+    // buffers are computed, not held in pointer arrays (a dynamically indexed pointer array lands
+    // in scratch).
     double* base;
     static constexpr int E = TileCfg<32>::ELEMS;
+    static constexpr int PAN = 10 * E + 32 * 33 + 64 + 16;   // after the words
     __device__ double* Db(int q) const { return base + q * E; }        // D_k (stride S)
     __device__ double* Ls(int q) const { return base + (2 + q) * E; }  // L(k,k-1)
     __device__ double* Ap(int q) const { return base + (4 + q) * E; }  // A''(k,k-1)
@@ -685,8 +687,24 @@ struct DiagLds {
     __device__ double* dg(int q) const { return base + 10 * E + 32 * 33 + 32 * q; }
     __device__ int* bad() const { return reinterpret_cast<int*>(base + 10 * E + 32 * 33 + 64); }
     __device__ int* w() const { return bad() + 2; }
+    __device__ double* pan(int q) const { return base + PAN + 1024 * q; }
+    __device__ double* dpv(int q) const { return base + PAN + 2048 + 128 * q; }
+    static constexpr size_t BYTES = sizeof(double) * (PAN + 2048 + 256);
 };
-enum { DW_LS = 0, DW_D, DW_LPUB, DW_DPUB, DW_PRE6, DW_PRE7, DW_BAR, DW_L2, DW_P2, DW_N };
+static_assert(DiagLds::BYTES <= FLOW_LDS_BYTES, "diag workgroup LDS carve");
+enum { DW_LS = 0, DW_D, DW_LPUB, DW_DPUB, DW_PRE6, DW_PRE7, DW_BAR, DW_L2, DW_P2, DW_PROG, DW_N };
+static_assert(DW_N <= 28, "progress words fit before the panels");
+
+// The diagonal factor of a chain step is split over two waves (tile_elim_w1_wave /
+// tile_rinv_w1_wave, mfgp_device.h): wave 0 eliminates, chain wave FLOW_RWAVE forms D_k from the
+// published round panels (its SIMD is shared with one band helper, so it raises its issue
+// priority while it runs).  FLOW_RWAVE = 0: the fused single-wave factor on wave 0.
+#ifndef FLOW_RWAVE
+#define FLOW_RWAVE 1
+#endif
+#ifndef FLOW_RPRIO
+#define FLOW_RPRIO 2
+#endif
 
 __device__ __forceinline__ int lds_get(const int* p) {
     return __hip_atomic_load(const_cast<int*>(p), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -778,12 +796,25 @@ __device__ __forceinline__ void diag_chain(FlowCtx& C, const DiagLds& B) {
         }
         chain_bar(&B.w()[DW_BAR], epoch);
         if (threadIdx.x == 0) lds_put(&B.w()[DW_P2], k);  // tile products of step k done
+#if FLOW_RWAVE
+        if (w == 0) {
+            if (a.trace && threadIdx.x == 0) a.trace[2 * T + k] = flow_clock() - C.t0;
+            tile_elim_w1_wave(B.fsc(), 33, B.pan(pk), &B.w()[DW_PROG], 8 * k);
+        } else if (w == FLOW_RWAVE) {
+            lds_spin_ge(&B.w()[DW_DPUB], k - 2);    // wave 4 is done with Db[pk] (D_{k-2})
+            __builtin_amdgcn_s_setprio(FLOW_RPRIO);
+            tile_rinv_w1_wave(B.pan(pk), &B.w()[DW_PROG], 8 * k, B.dpv(pk), B.Db(pk), B.dg(pk), &B.bad()[pk]);
+            __builtin_amdgcn_s_setprio(0);
+            if (l == 0) lds_put(&B.w()[DW_D], k);
+        }
+#else
         if (w == 0) {
             lds_spin_ge(&B.w()[DW_DPUB], k - 2);    // wave 4 is done with Db[pk] (D_{k-2})
             if (a.trace && threadIdx.x == 0) a.trace[2 * T + k] = flow_clock() - C.t0;
             tile_potrf_inv_w1_wave(B.fsc(), 33, B.fsc(), B.Db(pk), B.dg(pk), &B.bad()[pk]);
             if (l == 0) lds_put(&B.w()[DW_D], k);
         }
+#endif
     }
 }
 
@@ -965,8 +996,9 @@ __global__ __launch_bounds__(FLOW_THREADS) void k_chol_flow(FlowArgs a) {
 
 long flow_npub(int T, int Tp) { return 1024L * (T * (T - 1) / 2 + T + T * (T + 1) / 2 + T * Tp + 4 * T); }
 int flow_nflags(int T, int Tp) { (void)T; (void)Tp; return 1; }   // the abort word
-// layout: chain / helper stamps [8T] | worker summaries + item logs | wave-5 detail [2T] | k_gram [3 x 2048]
-int flow_trace_count(int T, int nwg) { return 8 * T + (3 + 4 * FLOW_LOG) * FLOW_WAVES * (nwg - 1) + 2 * T + 3 * 2048; }
+// layout: chain / helper stamps [8T] | worker summaries + item logs | wave-5 detail [2T] | k_gram timeline
+// [flow_gram_dbg_count(T)] (the last region)
+int flow_trace_count(int T, int nwg) { return 8 * T + (3 + 4 * FLOW_LOG) * FLOW_WAVES * (nwg - 1) + 2 * T + flow_gram_dbg_count(T); }
 
 void launch_chol_flow(const FlowArgs& a, int nwg, hipStream_t s) {
     static bool attr = false;

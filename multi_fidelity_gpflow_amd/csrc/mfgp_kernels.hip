@@ -637,7 +637,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram_flow(GramArgs a, int nblk) {
     const double nL2 = dot_rl<D4>(bl, bl);
     const double nD2 = a.rbf_only ? 0.0 : dot4(sD2 + c * D4, sD2 + c * D4, D4);
     __syncthreads();
-    if (a.dbg && t == 0) { a.dbg[3 * bx] = t0; a.dbg[3072 + 2 * bx + 1] = __builtin_amdgcn_s_memrealtime(); }
+    if (a.dbg && t == 0) { a.dbg[3 * bx] = t0; a.dbg[3 * gridDim.x + 2 * bx + 1] = __builtin_amdgcn_s_memrealtime(); }
     const bool L2 = (f2 == 0.0), H2 = (f2 == 1.0);
     const bool col_ok = fac || gj < a.npad;
     const int w = t >> 6;

@@ -86,8 +86,9 @@ class Engine:
         mfgp_flow_fence).  Two persistent k_chol_flow launches must never share the device: each
         needs every CU resident, and one that cannot get them stalls until its hand-off bound
         expires (a lost step).  The library fences every eager flow launch itself; this block is
-        for graph replays, whose flows were captured unfenced.  Device-side ordering only: no host
-        synchronisation."""
+        for graph replays, whose flows were captured unfenced.  Between WAIT and RECORD this host
+        thread holds the fence: a flow launched from another host thread blocks (on the host) until
+        the block ends.  No device synchronisation."""
         with torch.cuda.stream(stream):
             check(self.lib.mfgp_flow_fence(self.h, _lib.MFGP_FENCE_WAIT), "mfgp_flow_fence")
         try:

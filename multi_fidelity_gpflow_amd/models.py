@@ -143,6 +143,10 @@ class MultiFidelityGPModel(Module):
 
     # ------------------------------------------------------------ GPR surface
     def log_marginal_likelihood(self):
+        """GPR log marginal likelihood.  On the float32 path the value-only call takes one fp64
+        refinement step (mfgp_set_f32_refine), while log_marginal_likelihood_and_grad() and the
+        training steps return the unrefined fp32 value: at the Synth size the two differ by
+        ~8e-4 relative (the refined one is ~5e-5 from fp64).  On float64 they agree to rounding."""
         eng, X, Y = self._device_data()
         theta = torch.tensor(self._theta_map().theta(), dtype=torch.float64, device=eng.device)
         out, info = eng.gpr_lml(X, Y, theta, want_grad=False)
@@ -296,7 +300,10 @@ class AdamSession:
             n, p, d = self.X.shape[0], self.Y.shape[1], self.tm.d
             self.ws = self.eng.private_workspace(self.eng.gpr_workspace_bytes(n, p, d, self.X.dtype))
             self.eng.theta_from_u(self.st.u, self.st.theta, self.tm.noise_index)
-            self.eng.gpr_lml(self.X, self.Y, self.st.theta, want_grad=False, ws=self.ws)   # builds schedule tables
+            # one eager evaluation before any capture: builds the schedule tables and sets every
+            # step kernel's launch attributes; value + gradient, as the step (on the fp32 path a
+            # value-only call would also run the fp64 refinement, which the step never does)
+            self.eng.gpr_lml(self.X, self.Y, self.st.theta, want_grad=True, ws=self.ws)
         self.done = 0
         self.runner = _StepRunner(self._step, chunk if graph else 0)
 

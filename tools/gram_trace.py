@@ -36,8 +36,9 @@ def main():
         eng.gpr_lml(Xd, Yd, th, want_grad=True)
         torch.cuda.synchronize()
         ws = eng._ws["gpr"]
-        g = ws[off.value + 8 * (cnt.value - 3 * 2048): off.value + 8 * cnt.value].view(torch.int64).cpu().numpy()
-        h = g[3072: 3072 + 2 * (nblk + 1)].reshape(-1, 2).astype(np.float64)   # [unused, staged]
+        g = ws[off.value + 8 * (cnt.value - 5 * (T * (T + 1) // 2 + 4)): off.value + 8 * cnt.value].view(torch.int64).cpu().numpy()
+        grid = nblk + 3
+        h = g[3 * grid: 3 * grid + 2 * (nblk + 1)].reshape(-1, 2).astype(np.float64)   # [unused, staged]
         g = g.reshape(-1, 3)[:nblk + 3].astype(np.float64)
         z = g[:, 0].min()
         g = (g - z) / 100.0
