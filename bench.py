@@ -470,6 +470,33 @@ def synth_leg(steps=3, warmup=2):
     return out
 
 
+def shared_theta_leg(X, Yr, steps, warmup, device):
+    """The shared-theta (reference-parity) mode of an N > 1 run: one multi-bin model, each rank
+    its contiguous bin block, one RCCL all-reduce of 1 + G doubles per Adam step
+    (distributed.SharedThetaTrainer, linear.py:200-214 trajectory).  value = model steps / s
+    (strong scaling: the job's total work per step is fixed)."""
+    from multi_fidelity_gpflow_amd.distributed import SharedThetaTrainer
+    world = dist.get_world_size()
+    model = make_model(X, Yr)
+    sess = SharedThetaTrainer(model, 0.1, steps + warmup)
+    sess.run(warmup)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    sess.run(steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    dist.barrier()
+    t = torch.tensor([dt], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    sess.finish()
+    return {"mode": "shared", "scaling": "strong", "steps": steps, "warmup": warmup,
+            "ms_per_step": round(dt / steps * 1e3, 4), "value": round(steps / dt, 3), "unit": "evals/s",
+            "parallelism": f"bins{world}-shared-theta",
+            "collective": "one all-reduce of 1 + G doubles per step (eager launches, no graph replay)"}
+
+
 def dist_device_index() -> int:
     """LOCAL_RANK's GPU.  With fewer visible GPUs than ranks (a rehearsal of the N > 1 path on a
     one-GPU box) ranks share devices round-robin."""
@@ -609,6 +636,13 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             tp = float(t.item())
 
+    # N > 1, shard mode: the reference-parity figure of the same job beside it -- ONE model trained
+    # with the reference's trajectory (SharedThetaTrainer: every rank its bin block, one all-reduce
+    # of 1 + G doubles per step), so a scaling run records both
+    shared_sub = None
+    if world > 1 and args.mode == "shard" and not synth:
+        shared_sub = shared_theta_leg(X, Yr, min(K, 100), min(W, 10), device)
+
     roof = roofline_f32(model) if synth else roofline(model, n, Yr.shape[1], d)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -645,6 +679,8 @@ def main():
             "published_m1_cpu": None if synth else {"train_1000_adam_s": 142.36, "evals_per_s": 7.02,
                                                     "source": "notebooks/demo: goku power spectra.ipynb:120"},
         }
+        if shared_sub is not None:
+            line["shared_theta"] = shared_sub
         if world == 1 and args.config == "goku" and not args.no_extras:
             # every other BASELINE config, measured in this process after the headline timing
             line["hbs"] = hbs_leg()

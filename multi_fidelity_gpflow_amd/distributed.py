@@ -180,3 +180,119 @@ class SharedThetaTrainer:
                             f"and were retried; the trajectory is incomplete")
         if v != 0 or not np.all(np.isfinite(h)):
             raise CholeskyError("shared-theta optimize: Cholesky failed")
+
+
+class SharedInducingTrainer:
+    """SURVEY §8(e) sharding of ONE SingleBinSVGP (singlebin_svgp.py:39-62): every per-bin quantity
+    (kernel theta_l, q_mu[:, l], q_sqrt[l]) lives on the rank that owns bin l, while the inducing
+    inputs Z and the Gaussian noise are shared, trainable parameters of the one model.  The
+    objective is additive over bins (SeparateIndependent: ELBO = sum_l VE_l * scale - KL_l), so per
+    Adam iteration each rank evaluates its bins' ELBO and gradient, ONE all-reduce sums
+    [ELBO, KL, VE | failed-evaluation flag | dE/dZ (M (D+1)) | dE/dnoise] over the ranks, and every
+    rank applies the same Keras-Adam step: Z and the noise stay identical everywhere and the
+    trajectory is the single-process one (singlebin_svgp.py:64-97).
+
+    Device path (model = this rank's SingleBinSVGP of its bin block, Z identical on every rank,
+    e.g. broadcast_inducing): mfgp_svgp_elbo_grad -> pack -> dist.all_reduce (RCCL over xGMI) ->
+    unpack -> mfgp_adam_packed_ex gated on the reduced flag (a failed evaluation on any rank skips
+    the step everywhere).  Eager launches on the trainer's stream (no graph capture around the
+    collective).  Hooks (CPU rehearsal with gloo): grad() fills the tensors in `shared` (and
+    returns the local failure flag), adam(failed) applies the step."""
+
+    def __init__(self, model=None, data=None, max_iters=1, initial_lr=0.1, grad=None, shared=None, adam=None,
+                 allreduce=None):
+        self.tr = None
+        if grad is None:   # MI355X path
+            from .svgp import _SVGPTrainer
+            tr = _SVGPTrainer(model, data, max_iters, initial_lr, graph=False)
+            self.tr = tr
+            self.gate = torch.zeros((1,), dtype=torch.int32, device=tr.eng.device)
+            shared = [tr.out, tr.view(tr.g, "Z").reshape(-1), tr.view(tr.g, "noise").reshape(-1)]
+
+            def _grad():
+                tr._grad()
+                return (tr.info.max() != 0).to(torch.float64)
+
+            def _adam(failed):
+                self.gate.copy_((failed > 0).to(torch.int32).reshape(1))
+                tr.eng.adam_packed(tr.u, tr.c, tr.g, tr.mo, tr.vo, tr.trainable, tr.transform, tr.span, tr.step_t,
+                                   tr.lr, tr.b1, tr.b2, 1e-7, tr.out, tr.klm, tr.loss_hist, tr.kl_hist,
+                                   info=self.gate)
+            grad, adam = _grad, _adam
+            self.stream = tr.stream
+        else:
+            self.stream = None
+        self.grad_fn, self.adam_fn, self.shared = grad, adam, list(shared)
+        self.sizes = [t.numel() for t in self.shared]
+        t0 = self.shared[0]
+        self.buf = torch.zeros(sum(self.sizes) + 1, dtype=torch.float64, device=t0.device)
+        self.allreduce = allreduce or (lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM))
+        self.done = 0
+        self.max_iters = max(int(max_iters), 1)
+
+    def _ctx(self):
+        import contextlib
+        return torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()
+
+    def pack(self):
+        """Local evaluation, then its shared part into the reduction buffer."""
+        failed = self.grad_fn()
+        o = 0
+        for t, n in zip(self.shared, self.sizes):
+            self.buf[o:o + n].copy_(t.reshape(-1))
+            o += n
+        self.buf[o:o + 1].copy_(torch.as_tensor(failed, dtype=torch.float64).reshape(1))
+
+    def unpack_step(self):
+        """Reduced values back into the gradient / output views, then the Adam step."""
+        o = 0
+        for t, n in zip(self.shared, self.sizes):
+            t.copy_(self.buf[o:o + n].reshape(t.shape))
+            o += n
+        self.adam_fn(self.buf[o])
+        self.done += 1
+
+    def step(self):
+        with self._ctx():
+            self.pack()
+            self.allreduce(self.buf)
+            self.unpack_step()
+
+    def run(self, n):
+        if self.done + n > self.max_iters:
+            raise ValueError("SharedInducingTrainer: more iterations than max_iters")
+        for _ in range(n):
+            self.step()
+
+    def set_trainable(self, name, flag):
+        self.tr.set_trainable(name, flag)
+
+    def optimize(self, unfix_noise_after=None):
+        """singlebin_svgp.py:64-97 loop (the noise becomes trainable after iteration
+        unfix_noise_after), then the parameters and loss_history back into the model."""
+        while self.done < self.max_iters:
+            stop = self.max_iters
+            noise_fixed = not self.tr.model.likelihood.variance.trainable
+            if noise_fixed and unfix_noise_after is not None and self.done <= unfix_noise_after < self.max_iters:
+                stop = unfix_noise_after + 1
+            self.run(stop - self.done)
+            if noise_fixed and unfix_noise_after is not None and self.done == unfix_noise_after + 1:
+                self.set_trainable("noise", True)
+        self.finish()
+
+    def sync(self):
+        if self.tr is not None:
+            self.tr.sync()
+
+    def finish(self):
+        if self.tr is not None:
+            self.tr.finish()
+
+
+def broadcast_inducing(model, rank: int, world: int, device):
+    """Make the model's inducing inputs identical on every rank (rank 0's KMeans centres: the
+    host KMeans can differ in the last ulp between processes)."""
+    from .params import Parameter
+    Z = broadcast_arrays([model.inducing_variable.numpy()] if rank == 0 else None, rank, world, device)[0]
+    model.inducing_variable = Parameter(np.ascontiguousarray(Z, dtype=np.float64))
+    return model

@@ -347,3 +347,48 @@ def test_gradients_independent_of_workspace_contents(hbs):
     eo, ga = _autograd_grads(m, X, Y, m.kernel.W.numpy(), num_data=X.shape[0])
     assert abs(e - eo) < 1e-7 * abs(eo)
     _check_grads(gd, ga, 1e-6)
+
+
+def test_shared_inducing_two_blocks_match_single_model(hbs):
+    """SURVEY §8(e) single-bin SVGP mode on the device (distributed.SharedInducingTrainer): two bin
+    blocks (25 + 24 HBS bins) as two 'ranks' in one process -- each evaluates its bins' ELBO and
+    gradient (mfgp_svgp_elbo_grad), the [ELBO, KL, VE | flag | dZ | dnoise] buffers are summed (the
+    all-reduce), both apply the packed Adam step -- against ONE SingleBinSVGP over all 49 bins: the
+    same -ELBO trajectory, Z and noise to 1e-11."""
+    from multi_fidelity_gpflow_amd.distributed import SharedInducingTrainer, bin_block
+    from multi_fidelity_gpflow_amd.svgp import _SVGPTrainer
+    X, Y = hbs["X"], hbs["Y"]
+    steps = 8
+    kern = lambda: M.SquaredExponential(lengthscales=np.ones(5))
+    full = M.SingleBinSVGP(X, Y, kern(), kern(), 49, Z=np.zeros((50, 6)))
+    Z = full.inducing_variable.numpy()
+    ref = _SVGPTrainer(full, (X, Y), steps, 0.1, graph=False)
+    ref.run(steps)
+    ref.sync()
+    blocks = []
+    for r in range(2):
+        b0, b1 = bin_block(49, r, 2)
+        mr = M.SingleBinSVGP(X, np.ascontiguousarray(Y[:, b0:b1]), kern(), kern(), b1 - b0, Z=np.zeros((50, 6)))
+        mr.inducing_variable.assign(Z)
+        blocks.append(SharedInducingTrainer(mr, (X, np.ascontiguousarray(Y[:, b0:b1])), steps, 0.1))
+    for _ in range(steps):
+        for t in blocks:
+            with t._ctx():
+                t.pack()
+        torch.cuda.synchronize()
+        s = blocks[0].buf + blocks[1].buf
+        for t in blocks:
+            t.buf.copy_(s)
+        torch.cuda.synchronize()
+        for t in blocks:
+            with t._ctx():
+                t.unpack_step()
+    torch.cuda.synchronize()
+    h_ref = ref.loss_hist[:steps].cpu().numpy()
+    for t in blocks:
+        np.testing.assert_allclose(t.tr.loss_hist[:steps].cpu().numpy(), h_ref, rtol=1e-11)
+        np.testing.assert_allclose(t.tr.view(t.tr.c, "Z").cpu().numpy(), ref.view(ref.c, "Z").cpu().numpy(),
+                                   rtol=1e-11, atol=1e-13)
+        np.testing.assert_allclose(t.tr.view(t.tr.c, "noise").cpu().numpy(), ref.view(ref.c, "noise").cpu().numpy(),
+                                   rtol=1e-11)
+    assert int(blocks[0].tr.step_t.item()) == steps
