@@ -362,6 +362,8 @@ def bench_svgp(args):
     b0, b1 = bin_block(Y.shape[1], rank, world)
     Yr = np.ascontiguousarray(Y[:, b0:b1])
     leg = svgp_leg(X, Yr, Xt, args.steps, args.warmup, world, device, train_predict=not args.no_train_predict)
+    shared = shared_inducing_leg(X, Yr, min(args.steps, 50), min(args.warmup, 5), rank, world, device) \
+        if world > 1 else None
     if rank == 0:
         cfg = dict(leg.pop("config"), parallelism=f"bins{world}" if world > 1 else "single")
         line = {
@@ -373,11 +375,43 @@ def bench_svgp(args):
             "config": cfg,
         }
         line.update(leg)
+        if shared is not None:
+            line["shared_inducing"] = shared
         line["cpu_baseline"] = None
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
     return 0
+
+
+def shared_inducing_leg(X, Yr, steps, warmup, rank, world, device):
+    """N > 1: the reference's ONE SingleBinSVGP over all bins (singlebin_svgp.py:39-62): each rank
+    its bin block's per-bin state, Z (rank 0's KMeans centres) and the noise shared and trained,
+    one all-reduce of M (D+1) + 5 doubles per step (distributed.SharedInducingTrainer).  value =
+    model iterations / s (strong scaling)."""
+    import multi_fidelity_gpflow_amd as M
+    from multi_fidelity_gpflow_amd.distributed import SharedInducingTrainer, broadcast_inducing
+    d = X.shape[1] - 1
+    kern = lambda: M.SquaredExponential(lengthscales=np.ones(d))
+    model = broadcast_inducing(M.SingleBinSVGP(X, Yr, kern(), kern(), Yr.shape[1], Z=np.zeros((300, d + 1))),
+                               rank, world, device)
+    tr = SharedInducingTrainer(model, (X, Yr), steps + warmup, 0.1)
+    tr.run(warmup)
+    tr.sync()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tr.run(steps)
+    tr.sync()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    tr.finish()
+    return {"mode": "shared_inducing", "scaling": "strong", "steps": steps, "warmup": warmup,
+            "ms_per_step": round(dt / steps * 1e3, 4), "value": round(steps / dt, 3), "unit": "iters/s",
+            "collective": f"one all-reduce of {model.inducing_variable.numpy().size + 5} doubles per step"}
 
 
 HBS = os.path.join(ROOT, "tests", "golden", "data", "50_LR_3_HR")

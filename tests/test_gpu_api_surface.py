@@ -280,3 +280,30 @@ def test_flow_size_threshold(eng):
     small, large = 0, 1
     assert sizes["auto"][small] == sizes["steps"][small] < sizes["any"][small]   # HBS: T = 2
     assert sizes["auto"][large] == sizes["any"][large] > sizes["steps"][large]   # Goku: T = 37
+
+
+def test_session_pool_reuses_graphs_exactly(hbs, eng):
+    """A finished AdamSession's buffers and captured graphs are reused by the next fresh model of
+    the same shape (models._pool): no recapture, and the trajectories are bitwise those of eager
+    (graph=False) runs -- the reused graphs read only the new model's data and state."""
+    from multi_fidelity_gpflow_amd import models as MM
+    ref = _model(hbs)
+    ref.optimize(max_iters=100, learning_rate=0.1, verbose=False, graph=False)
+    m1 = _model(hbs)
+    m1.optimize(max_iters=100, learning_rate=0.1, verbose=False)
+    key = [k for k, v in MM._pool.items() if v and k[2] == tuple(hbs["X"].shape) and k[5] == 100 and k[6] == 50]
+    assert key, "the finished session was not pooled"
+    core = MM._pool[key[0]][0]
+    g_before = dict(core.graphs)
+    m2 = _model(hbs)
+    m2.kernel.kernel_L.variance.assign(1.3)     # a different initial state through the same graphs
+    ref2 = _model(hbs)
+    ref2.kernel.kernel_L.variance.assign(1.3)
+    ref2.optimize(max_iters=100, learning_rate=0.1, verbose=False, graph=False)
+    sess = m2.adam_session(0.1, 100)
+    assert sess._core is core and all(sess.runner.graphs[k] is g for k, g in g_before.items())
+    sess.run(100)
+    sess.finish()
+    np.testing.assert_array_equal(np.array(m1.loss_history), np.array(ref.loss_history))
+    np.testing.assert_array_equal(np.array(m2.loss_history), np.array(ref2.loss_history))
+    np.testing.assert_array_equal(m2.kernel.rho.numpy(), ref2.kernel.rho.numpy())

@@ -1,5 +1,6 @@
-"""Where the Goku train (1000 Adam steps) + predict_f wall-clock goes beyond the steps themselves:
-session set-up, graph capture, replay, finish, predict (GPU box, repo root)."""
+"""Where the train + predict wall-clock goes beyond the steps themselves: model construction,
+session set-up, graph capture, replay, finish, predict (GPU box, repo root).
+    python tools/tp_breakdown.py [goku|hbs]   (goku: 1000 Adam steps; hbs: the reference test's 100)"""
 import os
 import sys
 import time
@@ -9,7 +10,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-from bench import load_goku, make_model  # noqa: E402
+from bench import HBS, load_goku, make_model  # noqa: E402
 
 
 def clock():
@@ -18,21 +19,31 @@ def clock():
 
 
 torch.cuda.set_device(0)
-X, Y, Xt, _ = load_goku()
-for rep in range(3):
+which = sys.argv[1] if len(sys.argv) > 1 else "goku"
+if which == "hbs":
+    from multi_fidelity_gpflow_amd.data import PowerSpecs, multifidelity_training_set
+    ps = PowerSpecs()
+    ps.read_from_txt(HBS)
+    X, Y, Xt, _ = multifidelity_training_set(ps)
+    steps = 100
+else:
+    X, Y, Xt, _ = load_goku()
+    steps = 1000
+for rep in range(4):
+    tm = clock()
     m = make_model(X, Y)
     m._device_data()
     t0 = clock()
-    sess = m.adam_session(0.1, 1000, True, 50)
+    sess = m.adam_session(0.1, steps, True, 50)
     t1 = clock()
-    sess.prepare(1000)
+    sess.prepare(steps)
     t2 = clock()
-    sess.run(1000)
+    sess.run(steps)
     t3 = clock()
     sess.finish()
     t4 = clock()
     mean, var = m.predict_f(Xt)
     t5 = clock()
-    print(f"rep {rep}: session {1e3 * (t1 - t0):.1f} ms, capture {1e3 * (t2 - t1):.1f} ms, 1000 steps "
-          f"{1e3 * (t3 - t2):.1f} ms, finish {1e3 * (t4 - t3):.1f} ms, predict {1e3 * (t5 - t4):.1f} ms; "
-          f"total {1e3 * (t5 - t0):.1f} ms")
+    print(f"{which} rep {rep}: model {1e3 * (t0 - tm):.2f} ms, session {1e3 * (t1 - t0):.2f} ms, capture "
+          f"{1e3 * (t2 - t1):.2f} ms, {steps} steps {1e3 * (t3 - t2):.2f} ms, finish {1e3 * (t4 - t3):.2f} ms, "
+          f"predict {1e3 * (t5 - t4):.2f} ms; total {1e3 * (t5 - tm):.2f} ms", flush=True)
