@@ -39,9 +39,12 @@ def test_goku_adam_first_100(goku, kats):
 
 
 def test_forrester_lbfgs_rho(kats):
-    """GPflow-faithful two-pass L-BFGS-B.  The objective is degenerate once the noise
-    hits its 1e-6 floor; 1-ulp changes move the stopping point along a flat valley,
-    so the recorded rho is reproduced to 1e-4 (this restatement: 5.6e-5)."""
+    """GPflow-faithful two-pass L-BFGS-B (variable order, TFP softplus_inverse start values, the
+    noise as Shift(1e-6) o Softplus, options={"maxiter": ...} only, as gpflow.optimizers.Scipy
+    passes them).  The objective is degenerate once the noise hits its 1e-6 floor: 1-ulp changes
+    in the value or gradient move the stopping point along a flat valley (a torch-autograd
+    gradient instead of the analytic one ends elsewhere or leaves the PD region), so the recorded
+    rho is reproduced to 1e-4 (this restatement: 3.7e-5; the device's flow schedule 6.6e-7)."""
     from conftest import forrester_demo_data
     X, Y = forrester_demo_data()
     p = O.lbfgs_train(X, Y, O.MFParams.initial(1, 1), max_iters=1000)
