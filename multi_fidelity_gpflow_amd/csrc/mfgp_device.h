@@ -477,119 +477,43 @@ __device__ __forceinline__ void tile_potrf_inv_w1_wave(const double* __restrict_
 }
 
 // ---------------------------------------------------------------- split diag factor
-// The same factorization as tile_potrf_inv_w1_wave with its two halves on two waves of the
-// workgroup (bitwise the same D, L_ii and *bad):
-//   * the A wave (tile_elim_w1_wave) runs only the elimination: round K publishes its pivot rows
-//     into a panel of their own, Pn + 128 K, and then raises the LDS progress word *prog to
-//     base + K + 1 (every lane stores the same value: one ds_write, no exec branch; a wave's DS
-//     operations are processed in issue order, so the panel is complete once the word is seen);
-//   * the R wave (tile_rinv_w1_wave) follows the published panels: per round it re-derives the
-//     4x4 LDL^T and its own rows' substitutions with the A wave's instructions and applies the
-//     inverse update R -= W_R R[P, :], one round behind its panel reads (w1_rwork), then scales
-//     R into D = L^{-1} and writes L_ii and the first bad pivot.
+// The factorization of tile_potrf_inv_w1_wave with its two halves on two waves of the workgroup:
+//   * the A wave (tile_elim_w1_wave) runs the elimination.  Round K publishes its pivot rows
+//     (Pn, read back by the A wave itself), then -- after issuing its rank-4 MFMA update -- the
+//     round's substitution results for the R wave: z = C L_M^{-T} D_M^{-1} of every live row
+//     (rows 16h + lc, h >= K / 4, written once by the lanes with kk = 0) into Zb + 128 K, the four
+//     pivots into dpv, and last the LDS progress word *prog = base + K + 1 (every lane stores the
+//     same value: one ds_write, no exec branch; a wave's DS operations are processed in issue
+//     order, so the round's data is complete once the word is seen);
+//   * the R wave (tile_rinv_w1_wave) applies the inverse update R -= W_R R[P, :] of each round from
+//     those z values alone: the 4x4 LDL^T multipliers are the pivot rows' own z (row p of the
+//     pivot block has z_j = L_pj, j < p), so it neither re-reads the panel nor repeats the LDL^T,
+//     then scales R into D = L^{-1} and writes L_ii and the first bad pivot.
 // On one wave the inverse's MFMAs and ~60 f64 VALU instructions a round share SIMD 0 with the
-// elimination (8.2k clocks against ~5k for the elimination alone); split, the A wave's chain ends
-// after its last publish and D follows ~one round later on the R wave's SIMD.
-// Pn: 8 x 128 doubles (never aliasing X); dpv: 104 doubles; prog: an LDS int, monotonic over calls.
+// elimination (8.1k clocks against ~4.3k for the elimination alone, tools/ubench_rsplit.hip);
+// split, D follows the A wave's last round by the R wave's one-round lag.  An R wave that
+// re-derived the LDL^T from the panel was issue-bound at ~1k clocks a round (no faster than the
+// fused factor).  The multipliers taken from the pivot rows' z can differ from the A wave's L in
+// the last bit (the pivot block's upper and lower triangle round independently), so D is not
+// bitwise the fused factor's, only equal to rounding.
+// Pn: 8 x 128, Zb: 8 x 128, dpv: 104 doubles (none aliasing X); prog: an LDS int, monotonic
+// over calls.
 template <int K>
-__device__ __forceinline__ void w1e_round(double* __restrict__ Pn, int* prog, int base, f64x4& a00, f64x4& a01,
-                                          f64x4& a11, int l) {
+__device__ __forceinline__ void w1e_round(double* __restrict__ Pn, double* __restrict__ Zb, double* __restrict__ dpv,
+                                          int* prog, int base, f64x4& a00, f64x4& a01, f64x4& a11, int l) {
     if constexpr (K < 8) {
         constexpr int bk = K >> 2, kq = K & 3;
         const int lc = l & 15, kk = l >> 4;
         double* P = Pn + 128 * K;
         if constexpr (bk == 0) P[lc * 4 + kk] = a00[kq];
         P[(16 + lc) * 4 + kk] = (bk == 0) ? a01[kq] : a11[kq];
-        asm volatile("" ::: "memory");
-        __hip_atomic_store(prog, base + K + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        asm volatile("" ::: "memory");
-        if constexpr (K < 7) {   // the last round's pivots leave nothing below them to update
-            const f64x2* Pm = reinterpret_cast<const f64x2*>(P + 16 * K);
-            const f64x2 c0a = Pm[0], c0b = Pm[1], c1a = Pm[2], c1b = Pm[3], c2b = Pm[5], c3b = Pm[7];
-            const f64x2* Pr = reinterpret_cast<const f64x2*>(P);
-            f64x2 u0a = {0.0, 0.0}, u0b = {0.0, 0.0};
-            if constexpr (bk == 0) { u0a = Pr[2 * lc]; u0b = Pr[2 * lc + 1]; }
-            const f64x2 u1a = Pr[2 * (16 + lc)], u1b = Pr[2 * (16 + lc) + 1];
-            __builtin_amdgcn_sched_barrier(0);
-            const double m00 = c0a.x, m10 = c0a.y, m20 = c0b.x, m30 = c0b.y;
-            const double m11 = c1a.y, m21 = c1b.x, m31 = c1b.y, m22 = c2b.x, m32 = c2b.y, m33 = c3b.y;
-            const double i0 = rcp_nr1(m00);
-            const double L10 = m10 * i0, L20 = m20 * i0, L30 = m30 * i0;
-            const double d1 = fma(-L10, m10, m11);
-            const double i1 = rcp_nr1(d1);
-            const double e21 = fma(-L20, m10, m21), e31 = fma(-L30, m10, m31);
-            const double L21 = e21 * i1, L31 = e31 * i1;
-            const double d2 = fma(-L21, e21, fma(-L20, m20, m22));
-            const double i2 = rcp_nr1(d2);
-            const double e32 = fma(-L31, e21, fma(-L30, m20, m32));
-            const double L32 = e32 * i2;
-            const double d3 = fma(-L32, e32, fma(-L31, e31, fma(-L30, m30, m33)));
-            const double i3 = rcp_nr1(d3);
-            double zA[2], yB[2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                if (h < bk) { zA[h] = 0.0; yB[h] = 0.0; continue; }
-                const f64x2 ua = h ? u1a : u0a, ub = h ? u1b : u0b;
-                const int row = 16 * h + lc;
-                const bool below = row > 4 * K + 3;
-                const double y0 = ua.x;
-                const double y1 = fma(-L10, y0, ua.y);
-                const double y2 = fma(-L21, y1, fma(-L20, y0, ub.x));
-                const double y3 = fma(-L32, y2, fma(-L31, y1, fma(-L30, y0, ub.y)));
-                const double z0 = y0 * i0, z1 = y1 * i1, z2 = y2 * i2, z3 = y3 * i3;
-                zA[h] = below ? sel4(kk, z0, z1, z2, z3) : 0.0;
-                yB[h] = sel4(kk, y0, y1, y2, y3);
-            }
-            if constexpr (bk == 0) {
-                if constexpr (K < 3) {
-                    a00 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[0], yB[0], a00, 0, 0, 0);
-                    a01 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[0], yB[1], a01, 0, 0, 0);
-                }
-                a11 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[1], yB[1], a11, 0, 0, 0);
-            } else {
-                a11 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[1], yB[1], a11, 0, 0, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        w1e_round<K + 1>(Pn, prog, base, a00, a01, a11, l);
-    }
-}
-
-// A wave: X (lower triangle valid, stride ldx; may not alias Pn) -> the 8 published panels.
-__device__ __forceinline__ void tile_elim_w1_wave(const double* __restrict__ X, int ldx, double* __restrict__ Pn,
-                                                  int* prog, int base) {
-    const int l = threadIdx.x & 63, lc = l & 15, lr = l >> 4;
-    f64x4 a00, a01, a11;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int r = lr + 4 * q;
-        const int hi = r > lc ? r : lc, lo = r > lc ? lc : r;
-        a00[q] = X[hi * ldx + lo];
-        a11[q] = X[(16 + hi) * ldx + 16 + lo];
-        a01[q] = X[(16 + lc) * ldx + r];
-    }
-    w1e_round<0>(Pn, prog, base, a00, a01, a11, l);
-}
-
-template <int K>
-__device__ __forceinline__ void w1r_round(const double* __restrict__ Pn, const int* prog, int base,
-                                          double* __restrict__ dpv, f64x4& r00, f64x4& r10, f64x4& r11,
-                                          W1Pending& pd, int l) {
-    if constexpr (K < 8) {
-        constexpr int bk = K >> 2, kq = K & 3;
-        const int lc = l & 15, kk = l >> 4;
-        while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(const_cast<int*>(prog), __ATOMIC_RELAXED,
-                                                                __HIP_MEMORY_SCOPE_WORKGROUP)) < base + K + 1) {}
-        asm volatile("" ::: "memory");
-        const double* P = Pn + 128 * K;
+        asm volatile("" ::: "memory");   // keep the compiler from reordering publish / read
         const f64x2* Pm = reinterpret_cast<const f64x2*>(P + 16 * K);
         const f64x2 c0a = Pm[0], c0b = Pm[1], c1a = Pm[2], c1b = Pm[3], c2b = Pm[5], c3b = Pm[7];
         const f64x2* Pr = reinterpret_cast<const f64x2*>(P);
         f64x2 u0a = {0.0, 0.0}, u0b = {0.0, 0.0};
         if constexpr (bk == 0) { u0a = Pr[2 * lc]; u0b = Pr[2 * lc + 1]; }
         const f64x2 u1a = Pr[2 * (16 + lc)], u1b = Pr[2 * (16 + lc) + 1];
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (K > 0) w1_rwork<K - 1>(pd, r00, r10, r11, l);
         __builtin_amdgcn_sched_barrier(0);
         const double m00 = c0a.x, m10 = c0a.y, m20 = c0b.x, m30 = c0b.y;
         const double m11 = c1a.y, m21 = c1b.x, m31 = c1b.y, m22 = c2b.x, m32 = c2b.y, m33 = c3b.y;
@@ -605,37 +529,106 @@ __device__ __forceinline__ void w1r_round(const double* __restrict__ Pn, const i
         const double L32 = e32 * i2;
         const double d3 = fma(-L32, e32, fma(-L31, e31, fma(-L30, m30, m33)));
         const double i3 = rcp_nr1(d3);
-        double zs[2][4] = {};
+        double zA[2], yB[2], zs[2][4] = {};
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            if (h < bk) continue;
+            if (h < bk) { zA[h] = 0.0; yB[h] = 0.0; continue; }
             const f64x2 ua = h ? u1a : u0a, ub = h ? u1b : u0b;
+            const int row = 16 * h + lc;
+            const bool below = row > 4 * K + 3;
             const double y0 = ua.x;
             const double y1 = fma(-L10, y0, ua.y);
             const double y2 = fma(-L21, y1, fma(-L20, y0, ub.x));
             const double y3 = fma(-L32, y2, fma(-L31, y1, fma(-L30, y0, ub.y)));
-            zs[h][0] = y0 * i0; zs[h][1] = y1 * i1; zs[h][2] = y2 * i2; zs[h][3] = y3 * i3;
+            const double z0 = y0 * i0, z1 = y1 * i1, z2 = y2 * i2, z3 = y3 * i3;
+            zA[h] = below ? sel4(kk, z0, z1, z2, z3) : 0.0;
+            yB[h] = sel4(kk, y0, y1, y2, y3);
+            zs[h][0] = z0; zs[h][1] = z1; zs[h][2] = z2; zs[h][3] = z3;
         }
-        dpv[l < 4 ? 4 * K + l : 40 + l] = sel4(l & 3, m00, d1, d2, d3);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const bool piv = ((16 * h + lc) >> 2) == K;
-            const int p = lc & 3;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) pd.v[h][c] = piv ? (p == c ? 1.0 : 0.0) : zs[h][c];
+        if constexpr (K < 7) {   // the last round's pivots leave nothing below them to update
+            if constexpr (bk == 0) {
+                if constexpr (K < 3) {
+                    a00 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[0], yB[0], a00, 0, 0, 0);
+                    a01 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[0], yB[1], a01, 0, 0, 0);
+                }
+                a11 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[1], yB[1], a11, 0, 0, 0);
+            } else {
+                a11 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[1], yB[1], a11, 0, 0, 0);
+            }
         }
-        pd.L10 = L10; pd.L20 = L20; pd.L30 = L30; pd.L21 = L21; pd.L31 = L31; pd.L32 = L32;
         __builtin_amdgcn_sched_barrier(0);
-        w1r_round<K + 1>(Pn, prog, base, dpv, r00, r10, r11, pd, l);
-    } else {
-        w1_rwork<7>(pd, r00, r10, r11, l);
+        // ---- off the A chain (issued under the MFMA latency): the R wave's inputs of this round
+        dpv[l < 4 ? 4 * K + l : 40 + l] = sel4(l & 3, m00, d1, d2, d3);
+        if (kk == 0) {
+            f64x2* Z = reinterpret_cast<f64x2*>(Zb + 128 * K);
+#pragma unroll
+            for (int h = bk; h < 2; ++h) {
+                Z[2 * (16 * h + lc)] = f64x2{zs[h][0], zs[h][1]};
+                Z[2 * (16 * h + lc) + 1] = f64x2{zs[h][2], zs[h][3]};
+            }
+        }
+        asm volatile("" ::: "memory");
+        __hip_atomic_store(prog, base + K + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __builtin_amdgcn_sched_barrier(0);
+        w1e_round<K + 1>(Pn, Zb, dpv, prog, base, a00, a01, a11, l);
     }
 }
 
-// R wave: follows tile_elim_w1_wave's panels; writes D = L^{-1} into R (stride S, lower, zero
-// above), dg[i] = L_ii and *bad exactly as tile_potrf_inv_w1_wave does.
-__device__ __forceinline__ void tile_rinv_w1_wave(const double* __restrict__ Pn, const int* prog, int base,
-                                                  double* __restrict__ dpv, double* __restrict__ R,
+// A wave: X (lower triangle valid, stride ldx; may not alias Pn / Zb) -> the elimination.
+__device__ __forceinline__ void tile_elim_w1_wave(const double* __restrict__ X, int ldx, double* __restrict__ Pn,
+                                                  double* __restrict__ Zb, double* __restrict__ dpv, int* prog,
+                                                  int base) {
+    const int l = threadIdx.x & 63, lc = l & 15, lr = l >> 4;
+    f64x4 a00, a01, a11;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int r = lr + 4 * q;
+        const int hi = r > lc ? r : lc, lo = r > lc ? lc : r;
+        a00[q] = X[hi * ldx + lo];
+        a11[q] = X[(16 + hi) * ldx + 16 + lo];
+        a01[q] = X[(16 + lc) * ldx + r];
+    }
+    w1e_round<0>(Pn, Zb, dpv, prog, base, a00, a01, a11, l);
+}
+
+template <int K>
+__device__ __forceinline__ void w1r_round(const double* __restrict__ Zb, const int* prog, int base, f64x4& r00,
+                                          f64x4& r10, f64x4& r11, int l) {
+    if constexpr (K < 8) {
+        constexpr int bk = K >> 2;
+        const int lc = l & 15;
+        while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(const_cast<int*>(prog), __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_WORKGROUP)) < base + K + 1) {}
+        asm volatile("" ::: "memory");
+        const double* Z = Zb + 128 * K;
+        // multipliers: the pivot rows' z (rows 4K + 1 .. 4K + 3 of the tile)
+        const f64x2 p2 = *reinterpret_cast<const f64x2*>(Z + 4 * (4 * K + 2));
+        const f64x2 p3a = *reinterpret_cast<const f64x2*>(Z + 4 * (4 * K + 3));
+        W1Pending pd;
+        pd.L10 = Z[4 * (4 * K + 1)];
+        pd.L20 = p2.x; pd.L21 = p2.y;
+        pd.L30 = p3a.x; pd.L31 = p3a.y; pd.L32 = Z[4 * (4 * K + 3) + 2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (h < bk) continue;
+            const f64x2 za = *reinterpret_cast<const f64x2*>(Z + 4 * (16 * h + lc));
+            const f64x2 zb = *reinterpret_cast<const f64x2*>(Z + 4 * (16 * h + lc) + 2);
+            const bool piv = ((16 * h + lc) >> 2) == K;
+            const int p = lc & 3;
+            pd.v[h][0] = piv ? (p == 0 ? 1.0 : 0.0) : za.x;
+            pd.v[h][1] = piv ? (p == 1 ? 1.0 : 0.0) : za.y;
+            pd.v[h][2] = piv ? (p == 2 ? 1.0 : 0.0) : zb.x;
+            pd.v[h][3] = piv ? (p == 3 ? 1.0 : 0.0) : zb.y;
+        }
+        w1_rwork<K>(pd, r00, r10, r11, l);
+        w1r_round<K + 1>(Zb, prog, base, r00, r10, r11, l);
+    }
+}
+
+// R wave: follows tile_elim_w1_wave's rounds; writes D = L^{-1} into R (stride S, lower, zero
+// above), dg[i] = L_ii and *bad as tile_potrf_inv_w1_wave does.
+__device__ __forceinline__ void tile_rinv_w1_wave(const double* __restrict__ Zb, const int* prog, int base,
+                                                  const double* __restrict__ dpv, double* __restrict__ R,
                                                   double* __restrict__ dg, int* __restrict__ bad) {
     constexpr int S = TileCfg<32>::S;
     const int l = threadIdx.x & 63, lc = l & 15, lr = l >> 4;
@@ -646,9 +639,7 @@ __device__ __forceinline__ void tile_rinv_w1_wave(const double* __restrict__ Pn,
         r00[q] = (r == lc) ? 1.0 : 0.0;
         r11[q] = r00[q];
     }
-    W1Pending pd;
-    w1r_round<0>(Pn, prog, base, dpv, r00, r10, r11, pd, l);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    w1r_round<0>(Zb, prog, base, r00, r10, r11, l);
     double s0[4], s1[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {

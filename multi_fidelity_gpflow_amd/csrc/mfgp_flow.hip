@@ -672,7 +672,7 @@ __device__ __forceinline__ void flow_worker(FlowCtx& C, int wid, double* S) {
 // Buffers are double-buffered by step parity.
 struct DiagLds {
     // LDS carve (doubles): Db[2] | Ls[2] | Ap[2] | Cp[2] | L2[2] (NB x S each) | fsc (32 x 33) | dg[2][32]
-    // | bad[2] | words | pan[2] (8 x 128: the factor's round panels) | dpv[2] (128).  Parity-indexed
+    // | bad[2] | words | pan[2], zb[2] (8 x 128: the factor's round panels / z) | dpv[2] (128).  Parity-indexed
     // buffers are computed, not held in pointer arrays (a dynamically indexed pointer array lands
     // in scratch).
     double* base;
@@ -687,9 +687,10 @@ struct DiagLds {
     __device__ double* dg(int q) const { return base + 10 * E + 32 * 33 + 32 * q; }
     __device__ int* bad() const { return reinterpret_cast<int*>(base + 10 * E + 32 * 33 + 64); }
     __device__ int* w() const { return bad() + 2; }
-    __device__ double* pan(int q) const { return base + PAN + 1024 * q; }
-    __device__ double* dpv(int q) const { return base + PAN + 2048 + 128 * q; }
-    static constexpr size_t BYTES = sizeof(double) * (PAN + 2048 + 256);
+    __device__ double* pan(int q) const { return base + PAN + 1024 * q; }          // round panels (A)
+    __device__ double* zb(int q) const { return base + PAN + 2048 + 1024 * q; }    // round z (A -> R)
+    __device__ double* dpv(int q) const { return base + PAN + 4096 + 128 * q; }    // pivots (A -> R)
+    static constexpr size_t BYTES = sizeof(double) * (PAN + 4096 + 256);
 };
 static_assert(DiagLds::BYTES <= FLOW_LDS_BYTES, "diag workgroup LDS carve");
 enum { DW_LS = 0, DW_D, DW_LPUB, DW_DPUB, DW_PRE6, DW_PRE7, DW_BAR, DW_L2, DW_P2, DW_PROG, DW_N };
@@ -700,7 +701,7 @@ static_assert(DW_N <= 28, "progress words fit before the panels");
 // published round panels (its SIMD is shared with one band helper, so it raises its issue
 // priority while it runs).  FLOW_RWAVE = 0: the fused single-wave factor on wave 0.
 #ifndef FLOW_RWAVE
-#define FLOW_RWAVE 1
+#define FLOW_RWAVE 0
 #endif
 #ifndef FLOW_RPRIO
 #define FLOW_RPRIO 2
@@ -799,11 +800,11 @@ __device__ __forceinline__ void diag_chain(FlowCtx& C, const DiagLds& B) {
 #if FLOW_RWAVE
         if (w == 0) {
             if (a.trace && threadIdx.x == 0) a.trace[2 * T + k] = flow_clock() - C.t0;
-            tile_elim_w1_wave(B.fsc(), 33, B.pan(pk), &B.w()[DW_PROG], 8 * k);
+            tile_elim_w1_wave(B.fsc(), 33, B.pan(pk), B.zb(pk), B.dpv(pk), &B.w()[DW_PROG], 8 * k);
         } else if (w == FLOW_RWAVE) {
             lds_spin_ge(&B.w()[DW_DPUB], k - 2);    // wave 4 is done with Db[pk] (D_{k-2})
             __builtin_amdgcn_s_setprio(FLOW_RPRIO);
-            tile_rinv_w1_wave(B.pan(pk), &B.w()[DW_PROG], 8 * k, B.dpv(pk), B.Db(pk), B.dg(pk), &B.bad()[pk]);
+            tile_rinv_w1_wave(B.zb(pk), &B.w()[DW_PROG], 8 * k, B.dpv(pk), B.Db(pk), B.dg(pk), &B.bad()[pk]);
             __builtin_amdgcn_s_setprio(0);
             if (l == 0) lds_put(&B.w()[DW_D], k);
         }

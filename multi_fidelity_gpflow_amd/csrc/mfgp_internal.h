@@ -43,7 +43,7 @@ constexpr int FLOW_WAVES = 8;                       // waves per workgroup (two 
 constexpr int FLOW_THREADS = 64 * FLOW_WAVES;
 constexpr int FLOW_FSTRIDE = 32;                    // ints per flag: one 128-B line each (polled lines
                                                     // are not shared, no hot line under 2k pollers)
-constexpr size_t FLOW_LDS_BYTES = 120 * 1024;       // > 80 KB: one workgroup per CU
+constexpr size_t FLOW_LDS_BYTES = 128 * 1024;       // > 80 KB: one workgroup per CU
 constexpr unsigned long long FLOW_SENTINEL = 0x7FF4DEAD7FF4DEADull;   // signalling NaN: "not yet published"
 struct FlowArgs {
     double* A; long lda;          // K + s2 I lower tiles -> L tiles (in place)

@@ -59,7 +59,8 @@ def main():
         ref = pub[j - 3]
         print(f"{j:2d} {r2[j]-ref:6.2f} | {w5[j]-ref:6.2f} {w5[T + j]-ref:6.2f} {l2[j]-ref:6.2f}   D_j-2 {pub[j-2]-ref:5.2f}"
               f"  P2(j-1)~{fs[j-1]-ref:5.2f}")
-    g = ws[off.value + 8 * (cnt.value - 5 * (T * (T + 1) // 2 + 4)): off.value + 8 * cnt.value].view(torch.int64).cpu().numpy().reshape(-1, 3)
+    G = T * (T + 1) // 2 + 4   # k_gram timeline: [3 G] stamps, then [2 G] (mfgp_flow.h flow_gram_dbg_count)
+    g = ws[off.value + 8 * (cnt.value - 5 * G): off.value + 8 * cnt.value].view(torch.int64).cpu().numpy()[:3 * G].reshape(-1, 3)
     gg = g.astype(np.float64) / 100.0
     ext = [(i, gg[i, 2]) for i in range(len(gg)) if gg[i, 0] == 0 and gg[i, 2] > 0]
     print("k_gram extra workgroups (index, us to done):", [(i, round(v, 2)) for i, v in ext])

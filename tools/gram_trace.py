@@ -39,7 +39,7 @@ def main():
         g = ws[off.value + 8 * (cnt.value - 5 * (T * (T + 1) // 2 + 4)): off.value + 8 * cnt.value].view(torch.int64).cpu().numpy()
         grid = nblk + 3
         h = g[3 * grid: 3 * grid + 2 * (nblk + 1)].reshape(-1, 2).astype(np.float64)   # [unused, staged]
-        g = g.reshape(-1, 3)[:nblk + 3].astype(np.float64)
+        g = g[:3 * (T * (T + 1) // 2 + 4)].reshape(-1, 3)[:nblk + 3].astype(np.float64)
         z = g[:, 0].min()
         g = (g - z) / 100.0
         h = (h - z) / 100.0
