@@ -70,14 +70,16 @@ struct GprLayout {
     long npub;
     long long* trace;   // k_chol_flow timeline (diagnostic; written only when enabled)
     int ntrace;
+    int sdelta, gchunk;   // FLOW_STILES levels left to k_grad (0: off); k_grad's task chunk (< 0: S tiles)
+    double* S;          // the flow's K^{-1} partial sums (FLOW_STILES)
     size_t bytes;
 };
 
 // The persistent Cholesky needs every workgroup resident (one per CU) and the owner table
 // to hold every tile; otherwise the launch-per-step sequence runs.
-static int flow_grid(int nb, int T, int Tp, int flow_wgs, int min_t) {
+static int flow_grid(int nb, int T, int Tp, int flow_wgs, int min_t, int sd = 0) {
     if (nb != 32 || flow_wgs < 2 || T > 255 || T < min_t) return 0;
-    if (flow_ntiles(T, Tp) > FLOW_WAVES * (flow_wgs - 1) * FLOW_MAXOWN) return 0;
+    if (flow_ntiles(T, Tp, sd) > FLOW_WAVES * (flow_wgs - 1) * FLOW_MAXOWN) return 0;
     return flow_wgs;
 }
 
@@ -91,7 +93,17 @@ static GprLayout gpr_layout(int nb, int n, int p, int d, void* ws, int grad_chun
     L.ppad = L.Tp * nb;
     L.G = kernel_theta_size(nlf, d);
     L.gstride = (L.G + 3) & ~3;
-    L.ng = grad_tasks(L.T, grad_chunk);
+    // the persistent flow (and with FLOW_STILES its K^{-1} partial sums, when the owner table
+    // holds them; else without)
+    L.sdelta = (nlf == 0 && FLOW_STILES > 0 && FLOW_STILES < L.T) ? FLOW_STILES : 0;
+    L.flow_wgs = flow_grid(nb, L.T, L.Tp, flow_wgs, flow_min_t, L.sdelta);
+    if (!L.flow_wgs && L.sdelta) {
+        L.sdelta = 0;
+        L.flow_wgs = flow_grid(nb, L.T, L.Tp, flow_wgs, flow_min_t, 0);
+    }
+    if (!L.flow_wgs) L.sdelta = 0;
+    L.gchunk = L.sdelta ? -L.sdelta : grad_chunk;
+    L.ng = grad_tasks(L.T, L.gchunk);
     Carve c(ws);
     const size_t ldr = (size_t)L.npad + L.ppad;
     L.A = c.take<double>((size_t)L.npad * L.npad);
@@ -106,7 +118,6 @@ static GprLayout gpr_layout(int nb, int n, int p, int d, void* ws, int grad_chun
     L.ncnt = 1;
     L.cnt = c.take<int>((size_t)L.ncnt);
     L.gorder = c.take<int>((size_t)L.ng + SCHED_KEY);
-    L.flow_wgs = flow_grid(nb, L.T, L.Tp, flow_wgs, flow_min_t);
     L.nflags = L.flow_wgs ? flow_nflags(L.T, L.Tp) : 0;
     L.flags = c.take<int>((size_t)L.nflags * FLOW_FSTRIDE);
     L.npub = L.flow_wgs ? flow_npub(L.T, L.Tp) : 0;
@@ -114,6 +125,7 @@ static GprLayout gpr_layout(int nb, int n, int p, int d, void* ws, int grad_chun
     L.own = c.take<int>(L.flow_wgs ? (size_t)FLOW_WAVES * (L.flow_wgs - 1) * FLOW_MAXOWN + SCHED_KEY : 0);
     L.ntrace = L.flow_wgs ? flow_trace_count(L.T, L.flow_wgs) : 0;
     L.trace = c.take<long long>((size_t)L.ntrace);
+    L.S = c.take<double>(L.sdelta ? (size_t)L.T * (L.T + 1) / 2 * 1024 : 0);
     L.bytes = c.off + 256;
     return L;
 }
@@ -253,9 +265,9 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
         g.padded = 1; g.npad = L.npad; g.tiles_c = L.T; g.add_noise = 1; g.diag_add = nlf ? GRAPH_JITTER : 0.0;
         g.Dd = L.Dd; g.sD = 0; g.ldiag = L.ldiag; g.sL = 0; g.info = info; g.nlf = nlf;
         g.cnt = L.cnt; g.ncnt = L.ncnt;
-        const bool order = want_grad && h->grad_chunk + L.Tp < 2048;   // gram LDS holds the histogram
-        if (order) { g.gorder = L.gorder; g.gT = L.T; g.gchunk = h->grad_chunk; g.gTp = L.Tp; }
-        if (L.flow_wgs) { g.fown = L.own; g.fW = FLOW_WAVES * (L.flow_wgs - 1); g.fflags = L.flags; g.nfflags = L.nflags; g.fpub = L.pub; g.npub = L.npub; }
+        const bool order = want_grad && std::abs(L.gchunk) + L.T + L.Tp < 2048;   // gram LDS holds the histogram
+        if (order) { g.gorder = L.gorder; g.gT = L.T; g.gchunk = L.gchunk; g.gTp = L.Tp; }
+        if (L.flow_wgs) { g.fown = L.own; g.fW = FLOW_WAVES * (L.flow_wgs - 1); g.fflags = L.flags; g.nfflags = L.nflags; g.fpub = L.pub; g.npub = L.npub; g.fsdelta = L.sdelta; }
         if (L.flow_wgs && h->flow_trace) g.dbg = L.trace + L.ntrace - flow_gram_dbg_count(L.T);   // k_gram timeline (diagnostic)
         const int extra = (order ? 1 : 0) + (L.flow_wgs ? 1 : 0);
         if (NB == 32 && L.flow_wgs && !nlf && !h->gram_legacy) {
@@ -281,6 +293,8 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
         fa.nwaves = FLOW_WAVES * (L.flow_wgs - 1);
         fa.timeout = h->flow_timeout;
         fa.d0 = (NB == 32 && !nlf && !h->gram_legacy && h->flow_d0) ? 1 : 0;
+        fa.S = L.S;
+        fa.sdelta = L.sdelta;
         fence_wait(h->device, s);
         launch_chol_flow(fa, L.flow_wgs, s);
         fence_record(h->device, s);
@@ -297,7 +311,7 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
     if (pm) pm->mark(s);
     if (want_grad) {
         GradArgs ga{L.Xo, ldr, X, (long)ldx, theta, L.gpart, L.gstride, L.T, L.Tp, n, p, d,
-                    h->grad_chunk, nlf, h->grad_chunk + L.Tp < 2048 ? L.gorder : nullptr};
+                    L.gchunk, nlf, std::abs(L.gchunk) + L.T + L.Tp < 2048 ? L.gorder : nullptr, L.S};
         launch_grad<NB>(ga, s);
     }
     if (pm) pm->mark(s);

@@ -550,6 +550,20 @@ __device__ __forceinline__ void flow_update(FlowCtx& C, const FlowTile& t, int l
         pub_op2(x, C.P.L(t.i, l), y, C.P.X(l, t.j), C);  // L(i,l), X(l,c)^T (B[k][j] = X(l,c)[k][j])
         wt_mma<true>(acc, x, y);                         // R(i,c) -= L(i,l) X(l,c)
         wt_store<false>(acc, dst, a.ldr);
+    } else if (t.type == FT_S) {
+        // K^{-1} partial sum (FLOW_STILES): S(i,j) += X(l,i)^T X(l,j), both operands from the X^T
+        // publication slots (A[i'][k] = X(l,i)[k][i'] = X^T(l,i)[i'][k], B[k][j'] likewise)
+        double* dst = a.S + ((long)t.i * (t.i + 1) / 2 + t.j) * 1024;
+        if (l == t.lo) wt_zero(acc);
+        else wt_load<false>(acc, dst, 32);
+        if (t.j != t.i) {
+            pub_op2(x, C.P.X(l, t.i), y, C.P.X(l, t.j), C);
+        } else {
+            pub_op(x, C.P.X(l, t.i), C);
+            y = x;
+        }
+        wt_mma<false>(acc, x, y);
+        wt_store<false>(acc, dst, 32);
     } else {
         const int c = t.i, cy = t.j;
         double* al = a.alpha + (long)c * 32 * a.ldal + (long)cy * 32;
@@ -596,7 +610,8 @@ __device__ __forceinline__ void flow_item_log(const FlowCtx& C, int wid, int n, 
 __device__ __forceinline__ int flow_prio(int code) {
     if (code < 0) return 1 << 30;
     const FlowTile t = flow_tile(code, 1024);
-    // H_k first: the R finalizes of the same level wait for it (a later slot would deadlock)
+    // H_k first: the R finalizes of the same level wait for it (a later slot would deadlock);
+    // S tiles (FT_S = 4) last: nothing in the launch waits for them
     const int rank = t.type == FT_H ? 0 : t.type + 1;
     return (rank << 16) | (t.i << 8) | t.j;
 }
@@ -932,13 +947,15 @@ __device__ __forceinline__ void diag_prefetch(FlowCtx& C, const DiagLds& B, bool
         double* dst = sub ? B.Ap(pj) : B.Cp(pj);
         WTile acc;
         WOp x, y;
-        if (j >= 4) pub_wt_op_direct(acc, C.P.H(sub ? 0 : 1, j), x, C.P.L(j, j - 3), C);
-        else {
+        if (j >= 4) {
+            if (FLOW_BAND3) pub_wt(acc, C.P.H(sub ? 0 : 1, j), C);
+            else pub_wt_op_direct(acc, C.P.H(sub ? 0 : 1, j), x, C.P.L(j, j - 3), C);
+        } else {
             wt_load<true>(acc, sub ? C.At(j, j - 1) : C.At(j, j), a.lda);   // k_gram's values
             if (j == 3) pub_op(x, C.P.L(j, j - 3), C);
         }
         if (a.trace && (threadIdx.x & 63) == 0) a.trace[(sub ? 5 : 6) * T + j] = flow_clock() - C.t0;
-        if (j >= 3) {
+        if (j == 3 || (j > 3 && !FLOW_BAND3)) {   // (FLOW_BAND3: the owner applied it, rows >= 4)
             // panel j-3 from the worker's L(j,j-3) and L(j-1,j-3) (wave 5, step j-1)
             lds_wait_ge(&B.w()[DW_P2], j - 1);
             if (sub) {

@@ -238,7 +238,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
     }
     if (!LEAN && a.fown && blockIdx.x == gridDim.x - 1 - (a.gorder ? 1 : 0)) {   // extra: flow owner table
         if (b == 0) build_flow_owner(a.npad / NB, a.ppad / NB, a.fW, a.fown, a.fflags, a.nfflags,
-                                     reinterpret_cast<int*>(smem));
+                                     reinterpret_cast<int*>(smem), a.fsdelta);
         if (a.dbg && threadIdx.x == 0) a.dbg[3 * blockIdx.x + 2] = __builtin_amdgcn_s_memrealtime() - dbg_t0;
         gram_fill_pub(a);
         return;
@@ -564,7 +564,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram_flow(GramArgs a, int nblk) {
     if (bx >= nblk + nfac) {   // set-up workgroups (LDS as int scratch)
         int* sh = reinterpret_cast<int*>(smem);
         if (a.gorder && bx == (int)gridDim.x - 1) build_grad_order(a.gT, a.gchunk, a.gTp, a.gorder, sh);
-        else if (a.fown) build_flow_owner(a.npad / 32, a.ppad / 32, a.fW, a.fown, a.fflags, a.nfflags, sh);
+        else if (a.fown) build_flow_owner(a.npad / 32, a.ppad / 32, a.fW, a.fown, a.fflags, a.nfflags, sh, a.fsdelta);
         if (a.dbg && t == 0) { a.dbg[3 * bx] = t0; a.dbg[3 * bx + 1] = __builtin_amdgcn_s_memrealtime(); }
         gram_fill_pub(a);
         if (a.dbg && t == 0) a.dbg[3 * bx + 2] = __builtin_amdgcn_s_memrealtime();
@@ -990,7 +990,11 @@ constexpr int GRAD_RLD = 65;   // 64 quad partials per gradient entry, +1 agains
 template <int NB>
 constexpr int GRAD_RED_OFF = (2 * NB * XS + 2 * NB + 1) & ~1;
 
-__host__ __device__ inline int grad_row_chunks(int T, int i, int ch) { return (T - i + ch - 1) / ch; }
+// ch < 0 (the flow's S tiles, FLOW_STILES = -ch): one task per lower tile, rows m >= max(i, T + ch)
+// on top of the flow's partial sum
+__host__ __device__ inline int grad_row_chunks(int T, int i, int ch) { return ch < 0 ? 1 : (T - i + ch - 1) / ch; }
+__host__ __device__ inline int grad_m0(int T, int i, int ch, int c) { return ch < 0 ? max(i, T + ch) : i + c * ch; }
+__host__ __device__ inline int grad_m1(int T, int m0, int ch) { return ch < 0 ? T : min(T, m0 + ch); }
 
 __host__ __device__ int grad_tasks(int T, int ch) {
     int s = 0;
@@ -1009,8 +1013,8 @@ __device__ __forceinline__ int grad_decode(int t, int T, int chunk, int Tp, int&
     const int nch = grad_row_chunks(T, i, chunk);
     j = t / nch;
     ch = t % nch;
-    const int m0 = i + ch * chunk;
-    return min(T, m0 + chunk) - m0 + (ch == 0 ? Tp : 0);
+    const int m0 = grad_m0(T, i, chunk, ch);
+    return grad_m1(T, m0, chunk) - m0 + (ch == 0 ? Tp : 0);
 }
 
 // Workgroup -> task table for k_grad.  All k_grad workgroups are resident at once and
@@ -1023,7 +1027,7 @@ __device__ __forceinline__ int grad_decode(int t, int T, int chunk, int Tp, int&
 constexpr int GRAD_ORDER_MAGIC = 0x4F524431;
 __device__ void build_grad_order(int T, int chunk, int Tp, int* order, int* hist) {
     const int ntask = grad_tasks(T, chunk);
-    const int lmax = chunk + Tp;
+    const int lmax = (chunk < 0 ? T : chunk) + Tp;
     unsigned* hs = reinterpret_cast<unsigned*>(hist + lmax + 1);
     if (sched_cached(order, ntask, GRAD_ORDER_MAGIC, T, chunk, Tp, hs)) return;
     for (int l = threadIdx.x; l <= lmax; l += NTHREADS) hist[l] = 0;
@@ -1077,13 +1081,14 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
     const int task = a.order ? a.order[blockIdx.x] : (int)blockIdx.x;
     int i, j, ch;
     grad_decode(task, a.T, a.chunk, a.Tp, i, j, ch);
-    const int m0 = i + ch * a.chunk;
-    const int m1 = min(a.T, m0 + a.chunk);
+    const int m0 = grad_m0(a.T, i, a.chunk, ch);
+    const int m1 = grad_m1(a.T, m0, a.chunk);
     auto Xt = [&](int r, int c) { return a.Xo + (long)r * NB * a.ldx + (long)c * NB; };
 
     // W_ij (tile) = [alpha_i alpha_j^T] - P * sum_m Linv_mi^T Linv_mj  (= -P * acc below)
     Acc<NB> acc;
     acc_zero(acc);
+    if (a.chunk < 0 && m0 > i) acc_load<NB>(acc, a.S + ((long)i * (i + 1) / 2 + j) * NB * NB, NB);   // flow's rows < m0
     const double negP = -(double)a.P;
     {   // Software-pipelined operand stream of TN items acc += A^T B (all unscaled):
         //   q < nm : A = Linv_{m,i}, B = Linv_{m,j}, m = m0 + q
