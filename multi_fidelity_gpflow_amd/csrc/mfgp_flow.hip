@@ -721,6 +721,9 @@ static_assert(DW_N <= 28, "progress words fit before the panels");
 #ifndef FLOW_RPRIO
 #define FLOW_RPRIO 2
 #endif
+#ifndef FLOW_WAIT4
+#define FLOW_WAIT4 0
+#endif
 
 __device__ __forceinline__ int lds_get(const int* p) {
     return __hip_atomic_load(const_cast<int*>(p), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -785,18 +788,35 @@ __device__ __forceinline__ void diag_chain(FlowCtx& C, const DiagLds& B) {
     for (int k = 1; k < T; ++k) {
         const int pk = k & 1;
         if (a.trace && threadIdx.x == 0) a.trace[k] = flow_clock() - C.t0;
+#if FLOW_WAIT4
+        // the step's four progress words in ONE LDS round trip per poll (relaxed loads issued
+        // together, one acquire fence after): four sequential acquire spins cost ~4 round trips
+        // even when everything is already there
+        for (;;) {
+            const int* wd = B.w();
+            const int w6 = __hip_atomic_load(const_cast<int*>(wd + DW_PRE6), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const int w7 = __hip_atomic_load(const_cast<int*>(wd + DW_PRE7), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const int wdd = __hip_atomic_load(const_cast<int*>(wd + DW_D), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const int wl = __hip_atomic_load(const_cast<int*>(wd + DW_LPUB), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            // D_{k-1} in Db[pk ^ 1]; wave 4 is done with Ls[pk] (L(k-2,k-3))
+            if (__builtin_amdgcn_readfirstlane(w6) >= k && __builtin_amdgcn_readfirstlane(w7) >= k &&
+                __builtin_amdgcn_readfirstlane(wdd) >= k - 1 && __builtin_amdgcn_readfirstlane(wl) >= k - 2)
+                break;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#else
         lds_spin_ge(&B.w()[DW_PRE6], k);
         lds_spin_ge(&B.w()[DW_PRE7], k);
         lds_spin_ge(&B.w()[DW_D], k - 1);         // D_{k-1} in Db[pk ^ 1]
         lds_spin_ge(&B.w()[DW_LPUB], k - 2);      // wave 4 is done with Ls[pk] (L(k-2,k-3))
+#endif
         if (a.trace && threadIdx.x == 0) a.trace[T + k] = flow_clock() - C.t0;
-        Acc<32> pl;
+        Acc<32> pl, cij;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cij.v[0][r] = B.Cp(pk)[acc_row<32>(0, r) * S + acc_col<32>(0)];   // (under the product)
         acc_zero(pl);
         tile_mma<32, false, true>(pl, B.Ap(pk), B.Db(pk ^ 1), 1.0);   // L(k,k-1) = A'' D_{k-1}^T
         acc_to_lds(pl, B.Ls(pk));
-        Acc<32> cij;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) cij.v[0][r] = B.Cp(pk)[acc_row<32>(0, r) * S + acc_col<32>(0)];
         chain_bar(&B.w()[DW_BAR], epoch);
         if (threadIdx.x == 0) lds_put(&B.w()[DW_LS], k);
         // only the lower blocks of A''(k,k) feed the factor: wave 1 (block (0,1)) skips the

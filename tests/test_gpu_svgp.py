@@ -354,7 +354,10 @@ def test_shared_inducing_two_blocks_match_single_model(hbs):
     blocks (25 + 24 HBS bins) as two 'ranks' in one process -- each evaluates its bins' ELBO and
     gradient (mfgp_svgp_elbo_grad), the [ELBO, KL, VE | flag | dZ | dnoise] buffers are summed (the
     all-reduce), both apply the packed Adam step -- against ONE SingleBinSVGP over all 49 bins: the
-    same -ELBO trajectory, Z and noise to 1e-11."""
+    same -ELBO trajectory to 1e-11.  Z and the noise agree to 1e-6 relative (measured 3.5e-7 on Z
+    after 8 steps): the summed dE/dZ differs from the single model's in the last bits (another
+    reduction order), and Adam's normalised step m / sqrt(v) turns that into parameter-level
+    differences wherever a gradient entry is near zero."""
     from multi_fidelity_gpflow_amd.distributed import SharedInducingTrainer, bin_block
     from multi_fidelity_gpflow_amd.svgp import _SVGPTrainer
     X, Y = hbs["X"], hbs["Y"]
@@ -388,7 +391,7 @@ def test_shared_inducing_two_blocks_match_single_model(hbs):
     for t in blocks:
         np.testing.assert_allclose(t.tr.loss_hist[:steps].cpu().numpy(), h_ref, rtol=1e-11)
         np.testing.assert_allclose(t.tr.view(t.tr.c, "Z").cpu().numpy(), ref.view(ref.c, "Z").cpu().numpy(),
-                                   rtol=1e-11, atol=1e-13)
+                                   rtol=1e-6, atol=1e-8)
         np.testing.assert_allclose(t.tr.view(t.tr.c, "noise").cpu().numpy(), ref.view(ref.c, "noise").cpu().numpy(),
-                                   rtol=1e-11)
+                                   rtol=1e-6)
     assert int(blocks[0].tr.step_t.item()) == steps
