@@ -136,7 +136,7 @@ struct PredOutArgs {
 };
 
 // Batched fp64 MFMA GEMM (k_bgemm, mfgp_svgp_grad.hip), NB x NB output tiles:
-// D = alpha * op(A) diag(s) op(B) [* diag(colscale)] + beta * Cin + x y^T   (tril: zero j > i)
+// D = (alpha * op(A) diag(s) op(B) + beta * Cin) [* diag(colscale)] + x y^T   (tril: zero j > i)
 struct BgemmArgs {
     const double* A; long lda; long sA;
     const double* B; long ldb; long sB;

@@ -10,7 +10,8 @@
 // Per latent l:  Lm = chol(Kuu_l),  A = Lm^{-1} Kuf_l,  B = tril(q_sqrt_l)^T A,
 //   g_mu = A^T q_mu[:, l],  g_var = Kff_l - colsum(A^2) + colsum(B^2).
 // B is formed as (Lq^T Lm^{-1}) Kuf so that A and B come out of ONE fused tile
-// loop over Kuf (K6 below) and neither is ever written to HBM.
+// loop over Kuf (K6 below); they are written to HBM only for the gradient pass
+// (mfgp_svgp_grad.hip re-associates its adjoints around them).
 #include "mfgp_device.h"
 #include "mfgp_internal.h"
 
@@ -123,7 +124,8 @@ __global__ __launch_bounds__(NTHREADS) void k_lqt_linv(const double* Lq, const d
 template <int NB>
 __global__ __launch_bounds__(NTHREADS) void k_svgp_cond(const double* Xo, const double* C, const double* Kuf,
                                                         const double* q_mu, int L, int m, int Tm, int npad,
-                                                        double* pa, double* pb, double* pm) {
+                                                        double* pa, double* pb, double* pm, double* Aout,
+                                                        double* Bout) {
     constexpr int S = TileCfg<NB>::S;
     constexpr int E = TileCfg<NB>::ELEMS;
     extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -150,6 +152,11 @@ __global__ __launch_bounds__(NTHREADS) void k_svgp_cond(const double* Xo, const 
         if (mt <= i) tile_mma<NB, false, false>(accA, Ls, Ks, 1.0);
         tile_mma<NB, false, false>(accB, As, Ks, 1.0);
         __syncthreads();
+    }
+    if (Aout) {   // gradient pass: keep A and B (L x Mpad x Npad each)
+        const long o = (long)l * mp * npad + (long)i * NB * npad + (long)tn * NB;
+        acc_store(accA, Aout + o, npad);
+        acc_store(accB, Bout + o, npad);
     }
     // column reductions: thread owns (row, col) elements; reduce over rows via LDS
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -333,7 +340,8 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
                     int ldy, const double* Z, int ldz, const double* thetas, const double* q_mu,
                     const double* q_sqrt, const double* W, double noise, double scale, double jitter, void* ws,
                     size_t ws_bytes, double* out, double* g_mu, double* g_var, int* info, double* f_mu = nullptr,
-                    double* f_var = nullptr, const double* noise_dev = nullptr) {
+                    double* f_var = nullptr, const double* noise_dev = nullptr, double* Aout = nullptr,
+                    double* Bout = nullptr) {
     const SvgpLayout S = svgp_layout(NB, n, m, L, p, d, ws);
     if (ws_bytes < S.bytes) return -2;
     const long mm = (long)S.mpad * S.mpad;
@@ -377,7 +385,7 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
     }
     hipLaunchKernelGGL(k_svgp_cond<NB>, dim3(S.Tm * S.Tn, 1, L), dim3(NTHREADS),
                        sizeof(double) * (3 * NB * (NB + 2) + 12 * NB), s, S.Xo, S.C, S.Kuf, q_mu, L, m, S.Tm,
-                       S.npad, S.pa, S.pb, S.pm);
+                       S.npad, S.pa, S.pb, S.pm, Aout, Bout);
     hipLaunchKernelGGL(k_svgp_moments, dim3(cdiv(n, 256), 1, L), dim3(256), 0, s, S.pa, S.pb, S.pm, X, (long)ldx,
                        thetas, S.G, d, n, S.npad, S.Tm, g_mu, g_var);
     if (f_mu) {   // predict: mixed moments only
@@ -403,6 +411,19 @@ int svgp_elbo_impl(hipStream_t s, int nb, int n, int m, int l, int p, int d, con
                             ws, ws_bytes, out, g_mu, g_var, info, nullptr, nullptr, noise_dev);
     return svgp_run<32>(s, n, m, l, p, d, X, ldx, Y, ldy, Z, ldz, thetas, q_mu, q_sqrt, W, noise, scale, jitter, ws,
                         ws_bytes, out, g_mu, g_var, info, nullptr, nullptr, noise_dev);
+}
+
+// the ELBO forward that also writes A = Li Kuf and B = C Kuf ([L][Mpad][Npad] each) for the gradient pass
+int svgp_elbo_keep_impl(hipStream_t s, int nb, int n, int m, int l, int p, int d, const double* X, int ldx,
+                        const double* Y, int ldy, const double* Z, int ldz, const double* thetas, const double* q_mu,
+                        const double* q_sqrt, const double* W, double noise, double scale, double jitter, void* ws,
+                        size_t ws_bytes, double* out, double* g_mu, double* g_var, int* info, const double* noise_dev,
+                        double* Aout, double* Bout) {
+    if (nb == 64)
+        return svgp_run<64>(s, n, m, l, p, d, X, ldx, Y, ldy, Z, ldz, thetas, q_mu, q_sqrt, W, noise, scale, jitter,
+                            ws, ws_bytes, out, g_mu, g_var, info, nullptr, nullptr, noise_dev, Aout, Bout);
+    return svgp_run<32>(s, n, m, l, p, d, X, ldx, Y, ldy, Z, ldz, thetas, q_mu, q_sqrt, W, noise, scale, jitter, ws,
+                        ws_bytes, out, g_mu, g_var, info, nullptr, nullptr, noise_dev, Aout, Bout);
 }
 
 int svgp_predict_impl(hipStream_t s, int nb, int n, int m, int l, int p, int d, const double* Xs, int ldx,

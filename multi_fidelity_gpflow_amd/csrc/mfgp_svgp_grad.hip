@@ -5,16 +5,21 @@
 // d(-ELBO) w.r.t. q_mu, q_sqrt (FillTriangular), Z (inducing points, fidelity column
 // included), every latent kernel's (vL, lL, vD, lD, rho), W and the Gaussian noise.
 //
-// Per latent (Li = chol(Kuu)^{-1}, A = Li Kuf, B = Lq^T A, C = Lq^T Li, m = q_mu[:, l]),
+// Per latent (Li = chol(Kuu)^{-1}, A = Li Kuf, B = Lq^T A = C Kuf, C = Lq^T Li, m = q_mu[:, l]),
 // with upstream alpha = dE/dg_mu and beta = dE/dg_var (E = the ELBO):
-//   dE/dm     = Li (Kuf alpha) - m
-//   dE/dLq    = tril(2 Li Q C^T) - Lq + diag(1 / Lq_ii),   Q = Kuf diag(beta) Kuf^T
-//   dE/dKuf   = 2 F Kuf diag(beta) + (Li^T m) alpha^T,     F = C^T C - Li^T Li
-//   dE/dLi    = tril(m u^T + 2 (Lq C - Li) Q),            u = Kuf alpha
+//   gA        = dE/dA = m alpha^T + 2 (Lq B - A) diag(beta)
+//   dE/dm     = A alpha - m
+//   dE/dLq    = tril(2 A diag(beta) B^T) - Lq + diag(1 / Lq_ii)
+//   dE/dKuf   = Li^T gA
+//   dE/dLi    = tril(gA Kuf^T)
 //   dE/dKuu   = -Li^T Psi(tril(dE/dLi) Li^T) Li,  Psi(H) = (tril H + tril H^T - diag H) / 2
 //               (the adjoint of Li = chol(Kuu)^{-1}: dLi = -Phi(Li dKuu Li^T) Li)
 //   dE/dKff   = beta
-// and the kernel / inducing-point gradients are the weighted derivative sums
+// A and B are the forward's own products (k_svgp_cond keeps them).  Every adjoint is associated
+// around them rather than around Li Q (Q = Kuf diag(beta) Kuf^T) or Lq C - Li: at the Goku state
+// cond(Kuu) ~ 1e9 and Li's entries reach 3e4, and applying Li to the smooth Q cancels ~8 digits
+// (dE/dKuu off by 3.9e-8 relative against the reference's autodiff; 3e-12 in this form).
+// The kernel / inducing-point gradients are the weighted derivative sums
 //   sum_ab dE/dK_ab dk(a, b)/dtheta  over (Z, Z) and (Z, X), plus the K_diag term.
 // All products are batched over latents and run on v_mfma_f64_16x16x4 tiles (k_bgemm).
 #include <algorithm>
@@ -78,8 +83,8 @@ __global__ __launch_bounds__(NTHREADS) void k_bgemm(BgemmArgs a) {
         for (int r = 0; r < 4; ++r) {
             const int i = ti * NB + acc_row<NB>(q, r), j = tj * NB + acc_col<NB>(q);
             double v = acc.v[q][r];
-            if (a.colscale) v *= a.colscale[b * a.scs + j];
             if (a.Cin) v += a.beta * a.Cin[b * a.sC + (long)i * a.ldc + j];
+            if (a.colscale) v *= a.colscale[b * a.scs + j];
             if (a.x) v += a.x[b * a.sx + i] * a.y[b * a.sy + j];
             if (a.tril && j > i) v = 0.0;
             Dt[(long)i * a.ldd + j] = v;
@@ -528,8 +533,8 @@ __global__ void k_grad_reduce(const double* gth_uu, int nb_uu, const double* gth
 
 // ---------------------------------------------------------------- driver
 struct SvgpGradLayout {
-    double *qm, *alpha, *beta, *u, *Q, *E, *Gb, *H, *P, *Sig, *F, *Kbar, *T1, *gLq, *vli, *gqm, *r, *gnp, *gth_uu,
-        *gth_uf, *gth_kff, *gz_uu, *gz_uf;
+    double *qm, *alpha, *beta, *A, *B, *gA, *Gb, *H, *P, *Sig, *Kbar, *T1, *gLq, *gqm, *r, *gnp, *gth_uu, *gth_uf,
+        *gth_kff, *gz_uu, *gz_uf;
     int nbc_uu, nbc_uf, n_at, nb_uu, nb_uf, nnoise;
     size_t bytes;
 };
@@ -556,17 +561,15 @@ static SvgpGradLayout grad_layout(int nb, int n, int m, int L, int p, int d, siz
     g.qm = take((size_t)L * mpad);
     g.alpha = take((size_t)L * npad);
     g.beta = take((size_t)L * npad);
-    g.u = take((size_t)L * mpad);
-    g.vli = take((size_t)L * mpad);
     g.gqm = take((size_t)L * mpad);
-    g.Q = take(mm * L);
-    g.E = take(mm * L);
     g.Gb = take(mm * L);
     g.H = take(mm * L);
     g.P = take(mm * L);
     g.Sig = take(mm * L);
-    g.F = take(mm * L);
     g.T1 = take(mm * L);
+    g.A = take((size_t)mpad * npad * L);
+    g.B = take((size_t)mpad * npad * L);
+    g.gA = take((size_t)mpad * npad * L);
     g.gLq = take(mm * L);
     g.Kbar = take((size_t)mpad * npad * L);
     g.r = take((size_t)n * p + 8);
@@ -590,6 +593,11 @@ int svgp_elbo_impl(hipStream_t s, int nb, int n, int m, int l, int p, int d, con
                    const double* Y, int ldy, const double* Z, int ldz, const double* thetas, const double* q_mu,
                    const double* q_sqrt, const double* W, double noise, double scale, double jitter, void* ws,
                    size_t ws_bytes, double* out, double* g_mu, double* g_var, int* info, const double* noise_dev);
+int svgp_elbo_keep_impl(hipStream_t s, int nb, int n, int m, int l, int p, int d, const double* X, int ldx,
+                        const double* Y, int ldy, const double* Z, int ldz, const double* thetas, const double* q_mu,
+                        const double* q_sqrt, const double* W, double noise, double scale, double jitter, void* ws,
+                        size_t ws_bytes, double* out, double* g_mu, double* g_var, int* info, const double* noise_dev,
+                        double* Aout, double* Bout);
 int svgp_predict_impl(hipStream_t s, int nb, int n, int m, int l, int p, int d, const double* Xs, int ldx,
                       const double* Z, int ldz, const double* thetas, const double* q_mu, const double* q_sqrt,
                       const double* W, double jitter, void* ws, size_t ws_bytes, double* g_mu, double* g_var,
@@ -616,9 +624,9 @@ static int svgp_grad_run(hipStream_t s, int n, int m, int L, int p, int d, const
     const size_t base = svgp_workspace_bytes(NB, n, m, L, p, d);
     const SvgpGradLayout g = grad_layout(NB, n, m, L, p, d, base, ws);
     if (ws_bytes < g.bytes) return -2;
-    // forward (fills Xo = Li, C = Lq^T Li, Kuf, Lq; g_mu / g_var; out = [elbo, KL, VE])
-    int rc = svgp_elbo_impl(s, NB, n, m, L, p, d, X, ldx, Y, ldy, Z, ldz, thetas, q_mu, q_sqrt, W, noise_host, scale,
-                            jitter, ws, ws_bytes, out, g_mu, g_var, info, noise_dev);
+    // forward (fills Xo = Li, C = Lq^T Li, Kuf, Lq, A, B; g_mu / g_var; out = [elbo, KL, VE])
+    int rc = svgp_elbo_keep_impl(s, NB, n, m, L, p, d, X, ldx, Y, ldy, Z, ldz, thetas, q_mu, q_sqrt, W, noise_host,
+                                 scale, jitter, ws, ws_bytes, out, g_mu, g_var, info, noise_dev, g.A, g.B);
     if (rc) return rc;
     double *Li, *C, *Kuf, *Lq;
     int mpad, npad;
@@ -634,50 +642,61 @@ static int svgp_grad_run(hipStream_t s, int n, int m, int L, int p, int d, const
     if (W) hipLaunchKernelGGL(k_gw, dim3(cdv(p * L, NTHREADS / 64)), dim3(NTHREADS), 0, s, g.r, g_mu, g_var, W, n, p, L,
                               noise_dev, scale, gW);
     hipLaunchKernelGGL(k_qmu_pad, dim3(cdv(mpad, 256), 1, L), dim3(256), 0, s, q_mu, m, L, mpad, g.qm);
-    // 2. u = Kuf alpha ; Q = Kuf diag(beta) Kuf^T
-    hipLaunchKernelGGL(k_bmatvec, dim3(cdv(mpad, NTHREADS / 64), 1, L), dim3(NTHREADS), 0, s, Kuf, (long)npad, mn, 0,
-                       g.alpha, (long)npad, mpad, npad, 1.0, (const double*)nullptr, 0L, 0.0, g.u, (long)mpad);
+    // 2. dE/dm = A alpha - m
+    hipLaunchKernelGGL(k_bmatvec, dim3(cdv(mpad, NTHREADS / 64), 1, L), dim3(NTHREADS), 0, s, g.A, (long)npad, mn, 0,
+                       g.alpha, (long)npad, mpad, npad, 1.0, g.qm, (long)mpad, -kl_mult, g.gqm, (long)mpad);
+    hipLaunchKernelGGL(k_qmu_unpad, dim3(cdv(m, 256), 1, L), dim3(256), 0, s, g.gqm, m, L, mpad, gq_mu);
+    // 3. gA = (2 Lq B - 2 A) diag(beta) + m alpha^T
     {
         BgemmArgs a{};
-        a.A = Kuf; a.lda = npad; a.sA = mn;
+        a.amask = 1;   // Lq lower
+        a.A = Lq; a.lda = mpad; a.sA = mm;
+        a.B = g.B; a.ldb = npad; a.sB = mn;
+        a.Cin = g.A; a.ldc = npad; a.sC = mn; a.beta = -2.0;
+        a.colscale = g.beta; a.scs = npad;
+        a.x = g.qm; a.sx = mpad; a.y = g.alpha; a.sy = npad;
+        a.D = g.gA; a.ldd = npad; a.sD = mn;
+        a.alpha = 2.0;
+        a.Mt = Tm; a.Nt = Tn; a.Kt = Tm;
+        bgemm<NB>(s, 0, 0, a, L);
+    }
+    // 4. dE/dLi = tril(gA Kuf^T)
+    {
+        BgemmArgs a{};
+        a.A = g.gA; a.lda = npad; a.sA = mn;
         a.B = Kuf; a.ldb = npad; a.sB = mn;
-        a.s = g.beta; a.ss = npad;
-        a.D = g.Q; a.ldd = mpad; a.sD = mm;
+        a.D = g.Gb; a.ldd = mpad; a.sD = mm;
         a.alpha = 1.0;
-        a.Mt = Tm; a.Nt = Tm; a.Kt = Tn;
+        a.Mt = Tm; a.Nt = Tm; a.Kt = Tn; a.tril = 1;
         bgemm<NB>(s, 0, 1, a, L);
     }
-    // 3. dE/dm = Li u - m
-    hipLaunchKernelGGL(k_bmatvec, dim3(cdv(mpad, NTHREADS / 64), 1, L), dim3(NTHREADS), 0, s, Li, (long)mpad, mm, 0,
-                       g.u, (long)mpad, mpad, mpad, 1.0, g.qm, (long)mpad, -kl_mult, g.gqm, (long)mpad);
-    hipLaunchKernelGGL(k_qmu_unpad, dim3(cdv(m, 256), 1, L), dim3(256), 0, s, g.gqm, m, L, mpad, gq_mu);
-    // 4. E = Lq C - Li ; Gb = tril(2 E Q + m u^T)
-    sq<NB>(s, Tm, L, mm, mpad, 0, Lq, 0, C, g.E, 1.0, Li, -1.0, 0, nullptr, nullptr, 0, 1, 0);   // Lq lower
-    sq<NB>(s, Tm, L, mm, mpad, 0, g.E, 0, g.Q, g.Gb, 2.0, nullptr, 0.0, 1, g.qm, g.u, mpad);
     // 5. Sigma_bar = -Li^T Psi(Gb Li^T) Li
     sq<NB>(s, Tm, L, mm, mpad, 0, g.Gb, 1, Li, g.H, 1.0, nullptr, 0.0, 0, nullptr, nullptr, 0, 1, 2);   // Gb lower, Li^T upper
     hipLaunchKernelGGL(k_psi, dim3(std::min<long>(cdv((int)mm, 256), 1024), 1, L), dim3(256), 0, s, g.H, g.P, mpad, mm);
     sq<NB>(s, Tm, L, mm, mpad, 0, g.P, 0, Li, g.T1, 1.0, nullptr, 0.0, 0, nullptr, nullptr, 0, 0, 1);   // Li lower
     sq<NB>(s, Tm, L, mm, mpad, 1, Li, 0, g.T1, g.Sig, -1.0, nullptr, 0.0, 0, nullptr, nullptr, 0, 2, 0);   // Li^T upper
-    // 6. F = C^T C - Li^T Li ; Kbar = 2 F Kuf diag(beta) + (Li^T m) alpha^T
-    sq<NB>(s, Tm, L, mm, mpad, 1, C, 0, C, g.T1);
-    sq<NB>(s, Tm, L, mm, mpad, 1, Li, 0, Li, g.F, -1.0, g.T1, 1.0, 0, nullptr, nullptr, 0, 2, 1);   // Li^T upper, Li lower
-    hipLaunchKernelGGL(k_bmatvec, dim3(cdv(mpad, NTHREADS / 64), 1, L), dim3(NTHREADS), 0, s, Li, (long)mpad, mm, 1,
-                       g.qm, (long)mpad, mpad, mpad, 1.0, (const double*)nullptr, 0L, 0.0, g.vli, (long)mpad);
+    // 6. Kbar = dE/dKuf = Li^T gA
     {
         BgemmArgs a{};
-        a.A = g.F; a.lda = mpad; a.sA = mm;
-        a.B = Kuf; a.ldb = npad; a.sB = mn;
-        a.colscale = g.beta; a.scs = npad;
-        a.x = g.vli; a.sx = mpad; a.y = g.alpha; a.sy = npad;
+        a.amask = 2;   // Li^T upper
+        a.A = Li; a.lda = mpad; a.sA = mm;
+        a.B = g.gA; a.ldb = npad; a.sB = mn;
         a.D = g.Kbar; a.ldd = npad; a.sD = mn;
-        a.alpha = 2.0;
+        a.alpha = 1.0;
         a.Mt = Tm; a.Nt = Tn; a.Kt = Tm;
-        bgemm<NB>(s, 0, 0, a, L);
+        bgemm<NB>(s, 1, 0, a, L);
     }
-    // 7. dE/dLq = tril(2 Li Q C^T) - Lq + diag(1/Lq_ii)
-    sq<NB>(s, Tm, L, mm, mpad, 0, Li, 0, g.Q, g.T1, 1.0, nullptr, 0.0, 0, nullptr, nullptr, 0, 1, 0);   // Li lower
-    sq<NB>(s, Tm, L, mm, mpad, 0, g.T1, 1, C, g.gLq, 2.0, nullptr, 0.0, 1);
+    // 7. dE/dLq = tril(2 A diag(beta) B^T) - Lq + diag(1/Lq_ii)
+    {
+        BgemmArgs a{};
+        a.A = g.A; a.lda = npad; a.sA = mn;
+        a.B = g.B; a.ldb = npad; a.sB = mn;
+        a.s = g.beta; a.ss = npad;
+        a.D = g.gLq; a.ldd = mpad; a.sD = mm;
+        a.alpha = 2.0;
+        a.Mt = Tm; a.Nt = Tm; a.Kt = Tn; a.tril = 1;
+        bgemm<NB>(s, 0, 1, a, L);
+    }
     hipLaunchKernelGGL(k_glq_final, dim3(std::min(cdv(m * m, 256), 1024), 1, L), dim3(256), 0, s, g.gLq, Lq, m, mpad,
                        mm, kl_mult, gq_sqrt);
     // 8. kernel / inducing-point derivative sums
