@@ -986,18 +986,21 @@ __device__ __forceinline__ void diag_prefetch(FlowCtx& C, const DiagLds& B, bool
             }
             wt_mma<true>(acc, x, y);
         }
+        long long* tw = a.trace ? a.trace + 8 * T + 3 * a.nwaves + 4 * FLOW_LOG * a.nwaves + (sub ? 2 : 4) * T : nullptr;
         if (j >= 2) {
             WOp x, y;
             lds_wait_ge(&B.w()[DW_P2], j - 1);
             lds_wait_ge(&B.w()[DW_L2], j);
             op_rows_lds_ld(x, B.L2(pj), S);
             lds_wait_ge(&B.w()[DW_LS], j - 1);
+            if (tw && (threadIdx.x & 63) == 0) tw[j] = flow_clock() - C.t0;
             if (sub) op_rows_lds_ld(y, B.Ls(pj ^ 1), S);
             else y = x;
             wt_mma<true>(acc, x, y);
         }
         wt_to_lds_ld(acc, dst, S);
         if ((threadIdx.x & 63) == 0) lds_put(done, j);
+        if (tw && (threadIdx.x & 63) == 0) tw[T + j] = flow_clock() - C.t0;
     }
 }
 
@@ -1034,9 +1037,9 @@ __global__ __launch_bounds__(FLOW_THREADS) void k_chol_flow(FlowArgs a) {
 
 long flow_npub(int T, int Tp) { return 1024L * (T * (T - 1) / 2 + T + T * (T + 1) / 2 + T * Tp + 4 * T); }
 int flow_nflags(int T, int Tp) { (void)T; (void)Tp; return 1; }   // the abort word
-// layout: chain / helper stamps [8T] | worker summaries + item logs | wave-5 detail [2T] | k_gram timeline
-// [flow_gram_dbg_count(T)] (the last region)
-int flow_trace_count(int T, int nwg) { return 8 * T + (3 + 4 * FLOW_LOG) * FLOW_WAVES * (nwg - 1) + 2 * T + flow_gram_dbg_count(T); }
+// layout: chain / helper stamps [8T] | worker summaries + item logs | wave-5 detail [2T] | wave-6 / 7 detail
+// [2T each: last waits done, published] | k_gram timeline [flow_gram_dbg_count(T)] (the last region)
+int flow_trace_count(int T, int nwg) { return 8 * T + (3 + 4 * FLOW_LOG) * FLOW_WAVES * (nwg - 1) + 6 * T + flow_gram_dbg_count(T); }
 
 void launch_chol_flow(const FlowArgs& a, int nwg, hipStream_t s) {
     static bool attr = false;

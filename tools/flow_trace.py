@@ -43,7 +43,7 @@ def main():
         ref = pub[k - 3] if k >= 3 else 0.0
         print(f"{k:2d} {st[k]:7.2f} {rdy[k]:7.2f} {rdy[k]-st[k]:5.2f} {fs[k]:7.2f} {pub[k]:7.2f} {pub[k]-pub[k-1]:5.2f}"
               f" | {r2[k]-ref:6.2f} {pp[k]-ref:6.2f} {qq[k]-ref:6.2f} {l2[k]-ref:6.2f}")
-    Wn = (cnt.value - 8 * T - 2 * T - 5 * (T * (T + 1) // 2 + 4)) // (3 + 4 * 40)
+    Wn = (cnt.value - 8 * T - 6 * T - 5 * (T * (T + 1) // 2 + 4)) // (3 + 4 * 40)
     w = tr[8 * T: 8 * T + 3 * Wn].reshape(-1, 3)
     busy = w[:, 1] > 0
     w = w[busy]
@@ -52,13 +52,18 @@ def main():
           f" max {w[:,2].max():.1f}")
     late = np.argsort(-w[:, 1])[:8]
     print("latest workers (start, done, waited):", [tuple(np.round(w[i], 1)) for i in late])
-    W = (cnt.value - 8 * T - 2 * T - 5 * (T * (T + 1) // 2 + 4)) // (3 + 4 * 40)
-    w5 = tr[8 * T + 3 * W + 4 * 40 * W: 8 * T + 3 * W + 4 * 40 * W + 2 * T]
+    W = (cnt.value - 8 * T - 6 * T - 5 * (T * (T + 1) // 2 + 4)) // (3 + 4 * 40)
+    w5 = tr[8 * T + 3 * W + 4 * 40 * W: 8 * T + 3 * W + 4 * 40 * W + 6 * T]
     print(" j  got A(j,j-2) | gate open  waits done  L(j,j-2)   (wave 5, us after D_j-3 published; D_j-2 at)")
     for j in range(4, T):
         ref = pub[j - 3]
         print(f"{j:2d} {r2[j]-ref:6.2f} | {w5[j]-ref:6.2f} {w5[T + j]-ref:6.2f} {l2[j]-ref:6.2f}   D_j-2 {pub[j-2]-ref:5.2f}"
               f"  P2(j-1)~{fs[j-1]-ref:5.2f}")
+    print(" k  | chain: start  A'ready  fstart | w5 L(k,k-2) | w6 waits  done | w7 waits  done   (us after D_k-2 factor start)")
+    for k in range(4, T):
+        ref = fs[k - 2]
+        print(f"{k:2d}  | {st[k]-ref:6.2f} {rdy[k]-ref:7.2f} {fs[k]-ref:7.2f} | {l2[k]-ref:9.2f} |"
+              f" {w5[2 * T + k]-ref:7.2f} {w5[3 * T + k]-ref:6.2f} | {w5[4 * T + k]-ref:7.2f} {w5[5 * T + k]-ref:6.2f}")
     G = T * (T + 1) // 2 + 4   # k_gram timeline: [3 G] stamps, then [2 G] (mfgp_flow.h flow_gram_dbg_count)
     g = ws[off.value + 8 * (cnt.value - 5 * G): off.value + 8 * cnt.value].view(torch.int64).cpu().numpy()[:3 * G].reshape(-1, 3)
     gg = g.astype(np.float64) / 100.0
