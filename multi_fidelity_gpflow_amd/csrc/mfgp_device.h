@@ -345,9 +345,21 @@ __device__ __forceinline__ void w1_rwork(const W1Pending& pd, f64x4& r00, f64x4&
 }
 
 
-template <int K>
+// Round publication for a band wave (tile_band_w1_wave, PUB = true): round K writes, after its
+// rank-4 MFMA is issued, Yb[128 K + 4 row + c] = y_row[c] of the rows below the pivots (0 for the
+// pivot rows and above), Fb[16 K + 0 .. 9] = L10 L20 L30 L21 L31 L32 i0 i1 i2 i3 of the pivot
+// block, the pivots into dpv (as always), then the progress word *prog = base + K + 1.
+struct W1Pub {
+    double* Yb;
+    double* Fb;
+    int* prog;
+    int base;
+};
+
+template <int K, bool PUB = false>
 __device__ __forceinline__ void w1_round(double* __restrict__ Pn, double* __restrict__ dpv, f64x4& a00, f64x4& a01,
-                                         f64x4& a11, f64x4& r00, f64x4& r10, f64x4& r11, W1Pending& pd, int l) {
+                                         f64x4& a11, f64x4& r00, f64x4& r10, f64x4& r11, W1Pending& pd, int l,
+                                         const W1Pub& pub = W1Pub{}) {
     if constexpr (K < 8) {
         constexpr int bk = K >> 2, kq = K & 3;
         const int lc = l & 15, kk = l >> 4;
@@ -384,7 +396,7 @@ __device__ __forceinline__ void w1_round(double* __restrict__ Pn, double* __rest
         const double i3 = W1RCP(d3);
 #undef W1RCP
         // ---- per row: Y = C L_M^{-T}, Z = Y D_M^{-1}; A -= Z Y^T (symmetric form)
-        double zA[2], yB[2], zs[2][4] = {};
+        double zA[2], yB[2], ym[2] = {0.0, 0.0}, zs[2][4] = {};
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             if (h < bk) { zA[h] = 0.0; yB[h] = 0.0; continue; }
@@ -400,6 +412,7 @@ __device__ __forceinline__ void w1_round(double* __restrict__ Pn, double* __rest
             const double z0 = y0 * i0, z1 = y1 * i1, z2 = y2 * i2, z3 = y3 * i3;
             zA[h] = below ? sel4(kk, z0, z1, z2, z3) : 0.0;
             yB[h] = sel4(kk, y0, y1, y2, y3);
+            if constexpr (PUB) ym[h] = below ? yB[h] : 0.0;
             zs[h][0] = z0; zs[h][1] = z1; zs[h][2] = z2; zs[h][3] = z3;
         }
         // ---- rank-4 update of A on the matrix core (an f64 MFMA holds the SIMD for 64 clocks,
@@ -424,17 +437,28 @@ __device__ __forceinline__ void w1_round(double* __restrict__ Pn, double* __rest
             for (int c = 0; c < 4; ++c) pd.v[h][c] = piv ? (p == c ? 1.0 : 0.0) : zs[h][c];
         }
         pd.L10 = L10; pd.L20 = L20; pd.L30 = L30; pd.L21 = L21; pd.L31 = L31; pd.L32 = L32;
+        if constexpr (PUB) {
+            pub.Yb[128 * K + lc * 4 + kk] = ym[0];
+            pub.Yb[128 * K + (16 + lc) * 4 + kk] = ym[1];
+            const int g = l >> 2, c = l & 3;
+            const double f0 = sel4(c, L10, L20, L30, L21), f1 = sel4(c, L31, L32, i0, i1), f2 = sel4(c, i2, i3, 0.0, 0.0);
+            pub.Fb[16 * K + (l < 12 ? l : 12 + c)] = g == 0 ? f0 : (g == 1 ? f1 : f2);
+            asm volatile("" ::: "memory");
+            __hip_atomic_store(pub.prog, pub.base + K + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
         __builtin_amdgcn_sched_barrier(0);
-        w1_round<K + 1>(Pn, dpv, a00, a01, a11, r00, r10, r11, pd, l);
+        w1_round<K + 1, PUB>(Pn, dpv, a00, a01, a11, r00, r10, r11, pd, l, pub);
     } else {
         w1_rwork<7>(pd, r00, r10, r11, l);
     }
 }
 
-// Body run by ONE wave (any wave of the workgroup; no workgroup barrier inside).
+// Body run by ONE wave (any wave of the workgroup; no workgroup barrier inside).  PUB: also
+// publish every round for a band wave (W1Pub).
+template <bool PUB = false>
 __device__ __forceinline__ void tile_potrf_inv_w1_wave(const double* __restrict__ X, int ldx, double* __restrict__ Pn,
                                                        double* __restrict__ R, double* __restrict__ dg,
-                                                       int* __restrict__ bad) {
+                                                       int* __restrict__ bad, const W1Pub& pub = W1Pub{}) {
     constexpr int S = TileCfg<32>::S;
     {
         const int l = threadIdx.x & 63, lc = l & 15, lr = l >> 4;
@@ -452,7 +476,7 @@ __device__ __forceinline__ void tile_potrf_inv_w1_wave(const double* __restrict_
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // X fully read before Pn (may alias) is written
         double* dpv = Pn + 128;                                // [32] pivots + dump slots
         W1Pending pd;
-        w1_round<0>(Pn, dpv, a00, a01, a11, r00, r10, r11, pd, l);
+        w1_round<0, PUB>(Pn, dpv, a00, a01, a11, r00, r10, r11, pd, l, pub);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         // L^{-1} = diag(d)^{-1/2} L_u^{-1}; L_ii = sqrt(d_i); first bad pivot by one ballot
         double s0[4], s1[4];
@@ -657,6 +681,99 @@ __device__ __forceinline__ void tile_rinv_w1_wave(const double* __restrict__ Zb,
         R[r * S + 16 + lc] = 0.0;
         R[(16 + r) * S + lc] = r10[q] * s1[q];
         R[(16 + r) * S + 16 + lc] = (lc <= r) ? r11[q] * s1[q] : 0.0;
+    }
+}
+
+// ---------------------------------------------------------------- band wave (tall panel)
+// Eliminates the 32 x 32 sub-diagonal block B = A(k+1, k) of the tall panel [A(k,k); A(k+1,k)] in
+// lock-step with the diagonal factor's rounds (tile_potrf_inv_w1_wave<true> publishing Yb / Fb /
+// dpv / prog), so that L(k+1,k) = B L_kk^{-T} comes out of the elimination itself instead of a
+// product with D_k = L_kk^{-1}, and accumulates S = L(k+1,k) L(k+1,k)^T round by round (the
+// update of A(k+1,k+1)).  Round K: the pivot columns C_i = B[i, 4K .. 4K+3] (rows i = 16 ib + lc,
+// through a 128-double LDS scratch Q), y_i = C_i L_M^{-T}, z_i = y_i D_M^{-1} with the pivot
+// block's factors as the diagonal wave computed them (Fb), then
+//   B[i, j] -= z_i y_j   for the later pivot columns j (y_j: the diagonal wave's rows, Yb),
+//   S += y z^T,          L(k+1,k)[i, 4K + c] = y_i[c] / sqrt(d_{4K+c}).
+// B is held transposed in accumulator layout (bt[jb][ib]: rows j = 16 jb + (l >> 4) + 4q,
+// columns i = 16 ib + (l & 15)), so round K's pivot columns are register K & 3 of block row K / 4,
+// exactly as the diagonal wave holds its pivot rows.
+template <int K>
+__device__ __forceinline__ void w1b_round(const double* __restrict__ Yb, const double* __restrict__ Fb,
+                                          const double* __restrict__ dpv, const int* prog, int base,
+                                          double* __restrict__ Q, f64x4 (&bt)[2][2], f64x4& s00, f64x4& s10,
+                                          f64x4& s11, double* __restrict__ Lo, int ldl, int l) {
+    if constexpr (K < 8) {
+        constexpr int bk = K >> 2, kq = K & 3;
+        const int lc = l & 15, kk = l >> 4;
+        Q[lc * 4 + kk] = bt[bk][0][kq];
+        Q[(16 + lc) * 4 + kk] = bt[bk][1][kq];
+        asm volatile("" ::: "memory");
+        while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(const_cast<int*>(prog), __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_WORKGROUP)) < base + K + 1) {}
+        asm volatile("" ::: "memory");
+        const f64x2* Qr = reinterpret_cast<const f64x2*>(Q);
+        const f64x2 u0a = Qr[2 * lc], u0b = Qr[2 * lc + 1], u1a = Qr[2 * (16 + lc)], u1b = Qr[2 * (16 + lc) + 1];
+        const f64x2* F = reinterpret_cast<const f64x2*>(Fb + 16 * K);
+        const f64x2 f0 = F[0], f1 = F[1], f2 = F[2], f3 = F[3], f4 = F[4];
+        const double L10 = f0.x, L20 = f0.y, L30 = f1.x, L21 = f1.y, L31 = f2.x, L32 = f2.y;
+        const double i0 = f3.x, i1 = f3.y, i2 = f4.x, i3 = f4.y;
+        double yA[2] = {0.0, 0.0};
+#pragma unroll
+        for (int jb = bk; jb < 2; ++jb) yA[jb] = Yb[128 * K + (16 * jb + lc) * 4 + kk];
+        const double rs = rsq_nr(dpv[4 * K + kk]);
+        __builtin_amdgcn_sched_barrier(0);
+        double yk[2], zk[2];
+#pragma unroll
+        for (int ib = 0; ib < 2; ++ib) {
+            const f64x2 ua = ib ? u1a : u0a, ub = ib ? u1b : u0b;
+            const double y0 = ua.x;
+            const double y1 = fma(-L10, y0, ua.y);
+            const double y2 = fma(-L21, y1, fma(-L20, y0, ub.x));
+            const double y3 = fma(-L32, y2, fma(-L31, y1, fma(-L30, y0, ub.y)));
+            yk[ib] = sel4(kk, y0, y1, y2, y3);
+            zk[ib] = sel4(kk, y0 * i0, y1 * i1, y2 * i2, y3 * i3);
+        }
+        if constexpr (K < 7) {
+#pragma unroll
+            for (int jb = bk; jb < 2; ++jb) {
+                bt[jb][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(-yA[jb], zk[0], bt[jb][0], 0, 0, 0);
+                bt[jb][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(-yA[jb], zk[1], bt[jb][1], 0, 0, 0);
+            }
+        }
+        s00 = __builtin_amdgcn_mfma_f64_16x16x4f64(yk[0], zk[0], s00, 0, 0, 0);
+        s10 = __builtin_amdgcn_mfma_f64_16x16x4f64(yk[1], zk[0], s10, 0, 0, 0);
+        s11 = __builtin_amdgcn_mfma_f64_16x16x4f64(yk[1], zk[1], s11, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        Lo[lc * ldl + 4 * K + kk] = yk[0] * rs;
+        Lo[(16 + lc) * ldl + 4 * K + kk] = yk[1] * rs;
+        w1b_round<K + 1>(Yb, Fb, dpv, prog, base, Q, bt, s00, s10, s11, Lo, ldl, l);
+    }
+}
+
+// B: the sub-diagonal block (row-major, stride ldb, LDS or global); Lo: L(k+1,k) (stride ldl);
+// So: S = L L^T, lower 16 x 16 blocks (0,0), (1,0), (1,1) written (stride lds), (0,1) untouched.
+// Q: 128 doubles of LDS private to this wave.  Yb, Fb, dpv, prog, base: the diagonal wave's W1Pub
+// and pivots of the same step.
+__device__ __forceinline__ void tile_band_w1_wave(const double* __restrict__ B, int ldb, const double* __restrict__ Yb,
+                                                  const double* __restrict__ Fb, const double* __restrict__ dpv,
+                                                  const int* prog, int base, double* __restrict__ Q,
+                                                  double* __restrict__ Lo, int ldl, double* __restrict__ So, int lds) {
+    const int l = threadIdx.x & 63, lc = l & 15, lr = l >> 4;
+    f64x4 bt[2][2];
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+        for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) bt[jb][ib][q] = B[(16 * ib + lc) * ldb + 16 * jb + lr + 4 * q];
+    f64x4 s00 = {0.0, 0.0, 0.0, 0.0}, s10 = s00, s11 = s00;
+    w1b_round<0>(Yb, Fb, dpv, prog, base, Q, bt, s00, s10, s11, Lo, ldl, l);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int r = lr + 4 * q;
+        So[r * lds + lc] = s00[q];
+        So[(16 + r) * lds + lc] = s10[q];
+        So[(16 + r) * lds + 16 + lc] = s11[q];
     }
 }
 

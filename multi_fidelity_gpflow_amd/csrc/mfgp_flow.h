@@ -9,6 +9,11 @@ namespace mfgp {
 #ifndef FLOW_BAND3
 #define FLOW_BAND3 0
 #endif
+// FLOW_W5OWN: the band tile (k,k-2) of rows k >= 4 takes panel k-3 from its owner too, so wave 5
+// of the diag workgroup forms L(k,k-2) = A''(k,k-2) D_{k-2}^T as soon as D_{k-2} is out
+#ifndef FLOW_W5OWN
+#define FLOW_W5OWN 0
+#endif
 // FLOW_STILES = sd > 0: the flow's idle worker waves also accumulate the partial sums of the
 // gradient's K^{-1} = L^{-T} L^{-1} tiles, S(i,j) = sum_{l = i .. T-1-sd} X(l,i)^T X(l,j) (X = L^{-1}
 // row blocks, read from their publication slots as they come out), into a workspace buffer; k_grad
@@ -82,7 +87,12 @@ __host__ __device__ inline FlowTile flow_tile(int code, int T) {
         // FLOW_BAND3: (k,k-1) and (k,k) of rows k >= 4 also take panel k-3 here, so the diag
         // workgroup's prefetch waves apply only panel k-2 (the tiles are needed a step later than
         // (k,k-2), whose panel k-3 stays in diag ahead of its L(k,k-2) product)
-        if (t.i <= t.j + 2) { t.hi = (FLOW_BAND3 && t.i >= 4 && t.i < t.j + 2) ? t.i - 3 : t.i - 4; t.fin = -1; t.pub = 1; }
+        if (t.i <= t.j + 2) {
+            const bool own3 = t.i >= 4 && ((FLOW_BAND3 && t.i < t.j + 2) || (FLOW_W5OWN && t.i == t.j + 2));
+            t.hi = own3 ? t.i - 3 : t.i - 4;
+            t.fin = -1;
+            t.pub = 1;
+        }
         else { t.hi = t.j - 1; t.fin = t.j; }
     } else if (t.type == FT_R) {
         t.lo = (t.j < T) ? t.j : 0;

@@ -916,6 +916,9 @@ __device__ __forceinline__ void diag_publisher(FlowCtx& C, const DiagLds& B) {
 // wave 5 shares SIMD 1 with chain wave 1, whose last MFMA of a step is its block of the first
 // product (L(k,k-1))
 #define W5_GATE DW_LS
+#ifndef FLOW_W5GATE
+#define FLOW_W5GATE 1
+#endif
 __device__ __forceinline__ void diag_second(FlowCtx& C, const DiagLds& B) {
     constexpr int S = TileCfg<32>::S;
     const FlowArgs& a = C.a;
@@ -923,15 +926,17 @@ __device__ __forceinline__ void diag_second(FlowCtx& C, const DiagLds& B) {
     for (int j = 2; j < T; ++j) {
         WTile acc;
         WOp x, y;
-        if (j >= 4) pub_wt_op_direct(acc, C.P.H(2, j), x, C.P.L(j, j - 3), C);
-        else {
+        if (j >= 4) {
+            if (FLOW_W5OWN) pub_wt(acc, C.P.H(2, j), C);
+            else pub_wt_op_direct(acc, C.P.H(2, j), x, C.P.L(j, j - 3), C);
+        } else {
             wt_load<true>(acc, C.At(j, j - 2), a.lda);  // A(2,0), A(3,1): k_gram's values
             if (j == 3) pub_op(x, C.P.L(j, j - 3), C);
         }
         if (a.trace && (threadIdx.x & 63) == 0) a.trace[4 * T + j] = flow_clock() - C.t0;
-        if (j >= 3) {
+        if (j == 3 || (j > 3 && !FLOW_W5OWN)) {
             // panel j-3: A(j,j-2) -= L(j,j-3) L(j-2,j-3)^T  (the worker's L, the chain's Ls of step j-2)
-            lds_wait_ge(&B.w()[W5_GATE], j - 1);          // MFMA only once the chain's step j-1 products
+            if (FLOW_W5GATE) lds_wait_ge(&B.w()[W5_GATE], j - 1);   // MFMA only once the chain's step j-1 products
             lds_wait_ge(&B.w()[DW_LS], j - 2);            // on SIMD 1 are done (an earlier window in the
                                                           // factor, or none, measured slower)
             if (a.trace && (threadIdx.x & 63) == 0) a.trace[8 * T + 3 * a.nwaves + 4 * FLOW_LOG * a.nwaves + j] = flow_clock() - C.t0;
@@ -939,7 +944,7 @@ __device__ __forceinline__ void diag_second(FlowCtx& C, const DiagLds& B) {
             wt_mma<true>(acc, x, y);
         }
         lds_wait_ge(&B.w()[DW_D], j - 2);
-        lds_wait_ge(&B.w()[W5_GATE], j - 1);
+        if (FLOW_W5GATE) lds_wait_ge(&B.w()[W5_GATE], j - 1);
         lds_wait_ge(&B.w()[DW_PRE6], j - 1);              // L2[j & 1] = L(j-2,j-4): last read by
         lds_wait_ge(&B.w()[DW_PRE7], j - 2);              // wave 6 at j-1, wave 7 at j-2
         if (a.trace && (threadIdx.x & 63) == 0) a.trace[8 * T + 3 * a.nwaves + 4 * FLOW_LOG * a.nwaves + T + j] = flow_clock() - C.t0;

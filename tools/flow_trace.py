@@ -84,7 +84,7 @@ def main():
                 (0, kk, kk - 3), (0, kk - 1, kk - 5), (0, kk, kk - 5)}
         print(f"   (D_{kk-5} {pub[kk-5]:.2f}  D_{kk-4} {pub[kk-4]:.2f}  D_{kk-3} {pub[kk-3]:.2f})")
         for (wv, code, lev, b, r, e) in its:
-            ty, i, j = code >> 20, (code >> 10) & 1023, code & 1023
+            ty, i, j = (code >> 20) & 15, (code >> 10) & 1023, code & 1023
             if (ty, i, j) in want and lev >= kk - 7:
                 print(f"   {names[ty]}({i},{j}) lvl {lev:2d}: begin {b:7.2f} ready {r:7.2f} end {e:7.2f}  (work {e-r:5.2f})")
     # lag of the L^{-1} / Z / alpha pipelines behind the chain: per level, latest item end - D_l published
@@ -94,7 +94,7 @@ def main():
         for kind in ("A", "R", "Y", "al"):
             ends = []
             for (wv, code, lv, b, r, e) in its:
-                ty, i, j = code >> 20, (code >> 10) & 1023, code & 1023
+                ty, i, j = (code >> 20) & 15, (code >> 10) & 1023, code & 1023
                 k2 = {0: "A", 1: ("Y" if j >= T else "R"), 2: "al", 3: "H"}[ty]
                 if k2 != kind:
                     continue
@@ -107,7 +107,7 @@ def main():
     Tm = T - 1
     print(f"-- tail: last items of row {Tm} R / Y tiles and alpha tiles (D_{Tm} published at {pub[Tm]:.2f})")
     for (wv, code, lv, b, r, e) in sorted(its, key=lambda x: x[5]):
-        ty, i, j = code >> 20, (code >> 10) & 1023, code & 1023
+        ty, i, j = (code >> 20) & 15, (code >> 10) & 1023, code & 1023
         if lv < Tm - 3:
             continue
         if (ty == 1 and i == Tm and (j in (0, 10, 20, 30, Tm - 1) or j >= T)) or (ty == 2 and i in (0, 20, Tm)):
