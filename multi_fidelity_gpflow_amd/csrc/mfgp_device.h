@@ -684,6 +684,105 @@ __device__ __forceinline__ void tile_rinv_w1_wave(const double* __restrict__ Zb,
     }
 }
 
+// ---------------------------------------------------------------- two-half inverse
+// D = L^{-1} of tile_elim_w1_wave's elimination on TWO waves, by halves of the unit factor
+// L~ = [[A, 0], [B, C]] (16 x 16 blocks; L = L~ diag(d)^{1/2}):
+//   * wave Ra (tile_rinv_lo_w1_wave) follows rounds 0..3 only: A^{-1} by the rank-4 updates of the
+//     fused factor's R00 block, then T = B A^{-1} (4 MFMAs, B = the rows 16..31 z of rounds
+//     0..3) into LDS, and D00 = diag(d)^{-1/2} A^{-1};
+//   * wave Rb (tile_rinv_hi_w1_wave) follows rounds 4..7 only: C^{-1} (R11), D11 = diag(d)^{-1/2}
+//     C^{-1}, then D10 = -D11 T (4 MFMAs), dg and the first bad pivot.
+// Neither half waits on the other's rounds: the inverse's serial chain is half as long as the
+// single R wave's (tile_rinv_w1_wave), and C^{-1} starts as soon as round 4 is out.
+template <int K, int H>
+__device__ __forceinline__ void w1h_round(const double* __restrict__ Zb, const int* prog, int base, f64x4& r, int l) {
+    if constexpr (K < 4 * H + 4) {
+        constexpr int kq = K & 3;
+        const int lc = l & 15, kk = l >> 4, p = lc & 3;
+        while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(const_cast<int*>(prog), __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_WORKGROUP)) < base + K + 1) {}
+        asm volatile("" ::: "memory");
+        const double* Z = Zb + 128 * K;
+        const f64x2 p2 = *reinterpret_cast<const f64x2*>(Z + 4 * (4 * K + 2));
+        const f64x2 p3a = *reinterpret_cast<const f64x2*>(Z + 4 * (4 * K + 3));
+        const double L10 = Z[4 * (4 * K + 1)], L20 = p2.x, L21 = p2.y, L30 = p3a.x, L31 = p3a.y, L32 = Z[4 * (4 * K + 3) + 2];
+        const int row = 16 * H + lc;
+        const f64x2 za = *reinterpret_cast<const f64x2*>(Z + 4 * row);
+        const f64x2 zb = *reinterpret_cast<const f64x2*>(Z + 4 * row + 2);
+        const bool piv = (row >> 2) == K;
+        const bool below = row > 4 * K + 3;
+        const double v0 = piv ? (p == 0 ? 1.0 : 0.0) : za.x, v1 = piv ? (p == 1 ? 1.0 : 0.0) : za.y;
+        const double v2 = piv ? (p == 2 ? 1.0 : 0.0) : zb.x, v3 = piv ? (p == 3 ? 1.0 : 0.0) : zb.y;
+        const double x3 = v3;
+        const double x2 = fma(-L32, x3, v2);
+        const double x1 = fma(-L31, x3, fma(-L21, x2, v1));
+        const double x0 = fma(-L30, x3, fma(-L20, x2, fma(-L10, x1, v0)));
+        const double xk = sel4(kk, x0, x1, x2, x3);
+        const double wR = below ? xk : piv ? ((p == kk ? 1.0 : 0.0) - xk) : 0.0;
+        const double pR = r[kq];
+        r = __builtin_amdgcn_mfma_f64_16x16x4f64(-wR, pR, r, 0, 0, 0);
+        w1h_round<K + 1, H>(Zb, prog, base, r, l);
+    }
+}
+
+// Ra: D00 into R (stride S; D01 = 0), T = B A^{-1} into Tb (16 x 16, stride 17), then *tw = tv.
+__device__ __forceinline__ void tile_rinv_lo_w1_wave(const double* __restrict__ Zb, const int* prog, int base,
+                                                     const double* __restrict__ dpv, double* __restrict__ R,
+                                                     double* __restrict__ Tb, int* tw, int tv) {
+    constexpr int S = TileCfg<32>::S;
+    const int l = threadIdx.x & 63, lc = l & 15, lr = l >> 4;
+    f64x4 r;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) r[q] = (lr + 4 * q == lc) ? 1.0 : 0.0;
+    w1h_round<0, 0>(Zb, prog, base, r, l);
+    f64x4 t = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < 4; ++s)   // B[i][4s + kk] = z_{16+i}[kk] of round s
+        t = __builtin_amdgcn_mfma_f64_16x16x4f64(Zb[128 * s + 4 * (16 + lc) + lr], r[s], t, 0, 0, 0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int rr = lr + 4 * q;
+        const double s0 = rsq_nr(dpv[rr]);
+        R[rr * S + lc] = (lc <= rr) ? r[q] * s0 : 0.0;
+        R[rr * S + 16 + lc] = 0.0;
+        Tb[rr * 17 + lc] = t[q];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (l == 0) __hip_atomic_store(tw, tv, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Rb: D11, then (once *tw >= tv) D10 = -D11 T; dg[i] = L_ii and *bad as tile_rinv_w1_wave.
+__device__ __forceinline__ void tile_rinv_hi_w1_wave(const double* __restrict__ Zb, const int* prog, int base,
+                                                     const double* __restrict__ dpv, double* __restrict__ R,
+                                                     const double* __restrict__ Tb, const int* tw, int tv,
+                                                     double* __restrict__ dg, int* __restrict__ bad) {
+    constexpr int S = TileCfg<32>::S;
+    const int l = threadIdx.x & 63, lc = l & 15, lr = l >> 4;
+    f64x4 r;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) r[q] = (lr + 4 * q == lc) ? 1.0 : 0.0;
+    w1h_round<4, 1>(Zb, prog, base, r, l);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int rr = lr + 4 * q;
+        const double s1 = rsq_nr(dpv[16 + rr]);
+        R[(16 + rr) * S + 16 + lc] = (lc <= rr) ? r[q] * s1 : 0.0;
+    }
+    const double dl = dpv[l & 31];
+    const unsigned long long m = __ballot(l < 32 && !(dl > 0.0 && dl < INFINITY));
+    if (l < 32) dg[l] = dl * rsq_nr(dl);
+    if (l == 0) *bad = m ? __ffsll((long long)m) : 0;
+    while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(const_cast<int*>(tw), __ATOMIC_ACQUIRE,
+                                                            __HIP_MEMORY_SCOPE_WORKGROUP)) < tv) {}
+    f64x4 d = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < 4; ++s)   // A: D11[lc][4s + kk] (just written, same wave), B: T[4s + kk][lc]
+        d = __builtin_amdgcn_mfma_f64_16x16x4f64(-R[(16 + lc) * S + 16 + 4 * s + lr], Tb[(4 * s + lr) * 17 + lc], d,
+                                                 0, 0, 0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) R[(16 + lr + 4 * q) * S + lc] = d[q];
+}
+
 // ---------------------------------------------------------------- band wave (tall panel)
 // Eliminates the 32 x 32 sub-diagonal block B = A(k+1, k) of the tall panel [A(k,k); A(k+1,k)] in
 // lock-step with the diagonal factor's rounds (tile_potrf_inv_w1_wave<true> publishing Yb / Fb /

@@ -21,8 +21,8 @@ __global__ __launch_bounds__(512) void k_band(const double* Ag, const double* Bg
     extern __shared__ __attribute__((aligned(16))) double smem[];
     double* X = smem;                 // 32 x 33
     double* Bs = X + 32 * 33;         // 32 x 33
-    double* Pn = Bs + 32 * 33;        // 128
-    double* Yb = Pn + 128;            // 8 x 128
+    double* Pn = Bs + 32 * 33;        // 128 panel + 128 pivots (dpv = Pn + 128, the factor's own)
+    double* Yb = Pn + 256;            // 8 x 128
     double* Fb = Yb + 1024;           // 8 x 16
     double* dpv = Fb + 128;           // 128
     double* Q = dpv + 128;            // 128
@@ -55,7 +55,7 @@ __global__ __launch_bounds__(512) void k_band(const double* Ag, const double* Bg
             if (w == BW) {
                 if (LATE)
                     while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) < it + 1) {}
-                tile_band_w1_wave(Bs, 33, Yb, Fb, dpv, prog, 8 * it, Q, Lb, S, Sb, S);
+                tile_band_w1_wave(Bs, 33, Yb, Fb, Pn + 128, prog, 8 * it, Q, Lb, S, Sb, S);
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 if (it > 0) tb += __builtin_amdgcn_s_memtime() - t0;
             }
@@ -92,7 +92,7 @@ static double Rref[NB * NB];
 template <int V, int BW, bool LATE>
 static void run(const char* name, const double* hA, const double* hB, const double* dA, const double* dB, double* dR,
                 double* dd, double* dL, double* dS, long long* dc, int* db) {
-    const size_t sm = sizeof(double) * (2 * 32 * 33 + 128 + 1024 + 128 + 128 + 128 + 3 * TileCfg<NB>::ELEMS + 32 + 8);
+    const size_t sm = sizeof(double) * (2 * 32 * 33 + 256 + 1024 + 128 + 128 + 128 + 3 * TileCfg<NB>::ELEMS + 32 + 8);
     (void)hipMemset(dc, 0, 128);
     hipLaunchKernelGGL((k_band<V, BW, LATE>), dim3(1), dim3(512), sm, 0, dA, dB, dR, dd, dL, dS, dc, db, 50);
     if (hipDeviceSynchronize() != hipSuccess) { printf("launch failed\n"); exit(1); }

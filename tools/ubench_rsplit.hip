@@ -14,6 +14,7 @@ using namespace mfgp;
 constexpr int NB = 32;
 
 // V 0: fused (wave 0).  V 1: split, R on wave RW.  V 2: split + a load wave (LW) on the R wave's SIMD.
+// V 3: split, the inverse by halves: Ra on wave RW, Rb on wave LW (D done: Rb's end).
 template <int V, int RW, int LW>
 __global__ __launch_bounds__(512) void k_fac(const double* Ag, double* Rg, double* dgg, long long* cyc, int* badg,
                                              int reps, int nload) {
@@ -27,8 +28,10 @@ __global__ __launch_bounds__(512) void k_fac(const double* Ag, double* Rg, doubl
     double* dg = R + E;               // 32
     int* bad = reinterpret_cast<int*>(dg + 32);
     int* prog = bad + 2;
+    int* tw = bad + 3;
+    double* Tb = dg + 64;             // 16 x 17
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    if (threadIdx.x == 0) *prog = 0;
+    if (threadIdx.x == 0) { *prog = 0; *tw = 0; }
     long long ta = 0, td = 0;
     f64x4 junk = {0.0, 0.0, 0.0, 0.0};
     for (int it = 0; it < reps; ++it) {
@@ -40,13 +43,15 @@ __global__ __launch_bounds__(512) void k_fac(const double* Ag, double* Rg, doubl
         } else {
             if (w == 0) tile_elim_w1_wave(X, 33, Pn, Zb, dpv, prog, 8 * it);
             if (w == 0 && it > 0) ta += __builtin_amdgcn_s_memtime() - t0;
-            if (w == RW) tile_rinv_w1_wave(Zb, prog, 8 * it, dpv, R, dg, bad);
+            if (V != 3 && w == RW) tile_rinv_w1_wave(Zb, prog, 8 * it, dpv, R, dg, bad);
+            if (V == 3 && w == RW) tile_rinv_lo_w1_wave(Zb, prog, 8 * it, dpv, R, Tb, tw, it + 1);
+            if (V == 3 && w == LW) tile_rinv_hi_w1_wave(Zb, prog, 8 * it, dpv, R, Tb, tw, it + 1, dg, bad);
             if (V == 2 && w == LW) {
                 for (int q = 0; q < nload; ++q)
                     junk = __builtin_amdgcn_mfma_f64_16x16x4f64((double)l, 1.0, junk, 0, 0, 0);
             }
         }
-        if ((V == 0 && w == 0) || (V != 0 && w == RW)) {
+        if ((V == 0 && w == 0) || (V != 0 && V != 3 && w == RW) || (V == 3 && w == LW)) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             if (it > 0) td += __builtin_amdgcn_s_memtime() - t0;
         }
@@ -56,7 +61,8 @@ __global__ __launch_bounds__(512) void k_fac(const double* Ag, double* Rg, doubl
     tile_store<NB>(Rg, NB, R);
     if (threadIdx.x < NB) dgg[threadIdx.x] = dg[threadIdx.x];
     if (threadIdx.x == 0) { badg[0] = *bad; }
-    if ((V == 0 && w == 0 && l == 0) || (V != 0 && w == RW && l == 0)) cyc[1] = td / (reps - 1);
+    if ((V == 0 && w == 0 && l == 0) || (V != 0 && V != 3 && w == RW && l == 0) || (V == 3 && w == LW && l == 0))
+        cyc[1] = td / (reps - 1);
     if (V != 0 && w == 0 && l == 0) cyc[0] = ta / (reps - 1);
 }
 
@@ -85,7 +91,7 @@ static double Rref[NB * NB], dref[NB];
 template <int V, int RW, int LW>
 static void run(const char* name, const double* hA, const double* dA, double* dR, double* dd, long long* dc, int* db,
                 int nload) {
-    const size_t sm = sizeof(double) * (32 * 33 + 2048 + 128 + TileCfg<NB>::ELEMS + 32 + 8);
+    const size_t sm = sizeof(double) * (32 * 33 + 2048 + 128 + TileCfg<NB>::ELEMS + 64 + 16 * 17 + 8);
     (void)hipMemset(dc, 0, 128);
     hipLaunchKernelGGL((k_fac<V, RW, LW>), dim3(1), dim3(512), sm, 0, dA, dR, dd, dc, db, 50, nload);
     if (hipDeviceSynchronize() != hipSuccess) { printf("launch failed\n"); exit(1); }
@@ -138,6 +144,9 @@ int main() {
         run<2, 1, 5>("split + 32 MFMA load", hA[m], a, dR, dd, dc, db, 32);
         run<2, 1, 5>("split + 64 MFMA load", hA[m], a, dR, dd, dc, db, 64);
         run<2, 1, 5>("split + 128 MFMA load", hA[m], a, dR, dd, dc, db, 128);
+        run<3, 1, 2>("halves Ra w1 Rb w2", hA[m], a, dR, dd, dc, db, 0);
+        run<3, 1, 3>("halves Ra w1 Rb w3", hA[m], a, dR, dd, dc, db, 0);
+        run<3, 5, 6>("halves + SIMD sharers", hA[m], a, dR, dd, dc, db, 0);
     }
     return 0;
 }
