@@ -201,19 +201,22 @@ def test_f32_synth_adam_trajectory_vs_f64_path(eng, synth):
     """the fp32 training gradient is not refined, so bound what that does to
     training at the BASELINE Synth size: 100 optimize(use_adam=True) iterations (lr 0.1) in fp32
     against the same 100 on the HIP fp64 path, loss (-LML) trajectories compared step by step and
-    the learned parameters at the end."""
+    the learned parameters at the end.  Measured: loss within 1.8e-3 of the fp64 trajectory at every
+    step (1.2e-3 at step 0, 1.1e-4 at step 99), theta 3.4e-3 after 100 steps.  The loss is compared
+    relative to max(|loss_i|, 1e-2 max |loss|): -LML passes near zero around step 4, where a
+    plain relative error is meaningless (0.30 there)."""
     X, Y, _, _ = synth
     eng.set_f32_panel(6)
     m32, m64 = _model(X, Y), _model(X, Y, None)
     m32.optimize(max_iters=100, learning_rate=0.1, verbose=False)
     m64.optimize(max_iters=100, learning_rate=0.1, verbose=False)
     h32, h64 = np.array(m32.loss_history), np.array(m64.loss_history)
-    err = np.abs(h32 - h64) / np.abs(h64)
+    err = np.abs(h32 - h64) / np.maximum(np.abs(h64), 1e-2 * np.abs(h64).max())
     t32 = m32._theta_map().theta()
     t64 = m64._theta_map().theta()
     terr = np.max(np.abs(t32 - t64) / np.abs(t64))
     print(f"Synth 100-step Adam fp32 vs fp64: loss max rel {err.max():.2e} (step {int(err.argmax())}), "
-          f"first {err[0]:.2e}, last {err[-1]:.2e}; theta max rel {terr:.2e}")
+          f"first {err[0]:.2e}, last {err[-1]:.2e}; theta max rel {terr:.2e}; -LML steps 0-6 (fp64) {h64[:7]}")
     assert len(h32) == len(h64) == 100
-    assert err.max() < 2e-2
-    assert terr < 5e-2
+    assert err.max() < 5e-3
+    assert terr < 1e-2
