@@ -69,6 +69,21 @@ def pmc_traffic(kernel_prefix, nb, config="goku"):
     return None, None
 
 
+def pmc_step_traffic(config, step_kernel):
+    """(HBM bytes per step, source): every kernel's mean bytes per dispatch x its dispatches per
+    dispatch of step_kernel (one per step), from the committed PMC summary."""
+    path = latest_pmc_summary(config)
+    try:
+        with open(path) as f:
+            kern = json.load(f)["kernels"]
+    except (TypeError, OSError, ValueError, KeyError):
+        return None, None
+    steps = next((v["dispatches"] for n, v in kern.items() if n.startswith(step_kernel)), 0)
+    if not steps:
+        return None, None
+    return int(sum(v["hbm_bytes"] * v["dispatches"] for v in kern.values()) / steps), os.path.relpath(path, ROOT)
+
+
 def load_goku():
     from multi_fidelity_gpflow_amd.data import PowerSpecs, multifidelity_training_set
     ps = PowerSpecs()
@@ -346,6 +361,7 @@ def svgp_leg(X, Yr, Xt, steps, warmup, world=1, device=None, train_predict=True,
     achieved = fl * K / dt_sb / 1e12
     fx = svgp_step_mfma_flops(n, 300, pr)
     executed = fx * K / dt_sb / 1e12
+    tb, tsrc = pmc_step_traffic("goku_svgp", "mfgp::k_adam_packed")
     return {
         "steps": K, "warmup": W,
         "ms_per_step": round(dt_sb / K * 1e3, 4),
@@ -360,7 +376,11 @@ def svgp_leg(X, Yr, Xt, steps, warmup, world=1, device=None, train_predict=True,
         "roofline": {"kernel": "whole optimize() iteration (SURVEY §8(d) ELBO-value flops only; the gradient's "
                                "reverse pass is not counted, so this is a lower bound)",
                      "bound": "mfma", "achieved": round(achieved, 4), "peak": FP64_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 5), "traffic": None,
+                     "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 5), "traffic": tb,
+                     "traffic_unit": "HBM bytes per optimize() iteration (FETCH_SIZE x2 + WRITE_SIZE, every "
+                                     "kernel, single-bin model)",
+                     "traffic_source": tsrc,
+                     "traffic_gbs": None if tb is None else round(tb / (dt_sb / K) / 1e9, 1),
                      "flop_per_step": fl,
                      "executed": {"what": "f64 MFMA tile flops issued by the forward and reverse pass "
                                           "(padded NB = 32 tiles; svgp_step_mfma_flops)",
@@ -382,7 +402,8 @@ def bench_svgp(args):
     from multi_fidelity_gpflow_amd.distributed import bin_block
     b0, b1 = bin_block(Y.shape[1], rank, world)
     Yr = np.ascontiguousarray(Y[:, b0:b1])
-    leg = svgp_leg(X, Yr, Xt, args.steps, args.warmup, world, device, train_predict=not args.no_train_predict)
+    leg = svgp_leg(X, Yr, Xt, args.steps, args.warmup, world, device, train_predict=not args.no_train_predict,
+                   latent=not args.no_latent)
     shared = shared_inducing_leg(X, Yr, min(args.steps, 50), min(args.warmup, 5), rank, world, device) \
         if world > 1 else None
     if rank == 0:
@@ -590,6 +611,8 @@ def main():
     ap.add_argument("--tile", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-train-predict", action="store_true")
+    ap.add_argument("--no-latent", action="store_true",
+                    help="--config goku_svgp: time the single-bin model only (the PMC passes of tools/profile_all.sh)")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the hbs / synth / goku_svgp sub-objects of the default (Goku, N=1) line")
     ap.add_argument("--mode", choices=["shard", "shared"], default="shard",

@@ -34,6 +34,7 @@ struct mfgp_handle_s {
     int f32_lookahead;          // fp32 sweep: factor the next panel beside the trailing update
     int f32_reserve;            // CUs the capped trailing update leaves to the side stream
     int f32_refine;             // fp32 value-only LML (one step) / predict mean (this many steps): fp64 refinement (mfgp_set_f32_refine)
+    int tiny;                   // small problems (n, p <= 64, D <= 16, AR1 kernel): one-launch LML step (mfgp_set_tiny)
     hipStream_t side;           // its high-priority side stream + fork / join events (created with the handle)
     hipEvent_t ev_fork, ev_join;
 };
@@ -254,6 +255,17 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
     hipStream_t s = h->stream;
     const long ldr = L.npad + L.ppad;
     if (pm) pm->mark(s);
+    if (NB == 32 && h->tiny && gpr_tiny_fits(n, p, d, nlf)) {   // the whole step in one workgroup
+        FinArgs f{};
+        if (adam) f = *adam;
+        f.info = info; f.P = p; f.D = d; f.want_grad = want_grad; f.out = out; f.n = n;
+        f.adam = adam != nullptr;
+        f.G = L.G;
+        if (pm) pm->mark(s);
+        launch_gpr_tiny(X, ldx, Y, ldy, theta, n, p, d, want_grad, info, f, s);
+        if (pm) { pm->mark(s); pm->mark(s); pm->mark(s); }
+        return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;
+    }
     if (pm) pm->mark(s);
     {
         GramArgs g{};
@@ -680,6 +692,8 @@ int mfgp_create(int device, mfgp_handle_t* out) {
     if (const char* gv = getenv("MFGP_GRAM_WGS")) h->gram_wgs = atoi(gv);
     h->gram_legacy = 0;
     h->flow_d0 = 0;
+    h->tiny = 1;
+    if (const char* tv = getenv("MFGP_TINY")) h->tiny = atoi(tv) != 0;
 #ifdef MFGP_AB_KNOBS
     // A/B diagnostics only (a build with -DMFGP_AB_KNOBS, then tools/ab_env.sh): each switches the
     // production LML to another numerics path, so the shipped library never reads them
@@ -766,6 +780,12 @@ int mfgp_set_flow_timeout_us(mfgp_handle_t h, long long us) {
     CHECK_H(h);
     if (us < 0) return MFGP_ERR_ARG;
     h->flow_timeout = us * 100;   // s_memrealtime: 100 MHz
+    return MFGP_OK;
+}
+
+int mfgp_set_tiny(mfgp_handle_t h, int enable) {
+    if (!h) return MFGP_ERR_ARG;
+    h->tiny = enable != 0;
     return MFGP_OK;
 }
 

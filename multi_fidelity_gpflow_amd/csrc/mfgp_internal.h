@@ -250,6 +250,10 @@ template <int NB> void launch_first_factor(const double* A, long lda, long sA, d
 // dense layout, write extents wr1 x wr2 (>= n1 x n2; the excess is written 0.0)
 void launch_gram_dense(const GramArgs& g, int batch, int wr1, int wr2, hipStream_t s);
 void launch_gram_flow(const GramArgs& g, int extra, hipStream_t s);   // set-up launch of k_chol_flow
+// one-launch value + gradient (+ Adam) of the AR1 GPR LML for small problems (k_gpr_tiny)
+bool gpr_tiny_fits(int n, int p, int d, int nlf);
+void launch_gpr_tiny(const double* X, long ldx, const double* Y, long ldy, const double* theta, int n, int p, int d,
+                     int want_grad, int* info, const FinArgs& f, hipStream_t s);
 template <int NB> void launch_chol_steps(CholArgs c, int batch, hipStream_t s);
 template <int NB> void launch_grad(const GradArgs& g, hipStream_t s);
 template <int NB> void launch_pred(const PredAArgs& pa, const PredOutArgs& po, int T, hipStream_t s);

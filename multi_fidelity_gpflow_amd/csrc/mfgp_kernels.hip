@@ -1622,6 +1622,423 @@ void launch_pred(const PredAArgs& pa, const PredOutArgs& po, int T, hipStream_t 
                        sizeof(double) * (2 * NB * (NB + 2) + NB), s, po);
 }
 
+// ============================================================ small problems: one launch
+// The whole value + gradient (+ Keras Adam) evaluation of the AR1 kernel's GPR LML for n <= 64,
+// p <= 64, D <= TINY_MAXD in ONE workgroup (mfgpflow/linear.py:200-214 at the HBS size, N = 53,
+// P = 49, D = 5, where the step sequence k_gram -> k_chol_step -> k_grad -> k_reduce_items is four
+// dependent launches of a few microseconds of work each).  Everything stays in LDS, in NB = 32
+// tiles of stride S (the T <= 2 tile grid of the step schedule):
+//   K (the same entries as k_gram, bit for bit) -> D_0 = L_00^{-1} (tile_potrf_inv_w1_wave),
+//   L_10 = K_10 D_0^T, K_11 -= L_10 L_10^T -> D_1, L^{-1}_10 = -D_1 (L_10 D_0);
+//   Z = L^{-1} Y, alpha = L^{-T} Z, S_ij = sum_m L^{-1}_mi^T L^{-1}_mj - alpha_i alpha_j^T / P, and
+//   k_grad's epilogue (W = -P S against dK/dtheta recomputed from the inputs) on the three lower
+//   tiles; then finalize_body's LML / gradient output and adam_body's step.
+#ifndef TINY_KMFMA
+#define TINY_KMFMA 1
+#endif
+#ifndef TINY_STOP
+#define TINY_STOP 0   // diagnostic ablation (tools/tiny_abl.sh): return after phase TINY_STOP
+#endif
+constexpr int TINY_MAXD = 16, TINY_XS = TINY_MAXD + 1, TINY_N = 64, TINY_P = 64;
+
+struct TinyArgs {
+    const double* X; long ldx;
+    const double* Y; long ldy;
+    const double* theta;
+    int n, p, D, want_grad;
+    int* info;
+    FinArgs f;
+};
+
+__global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
+    constexpr int S = TileCfg<32>::S, E = TileCfg<32>::ELEMS;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int D = a.D, n = a.n, p = a.p;
+    const int T = (n + 31) / 32, Tp = (p + 31) / 32;
+    const int G = theta_size(D);
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    auto slot = [&](int i) { return smem + (long)i * E; };
+    double* K00 = slot(0); double* K10 = slot(1); double* K11 = slot(2);
+    double* D0 = slot(3); double* D1 = slot(4); double* L10 = slot(5);
+    auto Yt = [&](int r, int c) { return slot(6 + 2 * r + c); };
+    auto Zt = [&](int r, int c) { return r == 0 ? slot(c) : slot(c == 0 ? 2 : 10); };
+    double* xr = slot(11);                         // raw rows 64 x TINY_XS (gradient epilogue)
+    double* misc = slot(12);
+    double* dg = misc;                             // 64
+    int* bad = reinterpret_cast<int*>(misc + 64);  // 2
+    double* il = misc + 66;                        // 2 x TINY_MAXD   1/l    (Gram)
+    double* il2 = il + 2 * TINY_MAXD;              // 2 x TINY_MAXD   1/l^2  (gradient)
+    double* red = il2 + 2 * TINY_MAXD;             // (G + 2) x 4     wave partials
+    double* gsh = red + 4 * (2 * TINY_MAXD + 6);   // G + 2
+    int* tsh = reinterpret_cast<int*>(gsh + 2 * TINY_MAXD + 6);
+    double* lv = gsh + 2 * (2 * TINY_MAXD + 6);    // 2 x TINY_MAXD   the lengthscales
+    // Gram staging in the Y / alpha slots (free until Y is loaded)
+    double* aL = slot(6);
+    double* aD = aL + TINY_N * TINY_XS;
+    double* nL = aD + TINY_N * TINY_XS;
+    double* nD = nL + TINY_N;
+    double* fl = nD + TINY_N;
+    const MFTheta th{a.theta, D};
+    MFScal sc{a.theta[0], a.theta[1 + D], a.theta[2 + 2 * D]};
+    const double noise = a.theta[3 + 2 * D];
+    // Y (zero padded), loaded now and put into its LDS tiles once the Gram staging is consumed
+    constexpr int YPER = TINY_N * TINY_P / NTHREADS;
+    double yv[YPER];
+#pragma unroll
+    for (int q = 0; q < YPER; ++q) {
+        const int e = t + q * NTHREADS, tl = e >> 10, r = (e >> 5) & 31, c = e & 31;
+        const int ti = tl / Tp, tc = tl % Tp;
+        const int gi = 32 * ti + r, gc = 32 * tc + c;
+        yv[q] = (e < T * Tp * 1024 && gi < n && gc < p) ? a.Y[(long)gi * a.ldy + gc] : 0.0;
+    }
+    // the Adam state, loaded now: its latency hides under the whole evaluation (adam_body would
+    // issue these loads, dependent on *step, at the very end)
+    const FinArgs& f = a.f;
+    double pu = 0.0, pm = 0.0, pv = 0.0;
+    int ptr = 0, ptie = 0, pst = 0;
+    if (f.adam) {
+        if (t < G) {
+            pu = f.u[t]; pm = f.m[t]; pv = f.v[t]; ptr = f.trainable[t];
+            ptie = f.tie ? f.tie[t] : t;
+        }
+        pst = *f.step;
+    }
+    // ---- stage: raw rows, scaled rows (x * rcp_nr(l), as k_gram), norms, fidelity flags
+    if (t < D) {
+        il[t] = rcp_nr(a.theta[1 + t]);
+        il[TINY_MAXD + t] = rcp_nr(a.theta[2 + D + t]);
+        il2[t] = 1.0 / (th.lL(t) * th.lL(t));
+        il2[TINY_MAXD + t] = 1.0 / (th.lD(t) * th.lD(t));
+        lv[t] = th.lL(t);
+        lv[TINY_MAXD + t] = th.lD(t);
+    }
+    const int D4 = pad4(D);
+    {   // every row element in flight before the first LDS store
+        constexpr int PER = (TINY_N * TINY_XS + NTHREADS - 1) / NTHREADS;
+        double v[PER];
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const int e = t + q * NTHREADS, r = e / TINY_XS, d = e % TINY_XS;
+            v[q] = (e < TINY_N * TINY_XS && r < n && d <= D) ? a.X[(long)r * a.ldx + d] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < PER; ++q)
+            if (t + q * NTHREADS < TINY_N * TINY_XS) xr[t + q * NTHREADS] = v[q];
+    }
+    __syncthreads();
+    for (int e = t; e < TINY_N * TINY_XS; e += NTHREADS) {
+        const int r = e / TINY_XS, d = e % TINY_XS;
+        const double x = (d < D) ? xr[e] : 0.0;
+        aL[e] = (d < D4 && d < D) ? x * il[d] : 0.0;
+        aD[e] = (d < D4 && d < D) ? x * il[TINY_MAXD + d] : 0.0;
+    }
+    if (t < TINY_N) fl[t] = (t < n) ? xr[t * TINY_XS + D] : -1.0;
+    __syncthreads();
+    if (t < TINY_N) { nL[t] = dot4(aL + t * TINY_XS, aL + t * TINY_XS, D4); nD[t] = dot4(aD + t * TINY_XS, aD + t * TINY_XS, D4); }
+    __syncthreads();
+    // ---- K tiles (0,0), (1,0), (1,1): k_gram's padded-entry arithmetic; TINY_KMFMA: the dot
+    //      products a_i . a_j of the expanded r^2 on the matrix core (16 x 16 blocks, three per
+    //      wave, D4 / 4 v_mfma_f64_16x16x4 each) instead of a dot4 chain of 2 D4 LDS reads an entry
+#if TINY_KMFMA
+    {
+        const int lc = lane & 15, kk = lane >> 4;
+        const double rho = sc.rho();
+        for (int bq = 0; bq < 3; ++bq) {
+            const int blk = w * 3 + bq, tl = blk >> 2, sub = blk & 3;
+            const int ti = tl == 0 ? 0 : 1, tj = tl == 2 ? 1 : 0;
+            if (ti >= T) continue;
+            const int rb = 2 * ti + (sub >> 1), cb = 2 * tj + (sub & 1);
+            f64x4 dl = {0.0, 0.0, 0.0, 0.0}, dd = {0.0, 0.0, 0.0, 0.0};
+            for (int s4 = 0; s4 < D4; s4 += 4) {
+                dl = __builtin_amdgcn_mfma_f64_16x16x4f64(aL[(16 * rb + lc) * TINY_XS + s4 + kk],
+                                                          aL[(16 * cb + lc) * TINY_XS + s4 + kk], dl, 0, 0, 0);
+                dd = __builtin_amdgcn_mfma_f64_16x16x4f64(aD[(16 * rb + lc) * TINY_XS + s4 + kk],
+                                                          aD[(16 * cb + lc) * TINY_XS + s4 + kk], dd, 0, 0, 0);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int gi = 16 * rb + kk + 4 * q, gj = 16 * cb + lc;
+                const double kl = sc.vL() * exp(-0.5 * (-2.0 * dl[q] + (nL[gi] + nL[gj])));
+                const double fa = fl[gi], fb = fl[gj];
+                const bool L1 = (fa == 0.0), H1 = (fa == 1.0), L2 = (fb == 0.0), H2 = (fb == 1.0);
+                const double kD = (H1 && H2) ? sc.vD() * exp(-0.5 * (-2.0 * dd[q] + (nD[gi] + nD[gj]))) : 0.0;
+                const double vhh = kl * (rho * rho) + kD;
+                double v = (L1 && L2) ? kl : (!(H1 && H2) ? kl * rho : vhh);
+                if (!(L1 || H1) || !(L2 || H2)) v = 0.0;
+                if (gi == gj) v = (gi < n) ? v + noise : 1.0;
+                slot(tl)[(gi - 32 * ti) * S + gj - 32 * tj] = v;
+            }
+        }
+    }
+#else
+#pragma unroll 4
+    for (int e = t; e < 3 * 32 * 32; e += NTHREADS) {
+        const int tl = e >> 10, r = (e >> 5) & 31, c = e & 31;
+        const int ti = tl == 0 ? 0 : 1, tj = tl == 2 ? 1 : 0;
+        if (ti >= T) continue;
+        const int gi = 32 * ti + r, gj = 32 * tj + c;
+        const double dot = dot4(aL + gi * TINY_XS, aL + gj * TINY_XS, D4);
+        const double kl = sc.vL() * exp(-0.5 * (-2.0 * dot + (nL[gi] + nL[gj])));
+        const double fa = fl[gi], fb = fl[gj];
+        const bool L1 = (fa == 0.0), H1 = (fa == 1.0), L2 = (fb == 0.0), H2 = (fb == 1.0);
+        const double rho = sc.rho();
+        double kD = 0.0;
+        if (H1 && H2) {
+            const double dotD = dot4(aD + gi * TINY_XS, aD + gj * TINY_XS, D4);
+            kD = sc.vD() * exp(-0.5 * (-2.0 * dotD + (nD[gi] + nD[gj])));
+        }
+        const double vhh = kl * (rho * rho) + kD;
+        double v = (L1 && L2) ? kl : (!(H1 && H2) ? kl * rho : vhh);
+        if (!(L1 || H1) || !(L2 || H2)) v = 0.0;
+        if (gi == gj) v = (gi < n) ? v + noise : 1.0;
+        slot(tl)[r * S + c] = v;
+    }
+#endif
+    __syncthreads();
+    if (TINY_STOP == 1) { if (t == 0) { a.info[0] = 0; a.f.out[0] = 0.0; } return; }
+    // ---- factor: D_0; L_10, K_11 update, D_1, L^{-1}_10
+    if (w == 0) tile_potrf_inv_w1_wave(K00, S, K00, D0, dg, &bad[0]);
+    __syncthreads();
+    if (TINY_STOP == 2) { if (t == 0) { a.info[0] = 0; a.f.out[0] = 0.0; } return; }
+    if (T > 1) {
+        Acc<32> acc;
+        acc_zero(acc);
+        tile_mma<32, false, true>(acc, K10, D0, 1.0);      // L_10 = K_10 D_0^T
+        acc_to_lds(acc, L10);
+        __syncthreads();
+        acc_load<32>(acc, K11, S);
+        tile_mma<32, false, true>(acc, L10, L10, -1.0);    // K_11 - L_10 L_10^T
+        __syncthreads();
+        acc_to_lds(acc, K11);
+        acc_zero(acc);
+        tile_mma<32, false, false>(acc, L10, D0, 1.0);     // T = L_10 D_0 (into K10's slot)
+        acc_to_lds(acc, K10);
+        __syncthreads();
+        if (w == 0) tile_potrf_inv_w1_wave(K11, S, K11, D1, dg + 32, &bad[1]);
+        __syncthreads();
+        acc_zero(acc);
+        tile_mma<32, false, false>(acc, D1, K10, -1.0);    // L^{-1}_10 = -D_1 T (over L10)
+        acc_to_lds(acc, L10);
+    }
+    if (TINY_STOP == 3) { if (t == 0) { a.info[0] = 0; a.f.out[0] = 0.0; } return; }
+    // ---- Y tiles (zero padded; loaded at the start)
+#pragma unroll
+    for (int q = 0; q < YPER; ++q) {
+        const int e = t + q * NTHREADS, tl = e >> 10, r = (e >> 5) & 31, c = e & 31;
+        if (e < T * Tp * 1024) Yt(tl / Tp, tl % Tp)[r * S + c] = yv[q];
+    }
+    // ---- K^{-1} = L^{-T} L^{-1}, lower tiles (over the consumed K00 / T / K11 slots)
+    double* Ki00 = slot(0); double* Ki10 = slot(1); double* Ki11 = slot(2);
+    {
+        Acc<32> acc;
+        acc_zero(acc);
+        tile_mma<32, true, false>(acc, D0, D0, 1.0);
+        if (T > 1) tile_mma<32, true, false>(acc, L10, L10, 1.0);
+        acc_to_lds(acc, Ki00);
+        if (T > 1) {
+            acc_zero(acc);
+            tile_mma<32, true, false>(acc, D1, L10, 1.0);
+            acc_to_lds(acc, Ki10);
+            acc_zero(acc);
+            tile_mma<32, true, false>(acc, D1, D1, 1.0);
+            acc_to_lds(acc, Ki11);
+        }
+    }
+    __syncthreads();
+    if (TINY_STOP == 4) { if (t == 0) { a.info[0] = 0; a.f.out[0] = 0.0; } return; }
+    // ---- Z = L^{-1} Y (sum Z^2: the LML's quadratic term in the step path's form), then
+    //      alpha = L^{-T} Z; each column tile's results replace its Y tiles (all read first)
+    double z2 = 0.0;
+    for (int c = 0; c < Tp; ++c) {
+        Acc<32> z0, z1;
+        acc_zero(z0);
+        tile_mma<32, false, false>(z0, D0, Yt(0, c), 1.0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) z2 += z0.v[0][r] * z0.v[0][r];
+        if (T > 1) {
+            acc_zero(z1);
+            tile_mma<32, false, false>(z1, L10, Yt(0, c), 1.0);
+            tile_mma<32, false, false>(z1, D1, Yt(1, c), 1.0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) z2 += z1.v[0][r] * z1.v[0][r];
+        }
+        __syncthreads();
+        acc_to_lds(z0, Yt(0, c));
+        if (T > 1) acc_to_lds(z1, Yt(1, c));
+        __syncthreads();
+        Acc<32> a0, a1;
+        acc_zero(a0);
+        tile_mma<32, true, false>(a0, D0, Yt(0, c), 1.0);
+        if (T > 1) {
+            tile_mma<32, true, false>(a0, L10, Yt(1, c), 1.0);
+            acc_zero(a1);
+            tile_mma<32, true, false>(a1, D1, Yt(1, c), 1.0);
+        }
+        __syncthreads();
+        acc_to_lds(a0, Yt(0, c));
+        if (T > 1) acc_to_lds(a1, Yt(1, c));
+    }
+    auto At = [&](int r, int c) { return Yt(r, c); };
+    double ld = 0.0;
+    if (t < n) ld = log(dg[t]);
+    __syncthreads();
+    if (TINY_STOP == 5) { if (t == 0) { a.info[0] = 0; a.f.out[0] = 0.0; } return; }
+    // ---- gradient: S tiles and k_grad's epilogue (per element: its weights; per dimension: the
+    //      lengthscale sums, reduced at once, so no per-thread array is indexed at run time)
+    double cLe[12], cDe[12];
+    int gie[12], gje[12];
+    double gvL = 0.0, gvD = 0.0, grho = 0.0, gnoise = 0.0;
+#pragma unroll
+    for (int e = 0; e < 12; ++e) { cLe[e] = 0.0; cDe[e] = 0.0; gie[e] = 0; gje[e] = 0; }
+    if (a.want_grad) {
+        const double invP = 1.0 / (double)p;
+        const double rho = sc.rho();
+#pragma unroll
+        for (int tl = 0; tl < 3; ++tl) {
+            if (tl > 0 && T < 2) continue;
+            const int ti = tl == 0 ? 0 : 1, tj = tl == 2 ? 1 : 0;
+            Acc<32> acc;
+            acc_load<32>(acc, tl == 0 ? Ki00 : (tl == 1 ? Ki10 : Ki11), S);
+            for (int c = 0; c < Tp; ++c) tile_mma<32, false, true>(acc, At(ti, c), At(tj, c), -invP);
+            const double wscale = ((ti == tj) ? 0.5 : 1.0) * (-(double)p);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int e = 4 * tl + r;
+                const int gi = 32 * ti + acc_row<32>(0, r), gj = 32 * tj + acc_col<32>(0);
+                gie[e] = gi;
+                gje[e] = gj;
+                const double f1 = (gi < n) ? xr[gi * TINY_XS + D] : -1.0, f2 = (gj < n) ? xr[gj * TINY_XS + D] : -1.0;
+                const bool L1 = f1 == 0.0, H1 = f1 == 1.0, L2 = f2 == 0.0, H2 = f2 == 1.0;
+                const bool live = (L1 || H1) && (L2 || H2);
+                double s2 = 0.0, s2d = 0.0;
+                for (int d = 0; d < D; ++d) {
+                    const double df = xr[gi * TINY_XS + d] - xr[gj * TINY_XS + d];
+                    const double d2 = df * df;
+                    s2 += d2 * il2[d];
+                    s2d += d2 * il2[TINY_MAXD + d];
+                }
+                const double wv = acc.v[0][r] * wscale;
+                const double eL = live ? exp(-0.5 * s2) : 0.0;
+                const double kL = sc.vL() * eL;
+                const double eD = (H1 && H2) ? exp(-0.5 * s2d) : 0.0;
+                const double kD = sc.vD() * eD;
+                const double si = L1 ? 1.0 : (H1 ? rho : 0.0), sj = L2 ? 1.0 : (H2 ? rho : 0.0);
+                const double hi = H1 ? 1.0 : 0.0, hj = H2 ? 1.0 : 0.0;
+                cLe[e] = wv * si * sj * kL;
+                cDe[e] = wv * hi * hj * kD;
+                gvL += wv * si * sj * eL;
+                gvD += wv * hi * hj * eD;
+                grho += wv * (hi * sj + si * hj) * kL;
+                if (ti == tj && gi == gj && gi < n) gnoise += wv;
+            }
+        }
+    }
+    // ---- reductions (L^{-1} is consumed: its slots hold 64 quad partials per quantity): quantity
+    //      q < G the gradient entry q, G the quadratic term, G + 1 sum log L_ii
+    __syncthreads();
+    double* RB = slot(3);
+    if (TINY_STOP == 6) { if (t == 0) { a.info[0] = 0; a.f.out[0] = 0.0; } return; }
+    auto put = [&](int q, double v) {
+        v = quad_sum(v);
+        if ((lane & 3) == 0) RB[q * 64 + w * 16 + (lane >> 2)] = v;
+    };
+    put(G, z2);
+    put(G + 1, ld);
+    if (a.want_grad) {
+        put(0, gvL);
+        put(1 + D, gvD);
+        put(2 + 2 * D, grho);
+        put(3 + 2 * D, gnoise);
+        for (int d = 0; d < D; ++d) {
+            double tl = 0.0, td = 0.0;
+#pragma unroll
+            for (int e = 0; e < 12; ++e) {
+                const double df = xr[gie[e] * TINY_XS + d] - xr[gje[e] * TINY_XS + d];
+                tl += cLe[e] * df * df;
+                td += cDe[e] * df * df;
+            }
+            put(1 + d, tl);
+            put(2 + D + d, td);
+        }
+    }
+    __syncthreads();
+    for (int g0 = 0; g0 < G + 2; g0 += NTHREADS / 8) {
+        const int qx = g0 + (t >> 3), sub = t & 7;
+        double v = 0.0;
+        if (qx < G + 2 && (a.want_grad || qx >= G)) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v += RB[qx * 64 + sub * 8 + u];
+        }
+        v = quad_sum(v);
+        v += __shfl_xor(v, 4, 64);
+        if (sub == 0 && qx < G + 2) {
+            if (qx >= 1 && qx <= D) { const double l = lv[qx - 1]; v /= l * l * l; }
+            else if (qx >= 2 + D && qx <= 1 + 2 * D) { const double l = lv[TINY_MAXD + qx - 2 - D]; v /= l * l * l; }
+            if (qx < G) gsh[2 + qx] = v;
+            else gsh[qx - G] = v;
+        }
+    }
+    if (f.adam && t < G) tsh[t] = ptie;
+    if (t == 0) {
+        const int b0 = bad[0], b1 = (T > 1) ? bad[1] : 0;
+        a.info[0] = b0 ? b0 : (b1 ? 32 + b1 : 0);
+    }
+    __syncthreads();
+    // ---- finalize_body / adam_body (LDS staging instead of the item round trip)
+    const double LOG2PI = 1.8378770664093453;
+    const int info0 = (bad[0] != 0 || (T > 1 && bad[1] != 0)) ? 1 : 0;
+    const int st = pst;
+    double lml = -0.5 * gsh[0] - (double)p * gsh[1] - 0.5 * (double)n * (double)p * LOG2PI;
+    if (info0 != 0) lml = NAN;
+    if (f.adam && info0 == 0 && t < G && ptr) {   // adam_body's step on the prefetched state
+        const double tt = (double)(st + 1);
+        const double alpha = f.lr * sqrt(1.0 - pow(f.b2, tt)) / (1.0 - pow(f.b1, tt));
+        double gc = gsh[2 + t];
+        if (f.tie) {
+            gc = 0.0;
+            for (int r = 0; r < G; ++r)
+                if (tsh[r] == tsh[t]) gc += gsh[2 + r];
+        }
+        const double g = (-gc) / (exp(-pu) + 1.0);
+        double mq = pm, vq = pv;
+        mq += (g - mq) * (1.0 - f.b1);
+        vq += (g * g - vq) * (1.0 - f.b2);
+        const double un = pu - (mq * alpha) / (sqrt(vq) + f.eps);
+        f.m[t] = mq;
+        f.v[t] = vq;
+        f.u[t] = un;
+        f.theta[t] = tf_softplus(un) + (t == f.noise_index ? 1e-6 : 0.0);
+    }
+    if (t == 0) f.out[0] = lml;
+    if (a.want_grad)
+        for (int q = t; q < G; q += NTHREADS) f.out[1 + q] = gsh[2 + q];
+    if (!f.adam) return;
+    if (t == 0) {
+        f.loss_hist[st] = -lml;
+        if (info0 == 0) *f.step = st + 1;
+    }
+}
+
+size_t gpr_tiny_smem_bytes() {
+    return sizeof(double) * (13 * (size_t)TileCfg<32>::ELEMS);
+}
+
+bool gpr_tiny_fits(int n, int p, int d, int nlf) {
+    return nlf == 0 && n >= 1 && n <= TINY_N && p >= 1 && p <= TINY_P && d >= 1 && d <= TINY_MAXD;
+}
+
+void launch_gpr_tiny(const double* X, long ldx, const double* Y, long ldy, const double* theta, int n, int p, int d,
+                     int want_grad, int* info, const FinArgs& f, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gpr_tiny), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)gpr_tiny_smem_bytes());
+        attr = true;
+    }
+    TinyArgs a{X, ldx, Y, ldy, theta, n, p, d, want_grad, info, f};
+    hipLaunchKernelGGL(k_gpr_tiny, dim3(1), dim3(NTHREADS), gpr_tiny_smem_bytes(), s, a);
+}
+
 template void launch_gram<32>(const GramArgs&, int, int, hipStream_t);
 template void launch_first_factor<32>(const double*, long, long, double*, long, double*, long, int*, int, hipStream_t);
 template void launch_first_factor<64>(const double*, long, long, double*, long, double*, long, int*, int, hipStream_t);

@@ -135,6 +135,11 @@ class Engine:
         8 or more 32-tiles unless any_size) or one launch per step (False)."""
         check(self.lib.mfgp_set_flow(self.h, (3 if any_size else 1) if enable else 0), "mfgp_set_flow")
 
+    def set_tiny(self, enable: bool):
+        """One-launch LML step for small problems (n, p <= 64, D <= 16; default on) or the step
+        sequence of the general path (False)."""
+        check(self.lib.mfgp_set_tiny(self.h, 1 if enable else 0), "mfgp_set_tiny")
+
     def set_flow_timeout_us(self, us: int):
         """Bound of every k_chol_flow hand-off wait (default 50000 us; 0: diagnostic abort path)."""
         check(self.lib.mfgp_set_flow_timeout_us(self.h, int(us)), "mfgp_set_flow_timeout_us")

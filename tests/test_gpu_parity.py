@@ -24,16 +24,20 @@ def eng():
     e.set_tile(32)
 
 
-@pytest.fixture(params=[(32, True), (32, False), (64, False)], ids=["nb32-flow", "nb32-steps", "nb64"])
+@pytest.fixture(params=[(32, True, False), (32, False, False), (64, False, False), (32, False, True)],
+                ids=["nb32-flow", "nb32-steps", "nb64", "nb32-tiny"])
 def tile(request, eng):
-    """Tile size and Cholesky schedule: the persistent dataflow launch (k_chol_flow, NB = 32) or
-    the launch-per-step sequence (k_chol_step)."""
-    nb, flow = request.param
+    """Tile size and LML schedule: the persistent dataflow launch (k_chol_flow, NB = 32), the
+    launch-per-step sequence (k_chol_step), or the one-launch small-problem kernel (k_gpr_tiny:
+    n, p <= 64 -- HBS, Forrester; larger problems take the step sequence under this id)."""
+    nb, flow, tiny = request.param
     eng.set_tile(nb)
     eng.set_flow(flow, any_size=True)   # the flow even below its default size threshold
+    eng.set_tiny(tiny)
     yield nb
     eng.set_tile(32)
     eng.set_flow(True)
+    eng.set_tiny(True)
 
 
 def _params(D, P, seed=0, scale=1.0):
@@ -185,10 +189,12 @@ def test_flow_matches_step_schedule(n_lf, n_hf, p, eng):
     m = _model(X, Y, _params(D, p, seed=3))
     assert eng.flow() or torch.cuda.get_device_properties(0).multi_processor_count < 2
     vals = []
+    eng.set_tiny(False)
     for flow in (True, False):
         eng.set_flow(flow, any_size=True)
         vals.append(m.log_marginal_likelihood_and_grad())
     eng.set_flow(True)
+    eng.set_tiny(True)
     assert abs(vals[0][0] - vals[1][0]) < 1e-11 * abs(vals[1][0])
     np.testing.assert_allclose(vals[0][1], vals[1][1], rtol=0, atol=1e-9 * np.abs(vals[1][1]).max())
     lo, go = O.gpr_lml_and_grad(X, Y, _oracle_params(m))
@@ -279,7 +285,7 @@ def test_graph_and_eager_agree(hbs, eng):
     np.testing.assert_array_equal(hs[0], hs[1])
 
 
-@pytest.mark.parametrize("flow", [True, False], ids=["flow", "steps"])
+@pytest.mark.parametrize("flow", [True, False, "tiny"], ids=["flow", "steps", "tiny"])
 def test_lbfgs_forrester_kat(kats, eng, flow):
     """notebooks/demo.ipynb:233,257: rho 1.99976989, noise 1e-06 after GPflow's two L-BFGS
     passes.  With the variance gradients in TF's autodiff form (dK/dv = exp(-r2/2), finite
@@ -291,20 +297,71 @@ def test_lbfgs_forrester_kat(kats, eng, flow):
     noise floor, and the GPU objective along the first L-BFGS evaluations against the oracle."""
     from conftest import forrester_demo_data
     X, Y = forrester_demo_data()
-    eng.set_flow(flow, any_size=True)
+    tiny = flow == "tiny"
+    eng.set_flow(bool(flow) and not tiny, any_size=True)
+    eng.set_tiny(tiny)
     try:
         m = M.MultiFidelityGPModel(X, Y, M.SquaredExponential(), M.SquaredExponential())
         m.optimize(max_iters=1000, learning_rate=0.01, use_adam=False, unfix_noise_after=500, verbose=False)
     finally:
         eng.set_flow(True)
+        eng.set_tiny(True)
     rho = float(m.kernel.rho.numpy()[0, 0])
-    print(f"L-BFGS Forrester ({'flow' if flow else 'steps'}) rho {rho:.9f} vs recorded {kats['forrester_lbfgs']['rho']} "
+    print(f"L-BFGS Forrester ({'tiny' if tiny else ('flow' if flow else 'steps')}) rho {rho:.9f} vs recorded {kats['forrester_lbfgs']['rho']} "
           f"(rel {abs(rho - kats['forrester_lbfgs']['rho']) / kats['forrester_lbfgs']['rho']:.1e}), "
           f"noise {float(m.likelihood.variance.numpy()):.9e}")
     assert abs(rho - kats["forrester_lbfgs"]["rho"]) < 5e-5 * kats["forrester_lbfgs"]["rho"]
     assert float(m.likelihood.variance.numpy()) == pytest.approx(kats["forrester_lbfgs"]["noise"], rel=1e-6)
     _, trace = O.lbfgs_train(X, Y, O.MFParams.initial(1, 1), max_iters=1000, return_trace=True)
     np.testing.assert_allclose(m.loss_history[:8], trace[:8], rtol=1e-9)
+
+
+@pytest.mark.parametrize("n_lf,n_hf,p,D", [(50, 3, 49, 5), (20, 5, 1, 1), (24, 8, 32, 3), (40, 24, 64, 16),
+                                           (60, 4, 33, 7), (1, 1, 1, 2)])
+def test_tiny_matches_step_sequence(n_lf, n_hf, p, D, eng):
+    """k_gpr_tiny (the whole LML value + gradient in one workgroup, n, p <= 64) against the
+    four-launch step sequence and the oracle: T = 1 and 2 tiles, one and two column tiles of Y,
+    D = 1 .. 16, n = 64 and p = 64 at the edges, a fractional-fidelity row (an exact-mask zero row
+    of K, linear.py:67-70)."""
+    rng = np.random.default_rng(n_lf * 7 + p)
+    X = np.vstack([np.hstack([rng.random((n_lf, D)), np.zeros((n_lf, 1))]),
+                   np.hstack([rng.random((n_hf, D)), np.ones((n_hf, 1))])])
+    if n_lf + n_hf > 3:
+        X[1, -1] = 0.9999999999999999
+    Y = np.sin(X[:, :D] @ rng.standard_normal((D, p)) * 3.0)
+    m = _model(X, Y, _params(D, p, seed=9))
+    vals = []
+    for tiny in (True, False):
+        eng.set_tiny(tiny)
+        vals.append(m.log_marginal_likelihood_and_grad())
+        vals.append((float(m.log_marginal_likelihood()), None))
+    eng.set_tiny(True)
+    assert abs(vals[0][0] - vals[2][0]) < 1e-12 * abs(vals[2][0])
+    assert vals[0][0] == vals[1][0]                           # value-only call: the same kernel
+    np.testing.assert_allclose(vals[0][1], vals[2][1], rtol=0, atol=1e-10 * np.abs(vals[2][1]).max())
+    lo, go = O.gpr_lml_and_grad(X, Y, _oracle_params(m))
+    gov = np.concatenate([[go["vL"]], go["lL"], [go["vD"]], go["lD"], [go["rho0"]], [go["noise"]]])
+    assert abs(vals[0][0] - lo) < 1e-11 * abs(lo)
+    np.testing.assert_allclose(vals[0][1], gov, rtol=0, atol=1e-8 * np.abs(gov).max())
+
+
+def test_tiny_adam_matches_step_sequence(hbs, eng):
+    """The HBS Adam step (mfgp_gpr_adam_step, graph-captured) through k_gpr_tiny and through the
+    step sequence: 200 steps, the same loss history to rounding (the dynamics are smooth there)."""
+    from multi_fidelity_gpflow_amd import models as MM
+    hs = []
+    for tiny in (True, False):
+        eng.set_tiny(tiny)
+        MM._pool_clear()   # a pooled session would replay the other schedule's captured graphs
+        m = M.MultiFidelityGPModel(hbs["X"], hbs["Y"], M.SquaredExponential(lengthscales=np.ones(5)),
+                                   M.SquaredExponential(lengthscales=np.ones(5)))
+        m.optimize(max_iters=200, learning_rate=0.1, verbose=False)
+        hs.append(np.array(m.loss_history))
+    eng.set_tiny(True)
+    MM._pool_clear()
+    err = np.abs(hs[0] - hs[1]) / np.abs(hs[1])
+    print(f"tiny vs steps, 200 HBS Adam steps: max rel {err.max():.1e}")
+    assert err.max() < 1e-10
 
 
 def test_large_synthetic_properties(eng):

@@ -7,5 +7,5 @@ echo GOKU_DONE
 bash tools/profile_round.sh gpurun_out/$R/synth synth "--steps 6 --warmup 2" "--steps 2 --warmup 1"
 echo SYNTH_DONE
 bash tools/profile_round.sh gpurun_out/$R/goku_svgp goku_svgp "--steps 50 --warmup 20" \
-    "--steps 10 --warmup 10 --no-train-predict" "--steps 50 --warmup 20 --no-train-predict --no-cpu-baseline"
+    "--steps 10 --warmup 10 --no-train-predict --no-latent" "--steps 50 --warmup 20 --no-train-predict --no-cpu-baseline"
 echo SVGP_DONE
