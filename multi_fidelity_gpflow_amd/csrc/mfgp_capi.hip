@@ -34,7 +34,7 @@ struct mfgp_handle_s {
     int f32_lookahead;          // fp32 sweep: factor the next panel beside the trailing update
     int f32_reserve;            // CUs the capped trailing update leaves to the side stream
     int f32_refine;             // fp32 value-only LML (one step) / predict mean (this many steps): fp64 refinement (mfgp_set_f32_refine)
-    int tiny;                   // small problems (n, p <= 64, D <= 16, AR1 kernel): one-launch LML step (mfgp_set_tiny)
+    int tiny;                   // small problems (n, p <= 64, D <= 16, AR1 kernel): one-launch LML step (mfgp_set_tiny, default off)
     hipStream_t side;           // its high-priority side stream + fork / join events (created with the handle)
     hipEvent_t ev_fork, ev_join;
 };
@@ -692,7 +692,8 @@ int mfgp_create(int device, mfgp_handle_t* out) {
     if (const char* gv = getenv("MFGP_GRAM_WGS")) h->gram_wgs = atoi(gv);
     h->gram_legacy = 0;
     h->flow_d0 = 0;
-    h->tiny = 1;
+    h->tiny = 0;   // measured no faster than the step sequence at HBS (40.3 vs 43.5 us of kernel time, the
+                   // same wall time a step in the captured graph): opt-in (MFGP_TINY=1 / mfgp_set_tiny)
     if (const char* tv = getenv("MFGP_TINY")) h->tiny = atoi(tv) != 0;
 #ifdef MFGP_AB_KNOBS
     // A/B diagnostics only (a build with -DMFGP_AB_KNOBS, then tools/ab_env.sh): each switches the
