@@ -273,6 +273,35 @@ def test_adam_trajectory_kats(which, hbs, goku, kats, eng):
     assert float(m.likelihood.variance.numpy()) == pytest.approx(1e-3, rel=1e-12)
 
 
+def test_flow_trace_mode_stays_in_its_workspace(eng):
+    """in trace mode (mfgp_set_flow(h, 2)) k_gram_flow writes a per-workgroup
+    timeline at the end of the workspace; its region is sized from the k_gram_flow grid
+    (flow_gram_dbg_count).  At T = 132 tiles (n = 4200, a grid of ~2300 set-up workgroups) every
+    byte past the reported workspace size must stay untouched, and the trace mode must not change
+    the results."""
+    from multi_fidelity_gpflow_amd import _lib
+    rng = np.random.default_rng(31)
+    n_lf, n_hf, p, D = 3900, 300, 4, 3
+    X = np.vstack([np.hstack([rng.random((n_lf, D)), np.zeros((n_lf, 1))]),
+                   np.hstack([rng.random((n_hf, D)), np.ones((n_hf, 1))])])
+    Y = np.sin(X[:, :D] @ rng.standard_normal((D, p)) * 3.0)
+    Xd, Yd = torch.tensor(X, device=eng.device), torch.tensor(Y, device=eng.device)
+    th = torch.tensor(np.concatenate([[1.0], np.full(D, 0.3), [0.5], np.full(D, 0.4), [0.9, 1e-3]]), device=eng.device)
+    nbytes = eng.gpr_workspace_bytes(X.shape[0], p, D)
+    ws = torch.full((nbytes + (1 << 20),), 0x5A, dtype=torch.uint8, device=eng.device)
+    ref, _ = eng.gpr_lml(Xd, Yd, th, want_grad=True, ws=ws)
+    ref = ref.cpu().numpy().copy()
+    _lib.check(eng.lib.mfgp_set_flow(eng.h, 2), "mfgp_set_flow")
+    try:
+        got, info = eng.gpr_lml(Xd, Yd, th, want_grad=True, ws=ws)
+        torch.cuda.synchronize()
+    finally:
+        eng.set_flow(True)
+    assert int(info.item()) == 0
+    assert bool((ws[nbytes:] == 0x5A).all())
+    np.testing.assert_array_equal(got.cpu().numpy(), ref)
+
+
 def test_graph_and_eager_agree(hbs, eng):
     hs = []
     for graph in (True, False):
