@@ -310,10 +310,38 @@ __device__ __forceinline__ double sel4(int s, double v0, double v1, double v2, d
 
 // R work of round K, deferred into round K+1 (after its LDS reads are issued) so that the
 // in-order issue of the A chain is never held behind it: X = V L_M^{-1}, W_R, R -= W_R R[P, :].
+// W1_ONEHOT: the lane-constant selections of the single-wave factor (component kk = l >> 4 of a
+// row's four values, the unit vector e_p of pivot row p = l & 3) as one-hot products / selects of
+// per-lane constants formed once, instead of v_cndmask trees rebuilt every round
+#ifndef W1_ONEHOT
+#define W1_ONEHOT 1   // 8.1k -> 7.65k clocks for the fused NB = 32 factor, bit-identical (tools/ubench_rsplit.hip)
+#endif
 struct W1Pending {
     double L10, L20, L30, L21, L31, L32;
     double v[2][4];   // rows h = 0, 1: Z (rows below) or e_p (pivot rows)
+    double u[4];      // W1_ONEHOT: u[c] = (kk == c)
+    double e[4];      // W1_ONEHOT: e[c] = (p == c)
+    double ekk;       // W1_ONEHOT: (p == kk)
 };
+__device__ __forceinline__ void w1_consts(W1Pending& pd, int l) {
+    const int kk = l >> 4, p = l & 3;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        pd.u[c] = (kk == c) ? 1.0 : 0.0;
+        pd.e[c] = (p == c) ? 1.0 : 0.0;
+    }
+    pd.ekk = (p == kk) ? 1.0 : 0.0;
+}
+// component kk of (a0, a1, a2, a3): exact for finite values (one term is 1 x a_kk, the rest 0 x a_c)
+__device__ __forceinline__ double w1_pick(const W1Pending& pd, int kk, double a0, double a1, double a2, double a3) {
+#if W1_ONEHOT
+    (void)kk;
+    return fma(pd.u[3], a3, fma(pd.u[2], a2, fma(pd.u[1], a1, pd.u[0] * a0)));
+#else
+    (void)pd;
+    return sel4(kk, a0, a1, a2, a3);
+#endif
+}
 
 template <int K>
 __device__ __forceinline__ void w1_rwork(const W1Pending& pd, f64x4& r00, f64x4& r10, f64x4& r11, int l) {
@@ -330,8 +358,12 @@ __device__ __forceinline__ void w1_rwork(const W1Pending& pd, f64x4& r00, f64x4&
         const double x2 = fma(-pd.L32, x3, pd.v[h][2]);
         const double x1 = fma(-pd.L31, x3, fma(-pd.L21, x2, pd.v[h][1]));
         const double x0 = fma(-pd.L30, x3, fma(-pd.L20, x2, fma(-pd.L10, x1, pd.v[h][0])));
-        const double xk = sel4(kk, x0, x1, x2, x3);
+        const double xk = w1_pick(pd, kk, x0, x1, x2, x3);
+#if W1_ONEHOT
+        wR[h] = below ? xk : piv ? (pd.ekk - xk) : 0.0;
+#else
         wR[h] = below ? xk : piv ? ((p == kk ? 1.0 : 0.0) - xk) : 0.0;
+#endif
     }
     if constexpr (bk == 0) {
         const double pR0 = r00[kq];
@@ -410,8 +442,8 @@ __device__ __forceinline__ void w1_round(double* __restrict__ Pn, double* __rest
             const double y2 = fma(-L21, y1, fma(-L20, y0, ub.x));
             const double y3 = fma(-L32, y2, fma(-L31, y1, fma(-L30, y0, ub.y)));
             const double z0 = y0 * i0, z1 = y1 * i1, z2 = y2 * i2, z3 = y3 * i3;
-            zA[h] = below ? sel4(kk, z0, z1, z2, z3) : 0.0;
-            yB[h] = sel4(kk, y0, y1, y2, y3);
+            zA[h] = below ? w1_pick(pd, kk, z0, z1, z2, z3) : 0.0;
+            yB[h] = w1_pick(pd, kk, y0, y1, y2, y3);
             if constexpr (PUB) ym[h] = below ? yB[h] : 0.0;
             zs[h][0] = z0; zs[h][1] = z1; zs[h][2] = z2; zs[h][3] = z3;
         }
@@ -434,7 +466,11 @@ __device__ __forceinline__ void w1_round(double* __restrict__ Pn, double* __rest
             const bool piv = ((16 * h + lc) >> 2) == K;
             const int p = lc & 3;
 #pragma unroll
+#if W1_ONEHOT
+            for (int c = 0; c < 4; ++c) pd.v[h][c] = piv ? pd.e[c] : zs[h][c];
+#else
             for (int c = 0; c < 4; ++c) pd.v[h][c] = piv ? (p == c ? 1.0 : 0.0) : zs[h][c];
+#endif
         }
         pd.L10 = L10; pd.L20 = L20; pd.L30 = L30; pd.L21 = L21; pd.L31 = L31; pd.L32 = L32;
         if constexpr (PUB) {
@@ -476,6 +512,7 @@ __device__ __forceinline__ void tile_potrf_inv_w1_wave(const double* __restrict_
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // X fully read before Pn (may alias) is written
         double* dpv = Pn + 128;                                // [32] pivots + dump slots
         W1Pending pd;
+        w1_consts(pd, l);
         w1_round<0, PUB>(Pn, dpv, a00, a01, a11, r00, r10, r11, pd, l, pub);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         // L^{-1} = diag(d)^{-1/2} L_u^{-1}; L_ii = sqrt(d_i); first bad pivot by one ballot
@@ -629,6 +666,7 @@ __device__ __forceinline__ void w1r_round(const double* __restrict__ Zb, const i
         const f64x2 p2 = *reinterpret_cast<const f64x2*>(Z + 4 * (4 * K + 2));
         const f64x2 p3a = *reinterpret_cast<const f64x2*>(Z + 4 * (4 * K + 3));
         W1Pending pd;
+        w1_consts(pd, l);
         pd.L10 = Z[4 * (4 * K + 1)];
         pd.L20 = p2.x; pd.L21 = p2.y;
         pd.L30 = p3a.x; pd.L31 = p3a.y; pd.L32 = Z[4 * (4 * K + 3) + 2];

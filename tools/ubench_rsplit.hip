@@ -110,6 +110,10 @@ static void run(const char* name, const double* hA, const double* dA, double* dR
     bool same = true;
     if (V == 0) { memcpy(Rref, R, sizeof(R)); memcpy(dref, dg, sizeof(dg)); }
     else same = memcmp(Rref, R, sizeof(R)) == 0 && memcmp(dref, dg, sizeof(dg)) == 0;
+    unsigned long long hsh = 1469598103934665603ull;
+    for (int i = 0; i < NB * NB; ++i) { unsigned long long b; memcpy(&b, &R[i], 8); hsh = (hsh ^ b) * 1099511628211ull; }
+    for (int i = 0; i < NB; ++i) { unsigned long long b; memcpy(&b, &dg[i], 8); hsh = (hsh ^ b) * 1099511628211ull; }
+    printf("  [bits %016llx] ", hsh);
     printf("%-26s A done %6lld clk  D done %6lld clk  err D %.2e  L_ii %.2e  bad=%d  %s\n", name, c[0], c[1],
            (double)(eR / mR), (double)eD, b[0], V == 0 ? "(reference bits)" : (same ? "bitwise = fused" : "bits differ from fused (rounding)"));
 }
