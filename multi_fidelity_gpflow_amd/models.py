@@ -315,9 +315,20 @@ class _AdamCore:
             self.X = torch.empty_like(X)
             self.Y = torch.empty_like(Y)
             self.st = AdamState(eng.device, tm.u(), tm.trainable(), tm.tie(), lr)
+            G = self.st.u.numel()
+            # the moments and the two counters as views of one buffer each (one zeroing launch per
+            # load); the per-model inputs travel in ONE pinned host-to-device copy and the results
+            # back in ONE device-to-host copy (fewer synchronising transfers on the HBS protocol)
+            self.mv = torch.zeros((2 * G,), dtype=torch.float64, device=eng.device)
+            self.st.m, self.st.v = self.mv[:G], self.mv[G:]
+            self.si = torch.zeros((2,), dtype=torch.int32, device=eng.device)
+            self.st.step = self.si[0:1]
+            self.info = self.si[1:2]
+            self.h_in = torch.empty((3 * G,), dtype=torch.float64, pin_memory=True)
+            self.d_in = torch.empty((3 * G,), dtype=torch.float64, device=eng.device)
+            self.h_out = torch.empty((max_iters + G + 2,), dtype=torch.float64, pin_memory=True)
             self.hist = torch.zeros((max_iters,), dtype=torch.float64, device=eng.device)
             self.out = torch.empty((1 + theta_size(tm.d),), dtype=torch.float64, device=eng.device)
-            self.info = torch.zeros((1,), dtype=torch.int32, device=eng.device)
             n, p, d = X.shape[0], Y.shape[1], tm.d
             self.ws_bytes = eng.gpr_workspace_bytes(n, p, d, X.dtype)
             self.ws = eng.private_workspace(self.ws_bytes)
@@ -325,16 +336,20 @@ class _AdamCore:
 
     def load(self, X: torch.Tensor, Y: torch.Tensor, tm: "_ThetaMap"):
         """A model's data and initial state into the buffers (on the core's stream)."""
-        st, dev = self.st, self.eng.device
+        st = self.st
+        G = st.u.numel()
         self.X.copy_(X)
         self.Y.copy_(Y)
-        st.u.copy_(torch.as_tensor(tm.u(), dtype=torch.float64).to(dev, non_blocking=True))
-        st.trainable.copy_(torch.as_tensor(tm.trainable().astype(np.uint8)).to(dev, non_blocking=True))
-        st.tie.copy_(torch.as_tensor(tm.tie().astype(np.int32)).to(dev, non_blocking=True))
-        st.m.zero_()
-        st.v.zero_()
-        st.step.zero_()
-        self.info.zero_()
+        h = self.h_in.numpy()   # the previous load's copy from it completed before that session finished
+        h[:G] = tm.u()
+        h[G:2 * G] = tm.trainable()
+        h[2 * G:] = tm.tie()
+        self.d_in.copy_(self.h_in, non_blocking=True)
+        st.u.copy_(self.d_in[:G])
+        st.trainable.copy_(self.d_in[G:2 * G])
+        st.tie.copy_(self.d_in[2 * G:])
+        self.mv.zero_()
+        self.si.zero_()
         self.eng.theta_from_u(st.u, st.theta, tm.noise_index)
         if not self.warm:
             # one eager evaluation before any capture: builds the schedule tables and sets every
@@ -433,12 +448,18 @@ class AdamSession:
         self.close()
 
     def finish(self):
+        n, G, core = self.done, self.st.u.numel(), self._core
+        if core is None:
+            raise MFGPError("AdamSession: the session is finished")
+        with torch.cuda.stream(self.stream):   # loss history, u, info and step in one copy
+            packed = torch.cat([self.hist[:n], self.st.u, core.si.to(torch.float64)])
+            core.h_out[:n + G + 2].copy_(packed, non_blocking=True)
         self.sync()
-        h = self.hist[:self.done].cpu().numpy()
+        res = core.h_out.numpy()[:n + G + 2].copy()
+        h = res[:n]
         self.model.loss_history = [np.float64(v) for v in h]
-        self.tm.set_u(self.st.u.cpu().numpy())
-        v = int(self.info.item())
-        steps = int(self.st.step.item())
+        self.tm.set_u(res[n:n + G])
+        steps, v = int(res[n + G]), int(res[n + G + 1])
         self._retire()
         if v == 0 and steps != self.done and np.all(np.isfinite(h)):
             # a failed step leaves the step counter behind and the next one retries it, so a
