@@ -277,6 +277,7 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
         g.padded = 1; g.npad = L.npad; g.tiles_c = L.T; g.add_noise = 1; g.diag_add = nlf ? GRAPH_JITTER : 0.0;
         g.Dd = L.Dd; g.sD = 0; g.ldiag = L.ldiag; g.sL = 0; g.info = info; g.nlf = nlf;
         g.cnt = L.cnt; g.ncnt = L.ncnt;
+        if (MFGP_REDUCE_FLAG) { g.isent = L.items; g.nisent = L.G + 2; }
         const bool order = want_grad && std::abs(L.gchunk) + L.T + L.Tp < 2048;   // gram LDS holds the histogram
         if (order) { g.gorder = L.gorder; g.gT = L.T; g.gchunk = L.gchunk; g.gTp = L.Tp; }
         if (L.flow_wgs) { g.fown = L.own; g.fW = FLOW_WAVES * (L.flow_wgs - 1); g.fflags = L.flags; g.nfflags = L.nflags; g.fpub = L.pub; g.npub = L.npub; g.fsdelta = L.sdelta; }
@@ -338,6 +339,7 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
     f.items = L.items;
     f.G = L.G;
     f.cnt = L.cnt;
+    f.flag = MFGP_REDUCE_FLAG;   // the Gram launch above filled items[] with the sentinel
     hipLaunchKernelGGL(k_reduce_items, dim3(2 + (want_grad ? L.G : 0)), dim3(NTHREADS), 0, s, f);
     if (pm) pm->mark(s);
     return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;

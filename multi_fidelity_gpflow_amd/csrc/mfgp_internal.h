@@ -23,6 +23,7 @@ struct GramArgs {
     double* R; long ldr; long sR; const double* Y; long ldy; long sY; int p, ppad;
     int nlf;                                  // 0: LinearMultiFidelityKernel; m >= 1: graph kernel, m LF sources
     int* cnt; int ncnt;                       // arrival counters zeroed by workgroup 0 (reduce merge)
+    double* isent; int nisent;                // k_reduce_items' items, FLOW_SENTINEL-filled by workgroup 0 (FinArgs::flag)
     // k_grad task order (nullptr: none): one extra LAST workgroup builds it (grad_order)
     int* gorder; int gT, gchunk, gTp;
     // k_chol_flow owner table (nullptr: none): one more extra workgroup builds it and zeroes
@@ -97,6 +98,10 @@ struct GradArgs {
 };
 
 constexpr int FIN_MAXG = 254;   // theta entries finalize_body stages in LDS (graph kernel: <= 186)
+// k_reduce_items' sentinel protocol (FinArgs::flag) on the fp64 LML path; 0: arrival counter
+#ifndef MFGP_REDUCE_FLAG
+#define MFGP_REDUCE_FLAG 1
+#endif
 struct FinArgs {
     const double* zpart; int nz;
     const double* ldiag; int n;
@@ -117,6 +122,8 @@ struct FinArgs {
     double* items;                    // [2 + G] stage-1 reduction results
     int G;                            // theta entries (kernel_theta_size)
     int* cnt;                         // arrival counter (zero on entry): last item workgroup finalizes
+    int flag;                         // 1: items[] hold FLOW_SENTINEL on entry (the Gram launch filled them):
+                                      //    workgroup 0 finalizes once every other item is published
 };
 
 struct PredAArgs {

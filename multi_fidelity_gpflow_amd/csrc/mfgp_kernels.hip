@@ -12,6 +12,7 @@
 //
 // Every kernel runs 256-thread workgroups on NB x NB fp64 tiles; tile products
 // go through v_mfma_f64_16x16x4_f64 (mfgp_device.h).
+#include "../../include/mfgp.h"
 #include "mfgp_device.h"
 #include "mfgp_internal.h"
 #include "mfgp_flow.h"
@@ -153,6 +154,14 @@ __device__ __forceinline__ double gram_entry(const double* aL1, const double* aD
     return kL * (rho * rho) + kD;                      // K_HH (linear.py:96)
 }
 
+// k_reduce_items' item slots to FLOW_SENTINEL (sc1, as the publication area: no XCD's L2 may keep
+// a clean sentinel copy for the finalizer's sc1 polls), for its sentinel protocol (FinArgs::flag)
+__device__ __forceinline__ void gram_fill_items(const GramArgs& a) {
+    for (int e = threadIdx.x; e < a.nisent; e += NTHREADS)
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.isent) + e, FLOW_SENTINEL, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Sentinel fill of the k_chol_flow publication area (grid-stride over ALL workgroups of the
 // launch).  sc1 (write-through, line dropped from this XCD's L2): a plain store would leave a
 // clean copy of the sentinel in this XCD's L2 that the flow's sc1 polls could be served from.
@@ -245,6 +254,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
     }
     if (a.cnt && blockIdx.x == 0 && b == 0)
         for (int e = threadIdx.x; e < a.ncnt; e += NTHREADS) a.cnt[e] = 0;
+    if (a.isent && blockIdx.x == 0 && b == 0) gram_fill_items(a);
     const MFTheta th{a.theta + b * a.stheta, a.D};
     MFScal sc{0.0, 0.0, 0.0};
     double noise = 0.0;
@@ -566,6 +576,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram_flow(GramArgs a, int nblk) {
         if (a.gorder && bx == (int)gridDim.x - 1) build_grad_order(a.gT, a.gchunk, a.gTp, a.gorder, sh);
         else if (a.fown) build_flow_owner(a.npad / 32, a.ppad / 32, a.fW, a.fown, a.fflags, a.nfflags, sh, a.fsdelta);
         if (a.dbg && t == 0) { a.dbg[3 * bx] = t0; a.dbg[3 * bx + 1] = __builtin_amdgcn_s_memrealtime(); }
+        if (a.isent && bx == (int)gridDim.x - 1) gram_fill_items(a);   // (off the factor workgroup's path)
         gram_fill_pub(a);
         if (a.dbg && t == 0) a.dbg[3 * bx + 2] = __builtin_amdgcn_s_memrealtime();
         return;
@@ -1376,12 +1387,32 @@ size_t grad_smem_bytes(int nb, int G, int nil2) {
 
 // Stage 2: LML, gradient output and the optional Keras-Adam step; run by the last
 // item workgroup of k_reduce_items to arrive.
-__device__ void adam_body(const FinArgs& a, int G, int s, const double* gsh, const int* tsh);
+// Adam inputs of theta entry threadIdx.x, loaded at kernel start by the sentinel protocol
+struct FinPre {
+    double u, m, v;
+    int tr;
+};
+__device__ void adam_body(const FinArgs& a, int G, int s, const double* gsh, const int* tsh, const FinPre* pre);
 static_assert(FIN_MAXG >= kernel_theta_size(MFGP_MAX_LF, MAXD) && FIN_MAXG >= kernel_theta_size(0, MAXD),
               "finalize_body stages every theta entry in LDS");
+static_assert(FIN_MAXG <= NTHREADS, "one theta entry per finalize thread");
+// gsh = [sum Z^2, sum log L_ii, grad_0 .. grad_{G-1}] in LDS (read after a barrier)
+__device__ void finalize_from(const FinArgs& a, int G, const double* gsh, const int* tsh, int info0, int s,
+                              const FinPre* pre) {
+    const double LOG2PI = 1.8378770664093453;
+    double lml = -0.5 * gsh[0] - (double)a.P * gsh[1] - 0.5 * (double)a.n * (double)a.P * LOG2PI;
+    if (info0 != 0) lml = NAN;
+    if (a.adam && info0 == 0) adam_body(a, G, s, gsh + 2, a.tie ? tsh : nullptr, pre);
+    if (threadIdx.x == 0) a.out[0] = lml;
+    if (a.want_grad)
+        for (int q = threadIdx.x; q < G; q += NTHREADS) a.out[1 + q] = gsh[2 + q];
+    if (!a.adam) return;
+    if (threadIdx.x == 0) a.loss_hist[s] = -lml;
+    __syncthreads();   // every wave has read *a.step
+    if (threadIdx.x == 0 && info0 == 0) *a.step = s + 1;
+}
 __device__ void finalize_body(const FinArgs& a) {
     const int G = a.G ? a.G : theta_size(a.D);
-    const double LOG2PI = 1.8378770664093453;
     // every input in ONE round trip into LDS, before the first store (the outputs may alias them
     // as far as the compiler knows; a dependent sc1 load per tied entry cost ~8 us per step)
     __shared__ double gsh[FIN_MAXG + 2];   // [sum Z^2, sum log L_ii, grad_0 .. grad_{G-1}]
@@ -1392,24 +1423,15 @@ __device__ void finalize_body(const FinArgs& a) {
     const int info0 = a.info[0];
     const int s = a.adam ? *a.step : 0;
     __syncthreads();
-    double lml = -0.5 * gsh[0] - (double)a.P * gsh[1] - 0.5 * (double)a.n * (double)a.P * LOG2PI;
-    if (info0 != 0) lml = NAN;
-    if (a.adam && info0 == 0) adam_body(a, G, s, gsh + 2, a.tie ? tsh : nullptr);
-    if (threadIdx.x == 0) a.out[0] = lml;
-    if (a.want_grad)
-        for (int q = threadIdx.x; q < G; q += NTHREADS) a.out[1 + q] = gsh[2 + q];
-    if (!a.adam) return;
-    if (threadIdx.x == 0) a.loss_hist[s] = -lml;
-    __syncthreads();   // every wave has read *a.step
-    if (threadIdx.x == 0 && info0 == 0) *a.step = s + 1;
+    finalize_from(a, G, gsh, tsh, info0, s, nullptr);
 }
 
-__device__ void adam_body(const FinArgs& a, int G, int s, const double* gsh, const int* tsh) {
+__device__ void adam_body(const FinArgs& a, int G, int s, const double* gsh, const int* tsh, const FinPre* pre) {
     const double t = (double)(s + 1);
     const double alpha = a.lr * sqrt(1.0 - pow(a.b2, t)) / (1.0 - pow(a.b1, t));
     for (int q = threadIdx.x; q < G; q += NTHREADS) {
-        if (a.trainable[q]) {
-            const double uq = a.u[q];
+        if (pre ? pre->tr : a.trainable[q]) {
+            const double uq = pre ? pre->u : a.u[q];
             double gc = gsh[q];
             if (tsh) {   // a variable shared by several theta entries gets the summed gradient
                 gc = 0.0;
@@ -1417,7 +1439,7 @@ __device__ void adam_body(const FinArgs& a, int G, int s, const double* gsh, con
                     if (tsh[r] == tsh[q]) gc += gsh[r];
             }
             const double g = (-gc) / (exp(-uq) + 1.0);   // loss = -lml; TF SoftplusGrad form
-            double mq = a.m[q], vq = a.v[q];
+            double mq = pre ? pre->m : a.m[q], vq = pre ? pre->v : a.v[q];
             mq += (g - mq) * (1.0 - a.b1);
             vq += (g * g - vq) * (1.0 - a.b2);
             const double un = uq - (mq * alpha) / (sqrt(vq) + a.eps);
@@ -1429,12 +1451,55 @@ __device__ void adam_body(const FinArgs& a, int G, int s, const double* gsh, con
     }
 }
 
+// Sentinel protocol, workgroup 0 (FinArgs::flag): the finalize inputs (info, step, Adam state,
+// ties) are loaded before its own item is summed, then thread q < gridDim.x polls item q (sc1)
+// until it is no longer FLOW_SENTINEL.  Against store -> drain -> atomic arrival -> sc1 reload
+// by the last workgroup, two memory round trips fewer, and the Adam loads off the tail.  A poll
+// that exceeds REDUCE_TIMEOUT_TICKS (100 MHz) marks the evaluation failed: NaN LML, no Adam step.
+constexpr long long REDUCE_TIMEOUT_TICKS = 5000000;   // 50 ms
+__device__ void reduce_items_wg0(const FinArgs& a) {
+    __shared__ double gsh[FIN_MAXG + 2];
+    __shared__ int tsh[FIN_MAXG];
+    __shared__ double red[4];
+    __shared__ int tmo;
+    const int t = threadIdx.x;
+    const int G = a.G ? a.G : theta_size(a.D);
+    FinPre pre{0.0, 0.0, 0.0, 0};
+    if (a.adam && t < G) {
+        pre.tr = a.trainable[t];
+        pre.u = a.u[t];
+        pre.m = a.m[t];
+        pre.v = a.v[t];
+        if (a.tie) tsh[t] = a.tie[t];
+    }
+    int info0 = a.info[0];
+    const int s = a.adam ? *a.step : 0;
+    if (t == 0) tmo = 0;
+    double z = 0.0;
+    for (int e = t; e < a.nz; e += NTHREADS) z += a.zpart[e];
+    z = block_sum(z, red);   // (its barriers also order tmo = 0 before the polls)
+    if (t >= 1 && t < (int)gridDim.x) {
+        const long long t0 = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+            const double v = ld_coherent(a.items + t);
+            if ((unsigned long long)__double_as_longlong(v) != FLOW_SENTINEL) { gsh[t] = v; break; }
+            if (__builtin_amdgcn_s_memrealtime() - t0 > REDUCE_TIMEOUT_TICKS) { gsh[t] = NAN; tmo = 1; break; }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    if (t == 0) gsh[0] = z;
+    __syncthreads();
+    if (tmo && info0 == 0) info0 = MFGP_FLOW_TIMEOUT;
+    finalize_from(a, G, gsh, tsh, info0, s, &pre);
+}
+
 // Stage 1 of the step reduction: workgroup `it` sums item `it` of
 // [sum Z^2, sum log L_ii, grad_0 .. grad_{G-1}] (partials stored [item][task]) with
 // all 256 threads in flight at once; deterministic order.
 __global__ __launch_bounds__(NTHREADS) void k_reduce_items(FinArgs a) {
     __shared__ double red[4];
     const int it = blockIdx.x;
+    if (a.flag && it == 0) { reduce_items_wg0(a); return; }
     double s = 0.0;
     if (it == 0) {
         for (int e = threadIdx.x; e < a.nz; e += NTHREADS) s += a.zpart[e];
@@ -1460,6 +1525,10 @@ __global__ __launch_bounds__(NTHREADS) void k_reduce_items(FinArgs a) {
         s = (s + s1) + (s2 + s3);
     }
     s = block_sum(s, red);
+    if (a.flag) {   // sentinel protocol: workgroup 0 polls this item
+        if (threadIdx.x == 0) st_coherent(a.items + it, s);
+        return;
+    }
     __shared__ int last;
     if (threadIdx.x == 0) {
         st_coherent(a.items + it, s);
