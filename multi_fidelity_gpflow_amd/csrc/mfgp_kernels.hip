@@ -1489,7 +1489,10 @@ __device__ void reduce_items_wg0(const FinArgs& a) {
     }
     if (t == 0) gsh[0] = z;
     __syncthreads();
-    if (tmo && info0 == 0) info0 = MFGP_FLOW_TIMEOUT;
+    if (tmo && info0 == 0) {   // (eager callers see it as a timed-out evaluation)
+        info0 = MFGP_FLOW_TIMEOUT;
+        if (t == 0) const_cast<int*>(a.info)[0] = MFGP_FLOW_TIMEOUT;
+    }
     finalize_from(a, G, gsh, tsh, info0, s, &pre);
 }
 
