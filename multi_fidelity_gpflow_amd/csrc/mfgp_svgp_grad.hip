@@ -328,7 +328,20 @@ __global__ __launch_bounds__(NTHREADS) void k_kgrad(const double* P1, long ld1, 
     const int bbase = bc * KG_COLS;
     const int bend = min(n2, bbase + KG_COLS);
     const double* wrow = Wt + lat * sW + (long)a * ldw;
-    // b rows are staged KG_CHUNK per half at a time: [half][row][XS]
+    // b rows are staged KG_CHUNK per half at a time: [half][row][XS].  The pair weights of the next
+    // chunk are loaded (into registers) while this chunk's pairs are processed: loaded one step
+    // ahead, the strided W loads left every step waiting on a memory round trip.
+    constexpr int NST = KG_CHUNK / 4;
+    const int bhalf = bbase + (KG_COLS / 2) * half;
+    auto wload = [&](int c0, double* wv) {
+#pragma unroll
+        for (int s = 0; s < NST; ++s) {
+            const int b = bhalf + c0 + 4 * s + lk;
+            wv[s] = (aval && b < bend) ? wrow[b] : 0.0;
+        }
+    };
+    double wc[NST], wn[NST];
+    wload(0, wc);
     for (int c0 = 0; c0 < KG_COLS / 2; c0 += KG_CHUNK) {
         __syncthreads();   // the previous chunk is consumed
         for (int e = t; e < 2 * KG_CHUNK * XS; e += NTHREADS) {
@@ -343,21 +356,15 @@ __global__ __launch_bounds__(NTHREADS) void k_kgrad(const double* P1, long ld1, 
             lds_buf[e] = v;
         }
         __syncthreads();
+        if (c0 + KG_CHUNK < KG_COLS / 2) wload(c0 + KG_CHUNK, wn);   // in flight under this chunk's pairs
         const double* xs = lds_buf + half * KG_CHUNK * XS;
-        const int bh0 = bbase + (KG_COLS / 2) * half + c0;
-        // W of the first step; each step loads the next one's before its own work
-        double wnext = 0.0;
-        {
-            const int b = bh0 + lk;
-            if (aval && b < bend) wnext = wrow[b];
-        }
+        const int bh0 = bhalf + c0;
+#pragma unroll 1
         for (int s4 = 0; s4 < KG_CHUNK; s4 += 4) {
             const int r = s4 + lk, b = bh0 + r;
-            double wv = wnext;
-            {
-                const int bn = b + 4;
-                wnext = (aval && s4 + 4 < KG_CHUNK && bn < bend) ? wrow[bn] : 0.0;
-            }
+            double wv = wc[0];   // (the chunk's weights rotate through wc: a rolled loop, static indices)
+#pragma unroll
+            for (int s = 0; s + 1 < NST; ++s) wc[s] = wc[s + 1];
             const double* xr = xs + r * XS;
             const double fb = xr[DC];
             const bool Lb = (fb == 0.0), Hb = (fb == 1.0);
@@ -404,6 +411,8 @@ __global__ __launch_bounds__(NTHREADS) void k_kgrad(const double* P1, long ld1, 
                 if (anyhh) accD[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(wd, bv, accD[c], 0, 0, 0);
             }
         }
+#pragma unroll
+        for (int s = 0; s < NST; ++s) wc[s] = wn[s];
     }
     __syncthreads();   // lds_buf becomes the moment buffer
     // scalar theta partials: one LDS slot per wave
