@@ -1765,17 +1765,30 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
     }
     // the Adam state, loaded now: its latency hides under the whole evaluation (adam_body would
     // issue these loads, dependent on *step, at the very end)
+    // (theta entry q = t - 64: wave 1 owns the Adam step, so its step-size and softplus-gradient
+    // factors are formed while wave 0 factors D_0)
     const FinArgs& f = a.f;
+    const int aq = t - 64;
+    const bool aown = aq >= 0 && aq < G;
     double pu = 0.0, pm = 0.0, pv = 0.0;
     int ptr = 0, ptie = 0, pst = 0;
     if (f.adam) {
-        if (t < G) {
-            pu = f.u[t]; pm = f.m[t]; pv = f.v[t]; ptr = f.trainable[t];
-            ptie = f.tie ? f.tie[t] : t;
+        if (aown) {
+            pu = f.u[aq]; pm = f.m[aq]; pv = f.v[aq]; ptr = f.trainable[aq];
+            ptie = f.tie ? f.tie[aq] : aq;
         }
         pst = *f.step;
     }
-    // ---- stage: raw rows, scaled rows (x * rcp_nr(l), as k_gram), norms, fidelity flags
+    double a_alpha = 0.0, a_eu = 0.0;
+    // ---- stage: raw rows, scaled rows (x * rcp_nr(l), as k_gram), norms, fidelity flags.  The row
+    //      loads are issued before the lengthscale reciprocals wait on theta (one round trip)
+    constexpr int XPER = (TINY_N * TINY_XS + NTHREADS - 1) / NTHREADS;
+    double xv0[XPER];
+#pragma unroll
+    for (int q = 0; q < XPER; ++q) {
+        const int e = t + q * NTHREADS, r = e / TINY_XS, d = e % TINY_XS;
+        xv0[q] = (e < TINY_N * TINY_XS && r < n && d <= D) ? a.X[(long)r * a.ldx + d] : 0.0;
+    }
     if (t < D) {
         il[t] = rcp_nr(a.theta[1 + t]);
         il[TINY_MAXD + t] = rcp_nr(a.theta[2 + D + t]);
@@ -1785,18 +1798,9 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
         lv[TINY_MAXD + t] = th.lD(t);
     }
     const int D4 = pad4(D);
-    {   // every row element in flight before the first LDS store
-        constexpr int PER = (TINY_N * TINY_XS + NTHREADS - 1) / NTHREADS;
-        double v[PER];
 #pragma unroll
-        for (int q = 0; q < PER; ++q) {
-            const int e = t + q * NTHREADS, r = e / TINY_XS, d = e % TINY_XS;
-            v[q] = (e < TINY_N * TINY_XS && r < n && d <= D) ? a.X[(long)r * a.ldx + d] : 0.0;
-        }
-#pragma unroll
-        for (int q = 0; q < PER; ++q)
-            if (t + q * NTHREADS < TINY_N * TINY_XS) xr[t + q * NTHREADS] = v[q];
-    }
+    for (int q = 0; q < XPER; ++q)
+        if (t + q * NTHREADS < TINY_N * TINY_XS) xr[t + q * NTHREADS] = xv0[q];
     __syncthreads();
     for (int e = t; e < TINY_N * TINY_XS; e += NTHREADS) {
         const int r = e / TINY_XS, d = e % TINY_XS;
@@ -1870,6 +1874,11 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
     if (TINY_STOP == 1) { if (t == 0) { a.info[0] = 0; a.f.out[0] = 0.0; } return; }
     // ---- factor: D_0; L_10, K_11 update, D_1, L^{-1}_10
     if (w == 0) tile_potrf_inv_w1_wave(K00, S, K00, D0, dg, &bad[0]);
+    else if (w == 1 && f.adam && aown) {   // adam_body's step-size and SoftplusGrad factors
+        const double tt = (double)(pst + 1);
+        a_alpha = f.lr * sqrt(1.0 - pow(f.b2, tt)) / (1.0 - pow(f.b1, tt));
+        a_eu = exp(-pu) + 1.0;
+    }
     __syncthreads();
     if (TINY_STOP == 2) { if (t == 0) { a.info[0] = 0; a.f.out[0] = 0.0; } return; }
     if (T > 1) {
@@ -1973,22 +1982,30 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
             acc_load<32>(acc, tl == 0 ? Ki00 : (tl == 1 ? Ki10 : Ki11), S);
             for (int c = 0; c < Tp; ++c) tile_mma<32, false, true>(acc, At(ti, c), At(tj, c), -invP);
             const double wscale = ((ti == tj) ? 0.5 : 1.0) * (-(double)p);
+            // the four entries' scaled squared distances side by side (one LDS round trip a
+            // dimension for all four, each sum still in dimension order)
+            const int gj = 32 * tj + acc_col<32>(0);
+            double s2v[4] = {0.0, 0.0, 0.0, 0.0}, s2dv[4] = {0.0, 0.0, 0.0, 0.0};
+            for (int d = 0; d < D; ++d) {
+                const double xj = xr[gj * TINY_XS + d], i1 = il2[d], i2 = il2[TINY_MAXD + d];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const double df = xr[(32 * ti + acc_row<32>(0, r)) * TINY_XS + d] - xj;
+                    const double d2 = df * df;
+                    s2v[r] += d2 * i1;
+                    s2dv[r] += d2 * i2;
+                }
+            }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int e = 4 * tl + r;
-                const int gi = 32 * ti + acc_row<32>(0, r), gj = 32 * tj + acc_col<32>(0);
+                const int gi = 32 * ti + acc_row<32>(0, r);
                 gie[e] = gi;
                 gje[e] = gj;
                 const double f1 = (gi < n) ? xr[gi * TINY_XS + D] : -1.0, f2 = (gj < n) ? xr[gj * TINY_XS + D] : -1.0;
                 const bool L1 = f1 == 0.0, H1 = f1 == 1.0, L2 = f2 == 0.0, H2 = f2 == 1.0;
                 const bool live = (L1 || H1) && (L2 || H2);
-                double s2 = 0.0, s2d = 0.0;
-                for (int d = 0; d < D; ++d) {
-                    const double df = xr[gi * TINY_XS + d] - xr[gj * TINY_XS + d];
-                    const double d2 = df * df;
-                    s2 += d2 * il2[d];
-                    s2d += d2 * il2[TINY_MAXD + d];
-                }
+                const double s2 = s2v[r], s2d = s2dv[r];
                 const double wv = acc.v[0][r] * wscale;
                 const double eL = live ? exp(-0.5 * s2) : 0.0;
                 const double kL = sc.vL() * eL;
@@ -2050,7 +2067,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
             else gsh[qx - G] = v;
         }
     }
-    if (f.adam && t < G) tsh[t] = ptie;
+    if (f.adam && aown) tsh[aq] = ptie;
     if (t == 0) {
         const int b0 = bad[0], b1 = (T > 1) ? bad[1] : 0;
         a.info[0] = b0 ? b0 : (b1 ? 32 + b1 : 0);
@@ -2062,24 +2079,23 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
     const int st = pst;
     double lml = -0.5 * gsh[0] - (double)p * gsh[1] - 0.5 * (double)n * (double)p * LOG2PI;
     if (info0 != 0) lml = NAN;
-    if (f.adam && info0 == 0 && t < G && ptr) {   // adam_body's step on the prefetched state
-        const double tt = (double)(st + 1);
-        const double alpha = f.lr * sqrt(1.0 - pow(f.b2, tt)) / (1.0 - pow(f.b1, tt));
-        double gc = gsh[2 + t];
+    if (f.adam && info0 == 0 && aown && ptr) {   // adam_body's step on the prefetched state
+        const double alpha = a_alpha;
+        double gc = gsh[2 + aq];
         if (f.tie) {
             gc = 0.0;
             for (int r = 0; r < G; ++r)
-                if (tsh[r] == tsh[t]) gc += gsh[2 + r];
+                if (tsh[r] == tsh[aq]) gc += gsh[2 + r];
         }
-        const double g = (-gc) / (exp(-pu) + 1.0);
+        const double g = (-gc) / a_eu;
         double mq = pm, vq = pv;
         mq += (g - mq) * (1.0 - f.b1);
         vq += (g * g - vq) * (1.0 - f.b2);
         const double un = pu - (mq * alpha) / (sqrt(vq) + f.eps);
-        f.m[t] = mq;
-        f.v[t] = vq;
-        f.u[t] = un;
-        f.theta[t] = tf_softplus(un) + (t == f.noise_index ? 1e-6 : 0.0);
+        f.m[aq] = mq;
+        f.v[aq] = vq;
+        f.u[aq] = un;
+        f.theta[aq] = tf_softplus(un) + (aq == f.noise_index ? 1e-6 : 0.0);
     }
     if (t == 0) f.out[0] = lml;
     if (a.want_grad)

@@ -136,8 +136,8 @@ class Engine:
         check(self.lib.mfgp_set_flow(self.h, (3 if any_size else 1) if enable else 0), "mfgp_set_flow")
 
     def set_tiny(self, enable: bool):
-        """One-launch LML step for small problems (n, p <= 64, D <= 16) or the step sequence of the
-        general path (False, the default: the one launch measured no faster at HBS)."""
+        """One-launch LML step for small problems (n, p <= 64, D <= 16; True, the default) or the
+        step sequence of the general path (False)."""
         check(self.lib.mfgp_set_tiny(self.h, 1 if enable else 0), "mfgp_set_tiny")
 
     def set_flow_timeout_us(self, us: int):

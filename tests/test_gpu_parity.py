@@ -37,7 +37,7 @@ def tile(request, eng):
     yield nb
     eng.set_tile(32)
     eng.set_flow(True)
-    eng.set_tiny(False)
+    eng.set_tiny(True)   # the library default
 
 
 def _params(D, P, seed=0, scale=1.0):
@@ -332,7 +332,7 @@ def test_lbfgs_forrester_kat(kats, eng, flow):
         m.optimize(max_iters=1000, learning_rate=0.01, use_adam=False, unfix_noise_after=500, verbose=False)
     finally:
         eng.set_flow(True)
-        eng.set_tiny(False)
+        eng.set_tiny(True)   # the library default
     rho = float(m.kernel.rho.numpy()[0, 0])
     print(f"L-BFGS Forrester ({'tiny' if tiny else ('flow' if flow else 'steps')}) rho {rho:.9f} vs recorded {kats['forrester_lbfgs']['rho']} "
           f"(rel {abs(rho - kats['forrester_lbfgs']['rho']) / kats['forrester_lbfgs']['rho']:.1e}), "
@@ -362,7 +362,7 @@ def test_tiny_matches_step_sequence(n_lf, n_hf, p, D, eng):
         eng.set_tiny(tiny)
         vals.append(m.log_marginal_likelihood_and_grad())
         vals.append((float(m.log_marginal_likelihood()), None))
-    eng.set_tiny(False)
+    eng.set_tiny(True)   # the library default
     assert abs(vals[0][0] - vals[2][0]) < 1e-12 * abs(vals[2][0])
     assert vals[0][0] == vals[1][0]                           # value-only call: the same kernel
     np.testing.assert_allclose(vals[0][1], vals[2][1], rtol=0, atol=1e-10 * np.abs(vals[2][1]).max())
@@ -384,7 +384,7 @@ def test_tiny_adam_matches_step_sequence(hbs, eng):
                                    M.SquaredExponential(lengthscales=np.ones(5)))
         m.optimize(max_iters=200, learning_rate=0.1, verbose=False)
         hs.append(np.array(m.loss_history))
-    eng.set_tiny(False)
+    eng.set_tiny(True)   # the library default
     MM._pool_clear()
     err = np.abs(hs[0] - hs[1]) / np.abs(hs[1])
     print(f"tiny vs steps, 200 HBS Adam steps: max rel {err.max():.1e}")
