@@ -1899,7 +1899,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
         __syncthreads();
         acc_zero(acc);
         tile_mma<32, false, false>(acc, D1, K10, -1.0);    // L^{-1}_10 = -D_1 T (over L10)
-        acc_to_lds(acc, L10);
+        acc_to_lds(acc, L10);   // (read, and T's slot 1 rewritten as Ki10, only after the barrier below)
     }
     if (TINY_STOP == 3) { if (t == 0) { a.info[0] = 0; a.f.out[0] = 0.0; } return; }
     // ---- Y tiles (zero padded; loaded at the start)
@@ -1908,8 +1908,29 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
         const int e = t + q * NTHREADS, tl = e >> 10, r = (e >> 5) & 31, c = e & 31;
         if (e < T * Tp * 1024) Yt(tl / Tp, tl % Tp)[r * S + c] = yv[q];
     }
-    // ---- K^{-1} = L^{-T} L^{-1}, lower tiles (over the consumed K00 / T / K11 slots)
+    // ---- one stage of independent products: Z = L^{-1} Y for every column tile (registers; sum Z^2
+    //      is the LML's quadratic term in the step path's form) and K^{-1} = L^{-T} L^{-1} (lower
+    //      tiles, over the consumed K00 / T / K11 slots); then alpha = L^{-T} Z, each column tile's
+    //      results replacing its Y tiles (all read first)
+    __syncthreads();   // the Y tiles and every wave's block of L^{-1}_10 are in; every read of T is done
     double* Ki00 = slot(0); double* Ki10 = slot(1); double* Ki11 = slot(2);
+    double z2 = 0.0;
+    Acc<32> zc[2][2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        if (c >= Tp) break;
+        acc_zero(zc[c][0]);
+        tile_mma<32, false, false>(zc[c][0], D0, Yt(0, c), 1.0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) z2 += zc[c][0].v[0][r] * zc[c][0].v[0][r];
+        if (T > 1) {
+            acc_zero(zc[c][1]);
+            tile_mma<32, false, false>(zc[c][1], L10, Yt(0, c), 1.0);
+            tile_mma<32, false, false>(zc[c][1], D1, Yt(1, c), 1.0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) z2 += zc[c][1].v[0][r] * zc[c][1].v[0][r];
+        }
+    }
     {
         Acc<32> acc;
         acc_zero(acc);
@@ -1927,37 +1948,31 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
     }
     __syncthreads();
     if (TINY_STOP == 4) { if (t == 0) { a.info[0] = 0; a.f.out[0] = 0.0; } return; }
-    // ---- Z = L^{-1} Y (sum Z^2: the LML's quadratic term in the step path's form), then
-    //      alpha = L^{-T} Z; each column tile's results replace its Y tiles (all read first)
-    double z2 = 0.0;
-    for (int c = 0; c < Tp; ++c) {
-        Acc<32> z0, z1;
-        acc_zero(z0);
-        tile_mma<32, false, false>(z0, D0, Yt(0, c), 1.0);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) z2 += z0.v[0][r] * z0.v[0][r];
-        if (T > 1) {
-            acc_zero(z1);
-            tile_mma<32, false, false>(z1, L10, Yt(0, c), 1.0);
-            tile_mma<32, false, false>(z1, D1, Yt(1, c), 1.0);
+    for (int c = 0; c < 2; ++c) {
+        if (c >= Tp) break;
+        acc_to_lds(zc[c][0], Yt(0, c));
+        if (T > 1) acc_to_lds(zc[c][1], Yt(1, c));
+    }
+    __syncthreads();
+    Acc<32> ac[2][2];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) z2 += z1.v[0][r] * z1.v[0][r];
-        }
-        __syncthreads();
-        acc_to_lds(z0, Yt(0, c));
-        if (T > 1) acc_to_lds(z1, Yt(1, c));
-        __syncthreads();
-        Acc<32> a0, a1;
-        acc_zero(a0);
-        tile_mma<32, true, false>(a0, D0, Yt(0, c), 1.0);
+    for (int c = 0; c < 2; ++c) {
+        if (c >= Tp) break;
+        acc_zero(ac[c][0]);
+        tile_mma<32, true, false>(ac[c][0], D0, Yt(0, c), 1.0);
         if (T > 1) {
-            tile_mma<32, true, false>(a0, L10, Yt(1, c), 1.0);
-            acc_zero(a1);
-            tile_mma<32, true, false>(a1, D1, Yt(1, c), 1.0);
+            tile_mma<32, true, false>(ac[c][0], L10, Yt(1, c), 1.0);
+            acc_zero(ac[c][1]);
+            tile_mma<32, true, false>(ac[c][1], D1, Yt(1, c), 1.0);
         }
-        __syncthreads();
-        acc_to_lds(a0, Yt(0, c));
-        if (T > 1) acc_to_lds(a1, Yt(1, c));
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        if (c >= Tp) break;
+        acc_to_lds(ac[c][0], Yt(0, c));
+        if (T > 1) acc_to_lds(ac[c][1], Yt(1, c));
     }
     auto At = [&](int r, int c) { return Yt(r, c); };
     double ld = 0.0;
