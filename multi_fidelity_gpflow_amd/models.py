@@ -316,16 +316,23 @@ class _AdamCore:
             self.Y = torch.empty_like(Y)
             self.st = AdamState(eng.device, tm.u(), tm.trainable(), tm.tie(), lr)
             G = self.st.u.numel()
-            # the moments and the two counters as views of one buffer each (one zeroing launch per
-            # load); the per-model inputs travel in ONE pinned host-to-device copy and the results
-            # back in ONE device-to-host copy (fewer synchronising transfers on the HBS protocol)
-            self.mv = torch.zeros((2 * G,), dtype=torch.float64, device=eng.device)
-            self.st.m, self.st.v = self.mv[:G], self.mv[G:]
-            self.si = torch.zeros((2,), dtype=torch.int32, device=eng.device)
+            # the whole per-model state as typed views of ONE byte buffer -- u | m | v (f64), tie
+            # (i32), step | info (i32), trainable (u8) -- written by ONE pinned host-to-device copy
+            # per load (u, tie, trainable from the model, zero moments and counters); the results
+            # come back in ONE device-to-host copy (fewer launches and synchronising transfers on
+            # the HBS protocol)
+            self._off = o = {"u": 0, "m": 8 * G, "v": 16 * G, "tie": 24 * G, "si": 28 * G, "tr": 28 * G + 8,
+                             "end": 29 * G + 8}
+            self.d_in = torch.zeros((o["end"],), dtype=torch.uint8, device=eng.device)
+            self.h_in = torch.zeros((o["end"],), dtype=torch.uint8, pin_memory=True)
+            self.st.u = self.d_in[o["u"]:o["m"]].view(torch.float64)
+            self.st.m = self.d_in[o["m"]:o["v"]].view(torch.float64)
+            self.st.v = self.d_in[o["v"]:o["tie"]].view(torch.float64)
+            self.st.tie = self.d_in[o["tie"]:o["si"]].view(torch.int32)
+            self.si = self.d_in[o["si"]:o["tr"]].view(torch.int32)
             self.st.step = self.si[0:1]
             self.info = self.si[1:2]
-            self.h_in = torch.empty((3 * G,), dtype=torch.float64, pin_memory=True)
-            self.d_in = torch.empty((3 * G,), dtype=torch.float64, device=eng.device)
+            self.st.trainable = self.d_in[o["tr"]:o["end"]]
             self.h_out = torch.empty((max_iters + G + 2,), dtype=torch.float64, pin_memory=True)
             self.hist = torch.zeros((max_iters,), dtype=torch.float64, device=eng.device)
             self.out = torch.empty((1 + theta_size(tm.d),), dtype=torch.float64, device=eng.device)
@@ -337,19 +344,16 @@ class _AdamCore:
     def load(self, X: torch.Tensor, Y: torch.Tensor, tm: "_ThetaMap"):
         """A model's data and initial state into the buffers (on the core's stream)."""
         st = self.st
-        G = st.u.numel()
+        o = self._off
         self.X.copy_(X)
         self.Y.copy_(Y)
         h = self.h_in.numpy()   # the previous load's copy from it completed before that session finished
-        h[:G] = tm.u()
-        h[G:2 * G] = tm.trainable()
-        h[2 * G:] = tm.tie()
+        h[o["u"]:o["m"]].view(np.float64)[:] = tm.u()
+        h[o["m"]:o["tie"]] = 0                                  # moments
+        h[o["tie"]:o["si"]].view(np.int32)[:] = tm.tie()
+        h[o["si"]:o["tr"]] = 0                                  # step, info
+        h[o["tr"]:o["end"]] = np.asarray(tm.trainable()).astype(np.uint8)
         self.d_in.copy_(self.h_in, non_blocking=True)
-        st.u.copy_(self.d_in[:G])
-        st.trainable.copy_(self.d_in[G:2 * G])
-        st.tie.copy_(self.d_in[2 * G:])
-        self.mv.zero_()
-        self.si.zero_()
         self.eng.theta_from_u(st.u, st.theta, tm.noise_index)
         if not self.warm:
             # one eager evaluation before any capture: builds the schedule tables and sets every
