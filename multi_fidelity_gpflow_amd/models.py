@@ -127,8 +127,30 @@ class MultiFidelityGPModel(Module):
     def _device_data(self):
         eng = Engine.get()
         if self._dev is None or self._dev[0].device != eng.device:
-            self._dev = (to_dev(self._Xh, eng.device, self.dtype), to_dev(self._Yh, eng.device, self.dtype))
+            # X and Y as two views of one device buffer, filled by ONE pinned host-to-device copy
+            npdt = np.float32 if self.dtype == torch.float32 else np.float64
+            nx, ny = self._Xh.size, self._Yh.size
+            hb = torch.empty((nx + ny,), dtype=self.dtype, pin_memory=True)
+            hn = hb.numpy()
+            hn[:nx] = self._Xh.astype(npdt, copy=False).ravel()
+            hn[nx:] = self._Yh.astype(npdt, copy=False).ravel()
+            db = hb.to(eng.device, non_blocking=True)
+            self._dev = (db[:nx].view(self._Xh.shape), db[nx:].view(self._Yh.shape))
         return eng, self._dev[0], self._dev[1]
+
+    def _device_inputs(self, eng, Xnew):
+        """theta (fp64) and the new inputs (the model's dtype) on the device; on fp64 in ONE pinned
+        host-to-device copy"""
+        th = self._theta_map().theta()
+        if self.dtype != torch.float64 or isinstance(Xnew, torch.Tensor):
+            return (torch.tensor(th, dtype=torch.float64, device=eng.device), to_dev(Xnew, eng.device, self.dtype))
+        xh = np.asarray(Xnew, dtype=np.float64)
+        hb = torch.empty((th.size + xh.size,), dtype=torch.float64, pin_memory=True)
+        hn = hb.numpy()
+        hn[:th.size] = th
+        hn[th.size:] = xh.ravel()
+        db = hb.to(eng.device, non_blocking=True)
+        return db[:th.size], db[th.size:].view(xh.shape)
 
     @property
     def input_dim(self) -> int:
@@ -176,8 +198,7 @@ class MultiFidelityGPModel(Module):
         if full_output_cov:
             raise NotImplementedError("predict_f(full_output_cov=True): GPR has no output covariance to return")
         eng, X, Y = self._device_data()
-        Xs = to_dev(Xnew, eng.device, self.dtype)
-        theta = torch.tensor(self._theta_map().theta(), dtype=torch.float64, device=eng.device)
+        theta, Xs = self._device_inputs(eng, Xnew)
         if full_cov:
             mean, _, cov, info = eng.gpr_predict_cov(0, X, Y, Xs, theta)
             self._raise_info(info, "predict_f")
