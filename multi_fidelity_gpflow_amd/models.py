@@ -342,8 +342,9 @@ class _AdamCore:
             # per load (u, tie, trainable from the model, zero moments and counters); the results
             # come back in ONE device-to-host copy (fewer launches and synchronising transfers on
             # the HBS protocol)
-            self._off = o = {"u": 0, "m": 8 * G, "v": 16 * G, "tie": 24 * G, "si": 28 * G, "tr": 28 * G + 8,
-                             "end": 29 * G + 8}
+            b = 8 * max_iters   # the loss history first: finish() reads hist | u | ... | si as one range
+            self._off = o = {"hist": 0, "u": b, "m": b + 8 * G, "v": b + 16 * G, "tie": b + 24 * G,
+                             "si": b + 28 * G, "tr": b + 28 * G + 8, "end": b + 29 * G + 8}
             self.d_in = torch.zeros((o["end"],), dtype=torch.uint8, device=eng.device)
             self.h_in = torch.zeros((o["end"],), dtype=torch.uint8, pin_memory=True)
             self.st.u = self.d_in[o["u"]:o["m"]].view(torch.float64)
@@ -354,8 +355,8 @@ class _AdamCore:
             self.st.step = self.si[0:1]
             self.info = self.si[1:2]
             self.st.trainable = self.d_in[o["tr"]:o["end"]]
-            self.h_out = torch.empty((max_iters + G + 2,), dtype=torch.float64, pin_memory=True)
-            self.hist = torch.zeros((max_iters,), dtype=torch.float64, device=eng.device)
+            self.hist = self.d_in[o["hist"]:o["u"]].view(torch.float64)
+            self.h_out = torch.empty((o["tr"],), dtype=torch.uint8, pin_memory=True)
             self.out = torch.empty((1 + theta_size(tm.d),), dtype=torch.float64, device=eng.device)
             n, p, d = X.shape[0], Y.shape[1], tm.d
             self.ws_bytes = eng.gpr_workspace_bytes(n, p, d, X.dtype)
@@ -476,15 +477,16 @@ class AdamSession:
         n, G, core = self.done, self.st.u.numel(), self._core
         if core is None:
             raise MFGPError("AdamSession: the session is finished")
-        with torch.cuda.stream(self.stream):   # loss history, u, info and step in one copy
-            packed = torch.cat([self.hist[:n], self.st.u, core.si.to(torch.float64)])
-            core.h_out[:n + G + 2].copy_(packed, non_blocking=True)
+        o = core._off
+        with torch.cuda.stream(self.stream):   # loss history, u, step and info: one byte range, one copy
+            core.h_out.copy_(core.d_in[:o["tr"]], non_blocking=True)
         self.sync()
-        res = core.h_out.numpy()[:n + G + 2].copy()
-        h = res[:n]
+        res = core.h_out.numpy()
+        h = res[o["hist"]:o["u"]].view(np.float64)[:n].copy()
         self.model.loss_history = [np.float64(v) for v in h]
-        self.tm.set_u(res[n:n + G])
-        steps, v = int(res[n + G]), int(res[n + G + 1])
+        self.tm.set_u(res[o["u"]:o["m"]].view(np.float64).copy())
+        si = res[o["si"]:o["tr"]].view(np.int32)
+        steps, v = int(si[0]), int(si[1])
         self._retire()
         if v == 0 and steps != self.done and np.all(np.isfinite(h)):
             # a failed step leaves the step counter behind and the next one retries it, so a
