@@ -1736,6 +1736,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
     auto Zt = [&](int r, int c) { return r == 0 ? slot(c) : slot(c == 0 ? 2 : 10); };
     double* xr = slot(11);                         // raw rows 64 x TINY_XS (gradient epilogue)
     double* misc = slot(12);
+    auto ELt = [&](int tl) { return slot(13 + tl); };   // exp(-r^2 / 2) of the Gram's K_L, tiles (0,0) (1,0) (1,1)
     double* dg = misc;                             // 64
     int* bad = reinterpret_cast<int*>(misc + 64);  // 2
     double* il = misc + 66;                        // 2 x TINY_MAXD   1/l    (Gram)
@@ -1834,7 +1835,9 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int gi = 16 * rb + kk + 4 * q, gj = 16 * cb + lc;
-                const double kl = sc.vL() * exp(-0.5 * (-2.0 * dl[q] + (nL[gi] + nL[gj])));
+                const double el = exp(-0.5 * (-2.0 * dl[q] + (nL[gi] + nL[gj])));
+                const double kl = sc.vL() * el;
+                ELt(tl)[(gi - 32 * ti) * S + gj - 32 * tj] = el;   // dK/dvL for the gradient epilogue
                 const double fa = fl[gi], fb = fl[gj];
                 const bool L1 = (fa == 0.0), H1 = (fa == 1.0), L2 = (fb == 0.0), H2 = (fb == 1.0);
                 const double kD = (H1 && H2) ? sc.vD() * exp(-0.5 * (-2.0 * dd[q] + (nD[gi] + nD[gj]))) : 0.0;
@@ -1854,7 +1857,9 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
         if (ti >= T) continue;
         const int gi = 32 * ti + r, gj = 32 * tj + c;
         const double dot = dot4(aL + gi * TINY_XS, aL + gj * TINY_XS, D4);
-        const double kl = sc.vL() * exp(-0.5 * (-2.0 * dot + (nL[gi] + nL[gj])));
+        const double el = exp(-0.5 * (-2.0 * dot + (nL[gi] + nL[gj])));
+        const double kl = sc.vL() * el;
+        ELt(tl)[r * S + c] = el;
         const double fa = fl[gi], fb = fl[gj];
         const bool L1 = (fa == 0.0), H1 = (fa == 1.0), L2 = (fb == 0.0), H2 = (fb == 1.0);
         const double rho = sc.rho();
@@ -1997,18 +2002,27 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
             acc_load<32>(acc, tl == 0 ? Ki00 : (tl == 1 ? Ki10 : Ki11), S);
             for (int c = 0; c < Tp; ++c) tile_mma<32, false, true>(acc, At(ti, c), At(tj, c), -invP);
             const double wscale = ((ti == tj) ? 0.5 : 1.0) * (-(double)p);
-            // the four entries' scaled squared distances side by side (one LDS round trip a
-            // dimension for all four, each sum still in dimension order)
+            // dK/dvL = exp(-r^2 / 2) as the Gram formed it (the expanded r^2 of GPflow's K, whose
+            // TF gradient this is); the HF x HF part's squared distance (four entries side by side,
+            // one LDS round trip a dimension, each sum in dimension order) and exponential only in
+            // a wave that holds such a pair (HBS: 3 HF points)
             const int gj = 32 * tj + acc_col<32>(0);
-            double s2v[4] = {0.0, 0.0, 0.0, 0.0}, s2dv[4] = {0.0, 0.0, 0.0, 0.0};
-            for (int d = 0; d < D; ++d) {
-                const double xj = xr[gj * TINY_XS + d], i1 = il2[d], i2 = il2[TINY_MAXD + d];
+            const bool H2c = gj < n && xr[gj * TINY_XS + D] == 1.0;
+            bool hhw = false;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const double df = xr[(32 * ti + acc_row<32>(0, r)) * TINY_XS + d] - xj;
-                    const double d2 = df * df;
-                    s2v[r] += d2 * i1;
-                    s2dv[r] += d2 * i2;
+            for (int r = 0; r < 4; ++r) {
+                const int gi = 32 * ti + acc_row<32>(0, r);
+                hhw |= H2c && gi < n && xr[gi * TINY_XS + D] == 1.0;
+            }
+            double s2dv[4] = {0.0, 0.0, 0.0, 0.0};
+            if (__ballot(hhw) != 0) {   // wave-uniform
+                for (int d = 0; d < D; ++d) {
+                    const double xj = xr[gj * TINY_XS + d], i2 = il2[TINY_MAXD + d];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const double df = xr[(32 * ti + acc_row<32>(0, r)) * TINY_XS + d] - xj;
+                        s2dv[r] += (df * df) * i2;
+                    }
                 }
             }
 #pragma unroll
@@ -2020,11 +2034,12 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
                 const double f1 = (gi < n) ? xr[gi * TINY_XS + D] : -1.0, f2 = (gj < n) ? xr[gj * TINY_XS + D] : -1.0;
                 const bool L1 = f1 == 0.0, H1 = f1 == 1.0, L2 = f2 == 0.0, H2 = f2 == 1.0;
                 const bool live = (L1 || H1) && (L2 || H2);
-                const double s2 = s2v[r], s2d = s2dv[r];
+                const double s2d = s2dv[r];
                 const double wv = acc.v[0][r] * wscale;
-                const double eL = live ? exp(-0.5 * s2) : 0.0;
+                const double eL = live ? ELt(tl)[acc_row<32>(0, r) * S + acc_col<32>(0)] : 0.0;
                 const double kL = sc.vL() * eL;
-                const double eD = (H1 && H2) ? exp(-0.5 * s2d) : 0.0;
+                double eD = 0.0;
+                if (H1 && H2) eD = exp(-0.5 * s2d);
                 const double kD = sc.vD() * eD;
                 const double si = L1 ? 1.0 : (H1 ? rho : 0.0), sj = L2 ? 1.0 : (H2 ? rho : 0.0);
                 const double hi = H1 ? 1.0 : 0.0, hj = H2 ? 1.0 : 0.0;
@@ -2123,7 +2138,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
 }
 
 size_t gpr_tiny_smem_bytes() {
-    return sizeof(double) * (13 * (size_t)TileCfg<32>::ELEMS);
+    return sizeof(double) * (16 * (size_t)TileCfg<32>::ELEMS);
 }
 
 bool gpr_tiny_fits(int n, int p, int d, int nlf) {
