@@ -2056,7 +2056,14 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
     //      q < G the gradient entry q, G the quadratic term, G + 1 sum log L_ii
     __syncthreads();
     double* RB = slot(3);
-    if (TINY_STOP == 6) { if (t == 0) { a.info[0] = 0; a.f.out[0] = 0.0; } return; }
+    if (TINY_STOP == 6) {   // (keeps the epilogue live: every thread's partials reach memory)
+        double sink = gvL + gvD + grho + gnoise;
+#pragma unroll
+        for (int e = 0; e < 12; ++e) sink += cLe[e] + cDe[e] + (double)(gie[e] + gje[e]);
+        a.f.out[1 + (t & 7)] = sink;
+        if (t == 0) a.info[0] = 0;
+        return;
+    }
     auto put = [&](int q, double v) {
         v = quad_sum(v);
         if ((lane & 3) == 0) RB[q * 64 + w * 16 + (lane >> 2)] = v;
@@ -2096,6 +2103,12 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
             if (qx < G) gsh[2 + qx] = v;
             else gsh[qx - G] = v;
         }
+    }
+    if (TINY_STOP == 8) {   // after the reductions (gsh complete after the barrier below)
+        __syncthreads();
+        if (t < G + 2) a.f.out[t] = gsh[t];
+        if (t == 0) a.info[0] = 0;
+        return;
     }
     if (f.adam && aown) tsh[aq] = ptie;
     if (t == 0) {
