@@ -487,6 +487,10 @@ static int predict_impl(mfgp_handle_t h, int n, int p, int d, int nstar, const d
     const PredLayout P = pred_layout(NB, n, p, d, nstar, ws, h->grad_chunk, nlf, cov != nullptr);
     if (ws_bytes < P.bytes) return MFGP_ERR_WORKSPACE;
     hipStream_t s = h->stream;
+    if (NB == 32 && h->tiny && !nlf && !cov && gpr_tiny_pred_fits(n, p, d, nstar)) {   // small problems: one launch
+        launch_gpr_tiny_pred(X, ldx, Y, ldy, Xs, ldxs, nstar, theta, n, p, d, mean, ldm, var, info, s);
+        return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;
+    }
     const GprLayout& L = P.g;
     gram_lml_and_factor<NB>(s, L, n, p, d, X, ldx, Y, ldy, theta, info, nlf);
     if (nlf) (void)hipMemsetAsync(P.Kmn, 0, sizeof(double) * (size_t)L.npad * P.nspad, s);

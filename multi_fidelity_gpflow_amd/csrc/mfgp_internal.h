@@ -259,6 +259,10 @@ void launch_gram_dense(const GramArgs& g, int batch, int wr1, int wr2, hipStream
 void launch_gram_flow(const GramArgs& g, int extra, hipStream_t s);   // set-up launch of k_chol_flow
 // one-launch value + gradient (+ Adam) of the AR1 GPR LML for small problems (k_gpr_tiny)
 bool gpr_tiny_fits(int n, int p, int d, int nlf);
+bool gpr_tiny_pred_fits(int n, int p, int d, int nstar);
+void launch_gpr_tiny_pred(const double* X, long ldx, const double* Y, long ldy, const double* Xs, long ldxs, int nstar,
+                          const double* theta, int n, int p, int d, double* mean, long ldm, double* var, int* info,
+                          hipStream_t s);
 void launch_gpr_tiny(const double* X, long ldx, const double* Y, long ldy, const double* theta, int n, int p, int d,
                      int want_grad, int* info, const FinArgs& f, hipStream_t s);
 template <int NB> void launch_chol_steps(CholArgs c, int batch, hipStream_t s);

@@ -1720,8 +1720,16 @@ struct TinyArgs {
     int n, p, D, want_grad;
     int* info;
     FinArgs f;
+    // PRED (predict_f): X* rows (ns <= TINY_N), the mean [ns, p] and the variance [ns]
+    const double* Xs; long ldxs; int ns;
+    double* mean; long ldm;
+    double* var;
 };
 
+// PRED: the same factorization and Z = L^{-1} Y, then predict_f's A = L^{-1} K(X, X*), mean = A^T Z
+// and var = K_diag(X*) - colsum(A^2) (linear.py:237-286; predict_impl's k_pred_a / k_pred_out in
+// the same summation order) instead of the gradient
+template <bool PRED>
 __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
     constexpr int S = TileCfg<32>::S, E = TileCfg<32>::ELEMS;
     extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -1936,7 +1944,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
             for (int r = 0; r < 4; ++r) z2 += zc[c][1].v[0][r] * zc[c][1].v[0][r];
         }
     }
-    {
+    if (!PRED) {
         Acc<32> acc;
         acc_zero(acc);
         tile_mma<32, true, false>(acc, D0, D0, 1.0);
@@ -1960,6 +1968,90 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
         if (T > 1) acc_to_lds(zc[c][1], Yt(1, c));
     }
     __syncthreads();
+    if constexpr (PRED) {
+        const int ns = a.ns, Ts = (ns + 31) / 32;
+        const double rho = sc.rho();
+        double* xs = slot(13);   // raw X* rows (the Gram's exp tiles are not needed here)
+        auto Km = [&](int i, int c) { return slot(i == 0 ? c : (c == 0 ? 2 : 10)); };   // K(X, X*), then A
+        for (int e = t; e < TINY_N * TINY_XS; e += NTHREADS) {
+            const int r = e / TINY_XS, d = e % TINY_XS;
+            xs[e] = (r < ns && d <= D) ? a.Xs[(long)r * a.ldxs + d] : 0.0;
+        }
+        __syncthreads();
+        for (int e = t; e < T * Ts * 1024; e += NTHREADS) {   // K(X, X*): the AR1 kernel, exact masks
+            const int tl = e >> 10, r = (e >> 5) & 31, c = e & 31;
+            const int ti = tl / Ts, tc = tl % Ts;
+            const int gi = 32 * ti + r, gs = 32 * tc + c;
+            double v = 0.0;
+            if (gi < n && gs < ns) {
+                const double fa = xr[gi * TINY_XS + D], fb = xs[gs * TINY_XS + D];
+                const bool L1 = fa == 0.0, H1 = fa == 1.0, L2 = fb == 0.0, H2 = fb == 1.0;
+                double s2 = 0.0, s2d = 0.0;
+                for (int d = 0; d < D; ++d) {
+                    const double df = xr[gi * TINY_XS + d] - xs[gs * TINY_XS + d];
+                    s2 += (df * df) * il2[d];
+                    s2d += (df * df) * il2[TINY_MAXD + d];
+                }
+                const double kl = sc.vL() * exp(-0.5 * s2);
+                const double kD = (H1 && H2) ? sc.vD() * exp(-0.5 * s2d) : 0.0;
+                v = (L1 && L2) ? kl : (!(H1 && H2) ? kl * rho : kl * (rho * rho) + kD);
+                if (!(L1 || H1) || !(L2 || H2)) v = 0.0;
+            }
+            Km(ti, tc)[r * S + c] = v;
+        }
+        __syncthreads();
+        Acc<32> A0[2], A1[2];   // A = L^{-1} Kmn, column tile c
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            if (c >= Ts) break;
+            acc_zero(A0[c]);
+            tile_mma<32, false, false>(A0[c], D0, Km(0, c), 1.0);
+            if (T > 1) {
+                acc_zero(A1[c]);
+                tile_mma<32, false, false>(A1[c], L10, Km(0, c), 1.0);
+                tile_mma<32, false, false>(A1[c], D1, Km(1, c), 1.0);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            if (c >= Ts) break;
+            acc_to_lds(A0[c], Km(0, c));
+            if (T > 1) acc_to_lds(A1[c], Km(1, c));
+        }
+        __syncthreads();
+        for (int cs = 0; cs < Ts; ++cs)   // mean tile (cs, cy) = sum_i A(i, cs)^T Z(i, cy)
+            for (int cy = 0; cy < Tp; ++cy) {
+                Acc<32> m;
+                acc_zero(m);
+                tile_mma<32, true, false>(m, Km(0, cs), Yt(0, cy), 1.0);
+                if (T > 1) tile_mma<32, true, false>(m, Km(1, cs), Yt(1, cy), 1.0);
+#pragma unroll
+                for (int q = 0; q < TileCfg<32>::NBLK; ++q)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int gs = 32 * cs + acc_row<32>(q, r), gc = 32 * cy + acc_col<32>(q);
+                        if (gs < ns && gc < p) a.mean[(long)gs * a.ldm + gc] = m.v[q][r];
+                    }
+            }
+        if (t < ns) {   // var = K_diag(X*) - sum_i sum_r A(i, cs)[r][s]^2 (k_pred_out's order)
+            const int cs = t >> 5, cc = t & 31;
+            double sq = 0.0;
+            for (int i = 0; i < T; ++i)
+                for (int r = 0; r < 32; ++r) {
+                    const double v = Km(i, cs)[r * S + cc];
+                    sq += v * v;
+                }
+            const double fb = xs[t * TINY_XS + D];
+            const double kd = (fb == 0.0) ? sc.vL() : ((fb == 1.0) ? sc.vL() * (rho * rho) + sc.vD() : 0.0);
+            a.var[t] = kd - sq;
+        }
+        if (t == 0) {
+            const int b0 = bad[0], b1 = (T > 1) ? bad[1] : 0;
+            a.info[0] = b0 ? b0 : (b1 ? 32 + b1 : 0);
+        }
+        return;
+    }
     Acc<32> ac[2][2];
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
@@ -2162,12 +2254,30 @@ void launch_gpr_tiny(const double* X, long ldx, const double* Y, long ldy, const
                      int want_grad, int* info, const FinArgs& f, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gpr_tiny), hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gpr_tiny<false>), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)gpr_tiny_smem_bytes());
         attr = true;
     }
     TinyArgs a{X, ldx, Y, ldy, theta, n, p, d, want_grad, info, f};
-    hipLaunchKernelGGL(k_gpr_tiny, dim3(1), dim3(NTHREADS), gpr_tiny_smem_bytes(), s, a);
+    hipLaunchKernelGGL(k_gpr_tiny<false>, dim3(1), dim3(NTHREADS), gpr_tiny_smem_bytes(), s, a);
+}
+
+bool gpr_tiny_pred_fits(int n, int p, int d, int nstar) { return gpr_tiny_fits(n, p, d, 0) && nstar >= 1 && nstar <= TINY_N; }
+
+void launch_gpr_tiny_pred(const double* X, long ldx, const double* Y, long ldy, const double* Xs, long ldxs, int nstar,
+                          const double* theta, int n, int p, int d, double* mean, long ldm, double* var, int* info,
+                          hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gpr_tiny<true>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)gpr_tiny_smem_bytes());
+        attr = true;
+    }
+    TinyArgs a{};
+    a.X = X; a.ldx = ldx; a.Y = Y; a.ldy = ldy; a.theta = theta; a.n = n; a.p = p; a.D = d; a.want_grad = 0;
+    a.info = info;
+    a.Xs = Xs; a.ldxs = ldxs; a.ns = nstar; a.mean = mean; a.ldm = ldm; a.var = var;
+    hipLaunchKernelGGL(k_gpr_tiny<true>, dim3(1), dim3(NTHREADS), gpr_tiny_smem_bytes(), s, a);
 }
 
 template void launch_gram<32>(const GramArgs&, int, int, hipStream_t);
