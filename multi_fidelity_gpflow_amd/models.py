@@ -65,15 +65,21 @@ class _ThetaMap:
         assert len(self.entries) == theta_size(d)
         self.noise_index = theta_size(d) - 1
 
-    def _get(self, p: Parameter, idx, which: str):
-        arr = p.numpy() if which == "c" else p.unconstrained_variable
-        return float(arr if idx is None else arr[idx])
+    def _gather(self, which: str) -> np.ndarray:
+        # each Parameter's (constrained or unconstrained) array once, however many entries it owns
+        arrs, out = {}, []
+        for p, idx in self.entries:
+            arr = arrs.get(id(p))
+            if arr is None:
+                arr = arrs[id(p)] = p.numpy() if which == "c" else p.unconstrained_variable
+            out.append(float(arr if idx is None else arr[idx]))
+        return np.array(out)
 
     def theta(self) -> np.ndarray:
-        return np.array([self._get(p, i, "c") for p, i in self.entries])
+        return self._gather("c")
 
     def u(self) -> np.ndarray:
-        return np.array([self._get(p, i, "u") for p, i in self.entries])
+        return self._gather("u")
 
     def trainable(self) -> np.ndarray:
         return np.array([p.trainable for p, _ in self.entries], dtype=bool)
@@ -86,13 +92,17 @@ class _ThetaMap:
         return np.array(out, dtype=np.int32)
 
     def set_u(self, u: np.ndarray):
+        # one assignment per Parameter (entries in order: a later entry of the same index wins)
+        new = {}
         for (p, idx), val in zip(self.entries, u):
             if idx is None:
-                p.unconstrained_variable = np.full(p.shape, val)
+                new[id(p)] = (p, np.full(p.shape, val))
             else:
-                arr = p.unconstrained_variable.copy()
+                arr = new[id(p)][1] if id(p) in new else p.unconstrained_variable.copy()
                 arr[idx] = val
-                p.unconstrained_variable = arr
+                new[id(p)] = (p, arr)
+        for p, arr in new.values():
+            p.unconstrained_variable = arr
 
 
 class MultiFidelityGPModel(Module):
