@@ -64,9 +64,9 @@ int mfgp_get_tile(mfgp_handle_t h);
  * Results agree to rounding; a workspace must be sized under the setting it is used with. */
 int mfgp_set_flow(mfgp_handle_t h, int enable);   /* 2: flow + diagnostic timeline; 3: flow at every size */
 /* Small problems (n <= 64, p <= 64, D <= 16, the AR1 kernel, 32-tiles): the LML value + gradient
- * (+ the Adam step of mfgp_gpr_adam_step) as ONE launch instead of the step sequence (default 1:
- * 37 vs 43.5 us at HBS; 0, or MFGP_TINY=0 in the environment: the step sequence).  Same results
- * to rounding. */
+ * (+ the Adam step of mfgp_gpr_adam_step), and mfgp_gpr_predict for n* <= 64, as ONE launch each
+ * instead of the step sequence (default 1: 36 vs 43.5 us at HBS; 0, or MFGP_TINY=0 in the
+ * environment: the step sequence).  Same results to rounding. */
 int mfgp_set_tiny(mfgp_handle_t h, int enable);
 /* fp32 path (dtype MFGP_F32): iterative refinement with an fp64 residual for the value-only LML
  * (want_grad = 0; one step whenever steps >= 1) and the predictive mean (`steps` steps, 0..2;
