@@ -372,6 +372,33 @@ def test_tiny_matches_step_sequence(n_lf, n_hf, p, D, eng):
     np.testing.assert_allclose(vals[0][1], gov, rtol=0, atol=1e-8 * np.abs(gov).max())
 
 
+@pytest.mark.parametrize("n_lf,n_hf,p,D,ns", [(50, 3, 49, 5, 10), (24, 8, 32, 3, 1), (40, 24, 64, 16, 64),
+                                              (20, 5, 1, 1, 33)])
+def test_tiny_predict_matches_step_sequence(n_lf, n_hf, p, D, ns, eng):
+    """predict_f through k_gpr_tiny<true> (n, p, n* <= 64: one launch) against the seven-launch
+    sequence and the oracle: T = 1 / 2, one / two column tiles of Y and of X*, D up to 16, n = p =
+    n* = 64 at the edge, a fractional-fidelity test row (its K entries and K_diag are zero)."""
+    rng = np.random.default_rng(n_lf * 5 + ns)
+    X = np.vstack([np.hstack([rng.random((n_lf, D)), np.zeros((n_lf, 1))]),
+                   np.hstack([rng.random((n_hf, D)), np.ones((n_hf, 1))])])
+    Y = np.sin(X[:, :D] @ rng.standard_normal((D, p)) * 3.0)
+    Xs = np.hstack([rng.random((ns, D)), (np.arange(ns) % 2)[:, None].astype(float)])
+    if ns > 2:
+        Xs[2, -1] = 0.5
+    m = _model(X, Y, _params(D, p, seed=4))
+    out = []
+    for tiny in (True, False):
+        eng.set_tiny(tiny)
+        mean, var = m.predict_f(Xs)
+        out.append((mean.numpy(), var.numpy()))
+    eng.set_tiny(True)   # the library default
+    np.testing.assert_allclose(out[0][0], out[1][0], rtol=0, atol=1e-10 * max(1.0, np.abs(out[1][0]).max()))
+    np.testing.assert_allclose(out[0][1], out[1][1], rtol=0, atol=1e-10 * max(1.0, np.abs(out[1][1]).max()))
+    mo, vo = O.gpr_predict_f(X, Y, Xs, _oracle_params(m))
+    np.testing.assert_allclose(out[0][0], mo, rtol=0, atol=1e-9 * max(1.0, np.abs(mo).max()))
+    np.testing.assert_allclose(out[0][1], vo, rtol=0, atol=1e-9 * max(1.0, np.abs(vo).max()))
+
+
 def test_tiny_adam_matches_step_sequence(hbs, eng):
     """The HBS Adam step (mfgp_gpr_adam_step, graph-captured) through k_gpr_tiny and through the
     step sequence: 200 steps, the same loss history to rounding (the dynamics are smooth there)."""
