@@ -459,26 +459,70 @@ def shared_inducing_leg(X, Yr, steps, warmup, rank, world, device):
 HBS = os.path.join(ROOT, "tests", "golden", "data", "50_LR_3_HR")
 
 
-def hbs_leg(steps=200, warmup=20):
-    """BASELINE configs[1] (Ho-Bird-Shelton 50LF/3HF, D=5, P=49, fp64): pure latency, so the
-    figure is wall-clock.  train_predict_s = the reference's test protocol
-    (tests/test_ho2021_multibin.py:20-43: a fresh MultiFidelityGPModel, optimize(max_iters=100,
-    use_adam=True, learning_rate=0.1, unfix_noise_after=50), then predict_f on the 10 test
-    inputs), after one untimed run of the same protocol (per-process kernel loading and graph
-    set-up); ms_per_step = replayed Adam steps of a session, like the Goku line."""
+def hbs_data():
     from multi_fidelity_gpflow_amd.data import PowerSpecs, multifidelity_training_set
     ps = PowerSpecs()
     ps.read_from_txt(HBS)
-    X, Y, Xt, _ = multifidelity_training_set(ps)
+    return multifidelity_training_set(ps)
+
+
+def hbs_protocol(X, Y, Xt):
+    """tests/test_ho2021_multibin.py:20-43: a fresh MultiFidelityGPModel, optimize(max_iters=100,
+    use_adam=True, learning_rate=0.1, unfix_noise_after=50), then predict_f on the test inputs."""
+    m = make_model(X, Y)
+    m.optimize(max_iters=100, learning_rate=0.1, use_adam=True, unfix_noise_after=50, verbose=False)
+    mean, var = m.predict_f(Xt)
+    torch.cuda.synchronize()
+    return m
+
+
+def hbs_cold_child():
+    """--hbs-cold (run as a child process by hbs_leg): the reference test's protocol ONCE in a
+    fresh process, as the reference's test runs it -- kernel code loading, workspace sizing and the
+    step-graph capture included (the interpreter start, `import torch` and the CUDA context are
+    not: the reference's figure would not include TF's import either)."""
+    X, Y, Xt, _ = hbs_data()
+    torch.cuda.set_device(0)
+    torch.zeros(1, device="cuda")   # the context
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    hbs_protocol(X, Y, Xt)
+    dt = time.perf_counter() - t0
+    print(json.dumps({"train_predict_s_cold": dt}))
+    return 0
+
+
+def hbs_cold_run():
+    """train_predict_s_cold from a child process (None if it fails)."""
+    import subprocess
+    try:
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--hbs-cold"], capture_output=True,
+                           text=True, timeout=300)
+        for ln in r.stdout.splitlines()[::-1]:
+            if ln.startswith("{"):
+                return json.loads(ln)["train_predict_s_cold"]
+    except (OSError, ValueError, KeyError, subprocess.SubprocessError):
+        pass
+    return None
+
+
+def hbs_leg(steps=200, warmup=20):
+    """BASELINE configs[1] (Ho-Bird-Shelton 50LF/3HF, D=5, P=49, fp64): pure latency, so the
+    figure is wall-clock.
+      train_predict_s_cold  the reference's test protocol (hbs_protocol) run ONCE in a fresh child
+                            process, capture and kernel loading included (the reference's test runs
+                            it once per process);
+      train_predict_s       the same protocol in this process after one untimed run: a fresh model
+                            then reuses the pooled session's buffers and captured step graphs
+                            (models.py session pool), i.e. a warm-pool figure;
+      ms_per_step           replayed Adam steps of a session, like the Goku line.
+    roofline: at this size (n, p <= 64, D <= 16) the whole value + gradient + Adam step is ONE
+    launch of k_gpr_tiny (mfgp_set_tiny, the default), booked under its name with the SURVEY §8(d)
+    value+grad flops of the step; latency-bound."""
+    X, Y, Xt, _ = hbs_data()
     n, d, P = X.shape[0], X.shape[1] - 1, Y.shape[1]
-
-    def protocol():
-        m = make_model(X, Y)
-        m.optimize(max_iters=100, learning_rate=0.1, use_adam=True, unfix_noise_after=50, verbose=False)
-        mean, var = m.predict_f(Xt)
-        torch.cuda.synchronize()
-        return m
-
+    cold = hbs_cold_run()
+    protocol = lambda: hbs_protocol(X, Y, Xt)
     protocol()
     ts = []
     for _ in range(3):
@@ -499,11 +543,24 @@ def hbs_leg(steps=200, warmup=20):
     sess.finish()
     roof = roofline(model, n, P, d, pmc=False)
     roof["bound"] = "latency"
+    from multi_fidelity_gpflow_amd.engine import Engine
+    eng = Engine.get()
+    if eng.mode()[2] and n <= 64 and P <= 64 and d <= 16:
+        # the one-launch path: every phase mark but the first brackets k_gpr_tiny (or nothing)
+        us = sum(roof["phase_ms"].values()) * 1e3
+        fl = step_flops(n, P, d)
+        roof.update({"kernel": "k_gpr_tiny (the whole LML value + gradient (+ Adam) step in one workgroup)",
+                     "launches_per_step": 1, "avg_launch_us": round(us, 3), "flop_per_launch": fl,
+                     "achieved": round(fl / (us * 1e-6) / 1e12, 6),
+                     "frac": round(fl / (us * 1e-6) / 1e12 / FP64_PEAK_TFLOPS, 8),
+                     "flop_source": "SURVEY §8(d) value+grad unit (step_flops)"})
     return {
         "config": {"workload": "hbs_multibin_adam_step", "n_lf": int((X[:, -1] == 0).sum()),
                    "n_hf": int((X[:, -1] == 1).sum()), "d": d, "p": P},
         "dtype": "f64",
+        "train_predict_s_cold": None if cold is None else round(cold, 5),
         "train_predict_s": round(float(np.median(ts)), 5),
+        "train_predict_s_note": "warm pool: a fresh model of a seen shape replays the pooled session's graphs",
         "train_predict_s_runs": [round(t, 5) for t in ts],
         "protocol": "tests/test_ho2021_multibin.py:20-43 (optimize 100 Adam steps, lr 0.1, then predict_f(X_test))",
         "steps": steps, "warmup": warmup,
@@ -618,10 +675,13 @@ def main():
     ap.add_argument("--mode", choices=["shard", "shared"], default="shard",
                     help="shard: per-shard-theta bin blocks (no inner-loop collective); shared: one model, "
                          "one all-reduce of 1+G doubles per step (reference-parity mode, SURVEY 8(e))")
+    ap.add_argument("--hbs-cold", action="store_true", help=argparse.SUPPRESS)   # hbs_leg's child
     ap.add_argument("--config", choices=["goku", "synth", "goku_svgp"], default="goku",
                     help="goku: the BASELINE metric (fp64); synth: BASELINE configs[4] / SURVEY §8(d) "
                          "(N=18432, P=512, fp32)")
     args = ap.parse_args()
+    if args.hbs_cold:
+        return hbs_cold_child()
     world_env = os.environ.get("WORLD_SIZE")
     if world_env is None and args.gpus > 1:
         # not launched by torchrun: start one rank per GPU (before this process touches the GPU)

@@ -43,6 +43,10 @@ typedef struct mfgp_handle_s* mfgp_handle_t;
 #define MFGP_ERR_WORKSPACE (-2)
 #define MFGP_ERR_LAUNCH (-3)
 #define MFGP_ERR_DIM (-4)
+/* mfgp_flow_fence / a flow-bearing call found the device's flow fence held by another host thread
+ * for longer than the library's bound (10 s): an MFGP_FENCE_WAIT that was never paired with its
+ * MFGP_FENCE_RECORD.  Nothing of the failed call was enqueued. */
+#define MFGP_ERR_FENCE (-5)
 #define MFGP_MAX_D 32
 /* info value written when the persistent Cholesky launch gave up waiting (bounded spin) */
 #define MFGP_FLOW_TIMEOUT (-100)
@@ -68,6 +72,9 @@ int mfgp_set_flow(mfgp_handle_t h, int enable);   /* 2: flow + diagnostic timeli
  * instead of the step sequence (default 1: 36 vs 43.5 us at HBS; 0, or MFGP_TINY=0 in the
  * environment: the step sequence).  Same results to rounding. */
 int mfgp_set_tiny(mfgp_handle_t h, int enable);
+int mfgp_get_tiny(mfgp_handle_t h);
+/* k_grad m-tiles per task (fixed at mfgp_create; env MFGP_GRAD_CHUNK).  Workspace sizes depend on it. */
+int mfgp_get_grad_chunk(mfgp_handle_t h);
 /* fp32 path (dtype MFGP_F32): iterative refinement with an fp64 residual for the value-only LML
  * (want_grad = 0; one step whenever steps >= 1) and the predictive mean (`steps` steps, 0..2;
  * default 2; 0: plain fp32 solve).  The gradient / Adam calls are never refined.  Workspace sizes follow the setting (size after
@@ -88,7 +95,10 @@ int mfgp_set_flow_timeout_us(mfgp_handle_t h, long long us);
  * mfgp_flow_fence(h, MFGP_FENCE_RECORD).  Between the two the calling host thread holds the
  * fence: a flow launch or fence call from another host thread blocks on the host until the
  * RECORD (so it cannot land beside the replay's unfenced flows); the holder's own calls pass.
- * Device ordering is stream-ordered only (no device synchronisation). */
+ * Every WAIT MUST be paired with a RECORD from the same host thread (also on error paths).  Holds
+ * nest: a thread's nested WAIT / RECORD brackets release the fence only at the outermost RECORD.
+ * A thread that finds the fence held by another waits at most 10 s, then the call returns
+ * MFGP_ERR_FENCE.  Device ordering is stream-ordered only (no device synchronisation). */
 #define MFGP_FENCE_WAIT 0
 #define MFGP_FENCE_RECORD 1
 int mfgp_flow_fence(mfgp_handle_t h, int op);

@@ -8,7 +8,7 @@ All arithmetic of the hot path runs in libmfgp.so (hand-written HIP for gfx950).
 from .params import Parameter, positive, set_trainable, parameter_dict, multiple_assign  # noqa: F401
 from .kernels import (SquaredExponential, RBF, LinearMultiFidelityKernel,  # noqa: F401
                       LinearCoregionalization, SeparateIndependent)
-from .models import MultiFidelityGPModel, Gaussian, CholeskyError  # noqa: F401
+from .models import MultiFidelityGPModel, Gaussian, CholeskyError, clear_session_pool  # noqa: F401
 from .svgp import LatentMFCoregionalizationSVGP, SingleBinSVGP, initialize_W, initialize_W_pca  # noqa: F401
 from .kernels import GraphMultiFidelityKernel  # noqa: F401
 from .graph import GraphMultiFidelityGPModel  # noqa: F401

@@ -30,6 +30,8 @@ SIGNATURES = {
     "mfgp_get_tile": [_p],
     "mfgp_set_flow": [_p, _i],
     "mfgp_set_tiny": [_p, _i],
+    "mfgp_get_tiny": [_p],
+    "mfgp_get_grad_chunk": [_p],
     "mfgp_set_f32_refine": [_p, _i],
     "mfgp_get_flow": [_p],
     "mfgp_set_flow_timeout_us": [_p, C.c_longlong],

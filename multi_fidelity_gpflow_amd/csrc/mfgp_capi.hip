@@ -8,6 +8,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <condition_variable>
 #include <mutex>
 #include <thread>
@@ -26,15 +27,13 @@ struct mfgp_handle_s {
     int flow_min_t; // fewest 32-tiles a factorization needs to take the flow (below: the step launches)
     int ncu;        // compute units of the device
     int gram_wgs;   // k_gram tile workgroups, LML layout (0: one per CU; < 0: one per tile; MFGP_GRAM_WGS)
-    int gram_legacy;   // flow path: the looping k_gram instead of k_gram_flow (MFGP_GRAM_LEGACY, A/B only)
-    int flow_d0;       // flow path: the chain factors D_0 (no factor workgroup in k_gram_flow; MFGP_FLOW_D0)
     int flow_trace; // k_chol_flow writes its diagnostic timeline into the workspace
     long long flow_timeout;   // k_chol_flow hand-off wait bound (100 MHz ticks)
     int f32_panel;  // fp32 path: 128-wide tile columns per outer panel (trailing-update K = 128 * f32_panel)
     int f32_lookahead;          // fp32 sweep: factor the next panel beside the trailing update
     int f32_reserve;            // CUs the capped trailing update leaves to the side stream
     int f32_refine;             // fp32 value-only LML (one step) / predict mean (this many steps): fp64 refinement (mfgp_set_f32_refine)
-    int tiny;                   // small problems (n, p <= 64, D <= 16, AR1 kernel): one-launch LML step (mfgp_set_tiny, default off)
+    int tiny;                   // small problems (n, p <= 64, D <= 16, AR1 kernel): one-launch LML step (default on; MFGP_TINY=0 / mfgp_set_tiny(h, 0) disables)
     hipStream_t side;           // its high-priority side stream + fork / join events (created with the handle)
     hipEvent_t ev_fork, ev_join;
 };
@@ -71,16 +70,15 @@ struct GprLayout {
     long npub;
     long long* trace;   // k_chol_flow timeline (diagnostic; written only when enabled)
     int ntrace;
-    int sdelta, gchunk;   // FLOW_STILES levels left to k_grad (0: off); k_grad's task chunk (< 0: S tiles)
-    double* S;          // the flow's K^{-1} partial sums (FLOW_STILES)
+    int gchunk;         // k_grad's task chunk (m-tiles per task)
     size_t bytes;
 };
 
 // The persistent Cholesky needs every workgroup resident (one per CU) and the owner table
 // to hold every tile; otherwise the launch-per-step sequence runs.
-static int flow_grid(int nb, int T, int Tp, int flow_wgs, int min_t, int sd = 0) {
+static int flow_grid(int nb, int T, int Tp, int flow_wgs, int min_t) {
     if (nb != 32 || flow_wgs < 2 || T > 255 || T < min_t) return 0;
-    if (flow_ntiles(T, Tp, sd) > FLOW_WAVES * (flow_wgs - 1) * FLOW_MAXOWN) return 0;
+    if (flow_ntiles(T, Tp) > FLOW_WAVES * (flow_wgs - 1) * FLOW_MAXOWN) return 0;
     return flow_wgs;
 }
 
@@ -94,16 +92,8 @@ static GprLayout gpr_layout(int nb, int n, int p, int d, void* ws, int grad_chun
     L.ppad = L.Tp * nb;
     L.G = kernel_theta_size(nlf, d);
     L.gstride = (L.G + 3) & ~3;
-    // the persistent flow (and with FLOW_STILES its K^{-1} partial sums, when the owner table
-    // holds them; else without)
-    L.sdelta = (nlf == 0 && FLOW_STILES > 0 && FLOW_STILES < L.T) ? FLOW_STILES : 0;
-    L.flow_wgs = flow_grid(nb, L.T, L.Tp, flow_wgs, flow_min_t, L.sdelta);
-    if (!L.flow_wgs && L.sdelta) {
-        L.sdelta = 0;
-        L.flow_wgs = flow_grid(nb, L.T, L.Tp, flow_wgs, flow_min_t, 0);
-    }
-    if (!L.flow_wgs) L.sdelta = 0;
-    L.gchunk = L.sdelta ? -L.sdelta : grad_chunk;
+    L.flow_wgs = flow_grid(nb, L.T, L.Tp, flow_wgs, flow_min_t);
+    L.gchunk = grad_chunk;
     L.ng = grad_tasks(L.T, L.gchunk);
     Carve c(ws);
     const size_t ldr = (size_t)L.npad + L.ppad;
@@ -126,7 +116,6 @@ static GprLayout gpr_layout(int nb, int n, int p, int d, void* ws, int grad_chun
     L.own = c.take<int>(L.flow_wgs ? (size_t)FLOW_WAVES * (L.flow_wgs - 1) * FLOW_MAXOWN + SCHED_KEY : 0);
     L.ntrace = L.flow_wgs ? flow_trace_count(L.T, L.flow_wgs) : 0;
     L.trace = c.take<long long>((size_t)L.ntrace);
-    L.S = c.take<double>(L.sdelta ? (size_t)L.T * (L.T + 1) / 2 * 1024 : 0);
     L.bytes = c.off + 256;
     return L;
 }
@@ -152,12 +141,22 @@ constexpr int FLOW_MIN_TILES = 8;
 // synchronisation) until the holder records, so it cannot be enqueued beside the replay's
 // unfenced flows.  The holding thread itself passes (its eager calls inside the bracket are
 // ordered by their streams as usual).
+// Holds nest per thread (Engine.ordered blocks inside one another): only the outermost RECORD
+// releases.  A thread that finds the fence held by another waits at most fence_bound() on the
+// host (10 s; env MFGP_FENCE_BOUND_MS) and then fails with MFGP_ERR_FENCE (a client that issued
+// WAIT and never RECORD cannot block every other thread's flow launches for ever).
+static std::chrono::milliseconds fence_bound() {
+    const char* e = getenv("MFGP_FENCE_BOUND_MS");
+    const long ms = e ? atol(e) : 10000;
+    return std::chrono::milliseconds(ms > 0 ? ms : 10000);
+}
 struct FlowFence {
     std::mutex mu;
     std::condition_variable cv;
     hipEvent_t ev = nullptr;
     bool armed = false;
     bool held = false;
+    int depth = 0;   // WAITs of the holder not yet matched by a RECORD
     std::thread::id holder;
 };
 constexpr int FENCE_MAX_DEVICES = 64;
@@ -168,29 +167,35 @@ static bool stream_capturing(hipStream_t s) {
     return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
 }
 
-// with f.mu locked: wait until no other thread holds the fence
-static void fence_enter(FlowFence& f, std::unique_lock<std::mutex>& lk) {
+// with f.mu locked: wait (bounded) until no other thread holds the fence
+static bool fence_enter(FlowFence& f, std::unique_lock<std::mutex>& lk) {
     const std::thread::id me = std::this_thread::get_id();
-    f.cv.wait(lk, [&] { return !f.held || f.holder == me; });
+    return f.cv.wait_for(lk, fence_bound(), [&] { return !f.held || f.holder == me; });
 }
 
-static void fence_wait(int dev, hipStream_t s, bool hold = false) {
-    if (dev < 0 || dev >= FENCE_MAX_DEVICES || stream_capturing(s)) return;
+static int fence_wait(int dev, hipStream_t s, bool hold = false) {
+    if (dev < 0 || dev >= FENCE_MAX_DEVICES || stream_capturing(s)) return MFGP_OK;
     FlowFence& f = g_fence[dev];
     std::unique_lock<std::mutex> lk(f.mu);
-    fence_enter(f, lk);
+    if (!fence_enter(f, lk)) return MFGP_ERR_FENCE;
     if (f.armed) (void)hipStreamWaitEvent(s, f.ev, 0);
     if (hold) {
-        f.held = true;
-        f.holder = std::this_thread::get_id();
+        if (f.held) {
+            ++f.depth;   // nested hold of the same thread
+        } else {
+            f.held = true;
+            f.depth = 1;
+            f.holder = std::this_thread::get_id();
+        }
     }
+    return MFGP_OK;
 }
 
-static void fence_record(int dev, hipStream_t s, bool release = false) {
-    if (dev < 0 || dev >= FENCE_MAX_DEVICES || stream_capturing(s)) return;
+static int fence_record(int dev, hipStream_t s, bool release = false) {
+    if (dev < 0 || dev >= FENCE_MAX_DEVICES || stream_capturing(s)) return MFGP_OK;
     FlowFence& f = g_fence[dev];
     std::unique_lock<std::mutex> lk(f.mu);
-    fence_enter(f, lk);
+    if (!fence_enter(f, lk)) return MFGP_ERR_FENCE;
     if (!f.ev) {
         int cur = -1;
         (void)hipGetDevice(&cur);
@@ -199,11 +204,13 @@ static void fence_record(int dev, hipStream_t s, bool release = false) {
         if (cur >= 0 && cur != dev) (void)hipSetDevice(cur);
     }
     if (f.ev && hipEventRecord(f.ev, s) == hipSuccess) f.armed = true;
-    if (release && f.held) {
+    if (release && f.held && --f.depth <= 0) {   // the outermost RECORD of the holder
         f.held = false;
+        f.depth = 0;
         lk.unlock();
         f.cv.notify_all();
     }
+    return MFGP_OK;
 }
 
 // k_gram (LML layout) with more lower tiles than CUs: one workgroup per CU, tile (0,0) and its
@@ -267,6 +274,10 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
         return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;
     }
     if (pm) pm->mark(s);
+    // the flow fence before any launch of the sequence: a fence held past its bound by another
+    // host thread fails the call with nothing enqueued
+    int fence_rc = L.flow_wgs ? fence_wait(h->device, s) : MFGP_OK;
+    if (fence_rc != MFGP_OK) return fence_rc;
     {
         GramArgs g{};
         g.R = L.R; g.ldr = ldr; g.sR = 0; g.Y = Y; g.ldy = ldy; g.sY = 0; g.p = p; g.ppad = L.ppad;
@@ -278,14 +289,12 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
         g.Dd = L.Dd; g.sD = 0; g.ldiag = L.ldiag; g.sL = 0; g.info = info; g.nlf = nlf;
         g.cnt = L.cnt; g.ncnt = L.ncnt;
         if (MFGP_REDUCE_FLAG) { g.isent = L.items; g.nisent = L.G + 2; }
-        const bool order = want_grad && std::abs(L.gchunk) + L.T + L.Tp < 2048;   // gram LDS holds the histogram
+        const bool order = want_grad && L.gchunk + L.T + L.Tp < 2048;   // gram LDS holds the histogram
         if (order) { g.gorder = L.gorder; g.gT = L.T; g.gchunk = L.gchunk; g.gTp = L.Tp; }
-        if (L.flow_wgs) { g.fown = L.own; g.fW = FLOW_WAVES * (L.flow_wgs - 1); g.fflags = L.flags; g.nfflags = L.nflags; g.fpub = L.pub; g.npub = L.npub; g.fsdelta = L.sdelta; }
+        if (L.flow_wgs) { g.fown = L.own; g.fW = FLOW_WAVES * (L.flow_wgs - 1); g.fflags = L.flags; g.nfflags = L.nflags; g.fpub = L.pub; g.npub = L.npub; }
         if (L.flow_wgs && h->flow_trace) g.dbg = L.trace + L.ntrace - flow_gram_dbg_count(L.T);   // k_gram timeline (diagnostic)
         const int extra = (order ? 1 : 0) + (L.flow_wgs ? 1 : 0);
-        if (NB == 32 && L.flow_wgs && !nlf && !h->gram_legacy) {
-            if (h->flow_d0) g.Dd = nullptr;
-            if (h->flow_trace) if (const char* ge = getenv("MFGP_GRAM_EXPERIMENT")) g.exper = atoi(ge);   // diagnostic ablations
+        if (NB == 32 && L.flow_wgs && !nlf) {
             launch_gram_flow(g, extra, s);
         } else {
             g.tile_wgs = gram_tile_wgs(h, L.T, extra);
@@ -305,12 +314,9 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
         fa.trace = h->flow_trace ? L.trace : nullptr;
         fa.nwaves = FLOW_WAVES * (L.flow_wgs - 1);
         fa.timeout = h->flow_timeout;
-        fa.d0 = (NB == 32 && !nlf && !h->gram_legacy && h->flow_d0) ? 1 : 0;
-        fa.S = L.S;
-        fa.sdelta = L.sdelta;
-        fence_wait(h->device, s);
+        fa.d0 = 0;
         launch_chol_flow(fa, L.flow_wgs, s);
-        fence_record(h->device, s);
+        fence_rc = fence_record(h->device, s);
     } else {
         CholArgs c{};
         c.A = L.A; c.lda = L.npad; c.sA = 0;
@@ -324,7 +330,7 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
     if (pm) pm->mark(s);
     if (want_grad) {
         GradArgs ga{L.Xo, ldr, X, (long)ldx, theta, L.gpart, L.gstride, L.T, L.Tp, n, p, d,
-                    L.gchunk, nlf, std::abs(L.gchunk) + L.T + L.Tp < 2048 ? L.gorder : nullptr, L.S};
+                    L.gchunk, nlf, L.gchunk + L.T + L.Tp < 2048 ? L.gorder : nullptr};
         launch_grad<NB>(ga, s);
     }
     if (pm) pm->mark(s);
@@ -342,6 +348,7 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
     f.flag = MFGP_REDUCE_FLAG;   // the Gram launch above filled items[] with the sentinel
     hipLaunchKernelGGL(k_reduce_items, dim3(2 + (want_grad ? L.G : 0)), dim3(NTHREADS), 0, s, f);
     if (pm) pm->mark(s);
+    if (fence_rc != MFGP_OK) return fence_rc;
     return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;
 }
 
@@ -673,6 +680,7 @@ const char* mfgp_error_string(int code) {
         case MFGP_ERR_WORKSPACE: return "workspace too small";
         case MFGP_ERR_LAUNCH: return "kernel launch failed";
         case MFGP_ERR_DIM: return "unsupported input dimension (1 <= d <= 32)";
+        case MFGP_ERR_FENCE: return "flow fence held by another host thread past the bound (WAIT without RECORD?)";
         default: return "unknown error";
     }
 }
@@ -696,18 +704,10 @@ int mfgp_create(int device, mfgp_handle_t* out) {
     h->f32_reserve = 32;
     h->gram_wgs = 0;
     if (const char* gv = getenv("MFGP_GRAM_WGS")) h->gram_wgs = atoi(gv);
-    h->gram_legacy = 0;
-    h->flow_d0 = 0;
     h->tiny = 1;   // small problems (n, p <= 64, D <= 16) in one launch: 37.0 us against 43.5 us of kernel
                    // time for the step sequence at HBS, 3.93 vs 4.31 ms for 100 captured Adam steps
                    // (MFGP_TINY=0 / mfgp_set_tiny(h, 0): the step sequence)
     if (const char* tv = getenv("MFGP_TINY")) h->tiny = atoi(tv) != 0;
-#ifdef MFGP_AB_KNOBS
-    // A/B diagnostics only (a build with -DMFGP_AB_KNOBS, then tools/ab_env.sh): each switches the
-    // production LML to another numerics path, so the shipped library never reads them
-    if (const char* gl = getenv("MFGP_GRAM_LEGACY")) h->gram_legacy = atoi(gl) != 0;
-    if (const char* d0 = getenv("MFGP_FLOW_D0")) h->flow_d0 = atoi(d0) != 0;
-#endif
     if (const char* rv = getenv("MFGP_F32_RESERVE")) h->f32_reserve = std::max(0, atoi(rv));
     if (const char* la = getenv("MFGP_F32_LOOKAHEAD")) h->f32_lookahead = atoi(la) != 0;
     h->f32_refine = 2;
@@ -797,14 +797,19 @@ int mfgp_set_tiny(mfgp_handle_t h, int enable) {
     return MFGP_OK;
 }
 
+int mfgp_get_tiny(mfgp_handle_t h) { return h ? h->tiny : MFGP_ERR_ARG; }
+
+int mfgp_get_grad_chunk(mfgp_handle_t h) { return h ? h->grad_chunk : MFGP_ERR_ARG; }
+
 int mfgp_get_flow(mfgp_handle_t h) { return h ? (h->flow_wgs > 0 ? (h->flow_min_t ? 1 : 3) : 0) : MFGP_ERR_ARG; }
 
 int mfgp_flow_fence(mfgp_handle_t h, int op) {
     CHECK_H(h);
-    if (op == MFGP_FENCE_WAIT) fence_wait(h->device, h->stream, true);
-    else if (op == MFGP_FENCE_RECORD) fence_record(h->device, h->stream, true);
-    else return MFGP_ERR_ARG;
-    return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;
+    // only the fence's own outcome: it enqueues an event wait / record, no kernel (hipGetLastError
+    // would report whatever an earlier call left behind)
+    if (op == MFGP_FENCE_WAIT) return fence_wait(h->device, h->stream, true);
+    if (op == MFGP_FENCE_RECORD) return fence_record(h->device, h->stream, true);
+    return MFGP_ERR_ARG;
 }
 
 static int gram_common(mfgp_handle_t h, int n1, int n2, int d, const double* X1, int ldx1, const double* X2,

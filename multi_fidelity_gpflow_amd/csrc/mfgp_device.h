@@ -116,11 +116,7 @@ __device__ __forceinline__ void xcd_swizzle(int& x, int& z) {
     const int nwg = gx * gridDim.z;
     const int b = blockIdx.x + gx * blockIdx.z;
     const int cpx = nwg >> 3;
-#ifdef MFGP_NO_XCD_SWIZZLE   // A/B builds only
-    const int s = b;
-#else
     const int s = b < 8 * cpx ? (b & 7) * cpx + (b >> 3) : b;
-#endif
     x = s % gx;
     z = s / gx;
 }
@@ -310,18 +306,16 @@ __device__ __forceinline__ double sel4(int s, double v0, double v1, double v2, d
 
 // R work of round K, deferred into round K+1 (after its LDS reads are issued) so that the
 // in-order issue of the A chain is never held behind it: X = V L_M^{-1}, W_R, R -= W_R R[P, :].
-// W1_ONEHOT: the lane-constant selections of the single-wave factor (component kk = l >> 4 of a
-// row's four values, the unit vector e_p of pivot row p = l & 3) as one-hot products / selects of
-// per-lane constants formed once, instead of v_cndmask trees rebuilt every round
-#ifndef W1_ONEHOT
-#define W1_ONEHOT 1   // 8.1k -> 7.65k clocks for the fused NB = 32 factor, bit-identical (tools/ubench_rsplit.hip)
-#endif
+// The lane-constant selections of the single-wave factor (component kk = l >> 4 of a row's four
+// values, the unit vector e_p of pivot row p = l & 3) are one-hot products / selects of per-lane
+// constants formed once, instead of v_cndmask trees rebuilt every round (8.1k -> 7.65k clocks for
+// the NB = 32 factor, bit-identical; tools/ubench_rsplit.hip)
 struct W1Pending {
     double L10, L20, L30, L21, L31, L32;
     double v[2][4];   // rows h = 0, 1: Z (rows below) or e_p (pivot rows)
-    double u[4];      // W1_ONEHOT: u[c] = (kk == c)
-    double e[4];      // W1_ONEHOT: e[c] = (p == c)
-    double ekk;       // W1_ONEHOT: (p == kk)
+    double u[4];      // u[c] = (kk == c)
+    double e[4];      // e[c] = (p == c)
+    double ekk;       // (p == kk)
 };
 __device__ __forceinline__ void w1_consts(W1Pending& pd, int l) {
     const int kk = l >> 4, p = l & 3;
@@ -334,13 +328,8 @@ __device__ __forceinline__ void w1_consts(W1Pending& pd, int l) {
 }
 // component kk of (a0, a1, a2, a3): exact for finite values (one term is 1 x a_kk, the rest 0 x a_c)
 __device__ __forceinline__ double w1_pick(const W1Pending& pd, int kk, double a0, double a1, double a2, double a3) {
-#if W1_ONEHOT
     (void)kk;
     return fma(pd.u[3], a3, fma(pd.u[2], a2, fma(pd.u[1], a1, pd.u[0] * a0)));
-#else
-    (void)pd;
-    return sel4(kk, a0, a1, a2, a3);
-#endif
 }
 
 template <int K>
@@ -359,11 +348,7 @@ __device__ __forceinline__ void w1_rwork(const W1Pending& pd, f64x4& r00, f64x4&
         const double x1 = fma(-pd.L31, x3, fma(-pd.L21, x2, pd.v[h][1]));
         const double x0 = fma(-pd.L30, x3, fma(-pd.L20, x2, fma(-pd.L10, x1, pd.v[h][0])));
         const double xk = w1_pick(pd, kk, x0, x1, x2, x3);
-#if W1_ONEHOT
         wR[h] = below ? xk : piv ? (pd.ekk - xk) : 0.0;
-#else
-        wR[h] = below ? xk : piv ? ((p == kk ? 1.0 : 0.0) - xk) : 0.0;
-#endif
     }
     if constexpr (bk == 0) {
         const double pR0 = r00[kq];
@@ -376,22 +361,9 @@ __device__ __forceinline__ void w1_rwork(const W1Pending& pd, f64x4& r00, f64x4&
     }
 }
 
-
-// Round publication for a band wave (tile_band_w1_wave, PUB = true): round K writes, after its
-// rank-4 MFMA is issued, Yb[128 K + 4 row + c] = y_row[c] of the rows below the pivots (0 for the
-// pivot rows and above), Fb[16 K + 0 .. 9] = L10 L20 L30 L21 L31 L32 i0 i1 i2 i3 of the pivot
-// block, the pivots into dpv (as always), then the progress word *prog = base + K + 1.
-struct W1Pub {
-    double* Yb;
-    double* Fb;
-    int* prog;
-    int base;
-};
-
-template <int K, bool PUB = false>
+template <int K>
 __device__ __forceinline__ void w1_round(double* __restrict__ Pn, double* __restrict__ dpv, f64x4& a00, f64x4& a01,
-                                         f64x4& a11, f64x4& r00, f64x4& r10, f64x4& r11, W1Pending& pd, int l,
-                                         const W1Pub& pub = W1Pub{}) {
+                                         f64x4& a11, f64x4& r00, f64x4& r10, f64x4& r11, W1Pending& pd, int l) {
     if constexpr (K < 8) {
         constexpr int bk = K >> 2, kq = K & 3;
         const int lc = l & 15, kk = l >> 4;
@@ -428,7 +400,7 @@ __device__ __forceinline__ void w1_round(double* __restrict__ Pn, double* __rest
         const double i3 = W1RCP(d3);
 #undef W1RCP
         // ---- per row: Y = C L_M^{-T}, Z = Y D_M^{-1}; A -= Z Y^T (symmetric form)
-        double zA[2], yB[2], ym[2] = {0.0, 0.0}, zs[2][4] = {};
+        double zA[2], yB[2], zs[2][4] = {};
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             if (h < bk) { zA[h] = 0.0; yB[h] = 0.0; continue; }
@@ -444,7 +416,6 @@ __device__ __forceinline__ void w1_round(double* __restrict__ Pn, double* __rest
             const double z0 = y0 * i0, z1 = y1 * i1, z2 = y2 * i2, z3 = y3 * i3;
             zA[h] = below ? w1_pick(pd, kk, z0, z1, z2, z3) : 0.0;
             yB[h] = w1_pick(pd, kk, y0, y1, y2, y3);
-            if constexpr (PUB) ym[h] = below ? yB[h] : 0.0;
             zs[h][0] = z0; zs[h][1] = z1; zs[h][2] = z2; zs[h][3] = z3;
         }
         // ---- rank-4 update of A on the matrix core (an f64 MFMA holds the SIMD for 64 clocks,
@@ -464,37 +435,21 @@ __device__ __forceinline__ void w1_round(double* __restrict__ Pn, double* __rest
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const bool piv = ((16 * h + lc) >> 2) == K;
-            const int p = lc & 3;
 #pragma unroll
-#if W1_ONEHOT
             for (int c = 0; c < 4; ++c) pd.v[h][c] = piv ? pd.e[c] : zs[h][c];
-#else
-            for (int c = 0; c < 4; ++c) pd.v[h][c] = piv ? (p == c ? 1.0 : 0.0) : zs[h][c];
-#endif
         }
         pd.L10 = L10; pd.L20 = L20; pd.L30 = L30; pd.L21 = L21; pd.L31 = L31; pd.L32 = L32;
-        if constexpr (PUB) {
-            pub.Yb[128 * K + lc * 4 + kk] = ym[0];
-            pub.Yb[128 * K + (16 + lc) * 4 + kk] = ym[1];
-            const int g = l >> 2, c = l & 3;
-            const double f0 = sel4(c, L10, L20, L30, L21), f1 = sel4(c, L31, L32, i0, i1), f2 = sel4(c, i2, i3, 0.0, 0.0);
-            pub.Fb[16 * K + (l < 12 ? l : 12 + c)] = g == 0 ? f0 : (g == 1 ? f1 : f2);
-            asm volatile("" ::: "memory");
-            __hip_atomic_store(pub.prog, pub.base + K + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
         __builtin_amdgcn_sched_barrier(0);
-        w1_round<K + 1, PUB>(Pn, dpv, a00, a01, a11, r00, r10, r11, pd, l, pub);
+        w1_round<K + 1>(Pn, dpv, a00, a01, a11, r00, r10, r11, pd, l);
     } else {
         w1_rwork<7>(pd, r00, r10, r11, l);
     }
 }
 
-// Body run by ONE wave (any wave of the workgroup; no workgroup barrier inside).  PUB: also
-// publish every round for a band wave (W1Pub).
-template <bool PUB = false>
+// Body run by ONE wave (any wave of the workgroup; no workgroup barrier inside).
 __device__ __forceinline__ void tile_potrf_inv_w1_wave(const double* __restrict__ X, int ldx, double* __restrict__ Pn,
                                                        double* __restrict__ R, double* __restrict__ dg,
-                                                       int* __restrict__ bad, const W1Pub& pub = W1Pub{}) {
+                                                       int* __restrict__ bad) {
     constexpr int S = TileCfg<32>::S;
     {
         const int l = threadIdx.x & 63, lc = l & 15, lr = l >> 4;
@@ -513,7 +468,7 @@ __device__ __forceinline__ void tile_potrf_inv_w1_wave(const double* __restrict_
         double* dpv = Pn + 128;                                // [32] pivots + dump slots
         W1Pending pd;
         w1_consts(pd, l);
-        w1_round<0, PUB>(Pn, dpv, a00, a01, a11, r00, r10, r11, pd, l, pub);
+        w1_round<0>(Pn, dpv, a00, a01, a11, r00, r10, r11, pd, l);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         // L^{-1} = diag(d)^{-1/2} L_u^{-1}; L_ii = sqrt(d_i); first bad pivot by one ballot
         double s0[4], s1[4];
@@ -534,383 +489,6 @@ __device__ __forceinline__ void tile_potrf_inv_w1_wave(const double* __restrict_
             R[(16 + r) * S + lc] = r10[q] * s1[q];
             R[(16 + r) * S + 16 + lc] = (lc <= r) ? r11[q] * s1[q] : 0.0;
         }
-    }
-}
-
-// ---------------------------------------------------------------- split diag factor
-// The factorization of tile_potrf_inv_w1_wave with its two halves on two waves of the workgroup:
-//   * the A wave (tile_elim_w1_wave) runs the elimination.  Round K publishes its pivot rows
-//     (Pn, read back by the A wave itself), then -- after issuing its rank-4 MFMA update -- the
-//     round's substitution results for the R wave: z = C L_M^{-T} D_M^{-1} of every live row
-//     (rows 16h + lc, h >= K / 4, written once by the lanes with kk = 0) into Zb + 128 K, the four
-//     pivots into dpv, and last the LDS progress word *prog = base + K + 1 (every lane stores the
-//     same value: one ds_write, no exec branch; a wave's DS operations are processed in issue
-//     order, so the round's data is complete once the word is seen);
-//   * the R wave (tile_rinv_w1_wave) applies the inverse update R -= W_R R[P, :] of each round from
-//     those z values alone: the 4x4 LDL^T multipliers are the pivot rows' own z (row p of the
-//     pivot block has z_j = L_pj, j < p), so it neither re-reads the panel nor repeats the LDL^T,
-//     then scales R into D = L^{-1} and writes L_ii and the first bad pivot.
-// On one wave the inverse's MFMAs and ~60 f64 VALU instructions a round share SIMD 0 with the
-// elimination (8.1k clocks against ~4.3k for the elimination alone, tools/ubench_rsplit.hip);
-// split, D follows the A wave's last round by the R wave's one-round lag.  An R wave that
-// re-derived the LDL^T from the panel was issue-bound at ~1k clocks a round (no faster than the
-// fused factor).  The multipliers taken from the pivot rows' z can differ from the A wave's L in
-// the last bit (the pivot block's upper and lower triangle round independently), so D is not
-// bitwise the fused factor's, only equal to rounding.
-// Pn: 8 x 128, Zb: 8 x 128, dpv: 104 doubles (none aliasing X); prog: an LDS int, monotonic
-// over calls.
-template <int K>
-__device__ __forceinline__ void w1e_round(double* __restrict__ Pn, double* __restrict__ Zb, double* __restrict__ dpv,
-                                          int* prog, int base, f64x4& a00, f64x4& a01, f64x4& a11, int l) {
-    if constexpr (K < 8) {
-        constexpr int bk = K >> 2, kq = K & 3;
-        const int lc = l & 15, kk = l >> 4;
-        double* P = Pn + 128 * K;
-        if constexpr (bk == 0) P[lc * 4 + kk] = a00[kq];
-        P[(16 + lc) * 4 + kk] = (bk == 0) ? a01[kq] : a11[kq];
-        asm volatile("" ::: "memory");   // keep the compiler from reordering publish / read
-        const f64x2* Pm = reinterpret_cast<const f64x2*>(P + 16 * K);
-        const f64x2 c0a = Pm[0], c0b = Pm[1], c1a = Pm[2], c1b = Pm[3], c2b = Pm[5], c3b = Pm[7];
-        const f64x2* Pr = reinterpret_cast<const f64x2*>(P);
-        f64x2 u0a = {0.0, 0.0}, u0b = {0.0, 0.0};
-        if constexpr (bk == 0) { u0a = Pr[2 * lc]; u0b = Pr[2 * lc + 1]; }
-        const f64x2 u1a = Pr[2 * (16 + lc)], u1b = Pr[2 * (16 + lc) + 1];
-        __builtin_amdgcn_sched_barrier(0);
-        const double m00 = c0a.x, m10 = c0a.y, m20 = c0b.x, m30 = c0b.y;
-        const double m11 = c1a.y, m21 = c1b.x, m31 = c1b.y, m22 = c2b.x, m32 = c2b.y, m33 = c3b.y;
-        const double i0 = rcp_nr1(m00);
-        const double L10 = m10 * i0, L20 = m20 * i0, L30 = m30 * i0;
-        const double d1 = fma(-L10, m10, m11);
-        const double i1 = rcp_nr1(d1);
-        const double e21 = fma(-L20, m10, m21), e31 = fma(-L30, m10, m31);
-        const double L21 = e21 * i1, L31 = e31 * i1;
-        const double d2 = fma(-L21, e21, fma(-L20, m20, m22));
-        const double i2 = rcp_nr1(d2);
-        const double e32 = fma(-L31, e21, fma(-L30, m20, m32));
-        const double L32 = e32 * i2;
-        const double d3 = fma(-L32, e32, fma(-L31, e31, fma(-L30, m30, m33)));
-        const double i3 = rcp_nr1(d3);
-        double zA[2], yB[2], zs[2][4] = {};
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            if (h < bk) { zA[h] = 0.0; yB[h] = 0.0; continue; }
-            const f64x2 ua = h ? u1a : u0a, ub = h ? u1b : u0b;
-            const int row = 16 * h + lc;
-            const bool below = row > 4 * K + 3;
-            const double y0 = ua.x;
-            const double y1 = fma(-L10, y0, ua.y);
-            const double y2 = fma(-L21, y1, fma(-L20, y0, ub.x));
-            const double y3 = fma(-L32, y2, fma(-L31, y1, fma(-L30, y0, ub.y)));
-            const double z0 = y0 * i0, z1 = y1 * i1, z2 = y2 * i2, z3 = y3 * i3;
-            zA[h] = below ? sel4(kk, z0, z1, z2, z3) : 0.0;
-            yB[h] = sel4(kk, y0, y1, y2, y3);
-            zs[h][0] = z0; zs[h][1] = z1; zs[h][2] = z2; zs[h][3] = z3;
-        }
-        if constexpr (K < 7) {   // the last round's pivots leave nothing below them to update
-            if constexpr (bk == 0) {
-                if constexpr (K < 3) {
-                    a00 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[0], yB[0], a00, 0, 0, 0);
-                    a01 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[0], yB[1], a01, 0, 0, 0);
-                }
-                a11 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[1], yB[1], a11, 0, 0, 0);
-            } else {
-                a11 = __builtin_amdgcn_mfma_f64_16x16x4f64(-zA[1], yB[1], a11, 0, 0, 0);
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        // ---- off the A chain (issued under the MFMA latency): the R wave's inputs of this round
-        dpv[l < 4 ? 4 * K + l : 40 + l] = sel4(l & 3, m00, d1, d2, d3);
-        if (kk == 0) {
-            f64x2* Z = reinterpret_cast<f64x2*>(Zb + 128 * K);
-#pragma unroll
-            for (int h = bk; h < 2; ++h) {
-                Z[2 * (16 * h + lc)] = f64x2{zs[h][0], zs[h][1]};
-                Z[2 * (16 * h + lc) + 1] = f64x2{zs[h][2], zs[h][3]};
-            }
-        }
-        asm volatile("" ::: "memory");
-        __hip_atomic_store(prog, base + K + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __builtin_amdgcn_sched_barrier(0);
-        w1e_round<K + 1>(Pn, Zb, dpv, prog, base, a00, a01, a11, l);
-    }
-}
-
-// A wave: X (lower triangle valid, stride ldx; may not alias Pn / Zb) -> the elimination.
-__device__ __forceinline__ void tile_elim_w1_wave(const double* __restrict__ X, int ldx, double* __restrict__ Pn,
-                                                  double* __restrict__ Zb, double* __restrict__ dpv, int* prog,
-                                                  int base) {
-    const int l = threadIdx.x & 63, lc = l & 15, lr = l >> 4;
-    f64x4 a00, a01, a11;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int r = lr + 4 * q;
-        const int hi = r > lc ? r : lc, lo = r > lc ? lc : r;
-        a00[q] = X[hi * ldx + lo];
-        a11[q] = X[(16 + hi) * ldx + 16 + lo];
-        a01[q] = X[(16 + lc) * ldx + r];
-    }
-    w1e_round<0>(Pn, Zb, dpv, prog, base, a00, a01, a11, l);
-}
-
-template <int K>
-__device__ __forceinline__ void w1r_round(const double* __restrict__ Zb, const int* prog, int base, f64x4& r00,
-                                          f64x4& r10, f64x4& r11, int l) {
-    if constexpr (K < 8) {
-        constexpr int bk = K >> 2;
-        const int lc = l & 15;
-        while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(const_cast<int*>(prog), __ATOMIC_RELAXED,
-                                                                __HIP_MEMORY_SCOPE_WORKGROUP)) < base + K + 1) {}
-        asm volatile("" ::: "memory");
-        const double* Z = Zb + 128 * K;
-        // multipliers: the pivot rows' z (rows 4K + 1 .. 4K + 3 of the tile)
-        const f64x2 p2 = *reinterpret_cast<const f64x2*>(Z + 4 * (4 * K + 2));
-        const f64x2 p3a = *reinterpret_cast<const f64x2*>(Z + 4 * (4 * K + 3));
-        W1Pending pd;
-        w1_consts(pd, l);
-        pd.L10 = Z[4 * (4 * K + 1)];
-        pd.L20 = p2.x; pd.L21 = p2.y;
-        pd.L30 = p3a.x; pd.L31 = p3a.y; pd.L32 = Z[4 * (4 * K + 3) + 2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            if (h < bk) continue;
-            const f64x2 za = *reinterpret_cast<const f64x2*>(Z + 4 * (16 * h + lc));
-            const f64x2 zb = *reinterpret_cast<const f64x2*>(Z + 4 * (16 * h + lc) + 2);
-            const bool piv = ((16 * h + lc) >> 2) == K;
-            const int p = lc & 3;
-            pd.v[h][0] = piv ? (p == 0 ? 1.0 : 0.0) : za.x;
-            pd.v[h][1] = piv ? (p == 1 ? 1.0 : 0.0) : za.y;
-            pd.v[h][2] = piv ? (p == 2 ? 1.0 : 0.0) : zb.x;
-            pd.v[h][3] = piv ? (p == 3 ? 1.0 : 0.0) : zb.y;
-        }
-        w1_rwork<K>(pd, r00, r10, r11, l);
-        w1r_round<K + 1>(Zb, prog, base, r00, r10, r11, l);
-    }
-}
-
-// R wave: follows tile_elim_w1_wave's rounds; writes D = L^{-1} into R (stride S, lower, zero
-// above), dg[i] = L_ii and *bad as tile_potrf_inv_w1_wave does.
-__device__ __forceinline__ void tile_rinv_w1_wave(const double* __restrict__ Zb, const int* prog, int base,
-                                                  const double* __restrict__ dpv, double* __restrict__ R,
-                                                  double* __restrict__ dg, int* __restrict__ bad) {
-    constexpr int S = TileCfg<32>::S;
-    const int l = threadIdx.x & 63, lc = l & 15, lr = l >> 4;
-    f64x4 r00, r10 = {0.0, 0.0, 0.0, 0.0}, r11;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int r = lr + 4 * q;
-        r00[q] = (r == lc) ? 1.0 : 0.0;
-        r11[q] = r00[q];
-    }
-    w1r_round<0>(Zb, prog, base, r00, r10, r11, l);
-    double s0[4], s1[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        s0[q] = rsq_nr(dpv[lr + 4 * q]);
-        s1[q] = rsq_nr(dpv[16 + lr + 4 * q]);
-    }
-    const double dl = dpv[l & 31];
-    const unsigned long long m = __ballot(l < 32 && !(dl > 0.0 && dl < INFINITY));
-    if (l < 32) dg[l] = dl * rsq_nr(dl);
-    if (l == 0) *bad = m ? __ffsll((long long)m) : 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int r = lr + 4 * q;
-        R[r * S + lc] = (lc <= r) ? r00[q] * s0[q] : 0.0;
-        R[r * S + 16 + lc] = 0.0;
-        R[(16 + r) * S + lc] = r10[q] * s1[q];
-        R[(16 + r) * S + 16 + lc] = (lc <= r) ? r11[q] * s1[q] : 0.0;
-    }
-}
-
-// ---------------------------------------------------------------- two-half inverse
-// D = L^{-1} of tile_elim_w1_wave's elimination on TWO waves, by halves of the unit factor
-// L~ = [[A, 0], [B, C]] (16 x 16 blocks; L = L~ diag(d)^{1/2}):
-//   * wave Ra (tile_rinv_lo_w1_wave) follows rounds 0..3 only: A^{-1} by the rank-4 updates of the
-//     fused factor's R00 block, then T = B A^{-1} (4 MFMAs, B = the rows 16..31 z of rounds
-//     0..3) into LDS, and D00 = diag(d)^{-1/2} A^{-1};
-//   * wave Rb (tile_rinv_hi_w1_wave) follows rounds 4..7 only: C^{-1} (R11), D11 = diag(d)^{-1/2}
-//     C^{-1}, then D10 = -D11 T (4 MFMAs), dg and the first bad pivot.
-// Neither half waits on the other's rounds: the inverse's serial chain is half as long as the
-// single R wave's (tile_rinv_w1_wave), and C^{-1} starts as soon as round 4 is out.
-template <int K, int H>
-__device__ __forceinline__ void w1h_round(const double* __restrict__ Zb, const int* prog, int base, f64x4& r, int l) {
-    if constexpr (K < 4 * H + 4) {
-        constexpr int kq = K & 3;
-        const int lc = l & 15, kk = l >> 4, p = lc & 3;
-        while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(const_cast<int*>(prog), __ATOMIC_RELAXED,
-                                                                __HIP_MEMORY_SCOPE_WORKGROUP)) < base + K + 1) {}
-        asm volatile("" ::: "memory");
-        const double* Z = Zb + 128 * K;
-        const f64x2 p2 = *reinterpret_cast<const f64x2*>(Z + 4 * (4 * K + 2));
-        const f64x2 p3a = *reinterpret_cast<const f64x2*>(Z + 4 * (4 * K + 3));
-        const double L10 = Z[4 * (4 * K + 1)], L20 = p2.x, L21 = p2.y, L30 = p3a.x, L31 = p3a.y, L32 = Z[4 * (4 * K + 3) + 2];
-        const int row = 16 * H + lc;
-        const f64x2 za = *reinterpret_cast<const f64x2*>(Z + 4 * row);
-        const f64x2 zb = *reinterpret_cast<const f64x2*>(Z + 4 * row + 2);
-        const bool piv = (row >> 2) == K;
-        const bool below = row > 4 * K + 3;
-        const double v0 = piv ? (p == 0 ? 1.0 : 0.0) : za.x, v1 = piv ? (p == 1 ? 1.0 : 0.0) : za.y;
-        const double v2 = piv ? (p == 2 ? 1.0 : 0.0) : zb.x, v3 = piv ? (p == 3 ? 1.0 : 0.0) : zb.y;
-        const double x3 = v3;
-        const double x2 = fma(-L32, x3, v2);
-        const double x1 = fma(-L31, x3, fma(-L21, x2, v1));
-        const double x0 = fma(-L30, x3, fma(-L20, x2, fma(-L10, x1, v0)));
-        const double xk = sel4(kk, x0, x1, x2, x3);
-        const double wR = below ? xk : piv ? ((p == kk ? 1.0 : 0.0) - xk) : 0.0;
-        const double pR = r[kq];
-        r = __builtin_amdgcn_mfma_f64_16x16x4f64(-wR, pR, r, 0, 0, 0);
-        w1h_round<K + 1, H>(Zb, prog, base, r, l);
-    }
-}
-
-// Ra: D00 into R (stride S; D01 = 0), T = B A^{-1} into Tb (16 x 16, stride 17), then *tw = tv.
-__device__ __forceinline__ void tile_rinv_lo_w1_wave(const double* __restrict__ Zb, const int* prog, int base,
-                                                     const double* __restrict__ dpv, double* __restrict__ R,
-                                                     double* __restrict__ Tb, int* tw, int tv) {
-    constexpr int S = TileCfg<32>::S;
-    const int l = threadIdx.x & 63, lc = l & 15, lr = l >> 4;
-    f64x4 r;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) r[q] = (lr + 4 * q == lc) ? 1.0 : 0.0;
-    w1h_round<0, 0>(Zb, prog, base, r, l);
-    f64x4 t = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int s = 0; s < 4; ++s)   // B[i][4s + kk] = z_{16+i}[kk] of round s
-        t = __builtin_amdgcn_mfma_f64_16x16x4f64(Zb[128 * s + 4 * (16 + lc) + lr], r[s], t, 0, 0, 0);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int rr = lr + 4 * q;
-        const double s0 = rsq_nr(dpv[rr]);
-        R[rr * S + lc] = (lc <= rr) ? r[q] * s0 : 0.0;
-        R[rr * S + 16 + lc] = 0.0;
-        Tb[rr * 17 + lc] = t[q];
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (l == 0) __hip_atomic_store(tw, tv, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// Rb: D11, then (once *tw >= tv) D10 = -D11 T; dg[i] = L_ii and *bad as tile_rinv_w1_wave.
-__device__ __forceinline__ void tile_rinv_hi_w1_wave(const double* __restrict__ Zb, const int* prog, int base,
-                                                     const double* __restrict__ dpv, double* __restrict__ R,
-                                                     const double* __restrict__ Tb, const int* tw, int tv,
-                                                     double* __restrict__ dg, int* __restrict__ bad) {
-    constexpr int S = TileCfg<32>::S;
-    const int l = threadIdx.x & 63, lc = l & 15, lr = l >> 4;
-    f64x4 r;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) r[q] = (lr + 4 * q == lc) ? 1.0 : 0.0;
-    w1h_round<4, 1>(Zb, prog, base, r, l);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int rr = lr + 4 * q;
-        const double s1 = rsq_nr(dpv[16 + rr]);
-        R[(16 + rr) * S + 16 + lc] = (lc <= rr) ? r[q] * s1 : 0.0;
-    }
-    const double dl = dpv[l & 31];
-    const unsigned long long m = __ballot(l < 32 && !(dl > 0.0 && dl < INFINITY));
-    if (l < 32) dg[l] = dl * rsq_nr(dl);
-    if (l == 0) *bad = m ? __ffsll((long long)m) : 0;
-    while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(const_cast<int*>(tw), __ATOMIC_ACQUIRE,
-                                                            __HIP_MEMORY_SCOPE_WORKGROUP)) < tv) {}
-    f64x4 d = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int s = 0; s < 4; ++s)   // A: D11[lc][4s + kk] (just written, same wave), B: T[4s + kk][lc]
-        d = __builtin_amdgcn_mfma_f64_16x16x4f64(-R[(16 + lc) * S + 16 + 4 * s + lr], Tb[(4 * s + lr) * 17 + lc], d,
-                                                 0, 0, 0);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) R[(16 + lr + 4 * q) * S + lc] = d[q];
-}
-
-// ---------------------------------------------------------------- band wave (tall panel)
-// Eliminates the 32 x 32 sub-diagonal block B = A(k+1, k) of the tall panel [A(k,k); A(k+1,k)] in
-// lock-step with the diagonal factor's rounds (tile_potrf_inv_w1_wave<true> publishing Yb / Fb /
-// dpv / prog), so that L(k+1,k) = B L_kk^{-T} comes out of the elimination itself instead of a
-// product with D_k = L_kk^{-1}, and accumulates S = L(k+1,k) L(k+1,k)^T round by round (the
-// update of A(k+1,k+1)).  Round K: the pivot columns C_i = B[i, 4K .. 4K+3] (rows i = 16 ib + lc,
-// through a 128-double LDS scratch Q), y_i = C_i L_M^{-T}, z_i = y_i D_M^{-1} with the pivot
-// block's factors as the diagonal wave computed them (Fb), then
-//   B[i, j] -= z_i y_j   for the later pivot columns j (y_j: the diagonal wave's rows, Yb),
-//   S += y z^T,          L(k+1,k)[i, 4K + c] = y_i[c] / sqrt(d_{4K+c}).
-// B is held transposed in accumulator layout (bt[jb][ib]: rows j = 16 jb + (l >> 4) + 4q,
-// columns i = 16 ib + (l & 15)), so round K's pivot columns are register K & 3 of block row K / 4,
-// exactly as the diagonal wave holds its pivot rows.
-template <int K>
-__device__ __forceinline__ void w1b_round(const double* __restrict__ Yb, const double* __restrict__ Fb,
-                                          const double* __restrict__ dpv, const int* prog, int base,
-                                          double* __restrict__ Q, f64x4 (&bt)[2][2], f64x4& s00, f64x4& s10,
-                                          f64x4& s11, double* __restrict__ Lo, int ldl, int l) {
-    if constexpr (K < 8) {
-        constexpr int bk = K >> 2, kq = K & 3;
-        const int lc = l & 15, kk = l >> 4;
-        Q[lc * 4 + kk] = bt[bk][0][kq];
-        Q[(16 + lc) * 4 + kk] = bt[bk][1][kq];
-        asm volatile("" ::: "memory");
-        while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(const_cast<int*>(prog), __ATOMIC_RELAXED,
-                                                                __HIP_MEMORY_SCOPE_WORKGROUP)) < base + K + 1) {}
-        asm volatile("" ::: "memory");
-        const f64x2* Qr = reinterpret_cast<const f64x2*>(Q);
-        const f64x2 u0a = Qr[2 * lc], u0b = Qr[2 * lc + 1], u1a = Qr[2 * (16 + lc)], u1b = Qr[2 * (16 + lc) + 1];
-        const f64x2* F = reinterpret_cast<const f64x2*>(Fb + 16 * K);
-        const f64x2 f0 = F[0], f1 = F[1], f2 = F[2], f3 = F[3], f4 = F[4];
-        const double L10 = f0.x, L20 = f0.y, L30 = f1.x, L21 = f1.y, L31 = f2.x, L32 = f2.y;
-        const double i0 = f3.x, i1 = f3.y, i2 = f4.x, i3 = f4.y;
-        double yA[2] = {0.0, 0.0};
-#pragma unroll
-        for (int jb = bk; jb < 2; ++jb) yA[jb] = Yb[128 * K + (16 * jb + lc) * 4 + kk];
-        const double rs = rsq_nr(dpv[4 * K + kk]);
-        __builtin_amdgcn_sched_barrier(0);
-        double yk[2], zk[2];
-#pragma unroll
-        for (int ib = 0; ib < 2; ++ib) {
-            const f64x2 ua = ib ? u1a : u0a, ub = ib ? u1b : u0b;
-            const double y0 = ua.x;
-            const double y1 = fma(-L10, y0, ua.y);
-            const double y2 = fma(-L21, y1, fma(-L20, y0, ub.x));
-            const double y3 = fma(-L32, y2, fma(-L31, y1, fma(-L30, y0, ub.y)));
-            yk[ib] = sel4(kk, y0, y1, y2, y3);
-            zk[ib] = sel4(kk, y0 * i0, y1 * i1, y2 * i2, y3 * i3);
-        }
-        if constexpr (K < 7) {
-#pragma unroll
-            for (int jb = bk; jb < 2; ++jb) {
-                bt[jb][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(-yA[jb], zk[0], bt[jb][0], 0, 0, 0);
-                bt[jb][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(-yA[jb], zk[1], bt[jb][1], 0, 0, 0);
-            }
-        }
-        s00 = __builtin_amdgcn_mfma_f64_16x16x4f64(yk[0], zk[0], s00, 0, 0, 0);
-        s10 = __builtin_amdgcn_mfma_f64_16x16x4f64(yk[1], zk[0], s10, 0, 0, 0);
-        s11 = __builtin_amdgcn_mfma_f64_16x16x4f64(yk[1], zk[1], s11, 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        Lo[lc * ldl + 4 * K + kk] = yk[0] * rs;
-        Lo[(16 + lc) * ldl + 4 * K + kk] = yk[1] * rs;
-        w1b_round<K + 1>(Yb, Fb, dpv, prog, base, Q, bt, s00, s10, s11, Lo, ldl, l);
-    }
-}
-
-// B: the sub-diagonal block (row-major, stride ldb, LDS or global); Lo: L(k+1,k) (stride ldl);
-// So: S = L L^T, lower 16 x 16 blocks (0,0), (1,0), (1,1) written (stride lds), (0,1) untouched.
-// Q: 128 doubles of LDS private to this wave.  Yb, Fb, dpv, prog, base: the diagonal wave's W1Pub
-// and pivots of the same step.
-__device__ __forceinline__ void tile_band_w1_wave(const double* __restrict__ B, int ldb, const double* __restrict__ Yb,
-                                                  const double* __restrict__ Fb, const double* __restrict__ dpv,
-                                                  const int* prog, int base, double* __restrict__ Q,
-                                                  double* __restrict__ Lo, int ldl, double* __restrict__ So, int lds) {
-    const int l = threadIdx.x & 63, lc = l & 15, lr = l >> 4;
-    f64x4 bt[2][2];
-#pragma unroll
-    for (int jb = 0; jb < 2; ++jb)
-#pragma unroll
-        for (int ib = 0; ib < 2; ++ib)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) bt[jb][ib][q] = B[(16 * ib + lc) * ldb + 16 * jb + lr + 4 * q];
-    f64x4 s00 = {0.0, 0.0, 0.0, 0.0}, s10 = s00, s11 = s00;
-    w1b_round<0>(Yb, Fb, dpv, prog, base, Q, bt, s00, s10, s11, Lo, ldl, l);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int r = lr + 4 * q;
-        So[r * lds + lc] = s00[q];
-        So[(16 + r) * lds + lc] = s10[q];
-        So[(16 + r) * lds + 16 + lc] = s11[q];
     }
 }
 

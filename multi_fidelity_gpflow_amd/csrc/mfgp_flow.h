@@ -6,22 +6,6 @@
 
 namespace mfgp {
 
-#ifndef FLOW_BAND3
-#define FLOW_BAND3 0
-#endif
-// FLOW_W5OWN: the band tile (k,k-2) of rows k >= 4 takes panel k-3 from its owner too, so wave 5
-// of the diag workgroup forms L(k,k-2) = A''(k,k-2) D_{k-2}^T as soon as D_{k-2} is out
-#ifndef FLOW_W5OWN
-#define FLOW_W5OWN 0
-#endif
-// FLOW_STILES = sd > 0: the flow's idle worker waves also accumulate the partial sums of the
-// gradient's K^{-1} = L^{-T} L^{-1} tiles, S(i,j) = sum_{l = i .. T-1-sd} X(l,i)^T X(l,j) (X = L^{-1}
-// row blocks, read from their publication slots as they come out), into a workspace buffer; k_grad
-// then adds only the last sd row blocks and the alpha rows (grad_decode with chunk = -sd).
-#ifndef FLOW_STILES
-#define FLOW_STILES 0
-#endif
-
 // k_gram timeline of a trace-mode call (diagnostic): [3 G] per-workgroup stamps, then [2 G] staging
 // stamps at 3 gridDim.x; G bounds the grid of both set-up Grams (k_gram_flow: nb(nb+1)/2 blocks
 // of 64 + factor + two set-up workgroups; the looping k_gram: at most T(T+1)/2 tiles + two).
@@ -29,9 +13,8 @@ __host__ __device__ inline int flow_gram_dbg_wgs(int T) { return T * (T + 1) / 2
 __host__ __device__ inline int flow_gram_dbg_count(int T) { return 5 * flow_gram_dbg_wgs(T); }
 
 // ---------------------------------------------------------------- tile catalogue
-// code = sd << 24 | type << 20 | i << 10 | j ; R tiles use j = column tile c in [0, T + Tp); sd only
-// on S tiles
-enum : int { FT_A = 0, FT_R = 1, FT_AL = 2, FT_H = 3, FT_S = 4 };   // FT_H: coupling H_k = D_k L(k,k-1)
+// code = type << 20 | i << 10 | j ; R tiles use j = column tile c in [0, T + Tp)
+enum : int { FT_A = 0, FT_R = 1, FT_AL = 2, FT_H = 3 };   // FT_H: coupling H_k = D_k L(k,k-1)
 __host__ __device__ inline int flow_code(int type, int i, int j) { return (type << 20) | (i << 10) | j; }
 
 __host__ __device__ inline void flow_tri(int t, int& i, int& j) {   // row-major lower triangle
@@ -45,13 +28,11 @@ __host__ __device__ inline void flow_tri(int t, int& i, int& j) {   // row-major
 // Owned A tiles: every lower tile except (0,0) (k_gram) and the band tiles (k,k-2), (k,k-1),
 // (k,k) of rows k <= 3, which the diag workgroup takes from their initial values.
 __host__ __device__ inline int flow_nA(int T) { return T >= 4 ? T * (T + 1) / 2 - 9 : 0; }
-// S tiles (FLOW_STILES): the lower tiles (i, j) with i < T - sd, i.e. those with at least one level
-__host__ __device__ inline int flow_nS(int T, int sd) { const int m = T - sd; return (sd > 0 && m > 0) ? m * (m + 1) / 2 : 0; }
-__host__ __device__ inline int flow_ntiles(int T, int Tp, int sd = 0) {
-    return flow_nA(T) + T * (T - 1) / 2 + 2 * T * Tp + (T > 1 ? T - 1 : 0) + flow_nS(T, sd);
+__host__ __device__ inline int flow_ntiles(int T, int Tp) {
+    return flow_nA(T) + T * (T - 1) / 2 + 2 * T * Tp + (T > 1 ? T - 1 : 0);
 }
 
-__device__ inline int flow_decode(int g, int T, int Tp, int sd = 0) {
+__device__ inline int flow_decode(int g, int T, int Tp) {
     const int nA = flow_nA(T);
     int i, j;
     if (g < nA) { flow_tri(g == 0 ? 6 : g + 9, i, j); return flow_code(FT_A, i, j); }   // (3,0), then rows >= 4
@@ -63,11 +44,7 @@ __device__ inline int flow_decode(int g, int T, int Tp, int sd = 0) {
     g -= T * Tp;
     if (g < T * Tp) return flow_code(FT_AL, g / Tp, g % Tp);
     g -= T * Tp;
-    const int nH = T > 1 ? T - 1 : 0;
-    if (g < nH) return flow_code(FT_H, g + 1, 0);
-    g -= nH;
-    flow_tri(g, i, j);
-    return (sd << 24) | flow_code(FT_S, i, j);
+    return flow_code(FT_H, g + 1, 0);
 }
 
 // items of a tile: updates at levels [lo, hi] (hi < lo: none), finalize at level fin (-1: none),
@@ -83,13 +60,9 @@ __host__ __device__ inline FlowTile flow_tile(int code, int T) {
     t.pub = 0;
     if (t.type == FT_A) {
         t.lo = 0;
-        // band tiles (k,k), (k,k-1), (k,k-2): panels < k-3 here, the rest and L(k,k-2) in diag.
-        // FLOW_BAND3: (k,k-1) and (k,k) of rows k >= 4 also take panel k-3 here, so the diag
-        // workgroup's prefetch waves apply only panel k-2 (the tiles are needed a step later than
-        // (k,k-2), whose panel k-3 stays in diag ahead of its L(k,k-2) product)
+        // band tiles (k,k), (k,k-1), (k,k-2): panels < k-3 here, the rest and L(k,k-2) in diag
         if (t.i <= t.j + 2) {
-            const bool own3 = t.i >= 4 && ((FLOW_BAND3 && t.i < t.j + 2) || (FLOW_W5OWN && t.i == t.j + 2));
-            t.hi = own3 ? t.i - 3 : t.i - 4;
+            t.hi = t.i - 4;
             t.fin = -1;
             t.pub = 1;
         }
@@ -101,10 +74,6 @@ __host__ __device__ inline FlowTile flow_tile(int code, int T) {
     } else if (t.type == FT_AL) {
         t.lo = t.i;
         t.hi = T - 1;
-        t.fin = -1;
-    } else if (t.type == FT_S) {   // S(i,j) += X(l,i)^T X(l,j) at levels i .. T-1-sd
-        t.lo = t.i;
-        t.hi = T - 1 - (code >> 24);
         t.fin = -1;
     } else {   // FT_H: one item at level k, once D_k is out; the last one (k = T-1) is formed by
                // the diag workgroup itself (nothing else runs there by then), so it has no items
@@ -125,22 +94,19 @@ __host__ __device__ inline int flow_items(int code, int T) {
 // own holds W * FLOW_MAXOWN + SCHED_KEY ints: a table found intact from an earlier call with the
 // same (T, Tp, W) is kept (sched_cached); the flags are zeroed every call.
 constexpr int FLOW_OWN_MAGIC = 0x464C4F57;
-// Key: the item count (< 128: the flow's T is bounded by the owner table, ~90), S tiles after all
-// others (their items feed nothing in the launch).
-__host__ __device__ inline int flow_owner_key(int code, int T) {
-    return flow_items(code, T) + (((code >> 20) & 15) == FT_S ? 0 : 128);
-}
-__device__ inline void build_flow_owner(int T, int Tp, int W, int* own, int* flags, int nflags, int* sh, int sd = 0) {
+// Key: the item count (< 256: the flow's T is bounded by the owner table, ~90).
+__host__ __device__ inline int flow_owner_key(int code, int T) { return flow_items(code, T); }
+__device__ inline void build_flow_owner(int T, int Tp, int W, int* own, int* flags, int nflags, int* sh) {
     int* hist = sh;          // [256] count per key, then the start of its rank range
     int* cur = sh + 256;     // [256]
     unsigned* hs = reinterpret_cast<unsigned*>(sh + 512);
     for (int e = threadIdx.x; e < nflags; e += NTHREADS) flags[e * FLOW_FSTRIDE] = 0;
-    if (sched_cached(own, W * FLOW_MAXOWN, FLOW_OWN_MAGIC, T, Tp | (sd << 16), W, hs)) return;
+    if (sched_cached(own, W * FLOW_MAXOWN, FLOW_OWN_MAGIC, T, Tp, W, hs)) return;
     for (int e = threadIdx.x; e < 256; e += NTHREADS) { hist[e] = 0; cur[e] = 0; }
     for (int e = threadIdx.x; e < W * FLOW_MAXOWN; e += NTHREADS) own[e] = -1;
     __syncthreads();
-    const int n = flow_ntiles(T, Tp, sd);
-    for (int g = threadIdx.x; g < n; g += blockDim.x) atomicAdd(&hist[flow_owner_key(flow_decode(g, T, Tp, sd), T)], 1);
+    const int n = flow_ntiles(T, Tp);
+    for (int g = threadIdx.x; g < n; g += blockDim.x) atomicAdd(&hist[flow_owner_key(flow_decode(g, T, Tp), T)], 1);
     __syncthreads();
     if (threadIdx.x == 0) {
         int s = 0;
@@ -148,7 +114,7 @@ __device__ inline void build_flow_owner(int T, int Tp, int W, int* own, int* fla
     }
     __syncthreads();
     for (int g = threadIdx.x; g < n; g += blockDim.x) {
-        const int code = flow_decode(g, T, Tp, sd);
+        const int code = flow_decode(g, T, Tp);
         const int L = flow_owner_key(code, T);
         const int p = hist[L] + atomicAdd(&cur[L], 1);
         const int r = p / W, q = p % W;
@@ -159,7 +125,7 @@ __device__ inline void build_flow_owner(int T, int Tp, int W, int* own, int* fla
         const int w = (sn % nwg) * FLOW_WAVES + sn / nwg;
         if (r < FLOW_MAXOWN) own[w * FLOW_MAXOWN + r] = code;
     }
-    sched_seal(own, W * FLOW_MAXOWN, FLOW_OWN_MAGIC, T, Tp | (sd << 16), W, hs);
+    sched_seal(own, W * FLOW_MAXOWN, FLOW_OWN_MAGIC, T, Tp, W, hs);
 }
 
 }  // namespace mfgp

@@ -550,20 +550,6 @@ __device__ __forceinline__ void flow_update(FlowCtx& C, const FlowTile& t, int l
         pub_op2(x, C.P.L(t.i, l), y, C.P.X(l, t.j), C);  // L(i,l), X(l,c)^T (B[k][j] = X(l,c)[k][j])
         wt_mma<true>(acc, x, y);                         // R(i,c) -= L(i,l) X(l,c)
         wt_store<false>(acc, dst, a.ldr);
-    } else if (t.type == FT_S) {
-        // K^{-1} partial sum (FLOW_STILES): S(i,j) += X(l,i)^T X(l,j), both operands from the X^T
-        // publication slots (A[i'][k] = X(l,i)[k][i'] = X^T(l,i)[i'][k], B[k][j'] likewise)
-        double* dst = a.S + ((long)t.i * (t.i + 1) / 2 + t.j) * 1024;
-        if (l == t.lo) wt_zero(acc);
-        else wt_load<false>(acc, dst, 32);
-        if (t.j != t.i) {
-            pub_op2(x, C.P.X(l, t.i), y, C.P.X(l, t.j), C);
-        } else {
-            pub_op(x, C.P.X(l, t.i), C);
-            y = x;
-        }
-        wt_mma<false>(acc, x, y);
-        wt_store<false>(acc, dst, 32);
     } else {
         const int c = t.i, cy = t.j;
         double* al = a.alpha + (long)c * 32 * a.ldal + (long)cy * 32;
@@ -610,8 +596,7 @@ __device__ __forceinline__ void flow_item_log(const FlowCtx& C, int wid, int n, 
 __device__ __forceinline__ int flow_prio(int code) {
     if (code < 0) return 1 << 30;
     const FlowTile t = flow_tile(code, 1024);
-    // H_k first: the R finalizes of the same level wait for it (a later slot would deadlock);
-    // S tiles (FT_S = 4) last: nothing in the launch waits for them
+    // H_k first: the R finalizes of the same level wait for it (a later slot would deadlock)
     const int rank = t.type == FT_H ? 0 : t.type + 1;
     return (rank << 16) | (t.i << 8) | t.j;
 }
@@ -687,12 +672,10 @@ __device__ __forceinline__ void flow_worker(FlowCtx& C, int wid, double* S) {
 // Buffers are double-buffered by step parity.
 struct DiagLds {
     // LDS carve (doubles): Db[2] | Ls[2] | Ap[2] | Cp[2] | L2[2] (NB x S each) | fsc (32 x 33) | dg[2][32]
-    // | bad[2] | words | pan[2], zb[2] (8 x 128: the factor's round panels / z) | dpv[2] (128).  Parity-indexed
-    // buffers are computed, not held in pointer arrays (a dynamically indexed pointer array lands
-    // in scratch).
+    // | bad[2] | words.  Parity-indexed buffers are computed, not held in pointer arrays (a
+    // dynamically indexed pointer array lands in scratch).
     double* base;
     static constexpr int E = TileCfg<32>::ELEMS;
-    static constexpr int PAN = 10 * E + 32 * 33 + 64 + 16;   // after the words
     __device__ double* Db(int q) const { return base + q * E; }        // D_k (stride S)
     __device__ double* Ls(int q) const { return base + (2 + q) * E; }  // L(k,k-1)
     __device__ double* Ap(int q) const { return base + (4 + q) * E; }  // A''(k,k-1)
@@ -702,28 +685,11 @@ struct DiagLds {
     __device__ double* dg(int q) const { return base + 10 * E + 32 * 33 + 32 * q; }
     __device__ int* bad() const { return reinterpret_cast<int*>(base + 10 * E + 32 * 33 + 64); }
     __device__ int* w() const { return bad() + 2; }
-    __device__ double* pan(int q) const { return base + PAN + 1024 * q; }          // round panels (A)
-    __device__ double* zb(int q) const { return base + PAN + 2048 + 1024 * q; }    // round z (A -> R)
-    __device__ double* dpv(int q) const { return base + PAN + 4096 + 128 * q; }    // pivots (A -> R)
-    static constexpr size_t BYTES = sizeof(double) * (PAN + 4096 + 256);
+    static constexpr size_t BYTES = sizeof(double) * (10 * E + 32 * 33 + 64 + 16);
 };
 static_assert(DiagLds::BYTES <= FLOW_LDS_BYTES, "diag workgroup LDS carve");
-enum { DW_LS = 0, DW_D, DW_LPUB, DW_DPUB, DW_PRE6, DW_PRE7, DW_BAR, DW_L2, DW_P2, DW_PROG, DW_N };
-static_assert(DW_N <= 28, "progress words fit before the panels");
-
-// The diagonal factor of a chain step is split over two waves (tile_elim_w1_wave /
-// tile_rinv_w1_wave, mfgp_device.h): wave 0 eliminates, chain wave FLOW_RWAVE forms D_k from the
-// published round panels (its SIMD is shared with one band helper, so it raises its issue
-// priority while it runs).  FLOW_RWAVE = 0: the fused single-wave factor on wave 0.
-#ifndef FLOW_RWAVE
-#define FLOW_RWAVE 0
-#endif
-#ifndef FLOW_RPRIO
-#define FLOW_RPRIO 2
-#endif
-#ifndef FLOW_WAIT4
-#define FLOW_WAIT4 0
-#endif
+enum { DW_LS = 0, DW_D, DW_LPUB, DW_DPUB, DW_PRE6, DW_PRE7, DW_BAR, DW_L2, DW_P2, DW_N };
+static_assert(DW_N <= 28, "progress words fit in the carve");
 
 __device__ __forceinline__ int lds_get(const int* p) {
     return __hip_atomic_load(const_cast<int*>(p), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -788,28 +754,10 @@ __device__ __forceinline__ void diag_chain(FlowCtx& C, const DiagLds& B) {
     for (int k = 1; k < T; ++k) {
         const int pk = k & 1;
         if (a.trace && threadIdx.x == 0) a.trace[k] = flow_clock() - C.t0;
-#if FLOW_WAIT4
-        // the step's four progress words in ONE LDS round trip per poll (relaxed loads issued
-        // together, one acquire fence after): four sequential acquire spins cost ~4 round trips
-        // even when everything is already there
-        for (;;) {
-            const int* wd = B.w();
-            const int w6 = __hip_atomic_load(const_cast<int*>(wd + DW_PRE6), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const int w7 = __hip_atomic_load(const_cast<int*>(wd + DW_PRE7), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const int wdd = __hip_atomic_load(const_cast<int*>(wd + DW_D), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const int wl = __hip_atomic_load(const_cast<int*>(wd + DW_LPUB), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            // D_{k-1} in Db[pk ^ 1]; wave 4 is done with Ls[pk] (L(k-2,k-3))
-            if (__builtin_amdgcn_readfirstlane(w6) >= k && __builtin_amdgcn_readfirstlane(w7) >= k &&
-                __builtin_amdgcn_readfirstlane(wdd) >= k - 1 && __builtin_amdgcn_readfirstlane(wl) >= k - 2)
-                break;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-#else
         lds_spin_ge(&B.w()[DW_PRE6], k);
         lds_spin_ge(&B.w()[DW_PRE7], k);
         lds_spin_ge(&B.w()[DW_D], k - 1);         // D_{k-1} in Db[pk ^ 1]
         lds_spin_ge(&B.w()[DW_LPUB], k - 2);      // wave 4 is done with Ls[pk] (L(k-2,k-3))
-#endif
         if (a.trace && threadIdx.x == 0) a.trace[T + k] = flow_clock() - C.t0;
         Acc<32> pl, cij;
 #pragma unroll
@@ -832,25 +780,12 @@ __device__ __forceinline__ void diag_chain(FlowCtx& C, const DiagLds& B) {
         }
         chain_bar(&B.w()[DW_BAR], epoch);
         if (threadIdx.x == 0) lds_put(&B.w()[DW_P2], k);  // tile products of step k done
-#if FLOW_RWAVE
-        if (w == 0) {
-            if (a.trace && threadIdx.x == 0) a.trace[2 * T + k] = flow_clock() - C.t0;
-            tile_elim_w1_wave(B.fsc(), 33, B.pan(pk), B.zb(pk), B.dpv(pk), &B.w()[DW_PROG], 8 * k);
-        } else if (w == FLOW_RWAVE) {
-            lds_spin_ge(&B.w()[DW_DPUB], k - 2);    // wave 4 is done with Db[pk] (D_{k-2})
-            __builtin_amdgcn_s_setprio(FLOW_RPRIO);
-            tile_rinv_w1_wave(B.zb(pk), &B.w()[DW_PROG], 8 * k, B.dpv(pk), B.Db(pk), B.dg(pk), &B.bad()[pk]);
-            __builtin_amdgcn_s_setprio(0);
-            if (l == 0) lds_put(&B.w()[DW_D], k);
-        }
-#else
         if (w == 0) {
             lds_spin_ge(&B.w()[DW_DPUB], k - 2);    // wave 4 is done with Db[pk] (D_{k-2})
             if (a.trace && threadIdx.x == 0) a.trace[2 * T + k] = flow_clock() - C.t0;
             tile_potrf_inv_w1_wave(B.fsc(), 33, B.fsc(), B.Db(pk), B.dg(pk), &B.bad()[pk]);
             if (l == 0) lds_put(&B.w()[DW_D], k);
         }
-#endif
     }
 }
 
@@ -914,11 +849,8 @@ __device__ __forceinline__ void diag_publisher(FlowCtx& C, const DiagLds& B) {
 }
 
 // wave 5 shares SIMD 1 with chain wave 1, whose last MFMA of a step is its block of the first
-// product (L(k,k-1))
+// product (L(k,k-1)): its MFMA work waits for that product (W5_GATE)
 #define W5_GATE DW_LS
-#ifndef FLOW_W5GATE
-#define FLOW_W5GATE 1
-#endif
 __device__ __forceinline__ void diag_second(FlowCtx& C, const DiagLds& B) {
     constexpr int S = TileCfg<32>::S;
     const FlowArgs& a = C.a;
@@ -927,16 +859,15 @@ __device__ __forceinline__ void diag_second(FlowCtx& C, const DiagLds& B) {
         WTile acc;
         WOp x, y;
         if (j >= 4) {
-            if (FLOW_W5OWN) pub_wt(acc, C.P.H(2, j), C);
-            else pub_wt_op_direct(acc, C.P.H(2, j), x, C.P.L(j, j - 3), C);
+            pub_wt_op_direct(acc, C.P.H(2, j), x, C.P.L(j, j - 3), C);
         } else {
             wt_load<true>(acc, C.At(j, j - 2), a.lda);  // A(2,0), A(3,1): k_gram's values
             if (j == 3) pub_op(x, C.P.L(j, j - 3), C);
         }
         if (a.trace && (threadIdx.x & 63) == 0) a.trace[4 * T + j] = flow_clock() - C.t0;
-        if (j == 3 || (j > 3 && !FLOW_W5OWN)) {
+        if (j >= 3) {
             // panel j-3: A(j,j-2) -= L(j,j-3) L(j-2,j-3)^T  (the worker's L, the chain's Ls of step j-2)
-            if (FLOW_W5GATE) lds_wait_ge(&B.w()[W5_GATE], j - 1);   // MFMA only once the chain's step j-1 products
+            lds_wait_ge(&B.w()[W5_GATE], j - 1);          // MFMA only once the chain's step j-1 products
             lds_wait_ge(&B.w()[DW_LS], j - 2);            // on SIMD 1 are done (an earlier window in the
                                                           // factor, or none, measured slower)
             if (a.trace && (threadIdx.x & 63) == 0) a.trace[8 * T + 3 * a.nwaves + 4 * FLOW_LOG * a.nwaves + j] = flow_clock() - C.t0;
@@ -944,7 +875,7 @@ __device__ __forceinline__ void diag_second(FlowCtx& C, const DiagLds& B) {
             wt_mma<true>(acc, x, y);
         }
         lds_wait_ge(&B.w()[DW_D], j - 2);
-        if (FLOW_W5GATE) lds_wait_ge(&B.w()[W5_GATE], j - 1);
+        lds_wait_ge(&B.w()[W5_GATE], j - 1);
         lds_wait_ge(&B.w()[DW_PRE6], j - 1);              // L2[j & 1] = L(j-2,j-4): last read by
         lds_wait_ge(&B.w()[DW_PRE7], j - 2);              // wave 6 at j-1, wave 7 at j-2
         if (a.trace && (threadIdx.x & 63) == 0) a.trace[8 * T + 3 * a.nwaves + 4 * FLOW_LOG * a.nwaves + T + j] = flow_clock() - C.t0;
@@ -973,14 +904,13 @@ __device__ __forceinline__ void diag_prefetch(FlowCtx& C, const DiagLds& B, bool
         WTile acc;
         WOp x, y;
         if (j >= 4) {
-            if (FLOW_BAND3) pub_wt(acc, C.P.H(sub ? 0 : 1, j), C);
-            else pub_wt_op_direct(acc, C.P.H(sub ? 0 : 1, j), x, C.P.L(j, j - 3), C);
+            pub_wt_op_direct(acc, C.P.H(sub ? 0 : 1, j), x, C.P.L(j, j - 3), C);
         } else {
             wt_load<true>(acc, sub ? C.At(j, j - 1) : C.At(j, j), a.lda);   // k_gram's values
             if (j == 3) pub_op(x, C.P.L(j, j - 3), C);
         }
         if (a.trace && (threadIdx.x & 63) == 0) a.trace[(sub ? 5 : 6) * T + j] = flow_clock() - C.t0;
-        if (j == 3 || (j > 3 && !FLOW_BAND3)) {   // (FLOW_BAND3: the owner applied it, rows >= 4)
+        if (j >= 3) {
             // panel j-3 from the worker's L(j,j-3) and L(j-1,j-3) (wave 5, step j-1)
             lds_wait_ge(&B.w()[DW_P2], j - 1);
             if (sub) {

@@ -29,13 +29,12 @@ struct GramArgs {
     // k_chol_flow owner table (nullptr: none): one more extra workgroup builds it and zeroes
     // the flow flags (build_flow_owner); every workgroup fills its share of the publication
     // area with the sentinel
-    int* fown; int fW; int* fflags; int nfflags; int fsdelta;   // fsdelta: FLOW_STILES tiles in the table
+    int* fown; int fW; int* fflags; int nfflags;
     double* fpub; long npub;
     long long* dbg;               // diagnostic per-workgroup timeline (nullptr: off)
     // LML layout: > 0 -> that many tile workgroups, workgroup 0 takes tile (0,0) (and its fused
     // factor) alone on its CU, the others loop over the remaining tiles; 0 -> one tile each
     int tile_wgs;
-    int exper;                    // k_gram_flow diagnostic ablations (0: none; MFGP_GRAM_EXPERIMENT)
 };
 
 // k_chol_flow (mfgp_flow.hip): persistent dataflow Cholesky + L^{-1} + Z + alpha, NB = 32, batch 1
@@ -63,8 +62,6 @@ struct FlowArgs {
     int nwaves;                   // worker waves (trace layout)
     long long timeout;            // bound of every hand-off wait, 100 MHz ticks (FLOW_TIMEOUT_TICKS)
     int d0;                       // 1: the chain factors D_0 from A(0,0) (else D_0 is read from Dd)
-    double* S;                    // FLOW_STILES: K^{-1} partial sums, lower tile (i, j) at (i(i+1)/2 + j) * 1024
-    int sdelta;                   // levels T-sdelta .. T-1 left to k_grad (0: no S tiles)
 };
 constexpr long long FLOW_TIMEOUT_TICKS = 5000000;   // 50 ms (s_memrealtime is 100 MHz)
 int flow_trace_count(int T, int nwg);
@@ -94,7 +91,6 @@ struct GradArgs {
     int chunk;                            // m-tiles per task
     int nlf;                              // kernel family (GramArgs::nlf)
     const int* order;                     // workgroup -> task (nullptr: identity), see grad_order
-    const double* S;                      // chunk < 0: the flow's K^{-1} partial sums (FlowArgs::S)
 };
 
 constexpr int FIN_MAXG = 254;   // theta entries finalize_body stages in LDS (graph kernel: <= 186)

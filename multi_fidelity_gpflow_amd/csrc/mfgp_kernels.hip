@@ -247,7 +247,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
     }
     if (!LEAN && a.fown && blockIdx.x == gridDim.x - 1 - (a.gorder ? 1 : 0)) {   // extra: flow owner table
         if (b == 0) build_flow_owner(a.npad / NB, a.ppad / NB, a.fW, a.fown, a.fflags, a.nfflags,
-                                     reinterpret_cast<int*>(smem), a.fsdelta);
+                                     reinterpret_cast<int*>(smem));
         if (a.dbg && threadIdx.x == 0) a.dbg[3 * blockIdx.x + 2] = __builtin_amdgcn_s_memrealtime() - dbg_t0;
         gram_fill_pub(a);
         return;
@@ -574,7 +574,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram_flow(GramArgs a, int nblk) {
     if (bx >= nblk + nfac) {   // set-up workgroups (LDS as int scratch)
         int* sh = reinterpret_cast<int*>(smem);
         if (a.gorder && bx == (int)gridDim.x - 1) build_grad_order(a.gT, a.gchunk, a.gTp, a.gorder, sh);
-        else if (a.fown) build_flow_owner(a.npad / 32, a.ppad / 32, a.fW, a.fown, a.fflags, a.nfflags, sh, a.fsdelta);
+        else if (a.fown) build_flow_owner(a.npad / 32, a.ppad / 32, a.fW, a.fown, a.fflags, a.nfflags, sh);
         if (a.dbg && t == 0) { a.dbg[3 * bx] = t0; a.dbg[3 * bx + 1] = __builtin_amdgcn_s_memrealtime(); }
         if (a.isent && bx == (int)gridDim.x - 1) gram_fill_items(a);   // (off the factor workgroup's path)
         gram_fill_pub(a);
@@ -671,7 +671,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram_flow(GramArgs a, int nblk) {
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) kl[u] = -0.5 * (-2.0 * kl[u] + (nL1[rr[u]] + nL2));
-        if (!(a.exper & 2)) exp4(kl);
+        exp4(kl);
 #pragma unroll
         for (int u = 0; u < 4; ++u) kl[u] = vL * kl[u];
         MFGP_PIN4(kl);   // keep the four chains in one basic block (else each sinks into the branch below)
@@ -704,7 +704,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram_flow(GramArgs a, int nblk) {
                 // skipped: rows past npad, the upper tile of a diagonal block, tile (0,0) (the
                 // factor workgroup's, when there is one)
                 const bool keep = gi < a.npad && col_ok && (gi >> 5) >= (gj >> 5) && (!nfac || gi >= 32 || gj >= 32);
-                if (keep && !(a.exper & 1)) a.out[(long)gi * a.ldo + gj] = v;
+                if (keep) a.out[(long)gi * a.ldo + gj] = v;
             }
         }
     }
@@ -714,7 +714,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram_flow(GramArgs a, int nblk) {
         tile_store<32>(a.out, a.ldo, ftile);
         gram_first_factor<32>(ftile, frt, fdg, reinterpret_cast<int*>(fdg + 32), a.Dd, a.ldiag, a.info);
         if (a.dbg && t == 0) a.dbg[3 * bx + 1] = __builtin_amdgcn_s_memrealtime();
-    } else if (a.R != nullptr && !(a.exper & 8)) {   // Y block of R (rows < n, columns < p; zero padding), shared by the blocks
+    } else if (a.R != nullptr) {   // Y block of R (rows < n, columns < p; zero padding), shared by the blocks
         const long ne = (long)a.npad * a.ppad, st = (long)nblk * NTHREADS;
         const long e0 = blk * (long)NTHREADS + t;
         double yv[2];
@@ -734,7 +734,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram_flow(GramArgs a, int nblk) {
             a.R[(long)r * a.ldr + a.npad + cc] = (r < n && cc < a.p) ? a.Y[(long)r * a.ldy + cc] : 0.0;
         }
     }
-    if (!(a.exper & 4)) gram_fill_pub(a);
+    gram_fill_pub(a);
     if (a.dbg && t == 0) a.dbg[3 * bx + 2] = __builtin_amdgcn_s_memrealtime();
 }
 
@@ -992,20 +992,15 @@ __global__ void k_rhs_init(double* R, long ldr, long sR, int npad, int ppad, con
 // NB = 64 tiles are 33 KB each, so one).
 // After the loop the region is reused: raw rows xi, xj, flags fi, fj, then the
 // per-quad gradient partials R [G][GRAD_RLD] and the inverse squared lengthscales.
-#ifndef GRAD_ABL
-#define GRAD_ABL 0   // diagnostic ablation: 1 no epilogue, 2 no MFMA (tools/grad_variants.py)
-#endif
 template <int NB>
 constexpr int GRAD_NBUF = (NB == 32) ? 2 : 1;
 constexpr int GRAD_RLD = 65;   // 64 quad partials per gradient entry, +1 against bank conflicts
 template <int NB>
 constexpr int GRAD_RED_OFF = (2 * NB * XS + 2 * NB + 1) & ~1;
 
-// ch < 0 (the flow's S tiles, FLOW_STILES = -ch): one task per lower tile, rows m >= max(i, T + ch)
-// on top of the flow's partial sum
-__host__ __device__ inline int grad_row_chunks(int T, int i, int ch) { return ch < 0 ? 1 : (T - i + ch - 1) / ch; }
-__host__ __device__ inline int grad_m0(int T, int i, int ch, int c) { return ch < 0 ? max(i, T + ch) : i + c * ch; }
-__host__ __device__ inline int grad_m1(int T, int m0, int ch) { return ch < 0 ? T : min(T, m0 + ch); }
+__host__ __device__ inline int grad_row_chunks(int T, int i, int ch) { return (T - i + ch - 1) / ch; }
+__host__ __device__ inline int grad_m0(int T, int i, int ch, int c) { (void)T; return i + c * ch; }
+__host__ __device__ inline int grad_m1(int T, int m0, int ch) { return min(T, m0 + ch); }
 
 __host__ __device__ int grad_tasks(int T, int ch) {
     int s = 0;
@@ -1038,7 +1033,7 @@ __device__ __forceinline__ int grad_decode(int t, int T, int chunk, int Tp, int&
 constexpr int GRAD_ORDER_MAGIC = 0x4F524431;
 __device__ void build_grad_order(int T, int chunk, int Tp, int* order, int* hist) {
     const int ntask = grad_tasks(T, chunk);
-    const int lmax = (chunk < 0 ? T : chunk) + Tp;
+    const int lmax = chunk + Tp;
     unsigned* hs = reinterpret_cast<unsigned*>(hist + lmax + 1);
     if (sched_cached(order, ntask, GRAD_ORDER_MAGIC, T, chunk, Tp, hs)) return;
     for (int l = threadIdx.x; l <= lmax; l += NTHREADS) hist[l] = 0;
@@ -1099,7 +1094,6 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
     // W_ij (tile) = [alpha_i alpha_j^T] - P * sum_m Linv_mi^T Linv_mj  (= -P * acc below)
     Acc<NB> acc;
     acc_zero(acc);
-    if (a.chunk < 0 && m0 > i) acc_load<NB>(acc, a.S + ((long)i * (i + 1) / 2 + j) * NB * NB, NB);   // flow's rows < m0
     const double negP = -(double)a.P;
     {   // Software-pipelined operand stream of TN items acc += A^T B (all unscaled):
         //   q < nm : A = Linv_{m,i}, B = Linv_{m,j}, m = m0 + q
@@ -1135,9 +1129,7 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
             if (nq > 2) MFGP_GRAD_FETCH(ra0, rb0, 2);
             __syncthreads();
             for (int q = 0; q < nq; q += 2) {
-#if GRAD_ABL != 2
                 tile_mma<NB, true, false>(acc, A0, B0, 1.0);
-#endif
                 if (q + 1 < nq) {
                     tile_put<NB>(A1, ra1);
                     tile_put<NB>(B1, rb1);
@@ -1145,9 +1137,7 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
                 }
                 __syncthreads();
                 if (q + 1 < nq) {
-#if GRAD_ABL != 2
                     tile_mma<NB, true, false>(acc, A1, B1, 1.0);
-#endif
                     if (q + 2 < nq) {
                         tile_put<NB>(A0, ra0);
                         tile_put<NB>(B0, rb0);
@@ -1171,10 +1161,6 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
 #undef MFGP_GRAD_FETCH
     }
 
-#if GRAD_ABL == 1   // (NB = 32: the one accumulator block stays live, so no MFMA is dropped)
-    if (threadIdx.x < G) a.gpart[(long)threadIdx.x * gridDim.x + task] = acc.v[0][0];
-    return;
-#endif
     // stage the raw inputs of the two row tiles (operand buffers are free now)
     for (int e = threadIdx.x; e < NB * (a.D + 1); e += NTHREADS) {
         const int r = e / (a.D + 1), d = e % (a.D + 1);
@@ -1705,13 +1691,28 @@ void launch_pred(const PredAArgs& pa, const PredOutArgs& po, int T, hipStream_t 
 //   Z = L^{-1} Y, alpha = L^{-T} Z, S_ij = sum_m L^{-1}_mi^T L^{-1}_mj - alpha_i alpha_j^T / P, and
 //   k_grad's epilogue (W = -P S against dK/dtheta recomputed from the inputs) on the three lower
 //   tiles; then finalize_body's LML / gradient output and adam_body's step.
-#ifndef TINY_KMFMA
-#define TINY_KMFMA 1
-#endif
-#ifndef TINY_STOP
-#define TINY_STOP 0   // diagnostic ablation (tools/tiny_abl.sh): return after phase TINY_STOP
+// LDS hazard check (a debug build, -DTINY_POISON=1; tools/tiny_poison.sh): at every slot reuse the
+// dead slots are overwritten with a signalling NaN between two extra barriers, so a read that was
+// not ordered before the reuse by the barrier named at that point returns NaN instead of stale data
+// (the parity tests then fail).  Off in the library: no code.
+#ifndef TINY_POISON
+#define TINY_POISON 0
 #endif
 constexpr int TINY_MAXD = 16, TINY_XS = TINY_MAXD + 1, TINY_N = 64, TINY_P = 64;
+
+// slots in `mask` (bit i: LDS tile slot i of k_gpr_tiny) := signalling NaN
+__device__ __forceinline__ void tiny_poison(double* smem, unsigned mask) {
+    constexpr int E = TileCfg<32>::ELEMS;
+    const double snan = __builtin_bit_cast(double, 0x7FF4000000000000ull);
+    for (int sl = 0; sl < 16; ++sl)
+        if (mask & (1u << sl))
+            for (int e = threadIdx.x; e < E; e += NTHREADS) smem[(long)sl * E + e] = snan;
+}
+#if TINY_POISON
+#define TINY_REUSE(mask) do { __syncthreads(); tiny_poison(smem, (mask)); __syncthreads(); } while (0)
+#else
+#define TINY_REUSE(mask) do { } while (0)
+#endif
 
 struct TinyArgs {
     const double* X; long ldx;
@@ -1741,7 +1742,6 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
     double* K00 = slot(0); double* K10 = slot(1); double* K11 = slot(2);
     double* D0 = slot(3); double* D1 = slot(4); double* L10 = slot(5);
     auto Yt = [&](int r, int c) { return slot(6 + 2 * r + c); };
-    auto Zt = [&](int r, int c) { return r == 0 ? slot(c) : slot(c == 0 ? 2 : 10); };
     double* xr = slot(11);                         // raw rows 64 x TINY_XS (gradient epilogue)
     double* misc = slot(12);
     auto ELt = [&](int tl) { return slot(13 + tl); };   // exp(-r^2 / 2) of the Gram's K_L, tiles (0,0) (1,0) (1,1)
@@ -1821,10 +1821,9 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
     __syncthreads();
     if (t < TINY_N) { nL[t] = dot4(aL + t * TINY_XS, aL + t * TINY_XS, D4); nD[t] = dot4(aD + t * TINY_XS, aD + t * TINY_XS, D4); }
     __syncthreads();
-    // ---- K tiles (0,0), (1,0), (1,1): k_gram's padded-entry arithmetic; TINY_KMFMA: the dot
-    //      products a_i . a_j of the expanded r^2 on the matrix core (16 x 16 blocks, three per
-    //      wave, D4 / 4 v_mfma_f64_16x16x4 each) instead of a dot4 chain of 2 D4 LDS reads an entry
-#if TINY_KMFMA
+    // ---- K tiles (0,0), (1,0), (1,1): k_gram's padded-entry arithmetic, the dot products a_i . a_j
+    //      of the expanded r^2 on the matrix core (16 x 16 blocks, three per wave, D4 / 4
+    //      v_mfma_f64_16x16x4 each) instead of a dot4 chain of 2 D4 LDS reads an entry
     {
         const int lc = lane & 15, kk = lane >> 4;
         const double rho = sc.rho();
@@ -1857,34 +1856,9 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
             }
         }
     }
-#else
-#pragma unroll 4
-    for (int e = t; e < 3 * 32 * 32; e += NTHREADS) {
-        const int tl = e >> 10, r = (e >> 5) & 31, c = e & 31;
-        const int ti = tl == 0 ? 0 : 1, tj = tl == 2 ? 1 : 0;
-        if (ti >= T) continue;
-        const int gi = 32 * ti + r, gj = 32 * tj + c;
-        const double dot = dot4(aL + gi * TINY_XS, aL + gj * TINY_XS, D4);
-        const double el = exp(-0.5 * (-2.0 * dot + (nL[gi] + nL[gj])));
-        const double kl = sc.vL() * el;
-        ELt(tl)[r * S + c] = el;
-        const double fa = fl[gi], fb = fl[gj];
-        const bool L1 = (fa == 0.0), H1 = (fa == 1.0), L2 = (fb == 0.0), H2 = (fb == 1.0);
-        const double rho = sc.rho();
-        double kD = 0.0;
-        if (H1 && H2) {
-            const double dotD = dot4(aD + gi * TINY_XS, aD + gj * TINY_XS, D4);
-            kD = sc.vD() * exp(-0.5 * (-2.0 * dotD + (nD[gi] + nD[gj])));
-        }
-        const double vhh = kl * (rho * rho) + kD;
-        double v = (L1 && L2) ? kl : (!(H1 && H2) ? kl * rho : vhh);
-        if (!(L1 || H1) || !(L2 || H2)) v = 0.0;
-        if (gi == gj) v = (gi < n) ? v + noise : 1.0;
-        slot(tl)[r * S + c] = v;
-    }
-#endif
     __syncthreads();
-    if (TINY_STOP == 1) { if (t == 0) { a.info[0] = 0; a.f.out[0] = 0.0; } return; }
+    // reuse: the Gram staging (slots 6-8) is dead after the barrier above; slots 6-9 become Y tiles
+    TINY_REUSE(0x7C0u);
     // ---- factor: D_0; L_10, K_11 update, D_1, L^{-1}_10
     if (w == 0) tile_potrf_inv_w1_wave(K00, S, K00, D0, dg, &bad[0]);
     else if (w == 1 && f.adam && aown) {   // adam_body's step-size and SoftplusGrad factors
@@ -1893,16 +1867,19 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
         a_eu = exp(-pu) + 1.0;
     }
     __syncthreads();
-    if (TINY_STOP == 2) { if (t == 0) { a.info[0] = 0; a.f.out[0] = 0.0; } return; }
+    // reuse: K00 (slot 0, the factor's in-place scratch) is dead after the barrier above (Ki00 later)
+    TINY_REUSE(0x1u);
     if (T > 1) {
         Acc<32> acc;
         acc_zero(acc);
         tile_mma<32, false, true>(acc, K10, D0, 1.0);      // L_10 = K_10 D_0^T
         acc_to_lds(acc, L10);
         __syncthreads();
+        // reuse: K10 (slot 1) was last read by the product above, before this barrier; T goes there
+        TINY_REUSE(0x2u);
         acc_load<32>(acc, K11, S);
         tile_mma<32, false, true>(acc, L10, L10, -1.0);    // K_11 - L_10 L_10^T
-        __syncthreads();
+        __syncthreads();   // every read of K11 (acc_load) is done before K11 is rewritten
         acc_to_lds(acc, K11);
         acc_zero(acc);
         tile_mma<32, false, false>(acc, L10, D0, 1.0);     // T = L_10 D_0 (into K10's slot)
@@ -1910,11 +1887,13 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
         __syncthreads();
         if (w == 0) tile_potrf_inv_w1_wave(K11, S, K11, D1, dg + 32, &bad[1]);
         __syncthreads();
+        // reuse: K11 (slot 2, the factor's scratch) and L_10 (slot 5, last read by T = L_10 D_0
+        // before the barrier ahead of the factor) are dead; L^{-1}_10 is written over L_10 below
+        TINY_REUSE(0x24u);
         acc_zero(acc);
         tile_mma<32, false, false>(acc, D1, K10, -1.0);    // L^{-1}_10 = -D_1 T (over L10)
         acc_to_lds(acc, L10);   // (read, and T's slot 1 rewritten as Ki10, only after the barrier below)
     }
-    if (TINY_STOP == 3) { if (t == 0) { a.info[0] = 0; a.f.out[0] = 0.0; } return; }
     // ---- Y tiles (zero padded; loaded at the start)
 #pragma unroll
     for (int q = 0; q < YPER; ++q) {
@@ -1926,6 +1905,8 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
     //      tiles, over the consumed K00 / T / K11 slots); then alpha = L^{-T} Z, each column tile's
     //      results replacing its Y tiles (all read first)
     __syncthreads();   // the Y tiles and every wave's block of L^{-1}_10 are in; every read of T is done
+    // reuse: T (slot 1) is dead after the barrier above; Ki10 (or, in PRED, K(X, X*)) goes there
+    TINY_REUSE(T > 1 ? 0x2u : 0x0u);
     double* Ki00 = slot(0); double* Ki10 = slot(1); double* Ki11 = slot(2);
     double z2 = 0.0;
     Acc<32> zc[2][2];
@@ -1960,7 +1941,8 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
         }
     }
     __syncthreads();
-    if (TINY_STOP == 4) { if (t == 0) { a.info[0] = 0; a.f.out[0] = 0.0; } return; }
+    // reuse: the Y tiles (slots 6-9) were last read by the Z products, before the barrier above
+    TINY_REUSE(0x3C0u);
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
         if (c >= Tp) break;
@@ -1978,6 +1960,8 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
             xs[e] = (r < ns && d <= D) ? a.Xs[(long)r * a.ldxs + d] : 0.0;
         }
         __syncthreads();
+        // reuse: slots 0, 1, 2 (K00 / T / K11, consumed) and 10 become K(X, X*)
+        TINY_REUSE(0x407u);
         for (int e = t; e < T * Ts * 1024; e += NTHREADS) {   // K(X, X*): the AR1 kernel, exact masks
             const int tl = e >> 10, r = (e >> 5) & 31, c = e & 31;
             const int ti = tl / Ts, tc = tl % Ts;
@@ -2013,6 +1997,8 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
             }
         }
         __syncthreads();
+        // reuse: K(X, X*) (slots 0, 1, 2, 10) was last read by the A products, before the barrier above
+        TINY_REUSE(0x407u);
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             if (c >= Ts) break;
@@ -2065,6 +2051,8 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
         }
     }
     __syncthreads();
+    // reuse: the Z tiles (slots 6-9) were last read by the alpha products, before the barrier above
+    TINY_REUSE(0x3C0u);
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
         if (c >= Tp) break;
@@ -2075,7 +2063,6 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
     double ld = 0.0;
     if (t < n) ld = log(dg[t]);
     __syncthreads();
-    if (TINY_STOP == 5) { if (t == 0) { a.info[0] = 0; a.f.out[0] = 0.0; } return; }
     // ---- gradient: S tiles and k_grad's epilogue (per element: its weights; per dimension: the
     //      lengthscale sums, reduced at once, so no per-thread array is indexed at run time)
     double cLe[12], cDe[12];
@@ -2147,15 +2134,10 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
     // ---- reductions (L^{-1} is consumed: its slots hold 64 quad partials per quantity): quantity
     //      q < G the gradient entry q, G the quadratic term, G + 1 sum log L_ii
     __syncthreads();
+    // reuse: D_0, D_1, L^{-1}_10 (slots 3-5) were last read by the K^{-1} / Z / alpha products, before
+    // the barriers above; the reduction buffer RB spans them
+    TINY_REUSE(0x38u);
     double* RB = slot(3);
-    if (TINY_STOP == 6) {   // (keeps the epilogue live: every thread's partials reach memory)
-        double sink = gvL + gvD + grho + gnoise;
-#pragma unroll
-        for (int e = 0; e < 12; ++e) sink += cLe[e] + cDe[e] + (double)(gie[e] + gje[e]);
-        a.f.out[1 + (t & 7)] = sink;
-        if (t == 0) a.info[0] = 0;
-        return;
-    }
     auto put = [&](int q, double v) {
         v = quad_sum(v);
         if ((lane & 3) == 0) RB[q * 64 + w * 16 + (lane >> 2)] = v;
@@ -2195,12 +2177,6 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
             if (qx < G) gsh[2 + qx] = v;
             else gsh[qx - G] = v;
         }
-    }
-    if (TINY_STOP == 8) {   // after the reductions (gsh complete after the barrier below)
-        __syncthreads();
-        if (t < G + 2) a.f.out[t] = gsh[t];
-        if (t == 0) a.info[0] = 0;
-        return;
     }
     if (f.adam && aown) tsh[aq] = ptie;
     if (t == 0) {

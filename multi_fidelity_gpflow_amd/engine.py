@@ -114,11 +114,29 @@ class Engine:
         check(fn(self.h, *args, C.byref(out)), fn.__name__)
         return out.value
 
+    # callables run after any change of the handle's execution settings (tile, flow, tiny): the
+    # session pool (models.py) drops the cores whose captured graphs recorded the old settings
+    _mode_listeners: list = []
+
+    def _set_mode(self, fn, *args):
+        before = self.mode()
+        check(fn(self.h, *args), fn.__name__)
+        if self.mode() != before:
+            for cb in list(Engine._mode_listeners):
+                cb(self)
+
+    def mode(self) -> tuple:
+        """The handle's execution settings that captured step graphs and workspace sizes depend
+        on: (flow mode, tile size, one-launch small-problem path, k_grad chunk)."""
+        h = self.h
+        return (self.lib.mfgp_get_flow(h), self.lib.mfgp_get_tile(h), self.lib.mfgp_get_tiny(h),
+                self.lib.mfgp_get_grad_chunk(h))
+
     def tile(self) -> int:
         return self.lib.mfgp_get_tile(self.h)
 
     def set_tile(self, nb: int):
-        check(self.lib.mfgp_set_tile(self.h, nb), "mfgp_set_tile")
+        self._set_mode(self.lib.mfgp_set_tile, nb)
 
     def flow(self) -> bool:
         return self.lib.mfgp_get_flow(self.h) in (1, 3)
@@ -133,12 +151,12 @@ class Engine:
     def set_flow(self, enable: bool, any_size: bool = False):
         """Cholesky schedule of the LML path: persistent dataflow launch (True; for factorizations of
         8 or more 32-tiles unless any_size) or one launch per step (False)."""
-        check(self.lib.mfgp_set_flow(self.h, (3 if any_size else 1) if enable else 0), "mfgp_set_flow")
+        self._set_mode(self.lib.mfgp_set_flow, (3 if any_size else 1) if enable else 0)
 
     def set_tiny(self, enable: bool):
         """One-launch LML step for small problems (n, p <= 64, D <= 16; True, the default) or the
         step sequence of the general path (False)."""
-        check(self.lib.mfgp_set_tiny(self.h, 1 if enable else 0), "mfgp_set_tiny")
+        self._set_mode(self.lib.mfgp_set_tiny, 1 if enable else 0)
 
     def set_flow_timeout_us(self, us: int):
         """Bound of every k_chol_flow hand-off wait (default 50000 us; 0: diagnostic abort path)."""

@@ -22,6 +22,7 @@ from __future__ import annotations
 import atexit
 import threading
 import weakref
+from collections import OrderedDict
 
 import numpy as np
 import torch
@@ -313,23 +314,62 @@ class MultiFidelityGPModel(Module):
 # graphs of a finished one: its model's data and initial state are copied into the buffers the
 # graphs point at, so no capture, no allocation and no warm-up evaluation are repeated.  The
 # reference's multi-bin test (tests/test_ho2021_multibin.py:20-43) builds a fresh model per run;
-# at HBS size the capture of the 50-step graph was a third of the 100-step protocol.  Only
-# sessions whose private workspace is small are pooled (one idle core per shape); the pool is
-# emptied at interpreter exit, before the HIP runtime goes away.
+# at HBS size the capture of the 50-step graph was a third of the 100-step protocol.
+#
+# Retention: only sessions whose private workspace is at most _POOL_MAX_WS_BYTES are pooled, one
+# idle core per key (device, dtype, shapes, lr, max_iters, graph chunk and the handle's execution
+# settings, Engine.mode()), at most _POOL_MAX_ENTRIES cores and _POOL_MAX_BYTES of their device
+# buffers in all; beyond that the least recently used core is evicted (its graphs destroyed and its
+# buffers freed -- eviction runs in finish(), outside any capture).  Changing the handle's settings
+# (Engine.set_tile / set_flow / set_tiny) empties the pool, as does clear_session_pool() and
+# interpreter exit (before the HIP runtime goes away).
 _POOL_MAX_WS_BYTES = 96 << 20
-_pool: dict = {}
+_POOL_MAX_ENTRIES = 8
+_POOL_MAX_BYTES = 512 << 20
+_pool: "OrderedDict" = OrderedDict()   # key -> idle _AdamCore, least recently used first
 _pool_lock = threading.Lock()
 
 
-def _pool_clear():
-    with _pool_lock:
-        cores = [c for v in _pool.values() for c in v]
-        _pool.clear()
+def _release(cores):
     for c in cores:
-        c.graphs.clear()
+        c.release()
 
 
-atexit.register(_pool_clear)
+def clear_session_pool():
+    """Destroy every pooled training session core (captured graphs and device buffers).  Must not
+    run while a stream capture is in progress on the device."""
+    with _pool_lock:
+        cores = list(_pool.values())
+        _pool.clear()
+    _release(cores)
+
+
+_pool_clear = clear_session_pool   # earlier name, kept for the tests and tools that use it
+
+
+def _pool_put(key, core):
+    """Pool an idle core (False if its key already holds one); evicts LRU cores over the caps."""
+    evicted = []
+    with _pool_lock:
+        if key in _pool:
+            return False
+        _pool[key] = core
+        total = sum(c.nbytes for c in _pool.values())
+        while len(_pool) > _POOL_MAX_ENTRIES or (total > _POOL_MAX_BYTES and len(_pool) > 1):
+            _, old = _pool.popitem(last=False)
+            total -= old.nbytes
+            evicted.append(old)
+    _release(evicted)
+    return True
+
+
+def _pool_take(key):
+    with _pool_lock:
+        return _pool.pop(key, None)
+
+
+atexit.register(clear_session_pool)
+Engine._mode_listeners.append(lambda eng: clear_session_pool())
 
 
 class _AdamCore:
@@ -371,7 +411,14 @@ class _AdamCore:
             n, p, d = X.shape[0], Y.shape[1], tm.d
             self.ws_bytes = eng.gpr_workspace_bytes(n, p, d, X.dtype)
             self.ws = eng.private_workspace(self.ws_bytes)
+        self.nbytes = self.ws_bytes + 2 * o["end"] + X.numel() * X.element_size() + Y.numel() * Y.element_size()
         self.warm = False
+
+    def release(self):
+        """Destroy the captured graphs and drop every buffer (an evicted or cleared pool entry)."""
+        self.graphs.clear()
+        self.X = self.Y = self.st = self.ws = self.d_in = self.h_in = self.h_out = None
+        self.hist = self.si = self.info = self.out = None
 
     def load(self, X: torch.Tensor, Y: torch.Tensor, tm: "_ThetaMap"):
         """A model's data and initial state into the buffers (on the core's stream)."""
@@ -396,7 +443,8 @@ class _AdamCore:
 
 
 def _pool_key(eng, X, Y, lr, max_iters, chunk):
-    return (eng.index, X.dtype, tuple(X.shape), tuple(Y.shape), float(np.float32(lr)), int(max_iters), int(chunk))
+    return (eng.index, eng.mode(), X.dtype, tuple(X.shape), tuple(Y.shape), float(np.float32(lr)), int(max_iters),
+            int(chunk))
 
 
 class AdamSession:
@@ -415,11 +463,7 @@ class AdamSession:
         self.max_iters = max(int(max_iters), 1)
         chunk = chunk if graph else 0
         self._key = _pool_key(self.eng, Xm, Ym, lr, self.max_iters, chunk)
-        core = None
-        if chunk:
-            with _pool_lock:
-                idle = _pool.get(self._key)
-                core = idle.pop() if idle else None
+        core = _pool_take(self._key) if chunk else None
         if core is None:
             core = _AdamCore(self.eng, Xm, Ym, self.tm, lr, self.max_iters)
         self._core = core
@@ -441,6 +485,10 @@ class AdamSession:
             raise MFGPError("AdamSession: the session is finished")
         if self.done + n > self.max_iters:
             raise ValueError("AdamSession: more iterations than max_iters")
+        if self.eng.mode() != self._key[1]:
+            # the session's graphs and workspace belong to the settings it started under; a step
+            # captured now would run another schedule on them
+            raise MFGPError("AdamSession: the engine's tile / flow / tiny settings changed during the session")
         with torch.cuda.stream(self.stream), self.eng.ordered(self.stream):
             self.runner.run(n)
         self.done += n
@@ -468,19 +516,21 @@ class AdamSession:
         self.close()
 
     def _retire(self):
-        """Hand the core (buffers + graphs) to the pool, or release the graphs now."""
+        """Hand the core (buffers + graphs) to the pool, or release the graphs now.  Either way
+        this finished session drops its aliases of the core's buffers: a pooled core is reloaded
+        and overwritten by the next session of its shape."""
         core, self._core = self._core, None
         if core is None:
             return
+        self.st = self.hist = self.out = self.info = self.ws = self.X = self.Y = None
         if self.runner.chunk and self.runner.graphs and core.ws_bytes <= _POOL_MAX_WS_BYTES:
-            with _pool_lock:
-                idle = _pool.setdefault(self._key, [])
-                if not idle:
-                    idle.append(core)
-                    # this finished session must never touch the pooled graphs again (a close()
-                    # from it could destroy them while their next user captures)
-                    self.runner = _StepRunner(self._step, 0)
-                    return
+            # this finished session must never touch the pooled graphs again (a close() from it
+            # could destroy them while their next user captures)
+            runner, self.runner = self.runner, _StepRunner(self._step, 0)
+            if _pool_put(self._key, core):
+                return
+            runner.close()
+            return
         self.close()
 
     def finish(self):

@@ -151,13 +151,19 @@ class _SVGPBase(Module):
         return e, g
 
     def _optimize(self, data, max_iters, initial_lr, unfix_noise_after, kl_multiplier, reset_history, graph,
-                  graph_chunk, verbose, every):
-        tr = _SVGPTrainer(self, data, max_iters, initial_lr, kl_multiplier, graph=graph, graph_chunk=graph_chunk)
+                  graph_chunk, verbose, every, start=0):
+        """Iterations start..max_iters-1 with a fresh Adam over CosineDecay(initial_lr, max_iters)
+        whose step counter starts at 0 (the reference builds both inside optimize)."""
+        n = max_iters - start
+        if n <= 0:
+            return None
+        tr = _SVGPTrainer(self, data, n, initial_lr, kl_multiplier, graph=graph, graph_chunk=graph_chunk,
+                          decay_steps=max_iters)
         noise_fixed = not self.likelihood.variance.trainable
         done = 0
-        while done < max_iters:
-            stop = max_iters
-            if noise_fixed and unfix_noise_after is not None and done <= unfix_noise_after < max_iters:
+        while done < n:
+            stop = n
+            if noise_fixed and unfix_noise_after is not None and done <= unfix_noise_after < n:
                 stop = unfix_noise_after + 1
             if verbose:
                 stop = min(stop, done + every)
@@ -167,7 +173,7 @@ class _SVGPBase(Module):
                 tr.set_trainable("noise", True)
                 noise_fixed = False
             if verbose:
-                print(f"Iteration {done - 1}: loss = {tr.loss_at(done - 1)}", flush=True)
+                print(f"Iteration {start + done - 1}: loss = {tr.loss_at(done - 1)}", flush=True)
         tr.finish(reset_history)
         return tr
 
@@ -213,7 +219,10 @@ class _SVGPTrainer:
     iteration = one gradient call + one mfgp_adam_packed call; iterations are replayed
     from hipGraphs on a dedicated stream."""
 
-    def __init__(self, model, data, max_iters, initial_lr, kl_multiplier=1.0, graph=True, graph_chunk=50):
+    def __init__(self, model, data, max_iters, initial_lr, kl_multiplier=1.0, graph=True, graph_chunk=50,
+                 decay_steps=None):
+        """max_iters: the iterations this trainer runs; decay_steps (default max_iters): the
+        CosineDecay length, whose schedule starts at step 0 for this trainer's first iteration."""
         self.model = model
         self.eng = eng = Engine.get()
         dev = eng.device
@@ -301,7 +310,8 @@ class _SVGPTrainer:
             self.transform = torch.tensor(np.concatenate(tfs), device=dev)
             self.span = torch.tensor(np.concatenate(sps), device=dev)
             self.step_t = torch.zeros((1,), dtype=torch.int32, device=dev)
-            self.lr = torch.tensor(cosine_decay_schedule(initial_lr, max_iters, self.max_iters), **f64)
+            decay = self.max_iters if decay_steps is None else int(decay_steps)
+            self.lr = torch.tensor(cosine_decay_schedule(initial_lr, decay, self.max_iters), **f64)
             self.loss_hist = torch.zeros((self.max_iters,), **f64)
             self.kl_hist = torch.zeros((self.max_iters,), **f64)
             self.out = torch.zeros((3,), **f64)
@@ -451,10 +461,14 @@ class LatentMFCoregionalizationSVGP(_SVGPBase):
     def optimize(self, data, max_iters=10000, initial_lr=0.005, unfix_noise_after=5000, kl_multiplier=1.0,
                  verbose=False, graph=True, graph_chunk=50):
         """linear_svgp.py:153-203: Adam + CosineDecay(initial_lr, max_iters) on
-        -ELBO + (kl_multiplier - 1) KL; loss_history / kl_history are appended.  (The
-        reference's noise-unfix branch compares loss_type with 'gausssian' and never
-        fires: the noise keeps the trainable flag it has.)"""
-        self._optimize(data, max_iters, initial_lr, None, kl_multiplier, False, graph, graph_chunk, verbose, 100)
+        -ELBO + (kl_multiplier - 1) KL; loss_history / kl_history are appended.  Like the
+        reference it RESUMES: the loop is `for i in range(len(self.loss_history), max_iters)`
+        (linear_svgp.py:194) with a fresh Adam and a fresh CosineDecay(initial_lr, max_iters) whose
+        step counter starts at 0 each call (:169), so a second optimize(max_iters=N) after N steps
+        runs none.  (The reference's noise-unfix branch compares loss_type with 'gausssian' and
+        never fires: the noise keeps the trainable flag it has.)"""
+        self._optimize(data, max_iters, initial_lr, None, kl_multiplier, False, graph, graph_chunk, verbose, 100,
+                       start=len(self.loss_history))
 
     def save_model(self, filename="latent_mf_svgp.pkl"):
         """linear_svgp.py:206-212 (parameter_dict pickled)."""

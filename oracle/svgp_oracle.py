@@ -228,3 +228,15 @@ class LatentTrainer(SingleBinTrainer):
         Z, kps, q_mu, q_sqrt, noise = self.constrained()
         e, kl, _ = elbo_t(self.X, self.Y, Z, kps, q_mu, q_sqrt, self.vars["W"], noise, num_data=self.X.shape[0])
         return -e + (self.klm - 1.0) * kl
+
+    def optimize(self, history, max_iters, lr):
+        """One LatentMFCoregionalizationSVGP.optimize call (linear_svgp.py:169,194): a FRESH Keras Adam
+        (zero moments, iteration counter 0) over CosineDecay(lr, max_iters), stepping
+        `for i in range(len(history), max_iters)`; appends the pre-step losses to `history`."""
+        self.sched = cosine_decay_f32(lr, max_iters)
+        self.m = {k: torch.zeros_like(v) for k, v in self.vars.items()}
+        self.v = {k: torch.zeros_like(v) for k, v in self.vars.items()}
+        self.t = 0
+        for _ in range(len(history), max_iters):
+            history.append(self.step())
+        return history

@@ -69,3 +69,45 @@ def test_host_only_entry_points(lib):
     assert lib.mfgp_set_f32_panel(h, 0) == -1 and lib.mfgp_set_f32_panel(h, 6) == 0
     assert lib.mfgp_set_f32_reserve(h, -1) == -1 and lib.mfgp_set_f32_reserve(h, 32) == 0
     assert lib.mfgp_destroy(h) == 0
+
+
+def test_flow_fence_nests_and_is_bounded(lib, monkeypatch):
+    """mfgp_flow_fence: a thread's nested WAIT / RECORD brackets release the fence only
+    at the outermost RECORD; another thread that finds it held waits at most the bound
+    (MFGP_FENCE_BOUND_MS here) and gets MFGP_ERR_FENCE (-5) instead of blocking for ever.  Host
+    logic only: with no GPU the event wait / record are no-ops."""
+    import threading
+    import time
+    monkeypatch.setenv("MFGP_FENCE_BOUND_MS", "150")
+    WAIT, RECORD = 0, 1
+    ha, hb = C.c_void_p(), C.c_void_p()
+    assert lib.mfgp_create(0, C.byref(ha)) == 0 and lib.mfgp_create(0, C.byref(hb)) == 0
+    out = {}
+
+    def other(key):
+        t0 = time.perf_counter()
+        rc = lib.mfgp_flow_fence(hb, WAIT)
+        if rc == 0:
+            lib.mfgp_flow_fence(hb, RECORD)
+        out[key] = (rc, time.perf_counter() - t0)
+
+    try:
+        assert lib.mfgp_flow_fence(ha, WAIT) == 0
+        assert lib.mfgp_flow_fence(ha, WAIT) == 0          # nested hold of the same thread
+        assert lib.mfgp_flow_fence(ha, RECORD) == 0        # inner RECORD: still held
+        th = threading.Thread(target=other, args=("held",))
+        th.start()
+        th.join(5.0)
+        assert out["held"][0] == -5 and 0.1 < out["held"][1] < 3.0
+        assert lib.mfgp_error_string(-5).decode().startswith("flow fence held")
+        assert lib.mfgp_flow_fence(ha, RECORD) == 0        # outermost RECORD releases
+        th = threading.Thread(target=other, args=("free",))
+        th.start()
+        th.join(5.0)
+        assert out["free"][0] == 0 and out["free"][1] < 0.1
+        assert lib.mfgp_flow_fence(ha, 7) == -1
+        assert lib.mfgp_get_tiny(ha) in (0, 1) and lib.mfgp_set_tiny(ha, 0) == 0 and lib.mfgp_get_tiny(ha) == 0
+        assert lib.mfgp_get_grad_chunk(ha) >= 1
+    finally:
+        lib.mfgp_destroy(ha)
+        lib.mfgp_destroy(hb)

@@ -9,9 +9,8 @@ for small / ragged tile counts and small wave counts (several tiles per wave, wh
 items inside a wave matters)."""
 import pytest
 
-FT_A, FT_R, FT_AL, FT_H, FT_S = 0, 1, 2, 3, 4
+FT_A, FT_R, FT_AL, FT_H = 0, 1, 2, 3
 MAXOWN = 4
-SD = [0]          # FLOW_STILES: levels left to k_grad (0: no S tiles; set per test)
 
 
 def tri(t):
@@ -25,13 +24,8 @@ def n_a(T):
     return T * (T + 1) // 2 - 9 if T >= 4 else 0
 
 
-def n_s(T):
-    m = T - SD[0]
-    return m * (m + 1) // 2 if SD[0] > 0 and m > 0 else 0
-
-
 def ntiles(T, Tp):
-    return n_a(T) + T * (T - 1) // 2 + 2 * T * Tp + (T - 1 if T > 1 else 0) + n_s(T)
+    return n_a(T) + T * (T - 1) // 2 + 2 * T * Tp + (T - 1 if T > 1 else 0)
 
 
 def decode(g, T, Tp):
@@ -50,13 +44,7 @@ def decode(g, T, Tp):
     if g < T * Tp:
         return (FT_AL, g // Tp, g % Tp)
     g -= T * Tp
-    nH = T - 1 if T > 1 else 0
-    if g < nH:
-        return (FT_H, g + 1, 0)
-    return (FT_S,) + tri(g - nH)
-
-
-BAND3 = [False]   # FLOW_BAND3 (set per test)
+    return (FT_H, g + 1, 0)
 
 
 def tile(code, T):
@@ -64,14 +52,12 @@ def tile(code, T):
     ty, i, j = code
     if ty == FT_A:
         if i <= j + 2:
-            return 0, (i - 3 if BAND3[0] and i >= 4 and i < j + 2 else i - 4), -1, True
+            return 0, i - 4, -1, True
         return 0, j - 1, j, False
     if ty == FT_R:
         return (j if j < T else 0), i - 2, i, False      # panel i-1 through H_i in the finalize
     if ty == FT_AL:
         return i, T - 1, -1, False
-    if ty == FT_S:                                    # K^{-1} partial S(i,j), levels i .. T-1-sd
-        return i, T - 1 - SD[0], -1, False
     return 0, -1, (i if i < T - 1 else -1), False       # FT_H: H_k = D_k L(k,k-1) at level k
     #                                                     (H_{T-1}: the diag workgroup's publisher)
 
@@ -86,7 +72,7 @@ def owner_table(T, Tp, W):
     here; on the device the order inside one item count is arbitrary, which the simulation below
     covers by also trying the reversed order)."""
     codes = [decode(g, T, Tp) for g in range(ntiles(T, Tp))]
-    codes.sort(key=lambda c: -(items(c, T) + (0 if c[0] == FT_S else 128)))   # S tiles after all others
+    codes.sort(key=lambda c: -items(c, T))
     own = [[None] * MAXOWN for _ in range(W)]
     for p, c in enumerate(codes):
         r, q = divmod(p, W)
@@ -150,10 +136,6 @@ def needs_and_makes(item, T):
             make.append(("H", i, j))
     elif ty == FT_R:
         need += [("L", i, l), ("X", l, j)]
-    elif ty == FT_S:
-        need += [("X", l, i), ("X", l, j)]
-        if l == hi:
-            make.append(("S", i, j))                  # read by k_grad after the launch
     else:
         need += [("X", l, i), ("X", l, T + j)]
     return need, make
@@ -227,19 +209,10 @@ def test_every_tile_owned_once(T, Tp):
 @pytest.mark.parametrize("T,Tp,W", [(1, 2, 8), (2, 1, 8), (3, 2, 5), (4, 2, 16), (6, 1, 9), (12, 2, 40),
                                     (37, 2, 2040), (37, 2, 400), (20, 3, 120), (12, 2, 240), (30, 2, 1400)])
 @pytest.mark.parametrize("reverse", [False, True])
-@pytest.mark.parametrize("band3,sd", [(False, 0), (True, 0), (True, 2), (False, 1)])
-def test_schedule_runs_to_completion(T, Tp, W, reverse, band3, sd):
-    BAND3[0], SD[0] = band3, (sd if sd < T else 0)
-    try:
-        if ntiles(T, Tp) > W * MAXOWN:
-            pytest.skip("owner table too small: the host uses the step schedule")
-        dk, stuck, done = simulate(T, Tp, W, reverse)
-        if SD[0]:   # every S tile's partial sum is complete when the launch ends
-            for i in range(T - SD[0]):
-                for j in range(i + 1):
-                    assert ("S", i, j) in done, (i, j)
-    finally:
-        BAND3[0], SD[0] = False, 0
+def test_schedule_runs_to_completion(T, Tp, W, reverse):
+    if ntiles(T, Tp) > W * MAXOWN:
+        pytest.skip("owner table too small: the host uses the step schedule")
+    dk, stuck, done = simulate(T, Tp, W, reverse)
     assert dk == T and not stuck, (dk, stuck[:3])
     # alpha and Z of every row are complete
     for i in range(T):

@@ -291,9 +291,9 @@ def test_session_pool_reuses_graphs_exactly(hbs, eng):
     ref.optimize(max_iters=100, learning_rate=0.1, verbose=False, graph=False)
     m1 = _model(hbs)
     m1.optimize(max_iters=100, learning_rate=0.1, verbose=False)
-    key = [k for k, v in MM._pool.items() if v and k[2] == tuple(hbs["X"].shape) and k[5] == 100 and k[6] == 50]
+    key = [k for k in MM._pool if k[3] == tuple(hbs["X"].shape) and k[6] == 100 and k[7] == 50]
     assert key, "the finished session was not pooled"
-    core = MM._pool[key[0]][0]
+    core = MM._pool[key[0]]
     g_before = dict(core.graphs)
     m2 = _model(hbs)
     m2.kernel.kernel_L.variance.assign(1.3)     # a different initial state through the same graphs
@@ -307,3 +307,44 @@ def test_session_pool_reuses_graphs_exactly(hbs, eng):
     np.testing.assert_array_equal(np.array(m1.loss_history), np.array(ref.loss_history))
     np.testing.assert_array_equal(np.array(m2.loss_history), np.array(ref2.loss_history))
     np.testing.assert_array_equal(m2.kernel.rho.numpy(), ref2.kernel.rho.numpy())
+
+
+def test_session_pool_keys_on_handle_mode(hbs, eng):
+    """a pooled session's graphs were captured under the handle's settings (tile, flow,
+    one-launch path, k_grad chunk); changing any of them empties the pool, so the next session of
+    the same shape captures afresh under the new schedule.  A finished session drops its aliases
+    of the pooled buffers; the pool is capped (LRU) by entries and bytes."""
+    from multi_fidelity_gpflow_amd import models as MM
+    MM.clear_session_pool()
+    m1 = _model(hbs)
+    s1 = m1.adam_session(0.1, 60)
+    s1.run(60)
+    s1.finish()
+    assert s1.st is None and s1.hist is None and s1.out is None and s1.X is None
+    assert len(MM._pool) == 1
+    mode0 = eng.mode()
+    eng.set_tiny(not bool(mode0[2]))
+    try:
+        assert len(MM._pool) == 0 and eng.mode() != mode0
+        m2 = _model(hbs)
+        s2 = m2.adam_session(0.1, 60)
+        assert s2._key[1] == eng.mode()
+        s2.run(60)
+        s2.finish()
+    finally:
+        eng.set_tiny(bool(mode0[2]))
+    assert len(MM._pool) == 0
+    np.testing.assert_allclose(m2.loss_history, m1.loss_history, rtol=1e-10)
+    # LRU cap by entry count
+    old = MM._POOL_MAX_ENTRIES
+    MM._POOL_MAX_ENTRIES = 2
+    try:
+        for it in (40, 41, 42):
+            m = _model(hbs)
+            s = m.adam_session(0.1, it)
+            s.run(it)
+            s.finish()
+        assert [k[6] for k in MM._pool] == [41, 42]
+    finally:
+        MM._POOL_MAX_ENTRIES = old
+        MM.clear_session_pool()

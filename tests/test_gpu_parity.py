@@ -320,8 +320,10 @@ def test_lbfgs_forrester_kat(kats, eng, flow):
     stops at rho 1.999768564 with the persistent-flow Cholesky (6.6e-7 from the recorded value;
     5.6e-5 before round 3) and 2.7e-5 off with the launch-per-step Cholesky (the default below 8
     tiles): the line search's end points move with rounding-level differences of the objective,
-    and the fp64 oracle's own driver stops 3.7e-5 off.  Checked at 5e-5 on both schedules, the
-    noise floor, and the GPU objective along the first L-BFGS evaluations against the oracle."""
+    and the fp64 oracle's own driver stops 3.7e-5 off.  Bounds per schedule, at what each meets:
+    the one-launch kernel (the default at this size; 5.0e-8) 1e-6, the flow (6.6e-7) 5e-6, the
+    step launches (2.7e-5) 5e-5; the noise floor, and the GPU objective along the first L-BFGS
+    evaluations against the oracle."""
     from conftest import forrester_demo_data
     X, Y = forrester_demo_data()
     tiny = flow == "tiny"
@@ -337,7 +339,8 @@ def test_lbfgs_forrester_kat(kats, eng, flow):
     print(f"L-BFGS Forrester ({'tiny' if tiny else ('flow' if flow else 'steps')}) rho {rho:.9f} vs recorded {kats['forrester_lbfgs']['rho']} "
           f"(rel {abs(rho - kats['forrester_lbfgs']['rho']) / kats['forrester_lbfgs']['rho']:.1e}), "
           f"noise {float(m.likelihood.variance.numpy()):.9e}")
-    assert abs(rho - kats["forrester_lbfgs"]["rho"]) < 5e-5 * kats["forrester_lbfgs"]["rho"]
+    bound = 1e-6 if tiny else (5e-6 if flow else 5e-5)
+    assert abs(rho - kats["forrester_lbfgs"]["rho"]) < bound * kats["forrester_lbfgs"]["rho"]
     assert float(m.likelihood.variance.numpy()) == pytest.approx(kats["forrester_lbfgs"]["noise"], rel=1e-6)
     _, trace = O.lbfgs_train(X, Y, O.MFParams.initial(1, 1), max_iters=1000, return_trace=True)
     np.testing.assert_allclose(m.loss_history[:8], trace[:8], rtol=1e-9)
@@ -402,17 +405,14 @@ def test_tiny_predict_matches_step_sequence(n_lf, n_hf, p, D, ns, eng):
 def test_tiny_adam_matches_step_sequence(hbs, eng):
     """The HBS Adam step (mfgp_gpr_adam_step, graph-captured) through k_gpr_tiny and through the
     step sequence: 200 steps, the same loss history to rounding (the dynamics are smooth there)."""
-    from multi_fidelity_gpflow_amd import models as MM
     hs = []
     for tiny in (True, False):
-        eng.set_tiny(tiny)
-        MM._pool_clear()   # a pooled session would replay the other schedule's captured graphs
+        eng.set_tiny(tiny)   # empties the session pool: no graph captured under the other schedule is replayed
         m = M.MultiFidelityGPModel(hbs["X"], hbs["Y"], M.SquaredExponential(lengthscales=np.ones(5)),
                                    M.SquaredExponential(lengthscales=np.ones(5)))
         m.optimize(max_iters=200, learning_rate=0.1, verbose=False)
         hs.append(np.array(m.loss_history))
     eng.set_tiny(True)   # the library default
-    MM._pool_clear()
     err = np.abs(hs[0] - hs[1]) / np.abs(hs[1])
     print(f"tiny vs steps, 200 HBS Adam steps: max rel {err.max():.1e}")
     assert err.max() < 1e-10

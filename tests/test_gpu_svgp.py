@@ -316,6 +316,30 @@ def test_latent_training_matches_oracle(hbs):
     np.testing.assert_allclose(hist, oh, rtol=1e-6)
 
 
+def test_latent_optimize_resumes_from_history(hbs):
+    """LatentMFCoregionalizationSVGP.optimize resumes (linear_svgp.py:169,194): optimize(max_iters=20)
+    then optimize(max_iters=30) runs 10 more iterations under a FRESH Adam and a fresh
+    CosineDecay(lr, 30) whose counter starts at 0, and a third optimize(max_iters=30) runs none.
+    Checked against the torch oracle's loop with the same resume rule (1e-6 relative)."""
+    X, Y = hbs["X"], hbs["Y"]
+    D, P = X.shape[1] - 1, Y.shape[1]
+    kw = dict(num_latents=3, num_inducing=16, num_outputs=P, w_type='diagonal')
+    m = M.LatentMFCoregionalizationSVGP(X, Y, M.SquaredExponential(lengthscales=np.ones(D)),
+                                        M.SquaredExponential(lengthscales=np.ones(D)), **kw)
+    m.optimize((X, Y), max_iters=20, initial_lr=0.05)
+    assert len(m.loss_history) == 20 and len(m.kl_history) == 20
+    m.optimize((X, Y), max_iters=30, initial_lr=0.05)
+    assert len(m.loss_history) == 30 and len(m.kl_history) == 30
+    q_before = m.q_mu.numpy().copy()
+    m.optimize((X, Y), max_iters=30, initial_lr=0.05)   # nothing left to run
+    assert len(m.loss_history) == 30
+    np.testing.assert_array_equal(m.q_mu.numpy(), q_before)
+    ref = S.LatentTrainer(X, Y, kw, lr=0.05, max_iters=20)
+    oh = ref.optimize([], 20, 0.05)
+    oh = ref.optimize(oh, 30, 0.05)
+    np.testing.assert_allclose(np.array(m.loss_history), oh, rtol=1e-6)
+
+
 @pytest.mark.parametrize("which", ["singlebin", "latent"])
 def test_predict_f_covariance_forms(hbs, which):
     """SVGP.predict_f(full_cov / full_output_cov) (GPflow base_conditional_with_lm full_cov branch +
