@@ -73,6 +73,15 @@ int mfgp_set_flow(mfgp_handle_t h, int enable);   /* 2: flow + diagnostic timeli
  * environment: the step sequence).  Same results to rounding. */
 int mfgp_set_tiny(mfgp_handle_t h, int enable);
 int mfgp_get_tiny(mfgp_handle_t h);
+/* Resident workspace (default 0).  On the fp64 flow path (the AR1 kernel, 32-tiles, the persistent
+ * Cholesky) the Gram is formed inside the flow launch; the launch in front of it only sets up the
+ * workspace (the publication area's sentinel fill, schedule tables, reduction slots), and every
+ * value+grad call (mfgp_gpr_lml with want_grad, mfgp_gpr_adam_step) leaves exactly that set-up
+ * behind.  With resident = 1 a value+grad call whose workspace the previous fp64 LML call ON THIS
+ * HANDLE left set up for the same (n, p, d) skips the set-up launch and starts with the flow.  The
+ * caller guarantees that nothing else wrote the workspace in between (a training session's private
+ * workspace); graphs captured in this mode replay that way.  Results are identical either way. */
+int mfgp_set_resident(mfgp_handle_t h, int enable);
 /* k_grad m-tiles per task (fixed at mfgp_create; env MFGP_GRAD_CHUNK).  Workspace sizes depend on it. */
 int mfgp_get_grad_chunk(mfgp_handle_t h);
 /* fp32 path (dtype MFGP_F32): iterative refinement with an fp64 residual for the value-only LML

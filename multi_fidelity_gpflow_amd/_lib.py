@@ -31,6 +31,7 @@ SIGNATURES = {
     "mfgp_set_flow": [_p, _i],
     "mfgp_set_tiny": [_p, _i],
     "mfgp_get_tiny": [_p],
+    "mfgp_set_resident": [_p, _i],
     "mfgp_get_grad_chunk": [_p],
     "mfgp_set_f32_refine": [_p, _i],
     "mfgp_get_flow": [_p],

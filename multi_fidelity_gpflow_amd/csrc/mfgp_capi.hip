@@ -36,6 +36,11 @@ struct mfgp_handle_s {
     int tiny;                   // small problems (n, p <= 64, D <= 16, AR1 kernel): one-launch LML step (default on; MFGP_TINY=0 / mfgp_set_tiny(h, 0) disables)
     hipStream_t side;           // its high-priority side stream + fork / join events (created with the handle)
     hipEvent_t ev_fork, ev_join;
+    int resident;               // mfgp_set_resident: fp64 value+grad flow calls may skip the set-up launch
+    struct {                    // the last fp64 LML call on this handle, when it left its workspace set
+        const void* ws;         // up for the next one (k_grad's grad_next_setup); ws == nullptr: none
+        int n, p, d, flow_wgs;
+    } res;
 };
 
 namespace mfgp {
@@ -278,7 +283,17 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
     // host thread fails the call with nothing enqueued
     int fence_rc = L.flow_wgs ? fence_wait(h->device, s) : MFGP_OK;
     if (fence_rc != MFGP_OK) return fence_rc;
-    {
+    // The AR1 flow path (NB = 32, nlf = 0): the Gram is formed inside k_chol_flow, so the launch
+    // in front of it only sets up the workspace (sentinel fill, schedule tables, item slots) --
+    // and a value+grad call leaves exactly that set-up behind (k_grad's tail).  In resident mode
+    // a value+grad call whose workspace the previous fp64 LML call on this handle left set up for
+    // the same problem starts with the flow itself.
+    const bool flow_gram = NB == 32 && L.flow_wgs && !nlf;
+    const bool leaves_setup = flow_gram && want_grad;
+    const bool skip_prep = leaves_setup && h->resident && h->res.ws == ws && h->res.n == n && h->res.p == p &&
+                           h->res.d == d && h->res.flow_wgs == L.flow_wgs;
+    h->res.ws = nullptr;
+    if (!skip_prep) {
         GramArgs g{};
         g.R = L.R; g.ldr = ldr; g.sR = 0; g.Y = Y; g.ldy = ldy; g.sY = 0; g.p = p; g.ppad = L.ppad;
         g.X1 = X; g.ldx1 = ldx; g.sx1 = 0; g.n1 = n;
@@ -292,11 +307,11 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
         const bool order = want_grad && L.gchunk + L.T + L.Tp < 2048;   // gram LDS holds the histogram
         if (order) { g.gorder = L.gorder; g.gT = L.T; g.gchunk = L.gchunk; g.gTp = L.Tp; }
         if (L.flow_wgs) { g.fown = L.own; g.fW = FLOW_WAVES * (L.flow_wgs - 1); g.fflags = L.flags; g.nfflags = L.nflags; g.fpub = L.pub; g.npub = L.npub; }
-        if (L.flow_wgs && h->flow_trace) g.dbg = L.trace + L.ntrace - flow_gram_dbg_count(L.T);   // k_gram timeline (diagnostic)
         const int extra = (order ? 1 : 0) + (L.flow_wgs ? 1 : 0);
-        if (NB == 32 && L.flow_wgs && !nlf) {
-            launch_gram_flow(g, extra, s);
+        if (flow_gram) {
+            launch_flow_prep(g, std::max(h->ncu, 2) + extra, s);
         } else {
+            if (L.flow_wgs) g.Dd = nullptr;   // the flow factors D_0 itself
             g.tile_wgs = gram_tile_wgs(h, L.T, extra);
             launch_gram<NB>(g, (g.tile_wgs ? g.tile_wgs : L.T * (L.T + 1) / 2) + extra, 1, s);
         }
@@ -314,7 +329,8 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
         fa.trace = h->flow_trace ? L.trace : nullptr;
         fa.nwaves = FLOW_WAVES * (L.flow_wgs - 1);
         fa.timeout = h->flow_timeout;
-        fa.d0 = 0;
+        fa.X = X; fa.ldxi = ldx; fa.Y = Y; fa.ldy = ldy; fa.theta = theta; fa.D = d;
+        fa.gram = flow_gram ? 1 : 0;
         launch_chol_flow(fa, L.flow_wgs, s);
         fence_rc = fence_record(h->device, s);
     } else {
@@ -331,6 +347,10 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
     if (want_grad) {
         GradArgs ga{L.Xo, ldr, X, (long)ldx, theta, L.gpart, L.gstride, L.T, L.Tp, n, p, d,
                     L.gchunk, nlf, L.gchunk + L.T + L.Tp < 2048 ? L.gorder : nullptr};
+        if (leaves_setup) {   // the next evaluation's set-up, after the flow
+            ga.fpub = L.pub; ga.npub = L.npub;
+            ga.isent = L.items; ga.nisent = L.G + 2;
+        }
         launch_grad<NB>(ga, s);
     }
     if (pm) pm->mark(s);
@@ -345,11 +365,16 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
     f.items = L.items;
     f.G = L.G;
     f.cnt = L.cnt;
-    f.flag = MFGP_REDUCE_FLAG;   // the Gram launch above filled items[] with the sentinel
+    f.flag = MFGP_REDUCE_FLAG;   // the Gram / set-up launch (or the previous k_grad) filled items[] with the sentinel
+    f.abortw = L.flow_wgs ? L.flags : nullptr;
     hipLaunchKernelGGL(k_reduce_items, dim3(2 + (want_grad ? L.G : 0)), dim3(NTHREADS), 0, s, f);
     if (pm) pm->mark(s);
     if (fence_rc != MFGP_OK) return fence_rc;
-    return last() == hipSuccess ? MFGP_OK : MFGP_ERR_LAUNCH;
+    if (last() != hipSuccess) return MFGP_ERR_LAUNCH;
+    if (leaves_setup) {
+        h->res.ws = ws; h->res.n = n; h->res.p = p; h->res.d = d; h->res.flow_wgs = L.flow_wgs;
+    }
+    return MFGP_OK;
 }
 
 // ---------------------------------------------------------------- potrf_inv
@@ -798,6 +823,12 @@ int mfgp_set_tiny(mfgp_handle_t h, int enable) {
 }
 
 int mfgp_get_tiny(mfgp_handle_t h) { return h ? h->tiny : MFGP_ERR_ARG; }
+
+int mfgp_set_resident(mfgp_handle_t h, int enable) {
+    if (!h) return MFGP_ERR_ARG;
+    h->resident = enable != 0;
+    return MFGP_OK;
+}
 
 int mfgp_get_grad_chunk(mfgp_handle_t h) { return h ? h->grad_chunk : MFGP_ERR_ARG; }
 

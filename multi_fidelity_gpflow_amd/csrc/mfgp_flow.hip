@@ -224,6 +224,147 @@ __device__ __forceinline__ double wave_sum64(double v) {
     return v;
 }
 
+// ---------------------------------------------------------------- the Gram inside the launch
+// Tile (ti, tj) of the padded K + s2 I of the LML (mfgpflow/linear.py:55-104 via GPflow's
+// SquaredExponential.K: k = v exp(-r^2 / 2), expanded r^2 = -2 a.b + |a|^2 + |b|^2 on a = x / l,
+// no clamp; K = (s s^T) o K_L + (h h^T) o K_delta with rho[0]; exact fidelity masks; the noise on
+// the diagonal; identity on the padded diagonal, zero elsewhere in the padding), formed by ONE wave
+// and stored to dst (row stride ld; global or LDS) in the accumulator layout (lane (li, lq): rows
+// 16 bi + lq + 4 r, columns 16 bj + li), so the same wave reads its own entries back.
+// The dot products a_i . a_j run on the matrix core (the v_mfma_f64_16x16x4 operand layout IS
+// (row 16 b + li, dimension 4 s + lq)), the norms as partial sums over the lane's dimensions
+// reduced across the four lq lanes; the HF x HF part (K_delta) only when the tile holds such a pair.
+// Replaces the Gram launch in front of the flow (k_gram_flow, ~14 us at Goku): an owner forms its
+// tile before its first item, while the chain factors D_0.
+// One 16-row half of the tile at a time, dimensions in chunks of 16 (four MFMA k-steps of 4):
+// every global load of a chunk (with the fidelity flags and theta) is issued before the first is
+// used -- one memory round trip per half and chunk (a dependent load per k-step cost ~5 us a
+// tile), in ~120 VGPRs (the kernel's allocation stays at its roles' 183, so small kernels of
+// other streams still fit beside the flow's waves on a CU).
+__device__ __forceinline__ void flow_gram_tile(const double* __restrict__ X, long ldx, const double* __restrict__ th,
+                                               int n, int D, int ti, int tj, double* dst, long ld) {
+    constexpr int FS = 4;
+    const int l = threadIdx.x & 63, li = l & 15, lq = l >> 4;
+    int rj[2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) rj[b] = 32 * tj + 16 * b + li;
+#pragma unroll 1
+    for (int bi = 0; bi < 2; ++bi) {
+        const int ri = 32 * ti + 16 * bi + li;
+        double fi = X[(long)min(ri, n - 1) * ldx + D];
+        double fj[2];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) fj[b] = X[(long)min(rj[b], n - 1) * ldx + D];
+        const double vL = th[0], vD = th[1 + D], rho = th[2 + 2 * D], noise = th[3 + 2 * D];
+        f64x4 dl[2], dd[2];
+        double ni = 0.0, nid = 0.0, nj[2] = {0.0, 0.0}, njd[2] = {0.0, 0.0};
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            dl[q] = f64x4{0.0, 0.0, 0.0, 0.0};
+            dd[q] = f64x4{0.0, 0.0, 0.0, 0.0};
+        }
+        bool hh = false;
+        for (int c0 = 0; c0 < D; c0 += 4 * FS) {
+            double xi[FS], xj[2][FS], lL[FS], lD[FS];
+#pragma unroll
+            for (int k = 0; k < FS; ++k) {   // loads only (clamped in-range addresses)
+                const int d = min(c0 + 4 * k + lq, D - 1);
+                lL[k] = th[1 + d];
+                lD[k] = th[2 + D + d];
+                xi[k] = X[(long)min(ri, n - 1) * ldx + d];
+#pragma unroll
+                for (int b = 0; b < 2; ++b) xj[b][k] = X[(long)min(rj[b], n - 1) * ldx + d];
+            }
+            if (c0 == 0) {   // the flags arrived with the first chunk
+                if (ri >= n) fi = -1.0;
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+                    if (rj[b] >= n) fj[b] = -1.0;
+                hh = __ballot(fj[0] == 1.0 || fj[1] == 1.0) != 0 && __ballot(fi == 1.0) != 0;   // HF x HF pairs
+            }
+#pragma unroll
+            for (int k = 0; k < FS; ++k) {
+                const int d = c0 + 4 * k;
+                if (d >= D) break;
+                const bool dv = d + lq < D;
+                const double il = dv ? rcp_nr(lL[k]) : 0.0, ild = dv ? rcp_nr(lD[k]) : 0.0;   // a = x rcp_nr(l)
+                const double x1 = (dv && ri < n) ? xi[k] : 0.0;
+                const double ai = x1 * il, aid = x1 * ild;
+                ni = fma(ai, ai, ni);
+                nid = fma(aid, aid, nid);
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const double x2 = (dv && rj[q] < n) ? xj[q][k] : 0.0;
+                    const double aj = x2 * il, ajd = x2 * ild;
+                    nj[q] = fma(aj, aj, nj[q]);
+                    njd[q] = fma(ajd, ajd, njd[q]);
+                    dl[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai, aj, dl[q], 0, 0, 0);
+                    if (hh) dd[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(aid, ajd, dd[q], 0, 0, 0);
+                }
+            }
+        }
+        // full norms of rows 16 b + li (the four lq lanes' partial sums)
+        ni += __shfl_xor(ni, 16, 64); ni += __shfl_xor(ni, 32, 64);
+        nid += __shfl_xor(nid, 16, 64); nid += __shfl_xor(nid, 32, 64);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            nj[q] += __shfl_xor(nj[q], 16, 64); nj[q] += __shfl_xor(nj[q], 32, 64);
+            njd[q] += __shfl_xor(njd[q], 16, 64); njd[q] += __shfl_xor(njd[q], 32, 64);
+        }
+        double nr[4], nrd[4], fr[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {   // row 16 bi + lq + 4 r: held by lane lq + 4 r
+            nr[r] = __shfl(ni, lq + 4 * r, 64);
+            nrd[r] = __shfl(nid, lq + 4 * r, 64);
+            fr[r] = __shfl(fi, lq + 4 * r, 64);
+        }
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj) {
+            const bool L2 = fj[bj] == 0.0, H2 = fj[bj] == 1.0;
+            double kl[4], kd[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                kl[r] = -0.5 * (-2.0 * dl[bj][r] + (nr[r] + nj[bj]));
+                kd[r] = -0.5 * (-2.0 * dd[bj][r] + (nrd[r] + njd[bj]));
+            }
+            exp4(kl);
+            if (hh) exp4(kd);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = 16 * bi + lq + 4 * r;
+                const int gi = 32 * ti + row, gj = rj[bj];
+                double v;
+                if (gi < n && gj < n) {
+                    const double k1 = vL * kl[r];
+                    const bool L1 = fr[r] == 0.0, H1 = fr[r] == 1.0;
+                    const double kD = (H1 && H2) ? vD * kd[r] : 0.0;
+                    v = (L1 && L2) ? k1 : (!(H1 && H2) ? k1 * rho : k1 * (rho * rho) + kD);
+                    if (!(L1 || H1) || !(L2 || H2)) v = 0.0;   // linear.py:67-70 exact masks
+                    if (gi == gj) v = v + noise;
+                } else {
+                    v = (gi == gj) ? 1.0 : 0.0;                // identity padding
+                }
+                dst[(long)row * ld + 16 * bj + li] = v;   // the accumulator layout of wt_store_u
+            }
+        }
+    }
+}
+
+// Y column tile cy of R's row block i (rows >= n, columns >= p zero), accumulator layout: the
+// initial value of an R tile of the Z columns (the flow reads Y itself; no copy into R)
+__device__ __forceinline__ void flow_y_tile(const FlowArgs& a, int i, int cy, WTile& t) {
+    const int li = threadIdx.x & 15, lq = (threadIdx.x >> 4) & 3;
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = 32 * i + 16 * bi + lq + 4 * r, col = 32 * cy + 16 * bj + li;
+                t.v[bi][bj][r] = (row < a.n && col < a.p) ? a.Y[(long)row * a.ldy + col] : 0.0;
+            }
+}
+
 
 // ---------------------------------------------------------------- publication area
 // Tiles (32 x 32 row-major) in one sentinel-filled region: L(i,j) i > j | D_k | X^T(i,c)
@@ -473,6 +614,7 @@ __device__ __forceinline__ void flow_finalize_r(FlowCtx& C, const FlowTile& t, d
         // (j+1, j) of it has no update before its finalize, so R'' is its initial value, zero.
         WTile acc;
         if (t.j < T && i == t.j + 1) wt_zero(acc);
+        else if (t.j >= T && t.hi < t.lo) flow_y_tile(a, i, t.j - T, acc);   // no update: R'' = Y
         else wt_load<false>(acc, C.Rt(i, t.j), a.ldr);
         op_load_pub(d, Pd);
         if (cpl) {
@@ -544,8 +686,9 @@ __device__ __forceinline__ void flow_update(FlowCtx& C, const FlowTile& t, int l
         }
     } else if (t.type == FT_R) {
         double* dst = C.Rt(t.i, t.j);
-        // identity block: the first update (level j) starts from the initial value, zero (i > j + 1)
+        // first update: from the initial value -- zero (identity block, i > j + 1) or Y (Z columns)
         if (t.j < T && l == t.j) wt_zero(acc);
+        else if (t.j >= T && l == t.lo) flow_y_tile(a, t.i, t.j - T, acc);
         else wt_load<false>(acc, dst, a.ldr);
         pub_op2(x, C.P.L(t.i, l), y, C.P.X(l, t.j), C);  // L(i,l), X(l,c)^T (B[k][j] = X(l,c)[k][j])
         wt_mma<true>(acc, x, y);                         // R(i,c) -= L(i,l) X(l,c)
@@ -745,7 +888,8 @@ __device__ __forceinline__ void diag_chain(FlowCtx& C, const DiagLds& B) {
     const int T = a.T;
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     int epoch = 0;
-    if (a.d0 && w == 0) {   // D_0 from k_gram's A(0,0)
+    if (w == 0) {   // D_0: wave 0 forms tile (0,0) of K + s2 I and factors it
+        // tile (0,0): flow_gram_phase's (this wave wrote it), or the graph kernel's k_gram
         for (int e = l; e < 32 * 32; e += 64) B.fsc()[(e >> 5) * 33 + (e & 31)] = a.A[(long)(e >> 5) * a.lda + (e & 31)];
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         tile_potrf_inv_w1_wave(B.fsc(), 33, B.fsc(), B.Db(0), B.dg(0), &B.bad()[0]);
@@ -797,7 +941,7 @@ __device__ __forceinline__ void diag_publisher(FlowCtx& C, const DiagLds& B) {
     const int l = threadIdx.x & 63;
     for (int k = 0; k < T; ++k) {
         const int pk = k & 1;
-        if (k == 0 && a.d0) lds_wait_ge(&B.w()[DW_D], 0);
+        if (k == 0) lds_wait_ge(&B.w()[DW_D], 0);
         if (k > 0) {
             lds_wait_ge(&B.w()[DW_LS], k);
             double* dst = C.P.L(k, k - 1);
@@ -829,7 +973,7 @@ __device__ __forceinline__ void diag_publisher(FlowCtx& C, const DiagLds& B) {
             st_coherent(xt + c * 32 + r, v);             // X^T(k,k) = D_k^T
             xo[(long)r * a.ldx + c] = v;
         }
-        if (k > 0 || a.d0) {
+        {
             if (l < 32) a.ldiag[k * 32 + l] = B.dg(pk)[l];
             if (l == 0 && B.bad()[pk] && a.info[0] == 0) a.info[0] = k * 32 + B.bad()[pk];
         }
@@ -861,7 +1005,9 @@ __device__ __forceinline__ void diag_second(FlowCtx& C, const DiagLds& B) {
         if (j >= 4) {
             pub_wt_op_direct(acc, C.P.H(2, j), x, C.P.L(j, j - 3), C);
         } else {
-            wt_load<true>(acc, C.At(j, j - 2), a.lda);  // A(2,0), A(3,1): k_gram's values
+            // A(2,0), A(3,1): their initial values (flow_gram_phase: this wave wrote them)
+            if (a.gram) wt_load<false>(acc, C.At(j, j - 2), a.lda);
+            else wt_load<true>(acc, C.At(j, j - 2), a.lda);
             if (j == 3) pub_op(x, C.P.L(j, j - 3), C);
         }
         if (a.trace && (threadIdx.x & 63) == 0) a.trace[4 * T + j] = flow_clock() - C.t0;
@@ -906,7 +1052,9 @@ __device__ __forceinline__ void diag_prefetch(FlowCtx& C, const DiagLds& B, bool
         if (j >= 4) {
             pub_wt_op_direct(acc, C.P.H(sub ? 0 : 1, j), x, C.P.L(j, j - 3), C);
         } else {
-            wt_load<true>(acc, sub ? C.At(j, j - 1) : C.At(j, j), a.lda);   // k_gram's values
+            double* a0 = sub ? C.At(j, j - 1) : C.At(j, j);   // initial values of the rows <= 3
+            if (a.gram) wt_load<false>(acc, a0, a.lda);       // (flow_gram_phase: this wave wrote them)
+            else wt_load<true>(acc, a0, a.lda);
             if (j == 3) pub_op(x, C.P.L(j, j - 3), C);
         }
         if (a.trace && (threadIdx.x & 63) == 0) a.trace[(sub ? 5 : 6) * T + j] = flow_clock() - C.t0;
@@ -943,9 +1091,9 @@ __device__ __forceinline__ void flow_diag(FlowCtx& C, double* smem) {
     DiagLds B;
     B.base = smem;
     if (threadIdx.x < DW_N)
-        B.w()[threadIdx.x] = (threadIdx.x == DW_LPUB || threadIdx.x == DW_DPUB || (threadIdx.x == DW_D && C.a.d0)) ? -1 : 0;
+        B.w()[threadIdx.x] = (threadIdx.x == DW_LPUB || threadIdx.x == DW_DPUB || threadIdx.x == DW_D) ? -1 : 0;
     if (threadIdx.x < 2) B.bad()[threadIdx.x] = 0;
-    if (!C.a.d0) tile_load<32>(B.Db(0), C.a.Dd, 32);   // D_0: k_gram's fused factor (previous launch)
+    if (threadIdx.x == 0) C.a.info[0] = 0;   // first writer of info in the evaluation
     __syncthreads();
     const int w = threadIdx.x >> 6;
     if (w < 4) diag_chain(C, B);
@@ -954,8 +1102,39 @@ __device__ __forceinline__ void flow_diag(FlowCtx& C, double* smem) {
     else diag_prefetch(C, B, w == 6);
 }
 
+// The Gram phase (FlowArgs::gram), run by every wave before its role, where no role state is live
+// (the tile code inlined into the roles set the kernel's allocation to 254 VGPRs, so no other
+// kernel's wave fit beside the flow on a CU; as a call, 248): each worker wave forms its owned A
+// tiles, and in the diag workgroup wave 0 tile (0,0), wave 5 (2,0) and (3,1), wave 6 (1,0), (2,1),
+// (3,2), wave 7 (1,1), (2,2), (3,3) -- the band tiles of the rows <= 3 its role starts from.  Each
+// wave reads back only what it wrote itself (the stores drained first).
+__device__ __forceinline__ void flow_gram_phase(const FlowArgs& a) {
+    const int w = threadIdx.x >> 6;
+    auto tile = [&](int i, int j) {
+        if (i < a.T) flow_gram_tile(a.X, a.ldxi, a.theta, a.n, a.D, i, j, a.A + (long)i * 32 * a.lda + (long)j * 32, a.lda);
+    };
+    if (blockIdx.x == 0) {
+        if (w == 0) tile(0, 0);
+        else if (w == 5) { tile(2, 0); tile(3, 1); }
+        else if (w == 6) { tile(1, 0); tile(2, 1); tile(3, 2); }
+        else if (w == 7) { tile(1, 1); tile(2, 2); tile(3, 3); }
+    } else {
+        const int* own = a.own + ((blockIdx.x - 1) * FLOW_WAVES + w) * FLOW_MAXOWN;
+#pragma unroll 1
+        for (int s = 0; s < FLOW_MAXOWN; ++s) {
+            const int code = __builtin_amdgcn_readfirstlane(own[s]);
+            if (code < 0) continue;
+            const FlowTile t = flow_tile(code, a.T);
+            if (t.type == FT_A) tile(t.i, t.j);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+}
+
 __global__ __launch_bounds__(FLOW_THREADS) void k_chol_flow(FlowArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
+    if (a.gram) flow_gram_phase(a);
     FlowCtx C;
     C.a = a;
     C.P.base = a.pub;

@@ -61,7 +61,15 @@ struct FlowArgs {
     long long* trace;             // diagnostic timeline (nullptr: off), flow_trace_count entries
     int nwaves;                   // worker waves (trace layout)
     long long timeout;            // bound of every hand-off wait, 100 MHz ticks (FLOW_TIMEOUT_TICKS)
-    int d0;                       // 1: the chain factors D_0 from A(0,0) (else D_0 is read from Dd)
+    // the K + s2 I tiles are formed inside the launch (flow_gram_tile): each A tile by its owner
+    // wave before its first item, tile (0,0) and the band tiles of rows <= 3 by the diag
+    // workgroup's waves; the Y column tiles of R are read from Y on first touch
+    const double* X; long ldxi;   // inputs [n, D+1] (fidelity flag in column D)
+    const double* Y; long ldy;    // outputs [n, p]
+    const double* theta;          // [vL, lL(D), vD, lD(D), rho0, noise]
+    int D;
+    int gram;                     // 1: the AR1 Gram formed in the launch; 0: A holds K + s2 I already
+                                  // (the graph kernel's k_gram ran first)
 };
 constexpr long long FLOW_TIMEOUT_TICKS = 5000000;   // 50 ms (s_memrealtime is 100 MHz)
 int flow_trace_count(int T, int nwg);
@@ -91,6 +99,11 @@ struct GradArgs {
     int chunk;                            // m-tiles per task
     int nlf;                              // kernel family (GramArgs::nlf)
     const int* order;                     // workgroup -> task (nullptr: identity), see grad_order
+    // flow path: the next evaluation's set-up, done here after the flow has ended -- every
+    // workgroup sentinel-fills its share of the publication area, workgroup 0 the item slots of
+    // k_reduce_items (nullptr: none)
+    double* fpub; long npub;
+    double* isent; int nisent;
 };
 
 constexpr int FIN_MAXG = 254;   // theta entries finalize_body stages in LDS (graph kernel: <= 186)
@@ -120,6 +133,8 @@ struct FinArgs {
     int* cnt;                         // arrival counter (zero on entry): last item workgroup finalizes
     int flag;                         // 1: items[] hold FLOW_SENTINEL on entry (the Gram launch filled them):
                                       //    workgroup 0 finalizes once every other item is published
+    int* abortw;                      // flow path: k_chol_flow's abort word -- set: the evaluation timed
+                                      // out (info := MFGP_FLOW_TIMEOUT); workgroup 0 zeroes it for the next
 };
 
 struct PredAArgs {
@@ -252,7 +267,7 @@ template <int NB> void launch_first_factor(const double* A, long lda, long sA, d
                                            long sL, int* info, int batch, hipStream_t s);
 // dense layout, write extents wr1 x wr2 (>= n1 x n2; the excess is written 0.0)
 void launch_gram_dense(const GramArgs& g, int batch, int wr1, int wr2, hipStream_t s);
-void launch_gram_flow(const GramArgs& g, int extra, hipStream_t s);   // set-up launch of k_chol_flow
+void launch_flow_prep(const GramArgs& g, int nwg, hipStream_t s);    // set-up launch of k_chol_flow
 // one-launch value + gradient (+ Adam) of the AR1 GPR LML for small problems (k_gpr_tiny)
 bool gpr_tiny_fits(int n, int p, int d, int nlf);
 bool gpr_tiny_pred_fits(int n, int p, int d, int nstar);

@@ -542,235 +542,38 @@ void launch_gram_dense(const GramArgs& g, int batch, int wr1, int wr2, hipStream
 }
 
 // ------------------------------------------------------------ K1 flow set-up (LML layout, NB = 32)
-// The Gram launch in front of k_chol_flow, in the k_gram_dense form: workgroup b < nblk computes
-// lower 64 x 64 block b of the padded K + s2 I (row-major, ld = npad; identity on the padded
-// diagonal, zero elsewhere in the padding; the upper 32-tile of a diagonal block is skipped, and
-// tile (0,0) is left to the factor workgroup).  Workgroup nblk computes tile (0,0) into LDS and
-// runs the fused first diagonal factor (D_0, diag(L) 0..31, info); the set-up workgroups after it
-// build the flow owner table and the k_grad task order.  Every workgroup fills its share of the
-// publication area with the sentinel; the block workgroups copy the Y block of R.
-// It replaces k_gram's looping tile workgroups for this path: ~3 tiles each, one global round trip
-// per tile, and the fused factor's 256-VGPR allocation on every one (~18 us at Goku).
-// Entries: the same arithmetic as gram_entry (see k_gram_dense), K_ii = (k_ii + s2) + diag_add.
-// dbg (diagnostic): per workgroup [start, entries written / factor / table done, end], absolute
-// s_memrealtime ticks.
-template <int D4>
-__global__ __launch_bounds__(NTHREADS) void k_gram_flow(GramArgs a, int nblk) {
-    constexpr int S = TileCfg<32>::S;
+// The launch in front of k_chol_flow when the workspace is not known to be set up (eager calls,
+// value-only calls; mfgp_set_resident): every workgroup sentinel-fills its share of the
+// publication area; the last two build (or verify, when intact from an earlier call) the flow
+// owner table -- zeroing the abort word -- and the k_grad task order; workgroup 0 sentinel-fills
+// k_reduce_items' item slots and initialises info.  The Gram itself is formed inside the flow
+// (flow_gram_tile, mfgp_flow.hip), and the flow reads Y directly.
+__global__ __launch_bounds__(NTHREADS) void k_flow_prep(GramArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    double* sL1 = smem;                 // 64 x D4  row side, LF-scaled
-    double* sD1 = sL1 + GD_T * D4;      // 64 x D4  row side, HF-scaled
-    double* sD2 = sD1 + GD_T * D4;      // 64 x D4  column side, HF-scaled (K_HH pairs)
-    double* nL1 = sD2 + GD_T * D4;      // 64
-    double* nD1 = nL1 + GD_T;           // 64
-    double* f1 = nD1 + GD_T;            // 64 row fidelity flags (-1: padding)
-    double* il = f1 + GD_T;             // 2 x MAXD inverse lengthscales
-    double* ftile = il + 2 * MAXD;      // 32 x S  tile (0,0)       (factor workgroup)
-    double* frt = ftile + 32 * S;       // 32 x S  factor scratch   (factor workgroup)
-    double* fdg = frt + 32 * S;         // 32 pivots + the bad word
-    const int t = threadIdx.x, bx = blockIdx.x;
-    const int nfac = a.Dd ? 1 : 0;   // Dd == nullptr: k_chol_flow factors D_0 itself
-    const long long t0 = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
-    if (bx >= nblk + nfac) {   // set-up workgroups (LDS as int scratch)
-        int* sh = reinterpret_cast<int*>(smem);
-        if (a.gorder && bx == (int)gridDim.x - 1) build_grad_order(a.gT, a.gchunk, a.gTp, a.gorder, sh);
-        else if (a.fown) build_flow_owner(a.npad / 32, a.ppad / 32, a.fW, a.fown, a.fflags, a.nfflags, sh);
-        if (a.dbg && t == 0) { a.dbg[3 * bx] = t0; a.dbg[3 * bx + 1] = __builtin_amdgcn_s_memrealtime(); }
-        if (a.isent && bx == (int)gridDim.x - 1) gram_fill_items(a);   // (off the factor workgroup's path)
-        gram_fill_pub(a);
-        if (a.dbg && t == 0) a.dbg[3 * bx + 2] = __builtin_amdgcn_s_memrealtime();
-        return;
-    }
-    // workgroup 0: the factor workgroup (dispatched first: it is the launch's longest path)
-    const bool fac = nfac && bx == 0;
-    const int blk = bx - nfac;   // block index (block workgroups)
-    if (!nfac && bx == 0 && t == 0 && a.info) *a.info = 0;   // first writer of info in the sequence
-    int bi = 0, bj = 0;
-    if (!fac) flow_tri(blk, bi, bj);
-    const int r0 = bi * GD_T, c0 = bj * GD_T, nr = fac ? 32 : GD_T;
-    const int D = a.D, n = a.n1;
-    const double* tp = a.theta;
-    const double* X = a.X1;
-    if (t < D) {
-        il[t] = rcp_nr(tp[1 + t]);
-        il[MAXD + t] = a.rbf_only ? 1.0 : rcp_nr(tp[2 + D + t]);
-    }
-    const double vL = tp[0];
-    const double vD = a.rbf_only ? 0.0 : tp[1 + D];
-    const double rho = a.rbf_only ? 0.0 : tp[2 + 2 * D];
-    const double noise = a.add_noise ? tp[kernel_theta_size(0, D) - 1] : 0.0;
-    if (a.cnt && bx == 0)
-        for (int e = t; e < a.ncnt; e += NTHREADS) a.cnt[e] = 0;
-    __syncthreads();
-    // every global load issued before any is used (clamped, in-bounds addresses; the selects come
-    // after): a conditional load per element compiled to one memory round trip each
-    constexpr int SPT = (GD_T * D4 + NTHREADS - 1) / NTHREADS;   // staged elements per thread
-    const int c = fac ? (t & 31) : (t & 63), gj = c0 + c;
-    double x1v[SPT], x2v[SPT], xb[D4];
-#pragma unroll
-    for (int k = 0; k < SPT; ++k) {
-        const int e = t + k * NTHREADS, r = min(e / D4, nr - 1), d = min(e % D4, D - 1);
-        x1v[k] = X[(long)min(r0 + r, n - 1) * a.ldx1 + d];
-        x2v[k] = X[(long)min(c0 + r, n - 1) * a.ldx1 + d];
-    }
-#pragma unroll
-    for (int d = 0; d < D4; ++d) xb[d] = X[(long)min(gj, n - 1) * a.ldx1 + min(d, D - 1)];
-    const double fr = X[(long)min(r0 + min(t, nr - 1), n - 1) * a.ldx1 + D];   // fidelity flags
-    const double fc = X[(long)min(gj, n - 1) * a.ldx1 + D];
-#pragma unroll
-    for (int k = 0; k < SPT; ++k) {
-        const int e = t + k * NTHREADS;
-        if (e < nr * D4) {
-            const int r = e / D4, d = e % D4;
-            const bool in = d < D;
-            const double x1 = (in && r0 + r < n) ? x1v[k] : 0.0;
-            sL1[e] = in ? x1 * il[d] : 0.0;
-            if (!a.rbf_only) {
-                const double x2 = (in && c0 + r < n) ? x2v[k] : 0.0;
-                sD1[e] = in ? x1 * il[MAXD + d] : 0.0;
-                sD2[e] = in ? x2 * il[MAXD + d] : 0.0;
-            }
-        }
-    }
-    if (t < nr) f1[t] = (r0 + t < n) ? (a.rbf_only ? 0.0 : fr) : -1.0;
-    // lane -> column c (blocks: 64 columns, one row a wave step; factor tile: 32 columns, lanes
-    // 32-63 take the odd row of each pair, so all 64 lanes work)
-    const int half = fac ? ((t >> 5) & 1) : 0, rstep = fac ? 2 : 1;
-    double bl[D4];
-#pragma unroll
-    for (int d = 0; d < D4; ++d) bl[d] = (d < D && gj < n) ? xb[d] * il[d] : 0.0;
-    const double f2 = (gj < n) ? (a.rbf_only ? 0.0 : fc) : -1.0;
-    __syncthreads();
-    if (t < nr) {
-        nL1[t] = dot4(sL1 + t * D4, sL1 + t * D4, D4);
-        nD1[t] = a.rbf_only ? 0.0 : dot4(sD1 + t * D4, sD1 + t * D4, D4);
-    }
-    const double nL2 = dot_rl<D4>(bl, bl);
-    const double nD2 = a.rbf_only ? 0.0 : dot4(sD2 + c * D4, sD2 + c * D4, D4);
-    __syncthreads();
-    if (a.dbg && t == 0) { a.dbg[3 * bx] = t0; a.dbg[3 * gridDim.x + 2 * bx + 1] = __builtin_amdgcn_s_memrealtime(); }
-    const bool L2 = (f2 == 0.0), H2 = (f2 == 1.0);
-    const bool col_ok = fac || gj < a.npad;
-    const int w = t >> 6;
-    // rows w + 4 (rstep q + half), q < nr / (4 rstep): four at a time, stage by stage
-    for (int q0 = 0; q0 < nr / (4 * rstep); q0 += 4) {
-        int rr[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) rr[u] = w + 4 * (rstep * (q0 + u) + half);
-        double kl[4] = {0.0, 0.0, 0.0, 0.0};
-        double ra[4][D4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int d = 0; d < D4; ++d) ra[u][d] = sL1[rr[u] * D4 + d];
-#pragma unroll
-        for (int d = 0; d < D4; ++d) {   // dot4 / dot_rl order per entry
-#pragma unroll
-            for (int u = 0; u < 4; ++u) kl[u] += ra[u][d] * bl[d];
-            MFGP_PIN4(kl);
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) kl[u] = -0.5 * (-2.0 * kl[u] + (nL1[rr[u]] + nL2));
-        exp4(kl);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) kl[u] = vL * kl[u];
-        MFGP_PIN4(kl);   // keep the four chains in one basic block (else each sinks into the branch below)
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int gi = r0 + rr[u];
-            double v;
-            if (gi < n && gj < n) {
-                const double fa = f1[rr[u]];
-                if (a.rbf_only) {
-                    v = (fa < 0.0 || f2 < 0.0) ? 0.0 : kl[u];
-                } else {
-                    const bool L1 = (fa == 0.0), H1 = (fa == 1.0);
-                    double kD = 0.0;
-                    if (H1 && H2) {   // K_HH (linear.py:96)
-                        const double dotD = dot4(sD1 + rr[u] * D4, sD2 + c * D4, D4);
-                        kD = vD * exp(-0.5 * (-2.0 * dotD + (nD1[rr[u]] + nD2)));
-                    }
-                    const double vhh = kl[u] * (rho * rho) + kD;
-                    v = (L1 && L2) ? kl[u] : (!(H1 && H2) ? kl[u] * rho : vhh);
-                    if (!(L1 || H1) || !(L2 || H2)) v = 0.0;   // linear.py:67-70 exact masks
-                }
-                if (gi == gj) v = v + noise + a.diag_add;
-            } else {
-                v = (gi == gj) ? 1.0 : 0.0;                   // identity padding
-            }
-            if (fac) {
-                ftile[rr[u] * S + c] = v;
-            } else {
-                // skipped: rows past npad, the upper tile of a diagonal block, tile (0,0) (the
-                // factor workgroup's, when there is one)
-                const bool keep = gi < a.npad && col_ok && (gi >> 5) >= (gj >> 5) && (!nfac || gi >= 32 || gj >= 32);
-                if (keep) a.out[(long)gi * a.ldo + gj] = v;
-            }
-        }
-    }
-    if (a.dbg && t == 0) a.dbg[3 * bx + 1] = __builtin_amdgcn_s_memrealtime();
-    if (fac) {
-        __syncthreads();
-        tile_store<32>(a.out, a.ldo, ftile);
-        gram_first_factor<32>(ftile, frt, fdg, reinterpret_cast<int*>(fdg + 32), a.Dd, a.ldiag, a.info);
-        if (a.dbg && t == 0) a.dbg[3 * bx + 1] = __builtin_amdgcn_s_memrealtime();
-    } else if (a.R != nullptr) {   // Y block of R (rows < n, columns < p; zero padding), shared by the blocks
-        const long ne = (long)a.npad * a.ppad, st = (long)nblk * NTHREADS;
-        const long e0 = blk * (long)NTHREADS + t;
-        double yv[2];
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {   // loads first, then the stores (one round trip)
-            const long e = e0 + k * st;
-            const int r = (int)(e / a.ppad), cc = (int)(e % a.ppad);
-            yv[k] = (e < ne && r < n && cc < a.p) ? a.Y[(long)r * a.ldy + cc] : 0.0;
-        }
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const long e = e0 + k * st;
-            if (e < ne) a.R[(long)(e / a.ppad) * a.ldr + a.npad + e % a.ppad] = yv[k];
-        }
-        for (long e = e0 + 2 * st; e < ne; e += st) {
-            const int r = (int)(e / a.ppad), cc = (int)(e % a.ppad);
-            a.R[(long)r * a.ldr + a.npad + cc] = (r < n && cc < a.p) ? a.Y[(long)r * a.ldy + cc] : 0.0;
-        }
+    int* sh = reinterpret_cast<int*>(smem);
+    const int bx = blockIdx.x, last = (int)gridDim.x - 1;
+    if (a.gorder && bx == last) build_grad_order(a.gT, a.gchunk, a.gTp, a.gorder, sh);
+    else if (a.fown && bx == last - (a.gorder ? 1 : 0))
+        build_flow_owner(a.npad / 32, a.ppad / 32, a.fW, a.fown, a.fflags, a.nfflags, sh);
+    if (bx == 0) {
+        if (a.isent) gram_fill_items(a);
+        if (a.cnt)
+            for (int e = threadIdx.x; e < a.ncnt; e += NTHREADS) a.cnt[e] = 0;
+        if (threadIdx.x == 0 && a.info) *a.info = 0;
     }
     gram_fill_pub(a);
-    if (a.dbg && t == 0) a.dbg[3 * bx + 2] = __builtin_amdgcn_s_memrealtime();
 }
 
-static size_t gram_flow_smem_bytes(int D4) {
-    return sizeof(double) * (3 * (size_t)GD_T * D4 + 3 * GD_T + 2 * MAXD + 2 * 32 * TileCfg<32>::S + 32 + 2);
-}
+constexpr size_t FLOW_PREP_LDS = 16384;   // the set-up workgroups' tables (gorder: < 2048 ints + hash)
 
-template <int D4>
-static void launch_gram_flow_d4(const GramArgs& g, int nblk, int grid, hipStream_t s) {
+void launch_flow_prep(const GramArgs& g, int nwg, hipStream_t s) {
     static bool attr = false;
-    const size_t lds = gram_flow_smem_bytes(D4);
     if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gram_flow<D4>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_flow_prep),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)FLOW_PREP_LDS);
         attr = true;
     }
-    hipLaunchKernelGGL(k_gram_flow<D4>, dim3(grid), dim3(NTHREADS), lds, s, g, nblk);
-}
-
-// g: the LML-layout GramArgs of gpr_value_grad (batch 1, nlf = 0, NB = 32); extra: set-up
-// workgroups (flow owner table, k_grad order); g.Dd == nullptr: no factor workgroup (the flow
-// factors D_0 itself).
-void launch_gram_flow(const GramArgs& g, int extra, hipStream_t s) {
-    const int nb = (g.npad + GD_T - 1) / GD_T;
-    const int nblk = nb * (nb + 1) / 2;
-    const int grid = nblk + (g.Dd ? 1 : 0) + extra;
-    switch (pad4(g.D)) {
-        case 4: launch_gram_flow_d4<4>(g, nblk, grid, s); break;
-        case 8: launch_gram_flow_d4<8>(g, nblk, grid, s); break;
-        case 12: launch_gram_flow_d4<12>(g, nblk, grid, s); break;
-        case 16: launch_gram_flow_d4<16>(g, nblk, grid, s); break;
-        case 20: launch_gram_flow_d4<20>(g, nblk, grid, s); break;
-        case 24: launch_gram_flow_d4<24>(g, nblk, grid, s); break;
-        case 28: launch_gram_flow_d4<28>(g, nblk, grid, s); break;
-        default: launch_gram_flow_d4<32>(g, nblk, grid, s); break;
-    }
+    hipLaunchKernelGGL(k_flow_prep, dim3(nwg), dim3(NTHREADS), FLOW_PREP_LDS, s, g);
 }
 
 // ============================================================ K2: tile Cholesky step
@@ -1021,6 +824,30 @@ __device__ __forceinline__ int grad_decode(int t, int T, int chunk, int Tp, int&
     ch = t % nch;
     const int m0 = grad_m0(T, i, chunk, ch);
     return grad_m1(T, m0, chunk) - m0 + (ch == 0 ? Tp : 0);
+}
+
+// Flow path (GradArgs::fpub): the next evaluation's set-up, run by every k_grad workgroup after
+// its own work -- the flow has ended, so its publication area is dead: 16-B sc1 sentinel stores
+// (as gram_fill_pub) over a grid-stride share; workgroup 0 also refills k_reduce_items' item slots
+// (this evaluation's reduction polls them; k_reduce_items zeroes the abort word).  With it the next value+grad
+// evaluation of the same problem on the same workspace can start with the flow itself
+// (mfgp_set_resident): these stores land after the chain, where they slow no hand-off.
+__device__ __forceinline__ void grad_next_setup(const GradArgs& a) {
+    if (!a.fpub) return;
+    if (blockIdx.x == 0) {
+        for (int e = threadIdx.x; e < a.nisent; e += NTHREADS)
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.isent) + e, FLOW_SENTINEL, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(a.fpub, (short)0, (int)(a.npub * 8), 0x00020000);
+    const unsigned lo = (unsigned)(FLOW_SENTINEL & 0xffffffffull), hi = (unsigned)(FLOW_SENTINEL >> 32);
+    const fill_u32x4 v = {lo, hi, lo, hi};
+    const long npair = a.npub / 2;
+    for (long e = blockIdx.x * (long)NTHREADS + threadIdx.x; e < npair; e += (long)gridDim.x * NTHREADS)
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)(e * 16), 0, 16);
+    if ((a.npub & 1) && blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.fpub) + a.npub - 1, FLOW_SENTINEL,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Workgroup -> task table for k_grad.  All k_grad workgroups are resident at once and
@@ -1360,6 +1187,7 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
         else if (qx >= 2 + a.D && qx <= 1 + 2 * a.D) { const double l = th.lD(qx - 2 - a.D); v /= l * l * l; }
         return v;
     });
+    grad_next_setup(a);
 }
 
 size_t grad_smem_bytes(int nb, int G, int nil2) {
@@ -1474,11 +1302,15 @@ __device__ void reduce_items_wg0(const FinArgs& a) {
         }
     }
     if (t == 0) gsh[0] = z;
+    // the flow's abort word (a hand-off that gave up): the evaluation timed out, whatever info says
+    // (the flow initialises info in its first workgroup, which can land after an early give-up)
+    const int aborted = a.abortw ? __hip_atomic_load(a.abortw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
     __syncthreads();
-    if (tmo && info0 == 0) {   // (eager callers see it as a timed-out evaluation)
+    if ((tmo && info0 == 0) || aborted) {   // (eager callers see it as a timed-out evaluation)
         info0 = MFGP_FLOW_TIMEOUT;
         if (t == 0) const_cast<int*>(a.info)[0] = MFGP_FLOW_TIMEOUT;
     }
+    if (a.abortw && t == 0 && aborted) __hip_atomic_store(a.abortw, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     finalize_from(a, G, gsh, tsh, info0, s, &pre);
 }
 

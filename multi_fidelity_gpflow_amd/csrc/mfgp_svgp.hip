@@ -211,6 +211,150 @@ __global__ __launch_bounds__(NTHREADS) void k_svgp_cond(const double* Xo, const 
     (void)S;
 }
 
+// k_svgp_cond on a 64 x 64 block of (A, B) per workgroup (NB = 32 operands): wave w owns tile
+// (2 bi + (w >> 1), 2 bj + (w & 1)) of both A and B as 2 x 2 independent 16 x 16 accumulators
+// each; every m-step stages the two Kuf tiles, two Li tiles and two C tiles once for the four waves
+// (k_svgp_cond: one Kuf, one Li, one C tile per 32 x 32 output), the next m-step's loads issued
+// into registers before the current products.  Same per-block MFMA sequence and the same column
+// reduction order as k_svgp_cond, so A, B and the partials are bitwise its results.
+constexpr int SC2_E = 32 * 34;
+size_t svgp_cond2_smem() { return 6 * sizeof(double) * (size_t)SC2_E; }
+
+__global__ __launch_bounds__(NTHREADS) void k_svgp_cond2(const double* Xo, const double* C, const double* Kuf,
+                                                        const double* q_mu, int L, int m, int Tm, int npad,
+                                                        double* pa, double* pb, double* pm, double* Aout,
+                                                        double* Bout) {
+    constexpr int S = 34, NB = 32;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    int bx, l;
+    xcd_swizzle(bx, l);
+    const int Tn = npad / NB, Nb = (Tn + 1) >> 1;
+    const int bi = bx / Nb, bj = bx % Nb;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+    const int ti = 2 * bi + (w >> 1), tn = 2 * bj + (w & 1);
+    const bool live = ti < Tm && tn < Tn;
+    const long mp = (long)Tm * NB, mm = mp * mp;
+    const double* xo = Xo + l * mm;
+    const double* cc = C + l * mm;
+    const double* kuf = Kuf + (long)l * mp * npad;
+    const int r0 = min(2 * bi, Tm - 1), r1 = min(2 * bi + 1, Tm - 1);
+    const int c0 = min(2 * bj, Tn - 1), c1 = min(2 * bj + 1, Tn - 1);
+    TileRegs<32> rg[6];
+    auto fetch = [&](int mt) {
+        tile_fetch<32>(rg[0], kuf + (long)mt * NB * npad + (long)c0 * NB, npad);
+        tile_fetch<32>(rg[1], kuf + (long)mt * NB * npad + (long)c1 * NB, npad);
+        tile_fetch<32>(rg[2], xo + (long)r0 * NB * mp + (long)mt * NB, mp);
+        tile_fetch<32>(rg[3], xo + (long)r1 * NB * mp + (long)mt * NB, mp);
+        tile_fetch<32>(rg[4], cc + (long)r0 * NB * mp + (long)mt * NB, mp);
+        tile_fetch<32>(rg[5], cc + (long)r1 * NB * mp + (long)mt * NB, mp);
+    };
+    f64x4 accA[2][2], accB[2][2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            accA[p][q] = f64x4{0.0, 0.0, 0.0, 0.0};
+            accB[p][q] = f64x4{0.0, 0.0, 0.0, 0.0};
+        }
+    const double* Ks = smem + (w & 1) * SC2_E;          // Kuf(mt, tn)
+    const double* Ls = smem + (2 + (w >> 1)) * SC2_E;   // Li(ti, mt)
+    const double* Cs = smem + (4 + (w >> 1)) * SC2_E;   // C(ti, mt)
+    fetch(0);
+    for (int mt = 0; mt < Tm; ++mt) {
+#pragma unroll
+        for (int t = 0; t < 6; ++t) tile_put<32>(smem + t * SC2_E, rg[t]);
+        if (mt + 1 < Tm) fetch(mt + 1);
+        __syncthreads();
+        if (live) {
+            const bool doA = mt <= ti;   // Li lower
+#pragma unroll 4
+            for (int k0 = 0; k0 < NB; k0 += 4) {   // A: the old k_svgp_cond's first chain of the m-step
+                if (!doA) break;
+                const int k = k0 + lk;
+                double av[2], bv[2];
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    av[t] = 1.0 * Ls[(16 * t + li) * S + k];
+                    bv[t] = Ks[k * S + 16 * t + li];
+                }
+#pragma unroll
+                for (int p = 0; p < 2; ++p)
+#pragma unroll
+                    for (int q = 0; q < 2; ++q)
+                        accA[p][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[p], bv[q], accA[p][q], 0, 0, 0);
+            }
+#pragma unroll 4
+            for (int k0 = 0; k0 < NB; k0 += 4) {
+                const int k = k0 + lk;
+                double av[2], bv[2];
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    av[t] = 1.0 * Cs[(16 * t + li) * S + k];
+                    bv[t] = Ks[k * S + 16 * t + li];
+                }
+#pragma unroll
+                for (int p = 0; p < 2; ++p)
+#pragma unroll
+                    for (int q = 0; q < 2; ++q)
+                        accB[p][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[p], bv[q], accB[p][q], 0, 0, 0);
+            }
+        }
+        __syncthreads();
+    }
+    if (!live) return;
+    if (Aout) {   // gradient pass: keep A and B (L x Mpad x Npad each)
+        const long o = (long)l * mp * npad + (long)ti * NB * npad + (long)tn * NB;
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const long e = o + (long)(16 * p + lk + 4 * r) * npad + 16 * q + li;
+                    Aout[e] = accA[p][q][r];
+                    Bout[e] = accB[p][q][r];
+                }
+    }
+    // column partials of the tile: rows 0-15 then 16-31 (k_svgp_cond's two row-half slots)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        double ta = 0.0, tb = 0.0, tm = 0.0;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            double sa = 0.0, sb = 0.0, sm = 0.0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int gr = ti * NB + 16 * p + lk + 4 * r;
+                const double qm = (gr < m) ? q_mu[(long)gr * L + l] : 0.0;
+                const double a = accA[p][q][r], b = accB[p][q][r];
+                sa += a * a;
+                sb += b * b;
+                sm += a * qm;
+            }
+            sa += __shfl_xor(sa, 16, 64); sa += __shfl_xor(sa, 32, 64);
+            sb += __shfl_xor(sb, 16, 64); sb += __shfl_xor(sb, 32, 64);
+            sm += __shfl_xor(sm, 16, 64); sm += __shfl_xor(sm, 32, 64);
+            ta += sa;
+            tb += sb;
+            tm += sm;
+        }
+        if (lk == 0) {
+            const long o = ((long)l * Tm + ti) * npad + (long)tn * NB + 16 * q + li;
+            pa[o] = ta;
+            pb[o] = tb;
+            pm[o] = tm;
+        }
+    }
+}
+
+static bool svgp_cond2_on() {
+    static const int on = [] {
+        const char* e = getenv("MFGP_BGEMM2");
+        return e ? atoi(e) : 1;
+    }();
+    return on != 0;
+}
+
 // g_mu[l][n], g_var[l][n] from the partials (+ Kff = K_diag_l(X))
 __global__ void k_svgp_moments(const double* pa, const double* pb, const double* pm, const double* X, long ldx,
                                const double* thetas, int G, int D, int n, int npad, int Tm, double* g_mu,
@@ -383,9 +527,21 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
         g.padded = 0; g.tiles_c = S.Tn; g.diag_add = 0.0;
         launch_gram_dense(g, L, S.mpad, S.npad, s);   // zero padding written by the kernel
     }
-    hipLaunchKernelGGL(k_svgp_cond<NB>, dim3(S.Tm * S.Tn, 1, L), dim3(NTHREADS),
-                       sizeof(double) * (3 * NB * (NB + 2) + 12 * NB), s, S.Xo, S.C, S.Kuf, q_mu, L, m, S.Tm,
-                       S.npad, S.pa, S.pb, S.pm, Aout, Bout);
+    if (NB == 32 && svgp_cond2_on()) {
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_svgp_cond2),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)svgp_cond2_smem());
+            attr = true;
+        }
+        hipLaunchKernelGGL(k_svgp_cond2, dim3(((S.Tm + 1) >> 1) * ((S.Tn + 1) >> 1), 1, L), dim3(NTHREADS),
+                           svgp_cond2_smem(), s, S.Xo, S.C, S.Kuf, q_mu, L, m, S.Tm, S.npad, S.pa, S.pb, S.pm, Aout,
+                           Bout);
+    } else {
+        hipLaunchKernelGGL(k_svgp_cond<NB>, dim3(S.Tm * S.Tn, 1, L), dim3(NTHREADS),
+                           sizeof(double) * (3 * NB * (NB + 2) + 12 * NB), s, S.Xo, S.C, S.Kuf, q_mu, L, m, S.Tm,
+                           S.npad, S.pa, S.pb, S.pm, Aout, Bout);
+    }
     hipLaunchKernelGGL(k_svgp_moments, dim3(cdiv(n, 256), 1, L), dim3(256), 0, s, S.pa, S.pb, S.pm, X, (long)ldx,
                        thetas, S.G, d, n, S.npad, S.Tm, g_mu, g_var);
     if (f_mu) {   // predict: mixed moments only

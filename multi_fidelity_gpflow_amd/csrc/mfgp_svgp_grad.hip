@@ -93,8 +93,174 @@ __global__ __launch_bounds__(NTHREADS) void k_bgemm(BgemmArgs a) {
 
 size_t bgemm_smem(int nb) { return 2 * sizeof(double) * (size_t)nb * (nb + 2); }
 
+// The same products on NB = 32 operands, a 64 x 64 output block per workgroup: wave w computes
+// the 32 x 32 tile (2 bi + (w >> 1), 2 bj + (w & 1)) as 2 x 2 independent 16 x 16 accumulators
+// (k_bgemm: one 16 x 16 chain per wave), and each k-tile's two A tiles and two B tiles are staged
+// in LDS once for all four waves (twice k_bgemm's operand reuse), double-buffered, the next
+// k-tile's global loads issued into registers before the current products.  Every 16 x 16 block
+// runs the same MFMA sequence as tile_mma<32> (k-tiles ascending, 4-deep steps ascending, alpha
+// on the A operand), so the results are bitwise k_bgemm's.  Edge blocks (odd Mt / Nt) load a
+// clamped in-range tile for the missing half and store nothing from it.
+constexpr int BG2_E = 32 * 34;   // one 32-tile in LDS (TileCfg<32>)
+size_t bgemm2_smem() { return 2 * 4 * sizeof(double) * (size_t)BG2_E; }
+
+template <bool TA, bool TB>
+__global__ __launch_bounds__(NTHREADS) void k_bgemm2(BgemmArgs a) {
+    constexpr int S = 34, NB = 32;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    int bx, b;
+    xcd_swizzle(bx, b);
+    const int Nb = (a.Nt + 1) >> 1;
+    const int bi = bx / Nb, bj = bx % Nb;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+    const int ti = 2 * bi + (w >> 1), tj = 2 * bj + (w & 1);   // this wave's output tile
+    const bool live = ti < a.Mt && tj < a.Nt;
+    // k-range of a tile (ri, cj) under the operand masks
+    auto krange = [&](int ri, int cj, int& k0, int& k1) {
+        k0 = 0;
+        k1 = a.Kt;
+        if (a.amask == 1) k1 = min(k1, ri + 1);
+        else if (a.amask == 2) k0 = max(k0, ri);
+        if (a.bmask == 1) k0 = max(k0, cj);
+        else if (a.bmask == 2) k1 = min(k1, cj + 1);
+        if (a.tril && cj > ri) k1 = k0;   // strictly upper output tile of a lower-masked product
+    };
+    int kw0, kw1;
+    krange(ti, tj, kw0, kw1);
+    if (!live) kw1 = kw0;
+    // the workgroup's k-range: the union over its live tiles
+    int kb0 = a.Kt, kb1 = 0;
+    for (int q = 0; q < 4; ++q) {
+        const int r = 2 * bi + (q >> 1), c = 2 * bj + (q & 1);
+        if (r >= a.Mt || c >= a.Nt) continue;
+        int k0, k1;
+        krange(r, c, k0, k1);
+        if (k1 > k0) { kb0 = min(kb0, k0); kb1 = max(kb1, k1); }
+    }
+    const double* A = a.A + b * a.sA;
+    const double* B = a.B + b * a.sB;
+    const double* s = a.s ? a.s + b * a.ss : nullptr;
+    const int ra0 = min(2 * bi, a.Mt - 1), ra1 = min(2 * bi + 1, a.Mt - 1);
+    const int cb0 = min(2 * bj, a.Nt - 1), cb1 = min(2 * bj + 1, a.Nt - 1);
+    auto atile = [&](int ri, int kt) {
+        return TA ? A + (long)kt * NB * a.lda + (long)ri * NB : A + (long)ri * NB * a.lda + (long)kt * NB;
+    };
+    auto btile = [&](int cj, int kt) {
+        return TB ? B + (long)cj * NB * a.ldb + (long)kt * NB : B + (long)kt * NB * a.ldb + (long)cj * NB;
+    };
+    TileRegs<32> rg[4];
+    auto fetch = [&](int kt) {
+        tile_fetch<32>(rg[0], atile(ra0, kt), a.lda);
+        tile_fetch<32>(rg[1], atile(ra1, kt), a.lda);
+        tile_fetch<32>(rg[2], btile(cb0, kt), a.ldb);
+        tile_fetch<32>(rg[3], btile(cb1, kt), a.ldb);
+    };
+    auto put = [&](double* buf, int kt) {
+        tile_put<32>(buf, rg[0]);
+        tile_put<32>(buf + BG2_E, rg[1]);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            TileRegs<32>& r = rg[2 + h];
+            if (s) {   // k scaling of the B side (k_bgemm's Bs[r][c] *= s[k])
+#pragma unroll
+                for (int q = 0; q < 32 * 32 / 2 / NTHREADS; ++q) {
+                    const int p = threadIdx.x + q * NTHREADS;
+                    const int row = p / 16, c = 2 * (p % 16);
+                    r.v[q].x *= s[(long)kt * NB + (TB ? c : row)];
+                    r.v[q].y *= s[(long)kt * NB + (TB ? c + 1 : row)];
+                }
+            }
+            tile_put<32>(buf + (2 + h) * BG2_E, r);
+        }
+    };
+    f64x4 acc[2][2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) acc[p][q] = f64x4{0.0, 0.0, 0.0, 0.0};
+    if (kb1 > kb0) {
+        double* buf0 = smem;
+        double* buf1 = smem + 4 * BG2_E;
+        fetch(kb0);
+        put(buf0, kb0);
+        if (kb0 + 1 < kb1) fetch(kb0 + 1);
+        __syncthreads();
+        for (int kt = kb0; kt < kb1; ++kt) {
+            double* cur = ((kt - kb0) & 1) ? buf1 : buf0;
+            double* nxt = ((kt - kb0) & 1) ? buf0 : buf1;
+            if (kt >= kw0 && kt < kw1) {   // wave-uniform
+                const double* As = cur + (w >> 1) * BG2_E;
+                const double* Bs = cur + (2 + (w & 1)) * BG2_E;
+#pragma unroll 4
+                for (int k0 = 0; k0 < NB; k0 += 4) {
+                    const int k = k0 + lk;
+                    double av[2], bv[2];
+#pragma unroll
+                    for (int t = 0; t < 2; ++t) {
+                        const int i = 16 * t + li, j = 16 * t + li;
+                        av[t] = a.alpha * (TA ? As[k * S + i] : As[i * S + k]);
+                        bv[t] = TB ? Bs[j * S + k] : Bs[k * S + j];
+                    }
+#pragma unroll
+                    for (int p = 0; p < 2; ++p)
+#pragma unroll
+                        for (int q = 0; q < 2; ++q)
+                            acc[p][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[p], bv[q], acc[p][q], 0, 0, 0);
+                }
+            }
+            if (kt + 1 < kb1) {
+                put(nxt, kt + 1);
+                if (kt + 2 < kb1) fetch(kt + 2);
+            }
+            __syncthreads();
+        }
+    }
+    if (!live) return;
+    double* Dt = a.D + b * a.sD;
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = ti * NB + 16 * p + lk + 4 * r, j = tj * NB + 16 * q + li;
+                double v = acc[p][q][r];
+                if (a.Cin) v += a.beta * a.Cin[b * a.sC + (long)i * a.ldc + j];
+                if (a.colscale) v *= a.colscale[b * a.scs + j];
+                if (a.x) v += a.x[b * a.sx + i] * a.y[b * a.sy + j];
+                if (a.tril && j > i) v = 0.0;
+                Dt[(long)i * a.ldd + j] = v;
+            }
+}
+
+static bool bgemm2_on() {
+    static const int on = [] {
+        const char* e = getenv("MFGP_BGEMM2");
+        return e ? atoi(e) : 1;
+    }();
+    return on != 0;
+}
+
 template <int NB>
 static void bgemm(hipStream_t st, int ta, int tb, const BgemmArgs& a, int batch) {
+    if (NB == 32 && bgemm2_on()) {
+        static bool attr = false;
+        if (!attr) {
+            for (const void* f : {reinterpret_cast<const void*>(&k_bgemm2<false, false>),
+                                  reinterpret_cast<const void*>(&k_bgemm2<false, true>),
+                                  reinterpret_cast<const void*>(&k_bgemm2<true, false>),
+                                  reinterpret_cast<const void*>(&k_bgemm2<true, true>)})
+                (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bgemm2_smem());
+            attr = true;
+        }
+        dim3 g(((a.Mt + 1) >> 1) * ((a.Nt + 1) >> 1), 1, batch);
+        const size_t sm = bgemm2_smem();
+        if (!ta && !tb) hipLaunchKernelGGL((k_bgemm2<false, false>), g, dim3(NTHREADS), sm, st, a);
+        else if (!ta && tb) hipLaunchKernelGGL((k_bgemm2<false, true>), g, dim3(NTHREADS), sm, st, a);
+        else if (ta && !tb) hipLaunchKernelGGL((k_bgemm2<true, false>), g, dim3(NTHREADS), sm, st, a);
+        else hipLaunchKernelGGL((k_bgemm2<true, true>), g, dim3(NTHREADS), sm, st, a);
+        return;
+    }
     dim3 g(a.Mt * a.Nt, 1, batch);
     const size_t sm = bgemm_smem(NB);
     if (!ta && !tb) hipLaunchKernelGGL((k_bgemm<NB, false, false>), g, dim3(NTHREADS), sm, st, a);

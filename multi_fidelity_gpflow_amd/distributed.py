@@ -129,7 +129,10 @@ class SharedThetaTrainer:
             self.b1, self.b2 = float(np.float32(0.9)), float(np.float32(0.999))
 
             def _lml_grad():
-                out, info = eng.gpr_lml(self.X, self.Y, self.theta, want_grad=True)
+                # every step is a value+grad call of the same problem on the engine's workspace,
+                # which leaves it set up for the next (mfgp_set_resident)
+                with eng.resident():
+                    out, info = eng.gpr_lml(self.X, self.Y, self.theta, want_grad=True)
                 self.out.copy_(out)
                 self.info.copy_(info)
                 return self.out
@@ -251,6 +254,8 @@ class SharedInducingTrainer:
             o += n
         self.adam_fn(self.buf[o])
         self.done += 1
+        if self.tr is not None:   # the device trainer's own count (its finish() reads that many losses)
+            self.tr.done = self.done
 
     def step(self):
         with self._ctx():

@@ -158,6 +158,21 @@ class Engine:
         step sequence of the general path (False)."""
         self._set_mode(self.lib.mfgp_set_tiny, 1 if enable else 0)
 
+    @contextlib.contextmanager
+    def resident(self):
+        """Value+grad LML calls inside the block may skip the flow's set-up launch when the previous
+        fp64 LML call on this thread's handle left their workspace set up for the same problem
+        (include/mfgp.h mfgp_set_resident).  For training sessions, whose private workspace nothing
+        else writes."""
+        if not hasattr(self.lib, "mfgp_set_resident"):   # an older diagnostic build (MFGP_LIB_PATH)
+            yield
+            return
+        check(self.lib.mfgp_set_resident(self.h, 1), "mfgp_set_resident")
+        try:
+            yield
+        finally:
+            check(self.lib.mfgp_set_resident(self.h, 0), "mfgp_set_resident")
+
     def set_flow_timeout_us(self, us: int):
         """Bound of every k_chol_flow hand-off wait (default 50000 us; 0: diagnostic abort path)."""
         check(self.lib.mfgp_set_flow_timeout_us(self.h, int(us)), "mfgp_set_flow_timeout_us")

@@ -478,7 +478,10 @@ class AdamSession:
         self.runner = _StepRunner(self._step, chunk, graphs=core.graphs)
 
     def _step(self):
-        self.eng.gpr_adam_step(self.X, self.Y, self.st, self.hist, self.out, self.info, ws=self.ws)
+        # the session's private workspace is written by its own steps only (and its warm-up, a
+        # value+grad call): each step leaves it set up for the next (mfgp_set_resident)
+        with self.eng.resident():
+            self.eng.gpr_adam_step(self.X, self.Y, self.st, self.hist, self.out, self.info, ws=self.ws)
 
     def run(self, n: int):
         if self._core is None:
