@@ -14,9 +14,9 @@ __host__ __device__ inline int flow_gram_dbg_count(int T) { return 5 * flow_gram
 
 // ---------------------------------------------------------------- tile catalogue
 // code = type << 20 | i << 10 | j ; R tiles use j = column tile c in [0, T + Tp)
-// FT_H: coupling H_k = D_k L(k,k-1); FT_G: the initial value (K + s2 I) of a band tile (k,k-2),
-// (k,k-1), (k,k) of the rows 1 <= k <= 3, formed at the launch's start by an otherwise idle worker
-// wave and published to the diag workgroup (FlowArgs::gram)
+// FT_H: coupling H_k = D_k L(k,k-1); FT_G: the initial value (K + s2 I) of a band tile (3,1),
+// (3,2), (3,3), formed at the launch's start by an otherwise idle worker wave and published to the
+// diag workgroup (FlowArgs::gram)
 enum : int { FT_A = 0, FT_R = 1, FT_AL = 2, FT_H = 3, FT_G = 4 };
 __host__ __device__ inline int flow_code(int type, int i, int j) { return (type << 20) | (i << 10) | j; }
 
@@ -31,12 +31,11 @@ __host__ __device__ inline void flow_tri(int t, int& i, int& j) {   // row-major
 // Owned A tiles: every lower tile except (0,0) (k_gram) and the band tiles (k,k-2), (k,k-1),
 // (k,k) of rows k <= 3, which the diag workgroup takes from their initial values.
 __host__ __device__ inline int flow_nA(int T) { return T >= 4 ? T * (T + 1) / 2 - 9 : 0; }
-// the band tiles of rows 1..3 in that order: (1,0) (1,1) (2,0) (2,1) (2,2) (3,1) (3,2) (3,3)
-__host__ __device__ inline int flow_nG(int T) { return (T > 1 ? 2 : 0) + (T > 2 ? 3 : 0) + (T > 3 ? 3 : 0); }
+// the band tiles of row 3: (3,1) (3,2) (3,3) (rows 0-2: the diag workgroup's own Gram phase)
+__host__ __device__ inline int flow_nG(int T) { return T > 3 ? 3 : 0; }
 __host__ __device__ inline void flow_gtile(int g, int& i, int& j) {
-    const int I[8] = {1, 1, 2, 2, 2, 3, 3, 3}, J[8] = {0, 1, 0, 1, 2, 1, 2, 3};
-    i = I[g];
-    j = J[g];
+    i = 3;
+    j = 1 + g;
 }
 __host__ __device__ inline int flow_ntiles(int T, int Tp) {
     return flow_nA(T) + T * (T - 1) / 2 + 2 * T * Tp + (T > 1 ? T - 1 : 0) + flow_nG(T);

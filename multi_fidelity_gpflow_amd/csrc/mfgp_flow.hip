@@ -241,15 +241,19 @@ __device__ __forceinline__ double wave_sum64(double v) {
 // used -- one memory round trip per half and chunk (a dependent load per k-step cost ~5 us a
 // tile), in ~120 VGPRs (the kernel's allocation stays at its roles' 183, so small kernels of
 // other streams still fit beside the flow's waves on a CU).
+// SC1: publish (sc1 stores, for another wave); row halves [b0, b1) and the column halves in
+// cmask (bit b: columns 16 b ..) of the tile only.
+template <bool SC1>
 __device__ __forceinline__ void flow_gram_tile(const double* __restrict__ X, long ldx, const double* __restrict__ th,
-                                               int n, int D, int ti, int tj, double* dst, long ld) {
+                                               int n, int D, int ti, int tj, double* dst, long ld, int b0 = 0,
+                                               int b1 = 2, int cmask = 3) {
     constexpr int FS = 4;
     const int l = threadIdx.x & 63, li = l & 15, lq = l >> 4;
     int rj[2];
 #pragma unroll
     for (int b = 0; b < 2; ++b) rj[b] = 32 * tj + 16 * b + li;
 #pragma unroll 1
-    for (int bi = 0; bi < 2; ++bi) {
+    for (int bi = b0; bi < b1; ++bi) {
         const int ri = 32 * ti + 16 * bi + li;
         double fi = X[(long)min(ri, n - 1) * ldx + D];
         double fj[2];
@@ -294,6 +298,7 @@ __device__ __forceinline__ void flow_gram_tile(const double* __restrict__ X, lon
                 nid = fma(aid, aid, nid);
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
+                    if (!((cmask >> q) & 1)) continue;
                     const double x2 = (dv && rj[q] < n) ? xj[q][k] : 0.0;
                     const double aj = x2 * il, ajd = x2 * ild;
                     nj[q] = fma(aj, aj, nj[q]);
@@ -320,6 +325,7 @@ __device__ __forceinline__ void flow_gram_tile(const double* __restrict__ X, lon
         }
 #pragma unroll
         for (int bj = 0; bj < 2; ++bj) {
+            if (!((cmask >> bj) & 1)) continue;
             const bool L2 = fj[bj] == 0.0, H2 = fj[bj] == 1.0;
             double kl[4], kd[4];
 #pragma unroll
@@ -344,7 +350,8 @@ __device__ __forceinline__ void flow_gram_tile(const double* __restrict__ X, lon
                 } else {
                     v = (gi == gj) ? 1.0 : 0.0;                // identity padding
                 }
-                dst[(long)row * ld + 16 * bj + li] = v;   // the accumulator layout of wt_store_u
+                if constexpr (SC1) st_coherent(dst + (long)row * ld + 16 * bj + li, v);
+                else dst[(long)row * ld + 16 * bj + li] = v;   // the accumulator layout of wt_store_u
             }
         }
     }
@@ -831,7 +838,7 @@ struct DiagLds {
     static constexpr size_t BYTES = sizeof(double) * (10 * E + 32 * 33 + 64 + 16);
 };
 static_assert(DiagLds::BYTES <= FLOW_LDS_BYTES, "diag workgroup LDS carve");
-enum { DW_LS = 0, DW_D, DW_LPUB, DW_DPUB, DW_PRE6, DW_PRE7, DW_BAR, DW_L2, DW_P2, DW_N };
+enum { DW_LS = 0, DW_D, DW_LPUB, DW_DPUB, DW_PRE6, DW_PRE7, DW_BAR, DW_L2, DW_P2, DW_G0, DW_N };
 static_assert(DW_N <= 28, "progress words fit in the carve");
 
 __device__ __forceinline__ int lds_get(const int* p) {
@@ -861,6 +868,15 @@ __device__ __forceinline__ void wt_to_lds_ld(const WTile& t, double* S, int ld) 
 #pragma unroll
             for (int r = 0; r < 4; ++r) S[(16 * a + lq + 4 * r) * ld + 16 * b + li] = t.v[a][b][r];
 }
+__device__ __forceinline__ void lds_to_wt_ld(WTile& t, const double* S, int ld) {
+    const int li = threadIdx.x & 15, lq = (threadIdx.x >> 4) & 3;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) t.v[a][b][r] = S[(16 * a + lq + 4 * r) * ld + 16 * b + li];
+}
 __device__ __forceinline__ void op_rows_lds_ld(WOp& o, const double* S, int ld) {
     const int li = threadIdx.x & 15, lq = (threadIdx.x >> 4) & 3;
 #pragma unroll
@@ -889,9 +905,15 @@ __device__ __forceinline__ void diag_chain(FlowCtx& C, const DiagLds& B) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     int epoch = 0;
     if (w == 0) {   // D_0: wave 0 forms tile (0,0) of K + s2 I and factors it
-        // tile (0,0): flow_gram_phase's (this wave wrote it), or the graph kernel's k_gram
-        for (int e = l; e < 32 * 32; e += 64) B.fsc()[(e >> 5) * 33 + (e & 31)] = a.A[(long)(e >> 5) * a.lda + (e & 31)];
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        // tile (0,0): flow_gram_phase's (waves 0 and 1 formed it in fsc), or the graph kernel's k_gram
+        if (!a.gram) {
+            for (int e = l; e < 32 * 32; e += 64) B.fsc()[(e >> 5) * 33 + (e & 31)] = a.A[(long)(e >> 5) * a.lda + (e & 31)];
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        } else {
+            if (a.trace && l == 0) a.trace[0] = flow_clock() - C.t0;
+            lds_spin_ge(&B.w()[DW_G0], 2);   // the blocks of waves 1 and 4
+            if (a.trace && l == 0) a.trace[T] = flow_clock() - C.t0;
+        }
         tile_potrf_inv_w1_wave(B.fsc(), 33, B.fsc(), B.Db(0), B.dg(0), &B.bad()[0]);
         if (l == 0) lds_put(&B.w()[DW_D], 0);
     }
@@ -1005,8 +1027,10 @@ __device__ __forceinline__ void diag_second(FlowCtx& C, const DiagLds& B) {
         if (j >= 4) {
             pub_wt_op_direct(acc, C.P.H(2, j), x, C.P.L(j, j - 3), C);
         } else {
-            // A(2,0), A(3,1): their initial values (flow_gram_phase: this wave wrote them)
-            if (a.gram) wt_load<false>(acc, C.At(j, j - 2), a.lda);
+            // A(2,0), A(3,1): their initial values (Gram phase: A(2,0) this wave's, in L2[0];
+            // A(3,1) a worker wave's FT_G)
+            if (a.gram && j == 2) lds_to_wt_ld(acc, B.L2(0), S);
+            else if (a.gram) pub_wt(acc, C.P.H(2, j), C);
             else wt_load<true>(acc, C.At(j, j - 2), a.lda);
             if (j == 3) pub_op(x, C.P.L(j, j - 3), C);
         }
@@ -1044,7 +1068,8 @@ __device__ __forceinline__ void diag_prefetch(FlowCtx& C, const DiagLds& B, bool
     const FlowArgs& a = C.a;
     const int T = a.T;
     int* done = &B.w()[sub ? DW_PRE6 : DW_PRE7];
-    for (int j = 1; j < T; ++j) {
+    // Gram phase: step 1's tiles came from chain waves 2 / 3, step 2's are in dst (this wave's)
+    for (int j = a.gram ? 2 : 1; j < T; ++j) {
         const int pj = j & 1;
         double* dst = sub ? B.Ap(pj) : B.Cp(pj);
         WTile acc;
@@ -1052,9 +1077,10 @@ __device__ __forceinline__ void diag_prefetch(FlowCtx& C, const DiagLds& B, bool
         if (j >= 4) {
             pub_wt_op_direct(acc, C.P.H(sub ? 0 : 1, j), x, C.P.L(j, j - 3), C);
         } else {
-            double* a0 = sub ? C.At(j, j - 1) : C.At(j, j);   // initial values of the rows <= 3
-            if (a.gram) wt_load<false>(acc, a0, a.lda);       // (flow_gram_phase: this wave wrote them)
-            else wt_load<true>(acc, a0, a.lda);
+            // initial values of the rows <= 3
+            if (a.gram && j == 2) lds_to_wt_ld(acc, dst, S);
+            else if (a.gram) pub_wt(acc, C.P.H(sub ? 0 : 1, j), C);   // a worker wave's FT_G
+            else wt_load<true>(acc, sub ? C.At(j, j - 1) : C.At(j, j), a.lda);
             if (j == 3) pub_op(x, C.P.L(j, j - 3), C);
         }
         if (a.trace && (threadIdx.x & 63) == 0) a.trace[(sub ? 5 : 6) * T + j] = flow_clock() - C.t0;
@@ -1087,6 +1113,46 @@ __device__ __forceinline__ void diag_prefetch(FlowCtx& C, const DiagLds& B, bool
     }
 }
 
+// The diag workgroup's Gram phase (FlowArgs::gram): each wave forms the initial value of what its
+// role starts from, straight into LDS: waves 0 / 4 / 1 the lower 16 x 16 blocks (0,0) / (1,0) /
+// (1,1) of tile (0,0) into the factor's input (waves 4 and 1 count into DW_G0; the factor reads
+// the lower blocks only), chain waves 2 / 3 step 1's A(1,0) / A(1,1) into Ap[1] / Cp[1] (in place
+// of waves 6 / 7's j = 1, signalled through their words), wave 5 A(2,0) into L2[0], waves 6 / 7
+// A(2,1) / A(2,2) into their j = 2 destinations.  Row 3's band tiles are FT_G worker tiles; the
+// rest of the rows <= 3 are FT_A worker tiles.  Measured (tools/flow_trace.py, one call): block
+// (0,0) formed 0.5 -> 5.7 us into the launch (kernel arguments 0.5, X / theta round trip 1.3,
+// dots 1.2, norms 0.6, exp and stores ~1.5), D_0 at ~10-12 us (the first factor runs with a cold
+// instruction cache: ~5 us against ~3.9 in the chain); the base build's chain started at 2.4 us
+// with D_0 from the Gram launch before it.
+__device__ __forceinline__ void diag_gram_phase(const FlowArgs& a, const DiagLds& B, long long t0) {
+    constexpr int S = TileCfg<32>::S;
+    const int w = threadIdx.x >> 6, T = a.T;
+    auto tile = [&](int i, int j, double* dst, int ld, int b0, int b1) {
+        flow_gram_tile<false>(a.X, a.ldxi, a.theta, a.n, a.D, i, j, dst, ld, b0, b1);
+    };
+    auto signal = [&](int word, int v) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if ((threadIdx.x & 63) == 0) lds_put(&B.w()[word], v);
+    };
+    if (w < 2 || w == 4) {
+        // the factor reads the lower blocks only: (0,0) wave 0, (1,0) wave 4, (1,1) wave 1
+        flow_gram_tile<false>(a.X, a.ldxi, a.theta, a.n, a.D, 0, 0, B.fsc(), 33, w == 0 ? 0 : 1, w == 0 ? 1 : 2,
+                              w == 1 ? 2 : 1);
+        if (w != 0) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(&B.w()[DW_G0], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    } else if (w < 4) {
+        if (T > 1) {
+            tile(1, w - 2, w == 2 ? B.Ap(1) : B.Cp(1), S, 0, 2);
+            signal(w == 2 ? DW_PRE6 : DW_PRE7, 1);
+            if (a.trace && (threadIdx.x & 63) == 0 && w == 2) a.trace[2 * T] = flow_clock() - t0;
+        }
+    } else if (T > 2) {
+        tile(2, w - 5, w == 5 ? B.L2(0) : w == 6 ? B.Ap(0) : B.Cp(0), S, 0, 2);
+    }
+}
+
 __device__ __forceinline__ void flow_diag(FlowCtx& C, double* smem) {
     DiagLds B;
     B.base = smem;
@@ -1095,6 +1161,7 @@ __device__ __forceinline__ void flow_diag(FlowCtx& C, double* smem) {
     if (threadIdx.x < 2) B.bad()[threadIdx.x] = 0;
     if (threadIdx.x == 0) C.a.info[0] = 0;   // first writer of info in the evaluation
     __syncthreads();
+    if (C.a.gram) diag_gram_phase(C.a, B, C.t0);
     const int w = threadIdx.x >> 6;
     if (w < 4) diag_chain(C, B);
     else if (w == 4) diag_publisher(C, B);
@@ -1105,27 +1172,28 @@ __device__ __forceinline__ void flow_diag(FlowCtx& C, double* smem) {
 // The Gram phase (FlowArgs::gram), run by every wave before its role, where no role state is live
 // (the tile code inlined into the roles set the kernel's allocation to 254 VGPRs, so no other
 // kernel's wave fit beside the flow on a CU; as a call, 248): each worker wave forms its owned A
-// tiles, and in the diag workgroup wave 0 tile (0,0), wave 5 (2,0) and (3,1), wave 6 (1,0), (2,1),
-// (3,2), wave 7 (1,1), (2,2), (3,3) -- the band tiles of the rows <= 3 its role starts from.  Each
-// wave reads back only what it wrote itself (the stores drained first).
+// tiles (read back only by itself, the stores drained first) and publishes its FT_G band tiles of
+// row 3 to FlowPub::H for the diag waves 5-7 (the catalogue puts those on otherwise idle waves).
+// The diag workgroup has its own (diag_gram_phase).  Forming all band tiles of the rows <= 3 in
+// waves 0 / 5 / 6 / 7 (two or three each) delayed the chain's start by ~25 us a launch; the eight
+// as FT_G worker tiles, ~9.5 us (published ~11 us into the launch: their waves share SIMDs with
+// waves forming their own tiles).
 __device__ __forceinline__ void flow_gram_phase(const FlowArgs& a) {
     const int w = threadIdx.x >> 6;
-    auto tile = [&](int i, int j) {
-        if (i < a.T) flow_gram_tile(a.X, a.ldxi, a.theta, a.n, a.D, i, j, a.A + (long)i * 32 * a.lda + (long)j * 32, a.lda);
-    };
-    if (blockIdx.x == 0) {
-        if (w == 0) tile(0, 0);
-        else if (w == 5) { tile(2, 0); tile(3, 1); }
-        else if (w == 6) { tile(1, 0); tile(2, 1); tile(3, 2); }
-        else if (w == 7) { tile(1, 1); tile(2, 2); tile(3, 3); }
-    } else {
+    {
         const int* own = a.own + ((blockIdx.x - 1) * FLOW_WAVES + w) * FLOW_MAXOWN;
 #pragma unroll 1
         for (int s = 0; s < FLOW_MAXOWN; ++s) {
             const int code = __builtin_amdgcn_readfirstlane(own[s]);
             if (code < 0) continue;
             const FlowTile t = flow_tile(code, a.T);
-            if (t.type == FT_A) tile(t.i, t.j);
+            double* at = a.A + (long)t.i * 32 * a.lda + (long)t.j * 32;
+            if (t.type == FT_A) flow_gram_tile<false>(a.X, a.ldxi, a.theta, a.n, a.D, t.i, t.j, at, a.lda);
+            if (t.type == FT_G) {
+                const FlowPub P{a.pub, a.T, a.Tp};
+                flow_gram_tile<true>(a.X, a.ldxi, a.theta, a.n, a.D, t.i, t.j,
+                                     P.H(t.j == t.i ? 1 : t.j == t.i - 1 ? 0 : 2, t.i), 32);
+            }
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1134,13 +1202,13 @@ __device__ __forceinline__ void flow_gram_phase(const FlowArgs& a) {
 
 __global__ __launch_bounds__(FLOW_THREADS) void k_chol_flow(FlowArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    if (a.gram) flow_gram_phase(a);
     FlowCtx C;
+    C.t0 = flow_clock();
+    if (a.gram && blockIdx.x != 0) flow_gram_phase(a);
     C.a = a;
     C.P.base = a.pub;
     C.P.T = a.T;
     C.P.Tp = a.Tp;
-    C.t0 = flow_clock();
     if (blockIdx.x == 0) {
         flow_diag(C, smem);
         return;

@@ -9,7 +9,8 @@ for small / ragged tile counts and small wave counts (several tiles per wave, wh
 items inside a wave matters)."""
 import pytest
 
-FT_A, FT_R, FT_AL, FT_H = 0, 1, 2, 3
+FT_A, FT_R, FT_AL, FT_H, FT_G = 0, 1, 2, 3, 4
+G_TILES = [(3, 1), (3, 2), (3, 3)]   # flow_gtile (rows 0-2: the diag workgroup's Gram phase)
 MAXOWN = 4
 
 
@@ -24,8 +25,12 @@ def n_a(T):
     return T * (T + 1) // 2 - 9 if T >= 4 else 0
 
 
+def n_g(T):
+    return sum(1 for i, _ in G_TILES if i < T)
+
+
 def ntiles(T, Tp):
-    return n_a(T) + T * (T - 1) // 2 + 2 * T * Tp + (T - 1 if T > 1 else 0)
+    return n_a(T) + T * (T - 1) // 2 + 2 * T * Tp + (T - 1 if T > 1 else 0) + n_g(T)
 
 
 def decode(g, T, Tp):
@@ -44,7 +49,10 @@ def decode(g, T, Tp):
     if g < T * Tp:
         return (FT_AL, g // Tp, g % Tp)
     g -= T * Tp
-    return (FT_H, g + 1, 0)
+    if g < (T - 1 if T > 1 else 0):
+        return (FT_H, g + 1, 0)
+    g -= T - 1
+    return (FT_G,) + G_TILES[g]
 
 
 def tile(code, T):
@@ -58,8 +66,10 @@ def tile(code, T):
         return (j if j < T else 0), i - 2, i, False      # panel i-1 through H_i in the finalize
     if ty == FT_AL:
         return i, T - 1, -1, False
-    return 0, -1, (i if i < T - 1 else -1), False       # FT_H: H_k = D_k L(k,k-1) at level k
-    #                                                     (H_{T-1}: the diag workgroup's publisher)
+    if ty == FT_H:
+        return 0, -1, (i if i < T - 1 else -1), False   # H_k = D_k L(k,k-1) at level k
+        #                                                 (H_{T-1}: the diag workgroup's publisher)
+    return 0, -1, -1, False                             # FT_G: formed in the Gram phase, no items
 
 
 def items(code, T):
@@ -143,8 +153,9 @@ def needs_and_makes(item, T):
 
 def diag_needs(k, T):
     """Diag workgroup, chain step k (waves 5-7 prefetch + chain): what D_k, L(k,k-1), L(k,k-2),
-    X(k,k) wait for.  Tiles of rows <= 3 come from k_gram."""
-    need = []
+    X(k,k) wait for.  Row 3's band tiles are FT_G tiles, published by their owners in the Gram
+    phase at the start of the launch (rows 1-2: the diag workgroup's own)."""
+    need = [("G", 3, j) for j in (1, 2, 3)] if k == 3 else []
     if k >= 4:
         need += [("H", k, k - 2), ("H", k, k - 1), ("H", k, k)]
     if k >= 3:
@@ -158,8 +169,10 @@ def simulate(T, Tp, W, reverse=False):
         own = own[::-1]
     progs = [wave_program(s, T) for s in own]
     done = set()
-    # k_gram's outputs: D_0 published by the diag at start, plus X(0,0)
+    # D_0 (the diag's waves 0/1 form tile (0,0), wave 0 factors it) and X(0,0); the Gram phase's
+    # FT_G publications (before any wave's items: no inputs)
     done |= {("D", 0), ("X", 0, 0)}
+    done |= {("G", c[1], c[2]) for s in own for c in s if c is not None and c[0] == FT_G}
     pos = [0] * len(progs)
     dk = 1
     progress = True

@@ -37,6 +37,8 @@ def main():
     tr = ws[off.value: off.value + 8 * cnt.value].view(torch.int64).cpu().numpy() / 100.0   # us
     st, rdy, fs, pub = tr[:T], tr[T:2 * T], tr[2 * T:3 * T], tr[3 * T:4 * T]
     print(f"info {int(info.item())}  lml {float(out[0]):.6f}")
+    print(f"gram phase (us from launch): wave 0's block of (0,0) {st[0]:.2f}, waves 1 / 4's {rdy[0]:.2f},"
+          f" wave 2's A(1,0) {fs[0]:.2f}")
     r2, pp, qq, l2 = tr[4 * T:5 * T], tr[5 * T:6 * T], tr[6 * T:7 * T], tr[7 * T:8 * T]
     print(" k   start  A'ready  wait  factor  publish  step | got A(k,k-2) A(k,k-1) A(k,k)  L(k,k-2)  (rel. to publish of D_k-3)")
     for k in range(1, T):
