@@ -14,10 +14,10 @@ __host__ __device__ inline int flow_gram_dbg_count(int T) { return 5 * flow_gram
 
 // ---------------------------------------------------------------- tile catalogue
 // code = type << 20 | i << 10 | j ; R tiles use j = column tile c in [0, T + Tp)
-// FT_H: coupling H_k = D_k L(k,k-1); FT_G: the initial value (K + s2 I) of a band tile (3,1),
-// (3,2), (3,3), formed at the launch's start by an otherwise idle worker wave and published to the
-// diag workgroup (FlowArgs::gram)
-enum : int { FT_A = 0, FT_R = 1, FT_AL = 2, FT_H = 3, FT_G = 4 };
+// FT_G: the initial value (K + s2 I) of a band tile (3,1), (3,2), (3,3), formed at the launch's
+// start by an otherwise idle worker wave and published to the diag workgroup (FlowArgs::gram).
+// (Type 3 was the coupling H_k = D_k L(k,k-1) of the earlier R finalize, retired in round 5.)
+enum : int { FT_A = 0, FT_R = 1, FT_AL = 2, FT_G = 4 };
 __host__ __device__ inline int flow_code(int type, int i, int j) { return (type << 20) | (i << 10) | j; }
 
 __host__ __device__ inline void flow_tri(int t, int& i, int& j) {   // row-major lower triangle
@@ -38,7 +38,7 @@ __host__ __device__ inline void flow_gtile(int g, int& i, int& j) {
     j = 1 + g;
 }
 __host__ __device__ inline int flow_ntiles(int T, int Tp) {
-    return flow_nA(T) + T * (T - 1) / 2 + 2 * T * Tp + (T > 1 ? T - 1 : 0) + flow_nG(T);
+    return flow_nA(T) + T * (T - 1) / 2 + 2 * T * Tp + flow_nG(T);
 }
 
 __device__ inline int flow_decode(int g, int T, int Tp) {
@@ -53,9 +53,6 @@ __device__ inline int flow_decode(int g, int T, int Tp) {
     g -= T * Tp;
     if (g < T * Tp) return flow_code(FT_AL, g / Tp, g % Tp);
     g -= T * Tp;
-    const int nH = T > 1 ? T - 1 : 0;
-    if (g < nH) return flow_code(FT_H, g + 1, 0);
-    g -= nH;
     flow_gtile(g, i, j);
     return flow_code(FT_G, i, j);
 }
@@ -81,19 +78,18 @@ __host__ __device__ inline FlowTile flow_tile(int code, int T) {
         }
         else { t.hi = t.j - 1; t.fin = t.j; }
     } else if (t.type == FT_R) {
+        // every panel j .. i-1 as an update (the last one, panel i-1, needs only L(i,i-1), out a
+        // step before D_i), the finalize X(i,c) = D_i R''' merged into it: ONE product after D_i.
+        // (The coupling form D_i R'' - H_i X(i-1,c), H_i = D_i L(i,i-1) a worker item, put three
+        // after it: its column pipelines ran ~10 us behind the chain, the launch's tail 14 us
+        // past D_{T-1}.)
         t.lo = (t.j < T) ? t.j : 0;
-        t.hi = t.i - 2;                         // panel i-1 enters the finalize through H_i
+        t.hi = t.i - 1;
         t.fin = t.i;
     } else if (t.type == FT_AL) {
         t.lo = t.i;
         t.hi = T - 1;
         t.fin = -1;
-    } else if (t.type == FT_H) {   // one item at level k, once D_k is out; the last one (k = T-1) is
-                                   // formed by the diag workgroup itself (nothing else runs there by
-                                   // then), so it has no items
-        t.lo = 0;
-        t.hi = -1;
-        t.fin = t.i < T - 1 ? t.i : -1;
     } else {   // FT_G: no items (formed in the Gram phase at the start)
         t.lo = 0;
         t.hi = -1;

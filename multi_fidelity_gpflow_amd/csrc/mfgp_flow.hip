@@ -388,7 +388,6 @@ struct FlowPub {
         return tile(nL() + T + (c < T ? i * (i + 1) / 2 + c : T * (T + 1) / 2 + i * Tp + (c - T)));
     }
     __device__ double* H(int kind, int k) const { return tile(nL() + T + nX() + 3 * k + kind); }   // 0: (k,k-1) 1: (k,k) 2: (k,k-2)
-    __device__ double* Hk(int k) const { return tile(nL() + T + nX() + 3 * T + k); }   // H_k = D_k L(k,k-1)
 };
 
 struct FlowCtx {
@@ -583,18 +582,6 @@ __device__ __forceinline__ void flow_finalize_acc(FlowCtx& C, const FlowTile& t,
     wt_store<true>(out, C.P.L(t.i, t.j), 32);
 }
 
-// H_k = D_k L(k,k-1) for the L^{-1} / Z finalizes of row block k (a worker item, so the MFMA
-// work stays off the diag workgroup's SIMDs)
-__device__ __forceinline__ void flow_coupling(FlowCtx& C, int k, double* S) {
-    WTile lt, out;
-    WOp d;
-    pub_wt_op(lt, C.P.L(k, k - 1), d, C.P.D(k), C);   // both inputs in one round trip
-    wt_to_lds(lt, S);
-    wt_zero(out);
-    wt_mma_lds_b(out, d, S);                             // A[i][k'] = D_k[i][k'], B[k'][c] = L(k,k-1)[k'][c]
-    wt_store<true>(out, C.P.Hk(k), 32);
-}
-
 // A finalize with no update before it (tiles (i,0))
 __device__ __forceinline__ void flow_finalize(FlowCtx& C, const FlowTile& t, double* S) {
     WTile acc;
@@ -604,43 +591,18 @@ __device__ __forceinline__ void flow_finalize(FlowCtx& C, const FlowTile& t, dou
     flow_finalize_acc(C, t, acc, d, S);
 }
 
-// X(i,c) = D_i R''(i,c) - H_i X(i-1,c): row block i of [L^{-1} | Z], with R'' holding the panels
-// < i-1 and the last one folded in through H_i = D_i L(i,i-1) (diag publishes it), so a column
-// of L^{-1} / Z advances by one product per level once its previous block is out.
-__device__ __forceinline__ void flow_finalize_r(FlowCtx& C, const FlowTile& t, double* S) {
+// X(i,c) = D_i R'''(i,c): row block i of [L^{-1} | Z] from R''' (every panel < i applied) in
+// registers; published transposed first (it feeds the next row's last update and alpha), then
+// stored to Xo; a Z tile also leaves its sum of squares.
+__device__ __forceinline__ void flow_finish_r(FlowCtx& C, const FlowTile& t, const WTile& acc, const WOp& d,
+                                              double* S) {
     const FlowArgs& a = C.a;
     const int T = a.T;
     const int i = t.i;
-    const bool cpl = i >= 1;
-    const double* Pd = C.P.D(i);
-    const double* Ph = C.P.Hk(i);
-    const double* Pq = C.P.X(i - 1, t.j);
-    WOp d, h, q;
-    {   // R'' and the three published operands in one round trip (loads complete in order, so
-        // staging R'' waits for its own loads only).  R's identity block is never stored: a tile
-        // (j+1, j) of it has no update before its finalize, so R'' is its initial value, zero.
-        WTile acc;
-        if (t.j < T && i == t.j + 1) wt_zero(acc);
-        else if (t.j >= T && t.hi < t.lo) flow_y_tile(a, i, t.j - T, acc);   // no update: R'' = Y
-        else wt_load<false>(acc, C.Rt(i, t.j), a.ldr);
-        op_load_pub(d, Pd);
-        if (cpl) {
-            op_load_pub(h, Ph);
-            op_load_pub(q, Pq);
-        }
-        wt_to_lds(acc, S);
-    }
-    // a missing operand is waited for with the one-line probe (hundreds of R / Z finalizes can be
-    // waiting at once: full re-reads of three tiles per poll would flood the fabric)
-    if (op_missing(d)) pub_retry(d, Pd, C);
-    if (cpl) {
-        if (op_missing(h)) pub_retry(h, Ph, C);
-        if (op_missing(q)) pub_retry(q, Pq, C);
-    }
+    wt_to_lds(acc, S);
     WTile out;
     wt_zero(out);
-    wt_mma_lds_b(out, d, S);                             // D_i R''   (B[k][j] = R''[k][j])
-    if (cpl) wt_mma<true>(out, h, q);                    // - H_i X(i-1,c)   (B[k][j] = X^T(i-1,c)[j][k])
+    wt_mma_lds_b(out, d, S);                             // D_i R'''   (B[k][j] = R'''[k][j])
     wt_store_t_sc1(out, C.P.X(i, t.j), 32);              // X^T (published first: it feeds others)
     wt_store<false>(out, C.Xt(i, t.j), a.ldx);
     if (t.j >= T) {
@@ -661,6 +623,15 @@ __device__ __forceinline__ void flow_finalize_r(FlowCtx& C, const FlowTile& t, d
         z2 = wave_sum64(z2);
         if ((threadIdx.x & 63) == 0) a.zpart[i * a.Tp + cy] = z2;
     }
+}
+
+// The R tiles without an update: Z's row block 0, X(0,c) = D_0 Y(0,c)
+__device__ __forceinline__ void flow_finalize_r(FlowCtx& C, const FlowTile& t, double* S) {
+    WTile acc;
+    WOp d;
+    flow_y_tile(C.a, t.i, t.j - C.a.T, acc);
+    pub_op(d, C.P.D(t.i), C);
+    flow_finish_r(C, t, acc, d, S);
 }
 
 // Update at level l; a tile's last update runs straight into its finalize (same registers,
@@ -699,7 +670,12 @@ __device__ __forceinline__ void flow_update(FlowCtx& C, const FlowTile& t, int l
         else wt_load<false>(acc, dst, a.ldr);
         pub_op2(x, C.P.L(t.i, l), y, C.P.X(l, t.j), C);  // L(i,l), X(l,c)^T (B[k][j] = X(l,c)[k][j])
         wt_mma<true>(acc, x, y);                         // R(i,c) -= L(i,l) X(l,c)
-        wt_store<false>(acc, dst, a.ldr);
+        if (l == t.hi) {                                 // panel i-1: the finalize follows (D_i is
+            pub_op_direct(d, C.P.D(t.fin), C);           // published about when L(i,i-1) X(i-1,c) is)
+            flow_finish_r(C, t, acc, d, S);
+        } else {
+            wt_store<false>(acc, dst, a.ldr);
+        }
     } else {
         const int c = t.i, cy = t.j;
         double* al = a.alpha + (long)c * 32 * a.ldal + (long)cy * 32;
@@ -741,14 +717,13 @@ __device__ __forceinline__ void flow_item_log(const FlowCtx& C, int wid, int n, 
     e[3] = t1 - C.t0;
 }
 
-// Slot order of a worker wave: couplings H_k, then A tiles (they feed the chain), nearest the
-// diagonal first; then the R / Y tiles, then alpha.  Items run level by level in this order.
+// Slot order of a worker wave: A tiles (they feed the chain), nearest the diagonal first; then
+// the R / Y tiles, then alpha.  Items run level by level in this order (a merged finalize at level
+// l waits for D_{l+1}: everything of level l that the chain needs must come before it).
 __device__ __forceinline__ int flow_prio(int code) {
     if (code < 0) return 1 << 30;
     const FlowTile t = flow_tile(code, 1024);
-    // H_k first: the R finalizes of the same level wait for it (a later slot would deadlock)
-    const int rank = t.type == FT_H ? 0 : t.type + 1;
-    return (rank << 16) | (t.i << 8) | t.j;
+    return (t.type << 16) | (t.i << 8) | t.j;
 }
 
 __device__ __forceinline__ void flow_worker(FlowCtx& C, int wid, double* S) {
@@ -780,10 +755,9 @@ __device__ __forceinline__ void flow_worker(FlowCtx& C, int wid, double* S) {
             const int cs = pick(s);
             if (cs < 0) continue;
             const FlowTile t = flow_tile(cs, T);
-            if (t.fin == l && (t.type == FT_R || t.hi < t.lo)) {
+            if (t.fin == l && t.hi < t.lo) {
                 const long long i0 = flow_clock(), w0 = C.waited;
                 if (t.type == FT_R) flow_finalize_r(C, t, S);
-                else if (t.type == FT_H) flow_coupling(C, t.i, S);
                 else flow_finalize(C, t, S);
                 flow_item_log(C, wid, nitem++, cs, l, i0, w0);
             }
@@ -1001,16 +975,6 @@ __device__ __forceinline__ void diag_publisher(FlowCtx& C, const DiagLds& B) {
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (l == 0) lds_put(&B.w()[DW_DPUB], k);
-        if (k == T - 1 && k > 0) {
-            // the last coupling H_k = D_k L(k,k-1) from LDS: one hand-off less on the tail
-            WOp dr, lc;
-            op_rows_lds_ld(dr, D, S);                 // A[i][k'] = D_k[i][k']
-            op_cols_lds_ld(lc, B.Ls(pk), S);          // B[k'][c] = L(k,k-1)[k'][c]
-            WTile h;
-            wt_zero(h);
-            wt_mma<false>(h, dr, lc);
-            wt_store<true>(h, C.P.Hk(k), 32);
-        }
     }
 }
 
@@ -1217,7 +1181,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void k_chol_flow(FlowArgs a) {
     flow_worker(C, (blockIdx.x - 1) * FLOW_WAVES + w, smem + w * 32 * WLD);
 }
 
-long flow_npub(int T, int Tp) { return 1024L * (T * (T - 1) / 2 + T + T * (T + 1) / 2 + T * Tp + 4 * T); }
+long flow_npub(int T, int Tp) { return 1024L * (T * (T - 1) / 2 + T + T * (T + 1) / 2 + T * Tp + 3 * T); }
 int flow_nflags(int T, int Tp) { (void)T; (void)Tp; return 1; }   // the abort word
 // layout: chain / helper stamps [8T] | worker summaries + item logs | wave-5 detail [2T] | wave-6 / 7 detail
 // [2T each: last waits done, published] | k_gram timeline [flow_gram_dbg_count(T)] (the last region)

@@ -9,7 +9,7 @@ for small / ragged tile counts and small wave counts (several tiles per wave, wh
 items inside a wave matters)."""
 import pytest
 
-FT_A, FT_R, FT_AL, FT_H, FT_G = 0, 1, 2, 3, 4
+FT_A, FT_R, FT_AL, FT_G = 0, 1, 2, 4
 G_TILES = [(3, 1), (3, 2), (3, 3)]   # flow_gtile (rows 0-2: the diag workgroup's Gram phase)
 MAXOWN = 4
 
@@ -30,7 +30,7 @@ def n_g(T):
 
 
 def ntiles(T, Tp):
-    return n_a(T) + T * (T - 1) // 2 + 2 * T * Tp + (T - 1 if T > 1 else 0) + n_g(T)
+    return n_a(T) + T * (T - 1) // 2 + 2 * T * Tp + n_g(T)
 
 
 def decode(g, T, Tp):
@@ -49,9 +49,6 @@ def decode(g, T, Tp):
     if g < T * Tp:
         return (FT_AL, g // Tp, g % Tp)
     g -= T * Tp
-    if g < (T - 1 if T > 1 else 0):
-        return (FT_H, g + 1, 0)
-    g -= T - 1
     return (FT_G,) + G_TILES[g]
 
 
@@ -63,12 +60,9 @@ def tile(code, T):
             return 0, i - 4, -1, True
         return 0, j - 1, j, False
     if ty == FT_R:
-        return (j if j < T else 0), i - 2, i, False      # panel i-1 through H_i in the finalize
+        return (j if j < T else 0), i - 1, i, False      # every panel, the finalize merged into the last
     if ty == FT_AL:
         return i, T - 1, -1, False
-    if ty == FT_H:
-        return 0, -1, (i if i < T - 1 else -1), False   # H_k = D_k L(k,k-1) at level k
-        #                                                 (H_{T-1}: the diag workgroup's publisher)
     return 0, -1, -1, False                             # FT_G: formed in the Gram phase, no items
 
 
@@ -97,21 +91,20 @@ def owner_table(T, Tp, W):
 
 
 def prio(c):
-    rank = 0 if c[0] == FT_H else c[0] + 1          # flow_prio: H_k before the R finalizes needing it
-    return (rank << 16) | (c[1] << 8) | c[2]
+    return (c[0] << 16) | (c[1] << 8) | c[2]         # flow_prio: A, then R / Y, then alpha
 
 
 def wave_program(slots, T):
     """The item sequence of one worker wave (flow_worker): slots in priority order; per level
-    the stand-alone finalizes (R, H, and A tiles without updates), then the updates (an A tile's
-    last update carries its finalize)."""
+    the stand-alone finalizes (tiles without updates), then the updates (an A or R tile's last
+    update carries its finalize)."""
     slots = sorted([c for c in slots if c is not None], key=prio)
     last = max([max(tile(c, T)[1], tile(c, T)[2]) for c in slots] or [-1])
     prog = []
     for l in range(last + 1):
         for c in slots:
             lo, hi, fin, _ = tile(c, T)
-            if fin == l and (c[0] in (FT_R, FT_H) or hi < lo):
+            if fin == l and hi < lo:
                 prog.append(("fin", c, l))
         for c in slots:
             lo, hi, fin, _ = tile(c, T)
@@ -127,15 +120,7 @@ def needs_and_makes(item, T):
     need, make = [], []
     if kind == "fin":                                 # stand-alone finalize
         need.append(("D", fin))
-        if ty == FT_A:
-            make.append(("L", i, j))
-        elif ty == FT_H:
-            need.append(("L", i, i - 1))
-            make.append(("Hk", i))
-        else:                                         # X(i,c) = D_i R'' - H_i X(i-1,c)
-            if i >= 1:
-                need += [("Hk", i), ("X", i - 1, j)]
-            make.append(("X", i, j))
+        make.append(("L", i, j) if ty == FT_A else ("X", i, j))   # X(0,c) = D_0 Y(0,c)
         return need, make
     if ty == FT_A:
         need += [("L", i, l), ("L", j, l)]
@@ -146,6 +131,9 @@ def needs_and_makes(item, T):
             make.append(("H", i, j))
     elif ty == FT_R:
         need += [("L", i, l), ("X", l, j)]
+        if l == hi:                                   # merged finalize X(i,c) = D_i R'''
+            need.append(("D", fin))
+            make.append(("X", i, j))
     else:
         need += [("X", l, i), ("X", l, T + j)]
     return need, make
@@ -181,8 +169,6 @@ def simulate(T, Tp, W, reverse=False):
         # diag chain: step k needs the chain's own L(k-1,k-2) etc. (internal) and the band inputs
         while dk < T and all(n in done for n in diag_needs(dk, T)):
             done |= {("D", dk), ("X", dk, dk), ("L", dk, dk - 1)}
-            if dk == T - 1:
-                done.add(("Hk", dk))
             if dk >= 2:
                 done.add(("L", dk, dk - 2))
             dk += 1
