@@ -918,6 +918,26 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
     const int m1 = grad_m1(a.T, m0, a.chunk);
     auto Xt = [&](int r, int c) { return a.Xo + (long)r * NB * a.ldx + (long)c * NB; };
 
+    // The epilogue's inputs (raw rows of tiles i and j, 1 / l^2) are loaded now, into registers,
+    // and land in LDS after the operand stream: their round trip hides under it instead of
+    // following it.  (NB (D + 1) <= 2 x 256 entries each; larger D loads the rest afterwards.)
+    constexpr int GPRE = 2;
+    const int nraw = NB * (a.D + 1);
+    double pvi[GPRE], pvj[GPRE];
+#pragma unroll
+    for (int s = 0; s < GPRE; ++s) {
+        const int e = threadIdx.x + s * NTHREADS;
+        const int r = e / (a.D + 1), d = e % (a.D + 1);
+        const int gi = i * NB + r, gj = j * NB + r;
+        pvi[s] = (e < nraw && gi < a.n) ? a.X[(long)gi * a.ldxx + d] : 0.0;
+        pvj[s] = (e < nraw && gj < a.n) ? a.X[(long)gj * a.ldxx + d] : 0.0;
+    }
+    double pl = 1.0;
+    if (threadIdx.x < nsrc * a.D) {
+        const int src = threadIdx.x / a.D, d = threadIdx.x % a.D;
+        pl = a.nlf ? a.theta[src * (1 + a.D) + 1 + d] : (src == 0 ? th.lL(d) : th.lD(d));
+    }
+
     // W_ij (tile) = [alpha_i alpha_j^T] - P * sum_m Linv_mi^T Linv_mj  (= -P * acc below)
     Acc<NB> acc;
     acc_zero(acc);
@@ -989,18 +1009,27 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
     }
 
     // stage the raw inputs of the two row tiles (operand buffers are free now)
-    for (int e = threadIdx.x; e < NB * (a.D + 1); e += NTHREADS) {
+    auto stage = [&](int e, double vi, double vj) {
         const int r = e / (a.D + 1), d = e % (a.D + 1);
         const int gi = i * NB + r, gj = j * NB + r;
-        const double vi = (gi < a.n) ? a.X[(long)gi * a.ldxx + d] : 0.0;
-        const double vj = (gj < a.n) ? a.X[(long)gj * a.ldxx + d] : 0.0;
         if (d < a.D) { xi[r * XS + d] = vi; xj[r * XS + d] = vj; }
         else if (a.nlf) {   // graph kernel: source index
             fi[r] = (gi < a.n) ? (double)graph_source(vi, a.nlf) : -1.0;
             fj[r] = (gj < a.n) ? (double)graph_source(vj, a.nlf) : -1.0;
         } else { fi[r] = (gi < a.n) ? vi : -1.0; fj[r] = (gj < a.n) ? vj : -1.0; }
+    };
+#pragma unroll
+    for (int s = 0; s < GPRE; ++s) {
+        const int e = threadIdx.x + s * NTHREADS;
+        if (e < nraw) stage(e, pvi[s], pvj[s]);
     }
-    for (int e = threadIdx.x; e < nsrc * a.D; e += NTHREADS) {
+    for (int e = threadIdx.x + GPRE * NTHREADS; e < nraw; e += NTHREADS) {
+        const int r = e / (a.D + 1), d = e % (a.D + 1);
+        const int gi = i * NB + r, gj = j * NB + r;
+        stage(e, (gi < a.n) ? a.X[(long)gi * a.ldxx + d] : 0.0, (gj < a.n) ? a.X[(long)gj * a.ldxx + d] : 0.0);
+    }
+    if (threadIdx.x < nsrc * a.D) il2[threadIdx.x] = 1.0 / (pl * pl);
+    for (int e = threadIdx.x + NTHREADS; e < nsrc * a.D; e += NTHREADS) {
         const int src = e / a.D, d = e % a.D;
         const double l = a.nlf ? a.theta[src * (1 + a.D) + 1 + d] : (src == 0 ? th.lL(d) : th.lD(d));
         il2[e] = 1.0 / (l * l);
