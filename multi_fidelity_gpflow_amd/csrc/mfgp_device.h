@@ -889,4 +889,33 @@ __device__ __forceinline__ void exp4(double (&x)[4]) {
     }
 }
 
+// exp(x) for the kernels' exp(-r2/2) weights, bitwise the device library's exp (the same range
+// reduction, degree-11 polynomial and ldexp; the overflow select is moot for x <= 1024 and the
+// underflow one is what ldexp does below -1075).  Every polynomial step is ONE v_fma_f64 with its
+// coefficient in an SGPR pair: the library form accumulates into a VGPR copy of each coefficient
+// (a v_mov_b64 per step), and in a loop the compiler keeps all eleven copies live (~24 VGPRs,
+// ~12 extra instructions an exp).
+__device__ __forceinline__ double fma_s(double a, double b, double c) {
+    double d;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
+    return d;
+}
+__device__ __forceinline__ double exp_lib(double x) {
+    const double n = __builtin_rint(x * dbits(0x3ff71547652b82feull));
+    double r = fma_s(n, dbits(0xbfe62e42fefa39efull), x);
+    r = fma_s(n, dbits(0xbc7abc9e3b39803full), r);
+    double p = fma_s(r, dbits(0x3e5ade156a5dcb37ull), dbits(0x3e928af3fca7ab0cull));
+    p = fma_s(r, p, dbits(0x3ec71dee623fde64ull));
+    p = fma_s(r, p, dbits(0x3efa01997c89e6b0ull));
+    p = fma_s(r, p, dbits(0x3f2a01a014761f6eull));
+    p = fma_s(r, p, dbits(0x3f56c16c1852b7b0ull));
+    p = fma_s(r, p, dbits(0x3f81111111122322ull));
+    p = fma_s(r, p, dbits(0x3fa55555555502a1ull));
+    p = fma_s(r, p, dbits(0x3fc5555555555511ull));
+    p = fma_s(r, p, dbits(0x3fe000000000000bull));
+    p = fma_s(r, p, 1.0);
+    p = fma_s(r, p, 1.0);
+    return __builtin_ldexp(p, (int)n);
+}
+
 }  // namespace mfgp

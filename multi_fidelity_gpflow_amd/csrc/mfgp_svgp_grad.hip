@@ -447,19 +447,25 @@ __global__ __launch_bounds__(NTHREADS) void k_gw(const double* r, const double* 
 // Workgroup: 32 a rows x KG_COLS b columns; wave w: rows 16 (w & 1) .., b half w >> 1; the b rows
 // go through LDS KG_CHUNK per half at a time, W is loaded one step ahead.
 constexpr int KG_ROWS = 32, KG_COLS = 256, KG_CHUNK = 32;
+// Registers held to three waves per SIMD (168 VGPRs, no spills; unbounded the allocator took 148
+// VGPRs + AGPRs, two waves): 2.714 -> 2.672 ms a Goku SVGP step; four waves (10 spills) 2.675.
+constexpr int KG_WAVES = 3;
 template <int DC>
 constexpr int kg_ncb() { return (2 * DC + 1 + 15) / 16; }
 
 template <int DC>
-__global__ __launch_bounds__(NTHREADS) void k_kgrad(const double* P1, long ld1, int n1, const double* P2, long ld2,
+__global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(KG_WAVES))) void k_kgrad(const double* P1, long ld1, int n1, const double* P2, long ld2,
                                                     int n2, const double* Wt, long ldw, long sW, const double* thetas,
                                                     int G, int D, double zf, int nbc, double* gth_part,
                                                     double* gz_part) {
-    constexpr int NCB = kg_ncb<DC>(), SC = NCB * 16 + 1, XS = DC + 1;
-    constexpr int SACC = (NTHREADS / 64) * 16 * SC, XST = 2 * KG_CHUNK * XS;
+    constexpr int NCB = kg_ncb<DC>(), SC = NCB * 16 + 1, XS = DC + 1, NS = DC / 4;
+    static_assert(DC % 4 == 0, "dimension chunks of the distance MFMA");
+    constexpr int BS = NCB * 16 + 1;                                   // [1 | x | x^2] row stride
+    constexpr int SACC = (NTHREADS / 64) * 16 * SC, XST = 2 * KG_CHUNK * (XS + 2 + BS);
     __shared__ double il[DC], id[DC], cz[DC];
-    // the b rows of a chunk (centred; column DC holds the fidelity) during the pair loop, the
-    // moment accumulators after it
+    // the b rows of a chunk during the pair loop -- [half][row][XS] centred coordinates (column DC
+    // the fidelity), [half][row][2] their scaled squared norms, [half][row][BS] the B operand rows
+    // [1 | x | x^2] of the moment GEMM -- and the moment accumulators after it
     __shared__ double lds_buf[SACC > XST ? SACC : XST];
     auto sacc = reinterpret_cast<double(*)[16][SC]>(lds_buf);
     __shared__ double wred[NTHREADS / 64][4];
@@ -494,20 +500,42 @@ __global__ __launch_bounds__(NTHREADS) void k_kgrad(const double* P1, long ld1, 
     const int bbase = bc * KG_COLS;
     const int bend = min(n2, bbase + KG_COLS);
     const double* wrow = Wt + lat * sW + (long)a * ldw;
-    // b rows are staged KG_CHUNK per half at a time: [half][row][XS].  The pair weights of the next
-    // chunk are loaded (into registers) while this chunk's pairs are processed: loaded one step
-    // ahead, the strided W loads left every step waiting on a memory round trip.
-    constexpr int NST = KG_CHUNK / 4;
+    // Pairs in 16 x 16 blocks (16 a rows of the wave x 16 b rows of its half): the distances
+    // |za - xb|^2 / l^2 = |za/l|^2 + |xb/l|^2 - 2 (za/l).(xb/l) with the dot products on the matrix
+    // core (NS = DC / 4 steps of v_mfma_f64_16x16x4; lane (li, lq) then holds the pairs (a = li,
+    // b = lq + 4 r)), which are exactly the A-operand positions of the moment GEMM's step r: the
+    // VALU keeps one exp per pair (two for HF x HF pairs) and the weights.  (The direct-difference
+    // loop spent ~157 VALU instructions per 64 pairs; k_kgrad was 12.9% of a Goku SVGP step.)
+    // b rows are staged KG_CHUNK per half at a time.  The pair weights of the next chunk are loaded
+    // (into registers) while this chunk's pairs are processed.
     const int bhalf = bbase + (KG_COLS / 2) * half;
-    auto wload = [&](int c0, double* wv) {
+    // the 4 weights (b = b0 + 4 r + lk) of a block: unconditional loads (W is padded), then the mask
+    auto wload = [&](int b0, double* wv) {
 #pragma unroll
-        for (int s = 0; s < NST; ++s) {
-            const int b = bhalf + c0 + 4 * s + lk;
-            wv[s] = (aval && b < bend) ? wrow[b] : 0.0;
+        for (int r = 0; r < 4; ++r) {
+            const int b = b0 + 4 * r + lk;
+            const double w = wrow[min(b, bend - 1)];
+            wv[r] = (aval && b < bend) ? w : 0.0;
         }
     };
-    double wc[NST], wn[NST];
-    wload(0, wc);
+    double zl[NS], zd[NS];
+    double na = 0.0, nad = 0.0;
+#pragma unroll
+    for (int d = 0; d < DC; ++d) {
+        const double u = za[d] * il[d], v = za[d] * id[d];
+        na = fma(u, u, na);
+        nad = fma(v, v, nad);
+    }
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+        zl[q] = za[4 * q + lk] * il[4 * q + lk];
+        zd[q] = za[4 * q + lk] * id[4 * q + lk];
+    }
+    double* xsb = lds_buf;                                  // [2][KG_CHUNK][XS]
+    double* nrm = xsb + 2 * KG_CHUNK * XS;                  // [2][KG_CHUNK][2]
+    double* bop = nrm + 2 * KG_CHUNK * 2;                   // [2][KG_CHUNK][BS]
+    double wc[4], wn[4];
+    wload(bhalf, wc);
     for (int c0 = 0; c0 < KG_COLS / 2; c0 += KG_CHUNK) {
         __syncthreads();   // the previous chunk is consumed
         for (int e = t; e < 2 * KG_CHUNK * XS; e += NTHREADS) {
@@ -519,66 +547,99 @@ __global__ __launch_bounds__(NTHREADS) void k_kgrad(const double* P1, long ld1, 
                 if (d < D) v = P2[(long)b * ld2 + d] - cz[d];
                 else if (d == DC) v = P2[(long)b * ld2 + D];
             }
-            lds_buf[e] = v;
+            xsb[e] = v;
         }
         __syncthreads();
-        if (c0 + KG_CHUNK < KG_COLS / 2) wload(c0 + KG_CHUNK, wn);   // in flight under this chunk's pairs
-        const double* xs = lds_buf + half * KG_CHUNK * XS;
-        const int bh0 = bhalf + c0;
-#pragma unroll 1
-        for (int s4 = 0; s4 < KG_CHUNK; s4 += 4) {
-            const int r = s4 + lk, b = bh0 + r;
-            double wv = wc[0];   // (the chunk's weights rotate through wc: a rolled loop, static indices)
-#pragma unroll
-            for (int s = 0; s + 1 < NST; ++s) wc[s] = wc[s + 1];
-            const double* xr = xs + r * XS;
-            const double fb = xr[DC];
-            const bool Lb = (fb == 0.0), Hb = (fb == 1.0);
-            if (!(Lb || Hb)) wv = 0.0;
-            double rL = 0.0;
+        for (int e = t; e < 2 * KG_CHUNK * NCB * 16; e += NTHREADS) {
+            const int hr = e / (NCB * 16), j = e % (NCB * 16);   // hr = hf * KG_CHUNK + r
+            const int hf = hr / KG_CHUNK, r = hr % KG_CHUNK;
+            const int b = bbase + (KG_COLS / 2) * hf + c0 + r;
+            const double* xr = xsb + hr * XS;
+            double bv = 0.0;
+            if (j == 0) bv = (b < bend) ? 1.0 : 0.0;
+            else if (j <= D) bv = xr[j - 1];
+            else if (j <= 2 * D) {
+                const double x = xr[j - 1 - D];
+                bv = x * x;
+            }
+            bop[hr * BS + j] = bv;
+        }
+        if (t < 2 * KG_CHUNK) {   // wave 0: the scaled squared norms of the chunk's rows
+            const double* xr = xsb + t * XS;
+            double nl = 0.0, nd = 0.0;
 #pragma unroll
             for (int d = 0; d < DC; ++d) {
-                const double xl = (za[d] - xr[d]) * il[d];
-                rL = fma(xl, xl, rL);
+                const double u = xr[d] * il[d], v = xr[d] * id[d];
+                nl = fma(u, u, nl);
+                nd = fma(v, v, nd);
             }
-            const double sb = Lb ? 1.0 : rho;
-            const double eL = exp(-0.5 * rL);   // dk/dvL (TF form: finite where vL underflows)
-            const double kL = vL * eL;
-            const double wl = wv * sa * sb * kL;
-            gvL += wv * sa * sb * eL;
-            grho += wv * ((Ha ? sb : 0.0) + (Hb ? sa : 0.0)) * kL;
-            const bool hh = Ha && Hb && wv != 0.0;
-            const bool anyhh = __ballot(hh) != 0;   // wave-uniform
-            double wd = 0.0;
-            if (anyhh) {
-                double rD = 0.0;
+            nrm[t * 2] = nl;
+            nrm[t * 2 + 1] = nd;
+        }
+        __syncthreads();
+        const double* xs = xsb + half * KG_CHUNK * XS;
+        const double* nr = nrm + half * KG_CHUNK * 2;
+        const double* bo = bop + half * KG_CHUNK * BS;
 #pragma unroll
-                for (int d = 0; d < DC; ++d) {
-                    const double xd = (za[d] - xr[d]) * id[d];
-                    rD = fma(xd, xd, rD);
-                }
-                const double we = hh ? wv * exp(-0.5 * rD) : 0.0;
-                wd = we * vD;
+        for (int blk = 0; blk < KG_CHUNK / 16; ++blk) {
+            const int rb = 16 * blk;
+            if (bhalf + c0 + rb >= bend) break;             // wave-uniform: past the last b row
+            wload(bhalf + c0 + rb + 16, wn);                 // the next block's weights, in flight meanwhile
+            f64x4 dl = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int q = 0; q < NS; ++q)
+                dl = __builtin_amdgcn_mfma_f64_16x16x4f64(xs[(rb + li) * XS + 4 * q + lk] * il[4 * q + lk], zl[q], dl, 0, 0, 0);
+            // step r: the lane's pair (a = li, b = rb + 4 r + lk); its weight is the A operand of
+            // the moment GEMM's step r, B = [1 | x | x^2] of b
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int bl = rb + lk + 4 * r;
+                const double fb = xs[bl * XS + DC];
+                const bool Lb = (fb == 0.0), Hb = (fb == 1.0);
+                const double wv = (Lb || Hb) ? wc[r] : 0.0;
+                const double rL = fmax(na + nr[2 * bl] - 2.0 * dl[r], 0.0);
+                const double sb = Lb ? 1.0 : rho;
+                const double eL = exp_lib(-0.5 * rL);   // dk/dvL (TF form: finite where vL underflows)
+                const double kL = vL * eL;
+                const double wl = wv * sa * sb * kL;
+                gvL += wv * sa * sb * eL;
+                grho += wv * ((Ha ? sb : 0.0) + (Hb ? sa : 0.0)) * kL;
+#pragma unroll
+                for (int c = 0; c < NCB; ++c)
+                    accL[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(wl, bo[(rb + 4 * r + lk) * BS + 16 * c + li], accL[c], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) wc[r] = wn[r];
+        }
+        // HF x HF pairs (the delta kernel), in a pass of their own: few blocks hold any (Goku: X's
+        // HF rows are its last 36), and the hot pass above keeps its accumulators in place
+#pragma unroll
+        for (int blk = 0; blk < KG_CHUNK / 16; ++blk) {
+            const int rb = 16 * blk;
+            if (bhalf + c0 + rb >= bend) break;
+            bool hany = false;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) hany |= Ha && xs[(rb + lk + 4 * r) * XS + DC] == 1.0;
+            if (__ballot(hany) == 0) continue;   // wave-uniform
+            double wh[4];
+            wload(bhalf + c0 + rb, wh);
+            f64x4 dd = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int q = 0; q < NS; ++q)
+                dd = __builtin_amdgcn_mfma_f64_16x16x4f64(xs[(rb + li) * XS + 4 * q + lk] * id[4 * q + lk], zd[q], dd, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int bl = rb + lk + 4 * r;
+                const bool hh = Ha && xs[bl * XS + DC] == 1.0 && wh[r] != 0.0;
+                const double rD = fmax(nad + nr[2 * bl + 1] - 2.0 * dd[r], 0.0);
+                const double we = hh ? wh[r] * exp_lib(-0.5 * rD) : 0.0;
                 gvD += we;
-            }
-            // B operand: column j of [1 | x | x^2] of row b_k (rows past the end are zero and
-            // carry zero weight)
 #pragma unroll
-            for (int c = 0; c < NCB; ++c) {
-                const int j = 16 * c + li;
-                double bv = 0.0;
-                if (j == 0) bv = (b < bend) ? 1.0 : 0.0;
-                else if (j <= D) bv = xr[j - 1];
-                else if (j <= 2 * D) {
-                    const double x = xr[j - 1 - D];
-                    bv = x * x;
-                }
-                accL[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(wl, bv, accL[c], 0, 0, 0);
-                if (anyhh) accD[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(wd, bv, accD[c], 0, 0, 0);
+                for (int c = 0; c < NCB; ++c)
+                    accD[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(we * vD, bo[(rb + 4 * r + lk) * BS + 16 * c + li], accD[c], 0, 0, 0);
             }
         }
-#pragma unroll
-        for (int s = 0; s < NST; ++s) wc[s] = wn[s];
     }
     __syncthreads();   // lds_buf becomes the moment buffer
     // scalar theta partials: one LDS slot per wave
