@@ -169,6 +169,11 @@ struct BgemmArgs {
     // amask 1: op(A) lower (k-tile <= row tile), 2: op(A) upper (k-tile >= row tile);
     // bmask 1: op(B) lower (k-tile >= column tile), 2: op(B) upper (k-tile <= column tile)
     int amask, bmask;
+    // column statistics of the output (NB = 32, k_bgemm2 only; nullptr: none), one partial per
+    // 32-row output tile: csq[(b Mt + ti) ldcs + j] = sum over the tile's rows of D^2, and with
+    // qv, csq2 likewise of D[i][j] qv[i qs + b] over rows i < qn (the SVGP conditional's moments)
+    double* csq; double* csq2; long ldcs;
+    const double* qv; long qs; int qn;
 };
 void launch_bgemm(int nb, hipStream_t st, int ta, int tb, const BgemmArgs& a, int batch);
 

@@ -347,14 +347,6 @@ __global__ __launch_bounds__(NTHREADS) void k_svgp_cond2(const double* Xo, const
     }
 }
 
-static bool svgp_cond2_on() {
-    static const int on = [] {
-        const char* e = getenv("MFGP_BGEMM2");
-        return e ? atoi(e) : 1;
-    }();
-    return on != 0;
-}
-
 // g_mu[l][n], g_var[l][n] from the partials (+ Kff = K_diag_l(X))
 __global__ void k_svgp_moments(const double* pa, const double* pb, const double* pm, const double* X, long ldx,
                                const double* thetas, int G, int D, int n, int npad, int Tm, double* g_mu,
@@ -489,6 +481,12 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
     const SvgpLayout S = svgp_layout(NB, n, m, L, p, d, ws);
     if (ws_bytes < S.bytes) return -2;
     const long mm = (long)S.mpad * S.mpad;
+    // The gradient pass keeps A and B (Aout / Bout) anyway, so there they come from two batched
+    // GEMMs, A = Li Kuf (Li lower) and B = Lq^T A (Lq^T upper): 2 x 8.5 GF at Goku (L = 64)
+    // against the fused conditional's 8.5 + 17 (B = C Kuf with the full C = Lq^T Li, which it
+    // needs to form A and B in one tile loop without keeping A), and no C.  The column moments
+    // come out of the GEMMs' epilogues in the fused kernel's partial layout and order.
+    const bool two_gemm = NB == 32 && Aout != nullptr;
     (void)hipMemsetAsync(info, 0, sizeof(int) * L, s);
     // Kuu_l (+ jitter) by the lean Gram launch, then the first diagonal factor of every latent as a
     // launch of its own (fused into the Gram it set that launch's register allocation: 3.3% of a
@@ -514,8 +512,9 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
         launch_chol_steps<NB>(c, L, s);
         hipLaunchKernelGGL(k_zero_upper_tiles, dim3(blocks, 1, L), dim3(256), 0, s, S.Xo, NB, S.mpad, mm);
         hipLaunchKernelGGL(k_lq_pad, dim3(blocks, 1, L), dim3(256), 0, s, q_sqrt, m, S.mpad, S.Lq);
-        hipLaunchKernelGGL(k_lqt_linv<NB>, dim3(S.Tm * S.Tm, 1, L), dim3(NTHREADS),
-                           2 * sizeof(double) * NB * (NB + 2), s, S.Lq, S.Xo, S.C, S.Tm);
+        if (!(two_gemm))   // C = Lq^T Li: the fused conditional's B = C Kuf
+            hipLaunchKernelGGL(k_lqt_linv<NB>, dim3(S.Tm * S.Tm, 1, L), dim3(NTHREADS),
+                               2 * sizeof(double) * NB * (NB + 2), s, S.Lq, S.Xo, S.C, S.Tm);
     }
     // Kuf_l = K_l(Z, X), zero padded to Mpad x Npad
     {
@@ -527,7 +526,27 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
         g.padded = 0; g.tiles_c = S.Tn; g.diag_add = 0.0;
         launch_gram_dense(g, L, S.mpad, S.npad, s);   // zero padding written by the kernel
     }
-    if (NB == 32 && svgp_cond2_on()) {
+    if (two_gemm) {
+        const long mn = (long)S.mpad * S.npad;
+        BgemmArgs ga{};
+        ga.amask = 1;   // Li lower
+        ga.A = S.Xo; ga.lda = S.mpad; ga.sA = mm;
+        ga.B = S.Kuf; ga.ldb = S.npad; ga.sB = mn;
+        ga.D = Aout; ga.ldd = S.npad; ga.sD = mn;
+        ga.alpha = 1.0;
+        ga.Mt = S.Tm; ga.Nt = S.Tn; ga.Kt = S.Tm;
+        ga.csq = S.pa; ga.csq2 = S.pm; ga.ldcs = S.npad; ga.qv = q_mu; ga.qs = L; ga.qn = m;
+        launch_bgemm(NB, s, 0, 0, ga, L);
+        BgemmArgs gb{};
+        gb.amask = 2;   // Lq^T upper
+        gb.A = S.Lq; gb.lda = S.mpad; gb.sA = mm;
+        gb.B = Aout; gb.ldb = S.npad; gb.sB = mn;
+        gb.D = Bout; gb.ldd = S.npad; gb.sD = mn;
+        gb.alpha = 1.0;
+        gb.Mt = S.Tm; gb.Nt = S.Tn; gb.Kt = S.Tm;
+        gb.csq = S.pb; gb.ldcs = S.npad;
+        launch_bgemm(NB, s, 1, 0, gb, L);
+    } else if (NB == 32) {
         static bool attr = false;
         if (!attr) {
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_svgp_cond2),

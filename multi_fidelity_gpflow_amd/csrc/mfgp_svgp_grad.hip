@@ -231,19 +231,37 @@ __global__ __launch_bounds__(NTHREADS) void k_bgemm2(BgemmArgs a) {
                 if (a.tril && j > i) v = 0.0;
                 Dt[(long)i * a.ldd + j] = v;
             }
-}
-
-static bool bgemm2_on() {
-    static const int on = [] {
-        const char* e = getenv("MFGP_BGEMM2");
-        return e ? atoi(e) : 1;
-    }();
-    return on != 0;
+    if (a.csq) {   // column partials of the tile: rows 0-15 then 16-31, as k_svgp_cond2's
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            double ta = 0.0, tm = 0.0;
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                double sa = 0.0, sm = 0.0;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int gr = ti * NB + 16 * p + lk + 4 * r;
+                    const double v = acc[p][q][r];
+                    sa += v * v;
+                    if (a.csq2) sm += v * ((gr < a.qn) ? a.qv[(long)gr * a.qs + b] : 0.0);
+                }
+                sa += __shfl_xor(sa, 16, 64); sa += __shfl_xor(sa, 32, 64);
+                sm += __shfl_xor(sm, 16, 64); sm += __shfl_xor(sm, 32, 64);
+                ta += sa;
+                tm += sm;
+            }
+            if (lk == 0) {
+                const long o = ((long)b * a.Mt + ti) * a.ldcs + (long)tj * NB + 16 * q + li;
+                a.csq[o] = ta;
+                if (a.csq2) a.csq2[o] = tm;
+            }
+        }
+    }
 }
 
 template <int NB>
 static void bgemm(hipStream_t st, int ta, int tb, const BgemmArgs& a, int batch) {
-    if (NB == 32 && bgemm2_on()) {
+    if (NB == 32) {
         static bool attr = false;
         if (!attr) {
             for (const void* f : {reinterpret_cast<const void*>(&k_bgemm2<false, false>),
