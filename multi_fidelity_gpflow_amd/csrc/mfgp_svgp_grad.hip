@@ -96,13 +96,13 @@ size_t bgemm_smem(int nb) { return 2 * sizeof(double) * (size_t)nb * (nb + 2); }
 // The same products on NB = 32 operands, a 64 x 64 output block per workgroup: wave w computes
 // the 32 x 32 tile (2 bi + (w >> 1), 2 bj + (w & 1)) as 2 x 2 independent 16 x 16 accumulators
 // (k_bgemm: one 16 x 16 chain per wave), and each k-tile's two A tiles and two B tiles are staged
-// in LDS once for all four waves (twice k_bgemm's operand reuse), double-buffered, the next
-// k-tile's global loads issued into registers before the current products.  Every 16 x 16 block
+// in LDS once for all four waves (twice k_bgemm's operand reuse), one buffer, the next k-tile's
+// global loads issued into registers before the current products.  Every 16 x 16 block
 // runs the same MFMA sequence as tile_mma<32> (k-tiles ascending, 4-deep steps ascending, alpha
 // on the A operand), so the results are bitwise k_bgemm's.  Edge blocks (odd Mt / Nt) load a
 // clamped in-range tile for the missing half and store nothing from it.
 constexpr int BG2_E = 32 * 34;   // one 32-tile in LDS (TileCfg<32>)
-size_t bgemm2_smem() { return 2 * 4 * sizeof(double) * (size_t)BG2_E; }
+size_t bgemm2_smem() { return 4 * sizeof(double) * (size_t)BG2_E; }
 
 template <bool TA, bool TB>
 __global__ __launch_bounds__(NTHREADS) void k_bgemm2(BgemmArgs a) {
@@ -178,40 +178,37 @@ __global__ __launch_bounds__(NTHREADS) void k_bgemm2(BgemmArgs a) {
     for (int p = 0; p < 2; ++p)
 #pragma unroll
         for (int q = 0; q < 2; ++q) acc[p][q] = f64x4{0.0, 0.0, 0.0, 0.0};
-    if (kb1 > kb0) {
-        double* buf0 = smem;
-        double* buf1 = smem + 4 * BG2_E;
-        fetch(kb0);
-        put(buf0, kb0);
-        if (kb0 + 1 < kb1) fetch(kb0 + 1);
-        __syncthreads();
-        for (int kt = kb0; kt < kb1; ++kt) {
-            double* cur = ((kt - kb0) & 1) ? buf1 : buf0;
-            double* nxt = ((kt - kb0) & 1) ? buf0 : buf1;
-            if (kt >= kw0 && kt < kw1) {   // wave-uniform
-                const double* As = cur + (w >> 1) * BG2_E;
-                const double* Bs = cur + (2 + (w & 1)) * BG2_E;
+    auto mma_tile = [&](const double* cur) {
+        const double* As = cur + (w >> 1) * BG2_E;
+        const double* Bs = cur + (2 + (w & 1)) * BG2_E;
 #pragma unroll 4
-                for (int k0 = 0; k0 < NB; k0 += 4) {
-                    const int k = k0 + lk;
-                    double av[2], bv[2];
+        for (int k0 = 0; k0 < NB; k0 += 4) {
+            const int k = k0 + lk;
+            double av[2], bv[2];
 #pragma unroll
-                    for (int t = 0; t < 2; ++t) {
-                        const int i = 16 * t + li, j = 16 * t + li;
-                        av[t] = a.alpha * (TA ? As[k * S + i] : As[i * S + k]);
-                        bv[t] = TB ? Bs[j * S + k] : Bs[k * S + j];
-                    }
-#pragma unroll
-                    for (int p = 0; p < 2; ++p)
-#pragma unroll
-                        for (int q = 0; q < 2; ++q)
-                            acc[p][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[p], bv[q], acc[p][q], 0, 0, 0);
-                }
+            for (int t = 0; t < 2; ++t) {
+                const int i = 16 * t + li, j = 16 * t + li;
+                av[t] = a.alpha * (TA ? As[k * S + i] : As[i * S + k]);
+                bv[t] = TB ? Bs[j * S + k] : Bs[k * S + j];
             }
-            if (kt + 1 < kb1) {
-                put(nxt, kt + 1);
-                if (kt + 2 < kb1) fetch(kt + 2);
-            }
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+#pragma unroll
+                for (int q = 0; q < 2; ++q)
+                    acc[p][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[p], bv[q], acc[p][q], 0, 0, 0);
+        }
+    };
+    if (kb1 > kb0) {
+        // one LDS buffer, the next k-tile's loads in registers meanwhile: 35 KB of LDS, four
+        // workgroups per CU (the double-buffered form's 70 KB held two: these GEMMs have 5-37
+        // k-tiles, so a workgroup's load prologue and store epilogue need company to hide;
+        // Goku SVGP step 2.626 -> 2.370 ms)
+        fetch(kb0);
+        for (int kt = kb0; kt < kb1; ++kt) {
+            put(smem, kt);
+            if (kt + 1 < kb1) fetch(kt + 1);
+            __syncthreads();
+            if (kt >= kw0 && kt < kw1) mma_tile(smem);   // wave-uniform
             __syncthreads();
         }
     }
