@@ -140,17 +140,17 @@ __device__ __forceinline__ double gram_entry(const double* aL1, const double* aD
         if (f1 < 0.0 || f2 < 0.0) return 0.0;
         const double dot = dot4(aL1, aL2, D4);
         const double r2 = -2.0 * dot + (nL1 + nL2);
-        return th.vL() * exp(-0.5 * r2);
+        return th.vL() * exp_lib(-0.5 * r2);
     }
     const bool L1 = (f1 == 0.0), H1 = (f1 == 1.0), L2 = (f2 == 0.0), H2 = (f2 == 1.0);
     if (!(L1 || H1) || !(L2 || H2)) return 0.0;        // linear.py:67-70 exact masks
     const double dot = dot4(aL1, aL2, D4);
-    const double kL = th.vL() * exp(-0.5 * (-2.0 * dot + (nL1 + nL2)));
+    const double kL = th.vL() * exp_lib(-0.5 * (-2.0 * dot + (nL1 + nL2)));
     const double rho = th.rho();
     if (L1 && L2) return kL;                           // K_LL
     if (!(H1 && H2)) return kL * rho;                  // K_LH, K_HL
     const double dotD = dot4(aD1, aD2, D4);
-    const double kD = th.vD() * exp(-0.5 * (-2.0 * dotD + (nD1 + nD2)));
+    const double kD = th.vD() * exp_lib(-0.5 * (-2.0 * dotD + (nD1 + nD2)));
     return kL * (rho * rho) + kD;                      // K_HH (linear.py:96)
 }
 
@@ -346,7 +346,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
             const int e = threadIdx.x + k * NTHREADS;
             const int r = e / NB, c = e % NB;
             const double dot = dot4(aL1 + r * XS, aL2 + c * XS, D4);
-            kl[k] = sc.vL() * exp(-0.5 * (-2.0 * dot + (nL1[r] + nL2[c])));
+            kl[k] = sc.vL() * exp_lib(-0.5 * (-2.0 * dot + (nL1[r] + nL2[c])));
         }
 #pragma unroll
         for (int k = 0; k < PT; ++k) {
@@ -363,7 +363,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram(GramArgs a) {
                 double kD = 0.0;
                 if (H1 && H2) {   // K_HH (linear.py:96): rare, a branch of its own
                     const double dotD = dot4(aD1 + r * XS, aD2 + c * XS, D4);
-                    kD = sc.vD() * exp(-0.5 * (-2.0 * dotD + (nD1[r] + nD2[c])));
+                    kD = sc.vD() * exp_lib(-0.5 * (-2.0 * dotD + (nD1[r] + nD2[c])));
                 }
                 const double vhh = kl[k] * (rho * rho) + kD;
                 v = (L1 && L2) ? kl[k] : (!(H1 && H2) ? kl[k] * rho : vhh);
@@ -503,7 +503,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram_dense(GramArgs a, int wr1, in
         if (gi < a.n1 && gj < a.n2) {
             const double fa = f1[rr];
             const double dot = dot_rl<D4>(sL1 + rr * D4, bl);
-            const double kl = vL * exp(-0.5 * (-2.0 * dot + (nL1[rr] + nL2)));
+            const double kl = vL * exp_lib(-0.5 * (-2.0 * dot + (nL1[rr] + nL2)));
             if (a.rbf_only) {
                 v = (fa < 0.0 || f2 < 0.0) ? 0.0 : kl;
             } else {
@@ -511,7 +511,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram_dense(GramArgs a, int wr1, in
                 double kD = 0.0;
                 if (H1 && H2) {   // K_HH (linear.py:96)
                     const double dotD = dot4(sD1 + rr * D4, sD2 + c * D4, D4);
-                    kD = vD * exp(-0.5 * (-2.0 * dotD + (nD1[rr] + nD2)));
+                    kD = vD * exp_lib(-0.5 * (-2.0 * dotD + (nD1[rr] + nD2)));
                 }
                 const double vhh = kl * (rho * rho) + kD;
                 v = (L1 && L2) ? kl : (!(H1 && H2) ? kl * rho : vhh);
@@ -1181,10 +1181,10 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
             const bool live = (L1[e] || H1[e]) && (L2[e] || H2[e]);
             // dK/dv = exp(-r2/2), TF's autodiff of v * exp(-r2/2): finite where v underflows to 0
             // (the division form K / v gave 0/0 at L-BFGS line-search points)
-            const double eL = live ? exp(-0.5 * s2[e]) : 0.0;
+            const double eL = live ? exp_lib(-0.5 * s2[e]) : 0.0;
             const double kL = th.vL() * eL;
             double eD = 0.0;
-            if (anyHH && H1[e] && H2[e]) eD = exp(-0.5 * s2d[e]);
+            if (anyHH && H1[e] && H2[e]) eD = exp_lib(-0.5 * s2d[e]);
             const double kD = th.vD() * eD;
             const double si = L1[e] ? 1.0 : (H1[e] ? rho : 0.0), sj = L2[e] ? 1.0 : (H2[e] ? rho : 0.0);
             const double hi = H1[e] ? 1.0 : 0.0, hj = H2[e] ? 1.0 : 0.0;
