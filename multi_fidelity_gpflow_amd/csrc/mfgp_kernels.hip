@@ -766,6 +766,94 @@ __global__ __launch_bounds__(NTHREADS) void k_chol_step(CholArgs a) {
     }
 }
 
+// Batched systems (the SVGP K_uu of every latent, batch > 1): each step of k_chol_step as two
+// launches.  k_chol_step's tasks recompute L_ik = A_ik D_k^T (twice per trailing tile) and
+// X_kc = D_k R_kc per task -- three tile products for one update; here the panel launch forms
+// each L_ik (stored over A_ik, which no later step reads) and each X_kc (row k of [L^{-1} | Z],
+// stored to Xo) once, and the update launch does one product per tile (the trailing task of
+// tile (k+1, k+1) then factors it).  The same products in the same order: bitwise k_chol_step's
+// results.  (Goku SVGP, 64 latents x 10 tiles: 9 x 20.5 us of steps.)
+template <int NB>
+__global__ __launch_bounds__(NTHREADS) void k_chol_panel(CholArgs a) {
+    constexpr int E = TileCfg<NB>::ELEMS;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    double* Ds = smem;
+    double* T0 = Ds + E;
+    int t, b;
+    xcd_swizzle(t, b);
+    const int k = a.k, T = a.T, rem = T - k - 1;
+    tile_load<NB>(Ds, a.Dd + b * a.sD + (long)k * NB * NB, NB);
+    Acc<NB> acc;
+    acc_zero(acc);
+    if (t < rem) {   // L_ik = A_ik D_k^T
+        double* Aik = a.A + b * a.sA + (long)(k + 1 + t) * NB * a.lda + (long)k * NB;
+        tile_load<NB>(T0, Aik, a.lda);
+        __syncthreads();
+        tile_mma<NB, false, true>(acc, T0, Ds, 1.0);
+        acc_store(acc, Aik, a.lda);
+        return;
+    }
+    t -= rem;        // X_kc = D_k R_kc, c = 0..k, then the Y tiles
+    const int c = (t <= k) ? t : T + (t - k - 1);
+    tile_load<NB>(T0, a.R + b * a.sR + (long)k * NB * a.ldr + (long)c * NB, a.ldr);
+    __syncthreads();
+    tile_mma<NB, false, false>(acc, Ds, T0, 1.0);
+    acc_store(acc, a.Xo + b * a.sX + (long)k * NB * a.ldx + (long)c * NB, a.ldx);
+}
+
+template <int NB>
+__global__ __launch_bounds__(NTHREADS) void k_chol_update(CholArgs a) {
+    constexpr int E = TileCfg<NB>::ELEMS;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    double* T0 = smem + E;       // (the k_chol_step carve: Ds | T0 | Pi | Pj | dg | bad)
+    double* Pi = T0 + E;
+    double* Pj = Pi + E;
+    double* dg = Pj + E;
+    int& bad = *reinterpret_cast<int*>(dg + NB);
+    int t, b;
+    xcd_swizzle(t, b);
+    const int k = a.k, T = a.T, Tp = a.Tp;
+    double* A = a.A + b * a.sA;
+    auto At = [&](int i, int j) { return A + (long)i * NB * a.lda + (long)j * NB; };
+    const int rem = T - k - 1, nA = rem * (rem + 1) / 2, ncol = k + 1 + Tp;
+    Acc<NB> acc;
+    if (t < nA) {    // A_ij -= L_ik L_jk^T
+        int ii, jj;
+        tri_decode(t, ii, jj);
+        const int i = k + 1 + ii, j = k + 1 + jj;
+        tile_load<NB>(Pi, At(i, k), a.lda);
+        if (j != i) tile_load<NB>(Pj, At(j, k), a.lda);
+        acc_load(acc, At(i, j), a.lda);
+        __syncthreads();
+        tile_mma<NB, false, true>(acc, Pi, j != i ? Pj : Pi, -1.0);
+        if (i == j && i == k + 1) {
+            if constexpr (NB == 32) {
+                tile_potrf_inv_w1_acc(acc.v[0], T0, Pj, dg, &bad);
+            } else {
+                acc_to_lds(acc, T0);
+                __syncthreads();
+                tile_potrf_inv<NB>(T0, Pj, dg, &bad);
+            }
+            tile_store<NB>(a.Dd + b * a.sD + (long)(k + 1) * NB * NB, NB, Pj);
+            for (int r = threadIdx.x; r < NB; r += NTHREADS) a.ldiag[b * a.sL + (k + 1) * NB + r] = dg[r];
+            if (threadIdx.x == 0 && bad && a.info[b] == 0) a.info[b] = (k + 1) * NB + bad;
+        } else {
+            acc_store(acc, At(i, j), a.lda);
+        }
+        return;
+    }
+    t -= nA;         // R_ic -= L_ik X_kc
+    const int i = k + 1 + t / ncol, cc = t % ncol;
+    const int c = (cc <= k) ? cc : T + (cc - k - 1);
+    double* Ric = a.R + b * a.sR + (long)i * NB * a.ldr + (long)c * NB;
+    tile_load<NB>(Pi, At(i, k), a.lda);
+    tile_load<NB>(Pj, a.Xo + b * a.sX + (long)k * NB * a.ldx + (long)c * NB, a.ldx);
+    acc_load(acc, Ric, a.ldr);
+    __syncthreads();
+    tile_mma<NB, false, false>(acc, Pi, Pj, -1.0);
+    acc_store(acc, Ric, a.ldr);
+}
+
 int chol_step_blocks(int T, int Tp, int k, bool alpha) {
     const int rem = T - k - 1;
     return rem * (rem + 1) / 2 + rem * (k + 1 + Tp) + (alpha ? (k + 1) * Tp : 0) + ((k == T - 1) ? (T + Tp) : 0);
@@ -1518,7 +1606,19 @@ void launch_first_factor(const double* A, long lda, long sA, double* Dd, long sD
 }
 template <int NB>
 void launch_chol_steps(CholArgs c, int batch, hipStream_t s) {
-    if (batch != 1) c.alpha = nullptr;   // fused alpha: single system only
+    if (batch != 1) {   // panel + update launches a step (k_chol_panel); no fused alpha
+        c.alpha = nullptr;
+        for (int k = 0; k < c.T; ++k) {
+            c.k = k;
+            const int rem = c.T - k - 1, ncol = k + 1 + c.Tp;
+            hipLaunchKernelGGL(k_chol_panel<NB>, dim3(rem + ncol, 1, batch), dim3(NTHREADS),
+                               2 * sizeof(double) * TileCfg<NB>::ELEMS, s, c);
+            const int nu = rem * (rem + 1) / 2 + rem * ncol;
+            if (nu > 0)
+                hipLaunchKernelGGL(k_chol_update<NB>, dim3(nu, 1, batch), dim3(NTHREADS), chol_smem_bytes(NB), s, c);
+        }
+        return;
+    }
     for (int k = 0; k < c.T; ++k) {
         c.k = k;
         const int nb = chol_step_blocks(c.T, c.Tp, k, c.alpha != nullptr);
