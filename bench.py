@@ -294,13 +294,14 @@ def svgp_step_mfma_flops(n, m, L, nb=32):
     """Executed f64 MFMA flops of one SVGP optimize() step on the padded NB-tiles (2 NB^3 per tile
     product), forward and reverse pass, per the launch sequence of mfgp_svgp.hip / mfgp_svgp_grad.hip:
       forward  Kuu factor (blocked Cholesky + inverse, ~Tm^3/3 + Tm^3/6 tile products),
-               C = Lq^T Li (sum_{i,j} Tm - max(i, j)), A and B (k_svgp_cond: Tn (Tm(Tm+1)/2 + Tm^2));
+               A = Li Kuf and B = Lq^T A (the gradient pass's two triangular GEMMs: Tn Tm(Tm+1)/2
+               each; the value-only path's fused k_svgp_cond2 forms B = C Kuf with C = Lq^T Li);
       reverse  gA (Tn Tm(Tm+1)/2), dE/dLi (tril, Tn Tm(Tm+1)/2), Gb Li^T (sum min(i, j) + 1),
                Psi Li and Li^T (.) (Tm^2(Tm+1)/2 each), dE/dKuf (Tn Tm(Tm+1)/2),
                dE/dLq (tril, Tn Tm(Tm+1)/2)."""
     Tm, Tn = -(-m // nb), -(-n // nb)
     tri = Tm * (Tm + 1) // 2
-    fwd = Tm ** 3 / 3 + Tm ** 3 / 6 + sum(Tm - max(i, j) for i in range(Tm) for j in range(Tm)) + Tn * (tri + Tm * Tm)
+    fwd = Tm ** 3 / 3 + Tm ** 3 / 6 + 2 * Tn * tri
     rev = 4 * Tn * tri + sum(min(i, j) + 1 for i in range(Tm) for j in range(Tm)) + 2 * Tm * tri
     return L * (fwd + rev) * 2 * nb ** 3
 
