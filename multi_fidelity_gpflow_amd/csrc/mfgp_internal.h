@@ -62,8 +62,9 @@ struct FlowArgs {
     int nwaves;                   // worker waves (trace layout)
     long long timeout;            // bound of every hand-off wait, 100 MHz ticks (FLOW_TIMEOUT_TICKS)
     // the K + s2 I tiles are formed inside the launch (flow_gram_tile): each A tile by its owner
-    // wave before its first item, tile (0,0) and the band tiles of rows <= 3 by the diag
-    // workgroup's waves; the Y column tiles of R are read from Y on first touch
+    // wave before its first item, tile (0,0) and the band tiles of rows 1-2 by the diag
+    // workgroup's waves, row 3's by idle worker waves (FT_G); the Y column tiles of R are read
+    // from Y on first touch
     const double* X; long ldxi;   // inputs [n, D+1] (fidelity flag in column D)
     const double* Y; long ldy;    // outputs [n, p]
     const double* theta;          // [vL, lL(D), vD, lD(D), rho0, noise]
