@@ -1093,6 +1093,7 @@ int mfgp_svgp_elbo(mfgp_handle_t h, int n, int m, int l, int p, int d, const dou
     if (n < 1 || m < 1 || l < 1 || p < 1 || !X || !Y || !Z || !thetas || !q_mu || !q_sqrt || !ws || !out || !info)
         return MFGP_ERR_ARG;
     if (!W && l != p) return MFGP_ERR_ARG;
+    svgp_set_side(SvgpSide{h->side, h->ev_fork, h->ev_join});
     return svgp_elbo_impl(h->stream, h->nb, n, m, l, p, d, X, ldx, Y, ldy, Z, ldz, thetas, q_mu, q_sqrt, W, noise,
                           scale, jitter, ws, ws_bytes, out, g_mu, g_var, info, nullptr);
 }
@@ -1119,6 +1120,7 @@ int mfgp_svgp_elbo_grad(mfgp_handle_t h, int n, int m, int l, int p, int d, cons
     if (W == nullptr && l != p) return MFGP_ERR_ARG;
     if (W != nullptr && gW == nullptr) return MFGP_ERR_ARG;
     if (ldx < d + 1 || ldz < d + 1 || ldy < p) return MFGP_ERR_ARG;
+    svgp_set_side(SvgpSide{h->side, h->ev_fork, h->ev_join});
     return svgp_grad_impl(h->stream, h->nb, n, m, l, p, d, X, ldx, Y, ldy, Z, ldz, thetas, q_mu, q_sqrt, W, noise, 0.0,
                           scale, kl_mult, jitter, ws, ws_bytes, out, g_mu, g_var, gZ, gtheta, gq_mu, gq_sqrt, gW,
                           gnoise, info);
@@ -1158,6 +1160,7 @@ int mfgp_svgp_predict(mfgp_handle_t h, int nstar, int m, int l, int p, int d, co
         !g_var || !f_mu || !f_var || !info)
         return MFGP_ERR_ARG;
     if (!W && l != p) return MFGP_ERR_ARG;
+    svgp_set_side(SvgpSide{h->side, h->ev_fork, h->ev_join});
     return svgp_predict_impl(h->stream, h->nb, nstar, m, l, p, d, Xs, ldxs, Z, ldz, thetas, q_mu, q_sqrt, W, jitter,
                              ws, ws_bytes, g_mu, g_var, f_mu, f_var, info);
 }
@@ -1180,6 +1183,7 @@ int mfgp_svgp_predict_cov(mfgp_handle_t h, int mode, int nstar, int m, int l, in
         !ws || !g_mu || !g_var || !f_mu || !f_var || !f_cov || !info)
         return MFGP_ERR_ARG;
     if (!W && l != p) return MFGP_ERR_ARG;
+    svgp_set_side(SvgpSide{h->side, h->ev_fork, h->ev_join});
     const int rc = svgp_predict_cov_impl(h->stream, h->nb, mode, nstar, m, l, p, d, Xs, ldxs, Z, ldz, thetas, q_mu,
                                          q_sqrt, W, jitter, ws, ws_bytes, g_mu, g_var, f_mu, f_var, f_cov, info);
     return rc == -2 ? MFGP_ERR_WORKSPACE : (rc ? MFGP_ERR_LAUNCH : MFGP_OK);

@@ -178,6 +178,17 @@ struct BgemmArgs {
 };
 void launch_bgemm(int nb, hipStream_t st, int ta, int tb, const BgemmArgs& a, int batch);
 
+// The handle's side stream and fork / join events for the SVGP calls' independent branches (the
+// K_uu factorization beside the K_uf Gram; the reverse pass's dE/dm, dE/dLq and K_diag terms beside
+// the gA -> Sigma_bar / K_bar -> kernel-derivative chain).  Set by the C-ABI entry points for the
+// calling thread; side == nullptr: everything on the caller's stream.
+struct SvgpSide { hipStream_t side; hipEvent_t fork, join; };
+void svgp_set_side(const SvgpSide& sd);
+const SvgpSide& svgp_side();
+// fork the side stream off s (nothing without a side stream); returns the stream to launch on
+hipStream_t svgp_fork(hipStream_t s);
+void svgp_join(hipStream_t s);
+
 constexpr int MAXD_HOST = 32;
 
 // fp32 path (mfgp_f32.hip): one tall row-major matrix M, 128 x 128 tiles, ld = Npad; row tiles

@@ -19,6 +19,21 @@ namespace mfgp {
 
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
+static thread_local SvgpSide t_side{nullptr, nullptr, nullptr};
+void svgp_set_side(const SvgpSide& sd) { t_side = sd; }
+const SvgpSide& svgp_side() { return t_side; }
+hipStream_t svgp_fork(hipStream_t s) {
+    if (!t_side.side || !t_side.fork || !t_side.join) return s;
+    (void)hipEventRecord(t_side.fork, s);
+    (void)hipStreamWaitEvent(t_side.side, t_side.fork, 0);
+    return t_side.side;
+}
+void svgp_join(hipStream_t s) {
+    if (!t_side.side || !t_side.fork || !t_side.join) return;
+    (void)hipEventRecord(t_side.join, t_side.side);
+    (void)hipStreamWaitEvent(s, t_side.join, 0);
+}
+
 struct SvgpLayout {
     int nb, Tm, mpad, Tn, npad, G;
     double *Kuu, *R, *Xo, *Dd, *ldiag, *Lq, *C, *Kuf, *pa, *pb, *pm, *ve_part, *kl_part;
@@ -487,13 +502,16 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
     // needs to form A and B in one tile loop without keeping A), and no C.  The column moments
     // come out of the GEMMs' epilogues in the fused kernel's partial layout and order.
     const bool two_gemm = NB == 32 && Aout != nullptr;
-    (void)hipMemsetAsync(info, 0, sizeof(int) * L, s);
+    // the K_uu pipeline (latency-bound: ~20 launches of small grids) on the side stream, the K_uf
+    // Gram on the caller's beside it
+    hipStream_t sk = svgp_fork(s);
+    (void)hipMemsetAsync(info, 0, sizeof(int) * L, sk);
     // Kuu_l (+ jitter) by the lean Gram launch, then the first diagonal factor of every latent as a
     // launch of its own (fused into the Gram it set that launch's register allocation: 3.3% of a
     // single-bin iteration for a 300 x 300 Gram per latent); RHS = I
     {
         const int blocks = (int)std::min<long>((mm + 255) / 256, 2048);
-        hipLaunchKernelGGL(k_rhs_init, dim3(blocks, 1, L), dim3(256), 0, s, S.R, (long)S.mpad, mm, S.mpad, 0,
+        hipLaunchKernelGGL(k_rhs_init, dim3(blocks, 1, L), dim3(256), 0, sk, S.R, (long)S.mpad, mm, S.mpad, 0,
                            (const double*)nullptr, 0L, 0L, m, 0);
         GramArgs g{};
         g.X1 = Z; g.ldx1 = ldz; g.sx1 = 0; g.n1 = m;
@@ -501,20 +519,20 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
         g.theta = thetas; g.stheta = S.G; g.D = d; g.rbf_only = 0;
         g.out = S.Kuu; g.ldo = S.mpad; g.so = mm;
         g.padded = 1; g.npad = S.mpad; g.tiles_c = S.Tm; g.add_noise = 0; g.diag_add = jitter;
-        launch_gram<NB>(g, S.Tm * (S.Tm + 1) / 2, L, s);
-        launch_first_factor<NB>(S.Kuu, S.mpad, mm, S.Dd, (long)S.Tm * NB * NB, S.ldiag, S.mpad, info, L, s);
+        launch_gram<NB>(g, S.Tm * (S.Tm + 1) / 2, L, sk);
+        launch_first_factor<NB>(S.Kuu, S.mpad, mm, S.Dd, (long)S.Tm * NB * NB, S.ldiag, S.mpad, info, L, sk);
         CholArgs c{};
         c.A = S.Kuu; c.lda = S.mpad; c.sA = mm;
         c.R = S.R; c.ldr = S.mpad; c.sR = mm;
         c.Xo = S.Xo; c.ldx = S.mpad; c.sX = mm;
         c.Dd = S.Dd; c.sD = (long)S.Tm * NB * NB; c.ldiag = S.ldiag; c.sL = S.mpad; c.info = info;
         c.T = S.Tm; c.Tp = 0; c.k = 0;
-        launch_chol_steps<NB>(c, L, s);
-        hipLaunchKernelGGL(k_zero_upper_tiles, dim3(blocks, 1, L), dim3(256), 0, s, S.Xo, NB, S.mpad, mm);
-        hipLaunchKernelGGL(k_lq_pad, dim3(blocks, 1, L), dim3(256), 0, s, q_sqrt, m, S.mpad, S.Lq);
+        launch_chol_steps<NB>(c, L, sk);
+        hipLaunchKernelGGL(k_zero_upper_tiles, dim3(blocks, 1, L), dim3(256), 0, sk, S.Xo, NB, S.mpad, mm);
+        hipLaunchKernelGGL(k_lq_pad, dim3(blocks, 1, L), dim3(256), 0, sk, q_sqrt, m, S.mpad, S.Lq);
         if (!(two_gemm))   // C = Lq^T Li: the fused conditional's B = C Kuf
             hipLaunchKernelGGL(k_lqt_linv<NB>, dim3(S.Tm * S.Tm, 1, L), dim3(NTHREADS),
-                               2 * sizeof(double) * NB * (NB + 2), s, S.Lq, S.Xo, S.C, S.Tm);
+                               2 * sizeof(double) * NB * (NB + 2), sk, S.Lq, S.Xo, S.C, S.Tm);
     }
     // Kuf_l = K_l(Z, X), zero padded to Mpad x Npad
     {
@@ -526,6 +544,7 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
         g.padded = 0; g.tiles_c = S.Tn; g.diag_add = 0.0;
         launch_gram_dense(g, L, S.mpad, S.npad, s);   // zero padding written by the kernel
     }
+    svgp_join(s);
     if (two_gemm) {
         const long mn = (long)S.mpad * S.npad;
         BgemmArgs ga{};

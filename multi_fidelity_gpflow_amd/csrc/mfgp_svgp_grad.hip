@@ -893,11 +893,29 @@ static int svgp_grad_run(hipStream_t s, int n, int m, int L, int p, int d, const
     if (W) hipLaunchKernelGGL(k_gw, dim3(cdv(p * L, NTHREADS / 64)), dim3(NTHREADS), 0, s, g.r, g_mu, g_var, W, n, p, L,
                               noise_dev, scale, gW);
     hipLaunchKernelGGL(k_qmu_pad, dim3(cdv(mpad, 256), 1, L), dim3(256), 0, s, q_mu, m, L, mpad, g.qm);
+    // Side branch (svgp_fork): dE/dm, dE/dLq and the K_diag term need only the forward's A, B and
+    // the VE backward's alpha / beta; they run beside the gA -> Gb / Sigma_bar / Kbar -> k_kgrad chain.
+    hipStream_t sb = svgp_fork(s);
     // 2. dE/dm = A alpha - m  (folding its row products into step 3's epilogue, which reads A as
     //    Cin, measured slower: +45 us there and an 18 us partial reduction against this 51 us pass)
-    hipLaunchKernelGGL(k_bmatvec, dim3(cdv(mpad, NTHREADS / 64), 1, L), dim3(NTHREADS), 0, s, g.A, (long)npad, mn, 0,
+    hipLaunchKernelGGL(k_bmatvec, dim3(cdv(mpad, NTHREADS / 64), 1, L), dim3(NTHREADS), 0, sb, g.A, (long)npad, mn, 0,
                        g.alpha, (long)npad, mpad, npad, 1.0, g.qm, (long)mpad, -kl_mult, g.gqm, (long)mpad);
-    hipLaunchKernelGGL(k_qmu_unpad, dim3(cdv(m, 256), 1, L), dim3(256), 0, s, g.gqm, m, L, mpad, gq_mu);
+    hipLaunchKernelGGL(k_qmu_unpad, dim3(cdv(m, 256), 1, L), dim3(256), 0, sb, g.gqm, m, L, mpad, gq_mu);
+    // 7. dE/dLq = tril(2 A diag(beta) B^T) - Lq + diag(1/Lq_ii)
+    {
+        BgemmArgs a{};
+        a.A = g.A; a.lda = npad; a.sA = mn;
+        a.B = g.B; a.ldb = npad; a.sB = mn;
+        a.s = g.beta; a.ss = npad;
+        a.D = g.gLq; a.ldd = mpad; a.sD = mm;
+        a.alpha = 2.0;
+        a.Mt = Tm; a.Nt = Tm; a.Kt = Tn; a.tril = 1;
+        bgemm<NB>(sb, 0, 1, a, L);
+    }
+    hipLaunchKernelGGL(k_glq_final, dim3(std::min(cdv(m * m, 256), 1024), 1, L), dim3(256), 0, sb, g.gLq, Lq, m, mpad,
+                       mm, kl_mult, gq_sqrt);
+    hipLaunchKernelGGL(k_kff_grad, dim3(L), dim3(NTHREADS), 0, sb, X, (long)ldx, n, g.beta, npad, thetas, G, d,
+                       g.gth_kff);
     // 3. gA = (2 Lq B - 2 A) diag(beta) + m alpha^T
     {
         BgemmArgs a{};
@@ -938,19 +956,6 @@ static int svgp_grad_run(hipStream_t s, int n, int m, int L, int p, int d, const
         a.Mt = Tm; a.Nt = Tn; a.Kt = Tm;
         bgemm<NB>(s, 1, 0, a, L);
     }
-    // 7. dE/dLq = tril(2 A diag(beta) B^T) - Lq + diag(1/Lq_ii)
-    {
-        BgemmArgs a{};
-        a.A = g.A; a.lda = npad; a.sA = mn;
-        a.B = g.B; a.ldb = npad; a.sB = mn;
-        a.s = g.beta; a.ss = npad;
-        a.D = g.gLq; a.ldd = mpad; a.sD = mm;
-        a.alpha = 2.0;
-        a.Mt = Tm; a.Nt = Tm; a.Kt = Tn; a.tril = 1;
-        bgemm<NB>(s, 0, 1, a, L);
-    }
-    hipLaunchKernelGGL(k_glq_final, dim3(std::min(cdv(m * m, 256), 1024), 1, L), dim3(256), 0, s, g.gLq, Lq, m, mpad,
-                       mm, kl_mult, gq_sqrt);
     // 8. kernel / inducing-point derivative sums
     // compile-time bound on d: the per-dimension accumulators stay in registers
     auto kgrad = [&](auto dc) {
@@ -965,8 +970,7 @@ static int svgp_grad_run(hipStream_t s, int n, int m, int L, int p, int d, const
     else if (d <= 12) kgrad(std::integral_constant<int, 12>{});
     else if (d <= 16) kgrad(std::integral_constant<int, 16>{});
     else kgrad(std::integral_constant<int, 32>{});
-    hipLaunchKernelGGL(k_kff_grad, dim3(L), dim3(NTHREADS), 0, s, X, (long)ldx, n, g.beta, npad, thetas, G, d,
-                       g.gth_kff);
+    svgp_join(s);
     const int tot = L * G + m * (d + 1) + 1;
     hipLaunchKernelGGL(k_grad_reduce, dim3(cdv(tot * GR_LANES, 256)), dim3(256), 0, s, g.gth_uu, g.nb_uu, g.gth_uf, g.nb_uf,
                        g.gth_kff, g.gz_uu, g.gz_uf, g.n_at, g.nbc_uu, g.nbc_uf, L, G, d, m, g.gnp, g.nnoise, gtheta,
