@@ -19,7 +19,7 @@ namespace mfgp {
 
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
-static thread_local SvgpSide t_side{nullptr, nullptr, nullptr};
+static thread_local SvgpSide t_side{nullptr, nullptr, nullptr, nullptr};
 void svgp_set_side(const SvgpSide& sd) { t_side = sd; }
 const SvgpSide& svgp_side() { return t_side; }
 hipStream_t svgp_fork(hipStream_t s) {
@@ -32,6 +32,11 @@ void svgp_join(hipStream_t s) {
     if (!t_side.side || !t_side.fork || !t_side.join) return;
     (void)hipEventRecord(t_side.join, t_side.side);
     (void)hipStreamWaitEvent(s, t_side.join, 0);
+}
+void svgp_handoff(hipStream_t from, hipStream_t to) {
+    if (from == to || !t_side.mid) return;
+    (void)hipEventRecord(t_side.mid, from);
+    (void)hipStreamWaitEvent(to, t_side.mid, 0);
 }
 
 struct SvgpLayout {
@@ -502,15 +507,17 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
     // needs to form A and B in one tile loop without keeping A), and no C.  The column moments
     // come out of the GEMMs' epilogues in the fused kernel's partial layout and order.
     const bool two_gemm = NB == 32 && Aout != nullptr;
-    // the K_uu pipeline (latency-bound: ~20 launches of small grids) on the side stream, the K_uf
-    // Gram on the caller's beside it
+    // the K_uu pipeline (latency-bound: ~20 launches of small grids) on the side stream; the K_uf
+    // Gram, tril(q_sqrt), the zeros above Li's tiles (the step sequence never writes there) and
+    // the KL (q_mu, q_sqrt only) on the caller's beside it
     hipStream_t sk = svgp_fork(s);
+    const int blocks = (int)std::min<long>((mm + 255) / 256, 2048);
+    hipLaunchKernelGGL(k_zero_upper_tiles, dim3(blocks, 1, L), dim3(256), 0, s, S.Xo, NB, S.mpad, mm);
     (void)hipMemsetAsync(info, 0, sizeof(int) * L, sk);
     // Kuu_l (+ jitter) by the lean Gram launch, then the first diagonal factor of every latent as a
     // launch of its own (fused into the Gram it set that launch's register allocation: 3.3% of a
     // single-bin iteration for a 300 x 300 Gram per latent); RHS = I
     {
-        const int blocks = (int)std::min<long>((mm + 255) / 256, 2048);
         hipLaunchKernelGGL(k_rhs_init, dim3(blocks, 1, L), dim3(256), 0, sk, S.R, (long)S.mpad, mm, S.mpad, 0,
                            (const double*)nullptr, 0L, 0L, m, 0);
         GramArgs g{};
@@ -528,11 +535,6 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
         c.Dd = S.Dd; c.sD = (long)S.Tm * NB * NB; c.ldiag = S.ldiag; c.sL = S.mpad; c.info = info;
         c.T = S.Tm; c.Tp = 0; c.k = 0;
         launch_chol_steps<NB>(c, L, sk);
-        hipLaunchKernelGGL(k_zero_upper_tiles, dim3(blocks, 1, L), dim3(256), 0, sk, S.Xo, NB, S.mpad, mm);
-        hipLaunchKernelGGL(k_lq_pad, dim3(blocks, 1, L), dim3(256), 0, sk, q_sqrt, m, S.mpad, S.Lq);
-        if (!(two_gemm))   // C = Lq^T Li: the fused conditional's B = C Kuf
-            hipLaunchKernelGGL(k_lqt_linv<NB>, dim3(S.Tm * S.Tm, 1, L), dim3(NTHREADS),
-                               2 * sizeof(double) * NB * (NB + 2), sk, S.Lq, S.Xo, S.C, S.Tm);
     }
     // Kuf_l = K_l(Z, X), zero padded to Mpad x Npad
     {
@@ -543,6 +545,13 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
         g.out = S.Kuf; g.ldo = S.npad; g.so = (long)S.mpad * S.npad;
         g.padded = 0; g.tiles_c = S.Tn; g.diag_add = 0.0;
         launch_gram_dense(g, L, S.mpad, S.npad, s);   // zero padding written by the kernel
+    }
+    hipLaunchKernelGGL(k_lq_pad, dim3(blocks, 1, L), dim3(256), 0, s, q_sqrt, m, S.mpad, S.Lq);
+    if (!f_mu) hipLaunchKernelGGL(k_svgp_kl, dim3(KL_SLICES, L), dim3(NTHREADS), 0, s, q_mu, q_sqrt, m, L, S.kl_part);
+    if (!two_gemm) {   // C = Lq^T Li (the fused conditional's B = C Kuf), after Lq and Li
+        svgp_handoff(s, sk);
+        hipLaunchKernelGGL(k_lqt_linv<NB>, dim3(S.Tm * S.Tm, 1, L), dim3(NTHREADS), 2 * sizeof(double) * NB * (NB + 2),
+                           sk, S.Lq, S.Xo, S.C, S.Tm);
     }
     svgp_join(s);
     if (two_gemm) {
@@ -590,7 +599,6 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
     const int nve = 512;
     hipLaunchKernelGGL(k_svgp_ve, dim3(nve), dim3(NTHREADS), 0, s, g_mu, g_var, W, Y, (long)ldy, n, p, L, noise,
                        noise_dev, S.ve_part);
-    hipLaunchKernelGGL(k_svgp_kl, dim3(KL_SLICES, L), dim3(NTHREADS), 0, s, q_mu, q_sqrt, m, L, S.kl_part);
     hipLaunchKernelGGL(k_svgp_final, dim3(1), dim3(NTHREADS), 0, s, S.ve_part, nve, S.kl_part, L * KL_SLICES, m, L,
                        scale, info, out);
     return hipGetLastError() == hipSuccess ? 0 : -3;

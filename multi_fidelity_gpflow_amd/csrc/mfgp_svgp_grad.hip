@@ -894,7 +894,9 @@ static int svgp_grad_run(hipStream_t s, int n, int m, int L, int p, int d, const
                               noise_dev, scale, gW);
     hipLaunchKernelGGL(k_qmu_pad, dim3(cdv(mpad, 256), 1, L), dim3(256), 0, s, q_mu, m, L, mpad, g.qm);
     // Side branch (svgp_fork): dE/dm, dE/dLq and the K_diag term need only the forward's A, B and
-    // the VE backward's alpha / beta; they run beside the gA -> Gb / Sigma_bar / Kbar -> k_kgrad chain.
+    // the VE backward's alpha / beta; they run beside gA.  Then (svgp_handoff after gA) the side
+    // takes Kbar -> the (Z, X) derivative sums while the caller's stream runs Gb -> Sigma_bar ->
+    // the (Z, Z) sums.
     hipStream_t sb = svgp_fork(s);
     // 2. dE/dm = A alpha - m  (folding its row products into step 3's epilogue, which reads A as
     //    Cin, measured slower: +45 us there and an 18 us partial reduction against this 51 us pass)
@@ -912,10 +914,6 @@ static int svgp_grad_run(hipStream_t s, int n, int m, int L, int p, int d, const
         a.Mt = Tm; a.Nt = Tm; a.Kt = Tn; a.tril = 1;
         bgemm<NB>(sb, 0, 1, a, L);
     }
-    hipLaunchKernelGGL(k_glq_final, dim3(std::min(cdv(m * m, 256), 1024), 1, L), dim3(256), 0, sb, g.gLq, Lq, m, mpad,
-                       mm, kl_mult, gq_sqrt);
-    hipLaunchKernelGGL(k_kff_grad, dim3(L), dim3(NTHREADS), 0, sb, X, (long)ldx, n, g.beta, npad, thetas, G, d,
-                       g.gth_kff);
     // 3. gA = (2 Lq B - 2 A) diag(beta) + m alpha^T
     {
         BgemmArgs a{};
@@ -929,6 +927,18 @@ static int svgp_grad_run(hipStream_t s, int n, int m, int L, int p, int d, const
         a.alpha = 2.0;
         a.Mt = Tm; a.Nt = Tn; a.Kt = Tm;
         bgemm<NB>(s, 0, 0, a, L);
+    }
+    svgp_handoff(s, sb);
+    // 6. Kbar = dE/dKuf = Li^T gA (side)
+    {
+        BgemmArgs a{};
+        a.amask = 2;   // Li^T upper
+        a.A = Li; a.lda = mpad; a.sA = mm;
+        a.B = g.gA; a.ldb = npad; a.sB = mn;
+        a.D = g.Kbar; a.ldd = npad; a.sD = mn;
+        a.alpha = 1.0;
+        a.Mt = Tm; a.Nt = Tn; a.Kt = Tm;
+        bgemm<NB>(sb, 1, 0, a, L);
     }
     // 4. dE/dLi = tril(gA Kuf^T)
     {
@@ -945,31 +955,25 @@ static int svgp_grad_run(hipStream_t s, int n, int m, int L, int p, int d, const
     hipLaunchKernelGGL(k_psi, dim3(std::min<long>(cdv((int)mm, 256), 1024), 1, L), dim3(256), 0, s, g.H, g.P, mpad, mm);
     sq<NB>(s, Tm, L, mm, mpad, 0, g.P, 0, Li, g.T1, 1.0, nullptr, 0.0, 0, nullptr, nullptr, 0, 0, 1);   // Li lower
     sq<NB>(s, Tm, L, mm, mpad, 1, Li, 0, g.T1, g.Sig, -1.0, nullptr, 0.0, 0, nullptr, nullptr, 0, 2, 0);   // Li^T upper
-    // 6. Kbar = dE/dKuf = Li^T gA
-    {
-        BgemmArgs a{};
-        a.amask = 2;   // Li^T upper
-        a.A = Li; a.lda = mpad; a.sA = mm;
-        a.B = g.gA; a.ldb = npad; a.sB = mn;
-        a.D = g.Kbar; a.ldd = npad; a.sD = mn;
-        a.alpha = 1.0;
-        a.Mt = Tm; a.Nt = Tn; a.Kt = Tm;
-        bgemm<NB>(s, 1, 0, a, L);
-    }
-    // 8. kernel / inducing-point derivative sums
+    // 8. kernel / inducing-point derivative sums: (Z, X) on the side, (Z, Z) here
     // compile-time bound on d: the per-dimension accumulators stay in registers
     auto kgrad = [&](auto dc) {
         constexpr int DC = decltype(dc)::value;
+        launch_kgrad<DC>(sb, Z, ldz, m, X, ldx, n, g.Kbar, npad, mn, thetas, G, d, 1.0, g.n_at, g.nbc_uf, L, g.gth_uf,
+                         g.gz_uf);
         launch_kgrad<DC>(s, Z, ldz, m, Z, ldz, m, g.Sig, mpad, mm, thetas, G, d, 2.0, g.n_at, g.nbc_uu, L, g.gth_uu,
                          g.gz_uu);
-        launch_kgrad<DC>(s, Z, ldz, m, X, ldx, n, g.Kbar, npad, mn, thetas, G, d, 1.0, g.n_at, g.nbc_uf, L, g.gth_uf,
-                         g.gz_uf);
     };
     if (d <= 4) kgrad(std::integral_constant<int, 4>{});
     else if (d <= 8) kgrad(std::integral_constant<int, 8>{});
     else if (d <= 12) kgrad(std::integral_constant<int, 12>{});
     else if (d <= 16) kgrad(std::integral_constant<int, 16>{});
     else kgrad(std::integral_constant<int, 32>{});
+    // the side's short tail (after Kbar and its sums: those are on the longer branch's heels)
+    hipLaunchKernelGGL(k_glq_final, dim3(std::min(cdv(m * m, 256), 1024), 1, L), dim3(256), 0, sb, g.gLq, Lq, m, mpad,
+                       mm, kl_mult, gq_sqrt);
+    hipLaunchKernelGGL(k_kff_grad, dim3(L), dim3(NTHREADS), 0, sb, X, (long)ldx, n, g.beta, npad, thetas, G, d,
+                       g.gth_kff);
     svgp_join(s);
     const int tot = L * G + m * (d + 1) + 1;
     hipLaunchKernelGGL(k_grad_reduce, dim3(cdv(tot * GR_LANES, 256)), dim3(256), 0, s, g.gth_uu, g.nb_uu, g.gth_uf, g.nb_uf,
