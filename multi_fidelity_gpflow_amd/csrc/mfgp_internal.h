@@ -166,6 +166,10 @@ struct BgemmArgs {
     double* D; long ldd; long sD;
     double alpha;
     int Mt, Nt, Kt, tril;
+    // sym (k_bgemm2 only, with tril; a symmetric product formed from its lower tiles): 1 stores
+    // Psi(D) = (tril D + tril D^T - diag D) / 2, the lower tiles' values halved and mirrored
+    // across the diagonal; 2 stores tril D mirrored (D itself, exactly symmetric)
+    int sym;
     // known-zero triangles of the operands, so their k-tiles are skipped (never read):
     // amask 1: op(A) lower (k-tile <= row tile), 2: op(A) upper (k-tile >= row tile);
     // bmask 1: op(B) lower (k-tile >= column tile), 2: op(B) upper (k-tile <= column tile)

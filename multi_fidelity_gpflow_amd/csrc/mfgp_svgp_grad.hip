@@ -214,6 +214,22 @@ __global__ __launch_bounds__(NTHREADS) void k_bgemm2(BgemmArgs a) {
     }
     if (!live) return;
     double* Dt = a.D + b * a.sD;
+    if (a.sym) {   // tiles ti >= tj only (tril): v (Psi: 0.5 v) at (i, j) and (j, i)
+        if (tj > ti) return;
+        const double hs = a.sym == 1 ? 0.5 : 1.0;
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = ti * NB + 16 * p + lk + 4 * r, j = tj * NB + 16 * q + li;
+                    const double v = hs * acc[p][q][r];
+                    if (j <= i) Dt[(long)i * a.ldd + j] = v;
+                    if (j < i) Dt[(long)j * a.ldd + i] = v;
+                }
+        return;
+    }
 #pragma unroll
     for (int p = 0; p < 2; ++p)
 #pragma unroll
@@ -951,10 +967,34 @@ static int svgp_grad_run(hipStream_t s, int n, int m, int L, int p, int d, const
         bgemm<NB>(s, 0, 1, a, L);
     }
     // 5. Sigma_bar = -Li^T Psi(Gb Li^T) Li
-    sq<NB>(s, Tm, L, mm, mpad, 0, g.Gb, 1, Li, g.H, 1.0, nullptr, 0.0, 0, nullptr, nullptr, 0, 1, 2);   // Gb lower, Li^T upper
-    hipLaunchKernelGGL(k_psi, dim3(std::min<long>(cdv((int)mm, 256), 1024), 1, L), dim3(256), 0, s, g.H, g.P, mpad, mm);
+    //    (NB = 32: Psi in the first product's epilogue, only its lower tiles formed)
+    if (NB == 32) {
+        BgemmArgs a{};
+        a.amask = 1; a.bmask = 2;   // Gb lower, Li^T upper
+        a.A = g.Gb; a.lda = mpad; a.sA = mm;
+        a.B = Li; a.ldb = mpad; a.sB = mm;
+        a.D = g.P; a.ldd = mpad; a.sD = mm;
+        a.alpha = 1.0;
+        a.Mt = Tm; a.Nt = Tm; a.Kt = Tm; a.tril = 1; a.sym = 1;
+        bgemm<NB>(s, 0, 1, a, L);
+    } else {
+        sq<NB>(s, Tm, L, mm, mpad, 0, g.Gb, 1, Li, g.H, 1.0, nullptr, 0.0, 0, nullptr, nullptr, 0, 1, 2);   // Gb lower, Li^T upper
+        hipLaunchKernelGGL(k_psi, dim3(std::min<long>(cdv((int)mm, 256), 1024), 1, L), dim3(256), 0, s, g.H, g.P, mpad,
+                           mm);
+    }
     sq<NB>(s, Tm, L, mm, mpad, 0, g.P, 0, Li, g.T1, 1.0, nullptr, 0.0, 0, nullptr, nullptr, 0, 0, 1);   // Li lower
-    sq<NB>(s, Tm, L, mm, mpad, 1, Li, 0, g.T1, g.Sig, -1.0, nullptr, 0.0, 0, nullptr, nullptr, 0, 2, 0);   // Li^T upper
+    if (NB == 32) {   // Sigma_bar is symmetric: its lower tiles (the cheap ones under Li^T's mask), mirrored
+        BgemmArgs a{};
+        a.amask = 2;   // Li^T upper
+        a.A = Li; a.lda = mpad; a.sA = mm;
+        a.B = g.T1; a.ldb = mpad; a.sB = mm;
+        a.D = g.Sig; a.ldd = mpad; a.sD = mm;
+        a.alpha = -1.0;
+        a.Mt = Tm; a.Nt = Tm; a.Kt = Tm; a.tril = 1; a.sym = 2;
+        bgemm<NB>(s, 1, 0, a, L);
+    } else {
+        sq<NB>(s, Tm, L, mm, mpad, 1, Li, 0, g.T1, g.Sig, -1.0, nullptr, 0.0, 0, nullptr, nullptr, 0, 2, 0);   // Li^T upper
+    }
     // 8. kernel / inducing-point derivative sums: (Z, X) on the side, (Z, Z) here
     // compile-time bound on d: the per-dimension accumulators stay in registers
     auto kgrad = [&](auto dc) {
