@@ -801,6 +801,22 @@ __global__ __launch_bounds__(NTHREADS) void k_chol_panel(CholArgs a) {
     acc_store(acc, a.Xo + b * a.sX + (long)k * NB * a.ldx + (long)c * NB, a.ldx);
 }
 
+// Dispatch order of k_chol_update: task 0 of every batch entry (the trailing tile (k+1, k+1), which
+// also factors it: the longest task and the next step's critical path) in the first slots, then
+// the other tasks; both parts in XCD-aware chunks (xcd_swizzle's remap).  Placement only.
+__device__ __forceinline__ void chol_update_order(int per, int& t, int& b) {
+    const int nb = gridDim.z, g = blockIdx.x + gridDim.x * blockIdx.z;
+    if (g < nb) {
+        t = 0;
+        b = (nb % 8 == 0) ? (g & 7) * (nb >> 3) + (g >> 3) : g;
+        return;
+    }
+    const int r = g - nb, rest = per - 1, cpx = (nb * rest) >> 3;
+    const int s = r < 8 * cpx ? (r & 7) * cpx + (r >> 3) : r;
+    b = s / rest;
+    t = 1 + s % rest;
+}
+
 template <int NB>
 __global__ __launch_bounds__(NTHREADS) void k_chol_update(CholArgs a) {
     constexpr int E = TileCfg<NB>::ELEMS;
@@ -810,12 +826,12 @@ __global__ __launch_bounds__(NTHREADS) void k_chol_update(CholArgs a) {
     double* Pj = Pi + E;
     double* dg = Pj + E;
     int& bad = *reinterpret_cast<int*>(dg + NB);
-    int t, b;
-    xcd_swizzle(t, b);
     const int k = a.k, T = a.T, Tp = a.Tp;
+    const int rem = T - k - 1, nA = rem * (rem + 1) / 2, ncol = k + 1 + Tp;
+    int t, b;
+    chol_update_order(gridDim.x, t, b);
     double* A = a.A + b * a.sA;
     auto At = [&](int i, int j) { return A + (long)i * NB * a.lda + (long)j * NB; };
-    const int rem = T - k - 1, nA = rem * (rem + 1) / 2, ncol = k + 1 + Tp;
     Acc<NB> acc;
     if (t < nA) {    // A_ij -= L_ik L_jk^T
         int ii, jj;
