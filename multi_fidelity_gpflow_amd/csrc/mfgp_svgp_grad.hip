@@ -759,11 +759,9 @@ __global__ __launch_bounds__(NTHREADS) void k_kff_grad(const double* X, long ldx
 // Final reductions: gtheta[l][q] (kff + Kuu + Kuf partials), gZ[m][D+1] (sum over latents and
 // column blocks; fidelity column 0), gnoise.  GR_LANES lanes per output, lane j summing the
 // partials b = j mod GR_LANES, combined by a fixed xor tree (a thread per output walking its
-// partials in one dependent chain took 93 us at L = 64: 19 workgroups of 448-load chains).
-#ifndef MFGP_GR_LANES
-#define MFGP_GR_LANES 8
-#endif
-constexpr int GR_LANES = MFGP_GR_LANES;
+// partials in one dependent chain took 93 us at L = 64: 19 workgroups of 448-load chains; 8
+// lanes, 56-load chains, 31 us).
+constexpr int GR_LANES = 32;   // 8: 2.118 ms a Goku single-bin step, 32: 2.098, 64: 2.10
 __global__ void k_grad_reduce(const double* gth_uu, int nb_uu, const double* gth_uf, int nb_uf, const double* gth_kff,
                               const double* gz_uu, const double* gz_uf, int n_at, int nbc_uu, int nbc_uf, int L,
                               int G, int D, int m, const double* gnoise_part, int nnoise, double* gtheta, double* gZ,
