@@ -35,7 +35,7 @@ struct mfgp_handle_s {
     int f32_refine;             // fp32 value-only LML (one step) / predict mean (this many steps): fp64 refinement (mfgp_set_f32_refine)
     int tiny;                   // small problems (n, p <= 64, D <= 16, AR1 kernel): one-launch LML step (default on; MFGP_TINY=0 / mfgp_set_tiny(h, 0) disables)
     hipStream_t side;           // its high-priority side stream + fork / join events (created with the handle)
-    hipEvent_t ev_fork, ev_join, ev_mid;
+    hipEvent_t ev_fork, ev_join;
     int resident;               // mfgp_set_resident: fp64 value+grad flow calls may skip the set-up launch
     struct {                    // the last fp64 LML call on this handle, when it left its workspace set
         const void* ws;         // up for the next one (k_grad's grad_next_setup); ws == nullptr: none
@@ -746,7 +746,6 @@ int mfgp_create(int device, mfgp_handle_t* out) {
         if (hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, hi) != hipSuccess) h->side = nullptr;
         if (hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) != hipSuccess) h->ev_fork = nullptr;
         if (hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess) h->ev_join = nullptr;
-        if (hipEventCreateWithFlags(&h->ev_mid, hipEventDisableTiming) != hipSuccess) h->ev_mid = nullptr;
         if (cur >= 0) (void)hipSetDevice(cur);
     }
     if (const char* fp = getenv("MFGP_F32_PANEL")) h->f32_panel = std::max(1, atoi(fp));
@@ -763,7 +762,6 @@ int mfgp_destroy(mfgp_handle_t h) {
         if (h->side) (void)hipStreamDestroy(h->side);
         if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
         if (h->ev_join) (void)hipEventDestroy(h->ev_join);
-        if (h->ev_mid) (void)hipEventDestroy(h->ev_mid);
     }
     free(h);
     return MFGP_OK;
@@ -1095,7 +1093,7 @@ int mfgp_svgp_elbo(mfgp_handle_t h, int n, int m, int l, int p, int d, const dou
     if (n < 1 || m < 1 || l < 1 || p < 1 || !X || !Y || !Z || !thetas || !q_mu || !q_sqrt || !ws || !out || !info)
         return MFGP_ERR_ARG;
     if (!W && l != p) return MFGP_ERR_ARG;
-    svgp_set_side(SvgpSide{h->side, h->ev_fork, h->ev_join, h->ev_mid});
+    svgp_set_side(SvgpSide{h->side, h->ev_fork, h->ev_join});
     return svgp_elbo_impl(h->stream, h->nb, n, m, l, p, d, X, ldx, Y, ldy, Z, ldz, thetas, q_mu, q_sqrt, W, noise,
                           scale, jitter, ws, ws_bytes, out, g_mu, g_var, info, nullptr);
 }
@@ -1122,7 +1120,7 @@ int mfgp_svgp_elbo_grad(mfgp_handle_t h, int n, int m, int l, int p, int d, cons
     if (W == nullptr && l != p) return MFGP_ERR_ARG;
     if (W != nullptr && gW == nullptr) return MFGP_ERR_ARG;
     if (ldx < d + 1 || ldz < d + 1 || ldy < p) return MFGP_ERR_ARG;
-    svgp_set_side(SvgpSide{h->side, h->ev_fork, h->ev_join, h->ev_mid});
+    svgp_set_side(SvgpSide{h->side, h->ev_fork, h->ev_join});
     return svgp_grad_impl(h->stream, h->nb, n, m, l, p, d, X, ldx, Y, ldy, Z, ldz, thetas, q_mu, q_sqrt, W, noise, 0.0,
                           scale, kl_mult, jitter, ws, ws_bytes, out, g_mu, g_var, gZ, gtheta, gq_mu, gq_sqrt, gW,
                           gnoise, info);
@@ -1162,7 +1160,7 @@ int mfgp_svgp_predict(mfgp_handle_t h, int nstar, int m, int l, int p, int d, co
         !g_var || !f_mu || !f_var || !info)
         return MFGP_ERR_ARG;
     if (!W && l != p) return MFGP_ERR_ARG;
-    svgp_set_side(SvgpSide{h->side, h->ev_fork, h->ev_join, h->ev_mid});
+    svgp_set_side(SvgpSide{h->side, h->ev_fork, h->ev_join});
     return svgp_predict_impl(h->stream, h->nb, nstar, m, l, p, d, Xs, ldxs, Z, ldz, thetas, q_mu, q_sqrt, W, jitter,
                              ws, ws_bytes, g_mu, g_var, f_mu, f_var, info);
 }
@@ -1185,7 +1183,7 @@ int mfgp_svgp_predict_cov(mfgp_handle_t h, int mode, int nstar, int m, int l, in
         !ws || !g_mu || !g_var || !f_mu || !f_var || !f_cov || !info)
         return MFGP_ERR_ARG;
     if (!W && l != p) return MFGP_ERR_ARG;
-    svgp_set_side(SvgpSide{h->side, h->ev_fork, h->ev_join, h->ev_mid});
+    svgp_set_side(SvgpSide{h->side, h->ev_fork, h->ev_join});
     const int rc = svgp_predict_cov_impl(h->stream, h->nb, mode, nstar, m, l, p, d, Xs, ldxs, Z, ldz, thetas, q_mu,
                                          q_sqrt, W, jitter, ws, ws_bytes, g_mu, g_var, f_mu, f_var, f_cov, info);
     return rc == -2 ? MFGP_ERR_WORKSPACE : (rc ? MFGP_ERR_LAUNCH : MFGP_OK);

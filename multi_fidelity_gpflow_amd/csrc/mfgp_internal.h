@@ -186,12 +186,10 @@ void launch_bgemm(int nb, hipStream_t st, int ta, int tb, const BgemmArgs& a, in
 // K_uu factorization beside the K_uf Gram; the reverse pass's dE/dm, dE/dLq and K_diag terms beside
 // the gA -> Sigma_bar / K_bar -> kernel-derivative chain).  Set by the C-ABI entry points for the
 // calling thread; side == nullptr: everything on the caller's stream.
-struct SvgpSide { hipStream_t side; hipEvent_t fork, join, mid; };
+struct SvgpSide { hipStream_t side; hipEvent_t fork, join; };
 void svgp_set_side(const SvgpSide& sd);
 const SvgpSide& svgp_side();
-// a mid-branch dependency: work queued on `to` after this call waits for `from`'s work so far
-// (no-op without a side stream, or when from == to)
-void svgp_handoff(hipStream_t from, hipStream_t to);
+
 // fork the side stream off s (nothing without a side stream); returns the stream to launch on
 hipStream_t svgp_fork(hipStream_t s);
 void svgp_join(hipStream_t s);

@@ -19,7 +19,7 @@ namespace mfgp {
 
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
-static thread_local SvgpSide t_side{nullptr, nullptr, nullptr, nullptr};
+static thread_local SvgpSide t_side{nullptr, nullptr, nullptr};
 void svgp_set_side(const SvgpSide& sd) { t_side = sd; }
 const SvgpSide& svgp_side() { return t_side; }
 hipStream_t svgp_fork(hipStream_t s) {
@@ -33,11 +33,7 @@ void svgp_join(hipStream_t s) {
     (void)hipEventRecord(t_side.join, t_side.side);
     (void)hipStreamWaitEvent(s, t_side.join, 0);
 }
-void svgp_handoff(hipStream_t from, hipStream_t to) {
-    if (from == to || !t_side.mid) return;
-    (void)hipEventRecord(t_side.mid, from);
-    (void)hipStreamWaitEvent(to, t_side.mid, 0);
-}
+
 
 struct SvgpLayout {
     int nb, Tm, mpad, Tn, npad, G;
@@ -548,12 +544,10 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
     }
     hipLaunchKernelGGL(k_lq_pad, dim3(blocks, 1, L), dim3(256), 0, s, q_sqrt, m, S.mpad, S.Lq);
     if (!f_mu) hipLaunchKernelGGL(k_svgp_kl, dim3(KL_SLICES, L), dim3(NTHREADS), 0, s, q_mu, q_sqrt, m, L, S.kl_part);
-    if (!two_gemm) {   // C = Lq^T Li (the fused conditional's B = C Kuf), after Lq and Li
-        svgp_handoff(s, sk);
-        hipLaunchKernelGGL(k_lqt_linv<NB>, dim3(S.Tm * S.Tm, 1, L), dim3(NTHREADS), 2 * sizeof(double) * NB * (NB + 2),
-                           sk, S.Lq, S.Xo, S.C, S.Tm);
-    }
     svgp_join(s);
+    if (!two_gemm)   // C = Lq^T Li (the fused conditional's B = C Kuf), after Lq and Li
+        hipLaunchKernelGGL(k_lqt_linv<NB>, dim3(S.Tm * S.Tm, 1, L), dim3(NTHREADS), 2 * sizeof(double) * NB * (NB + 2),
+                           s, S.Lq, S.Xo, S.C, S.Tm);
     if (two_gemm) {
         const long mn = (long)S.mpad * S.npad;
         BgemmArgs ga{};

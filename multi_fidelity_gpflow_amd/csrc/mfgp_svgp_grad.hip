@@ -911,9 +911,10 @@ static int svgp_grad_run(hipStream_t s, int n, int m, int L, int p, int d, const
                               noise_dev, scale, gW);
     hipLaunchKernelGGL(k_qmu_pad, dim3(cdv(mpad, 256), 1, L), dim3(256), 0, s, q_mu, m, L, mpad, g.qm);
     // Side branch (svgp_fork): dE/dm, dE/dLq and the K_diag term need only the forward's A, B and
-    // the VE backward's alpha / beta; they run beside gA.  Then (svgp_handoff after gA) the side
-    // takes Kbar -> the (Z, X) derivative sums while the caller's stream runs Gb -> Sigma_bar ->
-    // the (Z, Z) sums.
+    // the VE backward's alpha / beta; they run beside gA -> Gb / Sigma_bar / Kbar -> the derivative
+    // sums.  (A second dependency, Kbar and the (Z, X) sums handed to the side after gA, measured
+    // 2.20 -> 2.11 ms alone but 2.23 -> 2.76 in a process with more streams than the 4 hardware
+    // queues: the graph's cross-queue waits stalled ~40 us at a time.)
     hipStream_t sb = svgp_fork(s);
     // 2. dE/dm = A alpha - m  (folding its row products into step 3's epilogue, which reads A as
     //    Cin, measured slower: +45 us there and an 18 us partial reduction against this 51 us pass)
@@ -945,8 +946,7 @@ static int svgp_grad_run(hipStream_t s, int n, int m, int L, int p, int d, const
         a.Mt = Tm; a.Nt = Tn; a.Kt = Tm;
         bgemm<NB>(s, 0, 0, a, L);
     }
-    svgp_handoff(s, sb);
-    // 6. Kbar = dE/dKuf = Li^T gA (side)
+    // 6. Kbar = dE/dKuf = Li^T gA
     {
         BgemmArgs a{};
         a.amask = 2;   // Li^T upper
@@ -955,7 +955,7 @@ static int svgp_grad_run(hipStream_t s, int n, int m, int L, int p, int d, const
         a.D = g.Kbar; a.ldd = npad; a.sD = mn;
         a.alpha = 1.0;
         a.Mt = Tm; a.Nt = Tn; a.Kt = Tm;
-        bgemm<NB>(sb, 1, 0, a, L);
+        bgemm<NB>(s, 1, 0, a, L);
     }
     // 4. dE/dLi = tril(gA Kuf^T)
     {
@@ -996,11 +996,11 @@ static int svgp_grad_run(hipStream_t s, int n, int m, int L, int p, int d, const
     } else {
         sq<NB>(s, Tm, L, mm, mpad, 1, Li, 0, g.T1, g.Sig, -1.0, nullptr, 0.0, 0, nullptr, nullptr, 0, 2, 0);   // Li^T upper
     }
-    // 8. kernel / inducing-point derivative sums: (Z, X) on the side, (Z, Z) here
+    // 8. kernel / inducing-point derivative sums
     // compile-time bound on d: the per-dimension accumulators stay in registers
     auto kgrad = [&](auto dc) {
         constexpr int DC = decltype(dc)::value;
-        launch_kgrad<DC>(sb, Z, ldz, m, X, ldx, n, g.Kbar, npad, mn, thetas, G, d, 1.0, g.n_at, g.nbc_uf, L, g.gth_uf,
+        launch_kgrad<DC>(s, Z, ldz, m, X, ldx, n, g.Kbar, npad, mn, thetas, G, d, 1.0, g.n_at, g.nbc_uf, L, g.gth_uf,
                          g.gz_uf);
         launch_kgrad<DC>(s, Z, ldz, m, Z, ldz, m, g.Sig, mpad, mm, thetas, G, d, 2.0, g.n_at, g.nbc_uu, L, g.gth_uu,
                          g.gz_uu);
@@ -1010,7 +1010,7 @@ static int svgp_grad_run(hipStream_t s, int n, int m, int L, int p, int d, const
     else if (d <= 12) kgrad(std::integral_constant<int, 12>{});
     else if (d <= 16) kgrad(std::integral_constant<int, 16>{});
     else kgrad(std::integral_constant<int, 32>{});
-    // the side's short tail (after Kbar and its sums: those are on the longer branch's heels)
+    // the side's short tail
     hipLaunchKernelGGL(k_glq_final, dim3(std::min(cdv(m * m, 256), 1024), 1, L), dim3(256), 0, sb, g.gLq, Lq, m, mpad,
                        mm, kl_mult, gq_sqrt);
     hipLaunchKernelGGL(k_kff_grad, dim3(L), dim3(NTHREADS), 0, sb, X, (long)ldx, n, g.beta, npad, thetas, G, d,
