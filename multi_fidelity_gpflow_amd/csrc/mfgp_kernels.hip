@@ -426,7 +426,8 @@ size_t gram_smem_bytes(int nb) {
 // read from LDS as a wave-wide broadcast.  Same arithmetic as gram_entry, bit for bit (same
 // scaling x * rcp_nr(l), same dot4 accumulation order, same expressions).
 // Entries with gi < wr1, gj < wr2 outside n1 x n2 are written 0.0 (the padded Kuf / Kmn buffers
-// need no memset).
+// need no memset), or 1.0 on the diagonal with GramArgs::padded (called directly, not through
+// launch_gram: the SVGP K_uu, whose padded rows factor as identity).
 constexpr int GD_T = 64;
 
 template <int D4>
@@ -518,6 +519,8 @@ __global__ __launch_bounds__(NTHREADS) void k_gram_dense(GramArgs a, int wr1, in
                 if (!(L1 || H1) || !(L2 || H2)) v = 0.0;   // linear.py:67-70 exact masks
             }
             if (gi == gj) v += a.diag_add;
+        } else if (a.padded && gi == gj) {
+            v = 1.0;   // identity padding (a batched K_uu for the step factorization)
         }
         out[(long)gi * a.ldo + gj] = v;
     }
