@@ -427,7 +427,8 @@ size_t gram_smem_bytes(int nb) {
 // scaling x * rcp_nr(l), same dot4 accumulation order, same expressions).
 // Entries with gi < wr1, gj < wr2 outside n1 x n2 are written 0.0 (the padded Kuf / Kmn buffers
 // need no memset), or 1.0 on the diagonal with GramArgs::padded (called directly, not through
-// launch_gram: the SVGP K_uu, whose padded rows factor as identity).
+// launch_gram: the SVGP K_uu, whose padded rows factor as identity; with GramArgs::R it also
+// writes that factorization's right-hand side R = I over the same extent).
 constexpr int GD_T = 64;
 
 template <int D4>
@@ -495,6 +496,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram_dense(GramArgs a, int wr1, in
     const double nD2 = a.rbf_only ? 0.0 : dot4(sD2 + c * D4, sD2 + c * D4, D4);
     __syncthreads();
     double* out = a.out + b * a.so;
+    double* Rb = (a.padded && a.R) ? a.R + b * a.sR : nullptr;   // fused RHS = I of the factorization
     const bool L2 = (f2 == 0.0), H2 = (f2 == 1.0);
     for (int rr = t >> 6; rr < GD_T; rr += NTHREADS / 64) {
         const int gi = r0 + rr;
@@ -523,6 +525,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gram_dense(GramArgs a, int wr1, in
             v = 1.0;   // identity padding (a batched K_uu for the step factorization)
         }
         out[(long)gi * a.ldo + gj] = v;
+        if (Rb) Rb[(long)gi * a.ldr + gj] = (gi == gj) ? 1.0 : 0.0;
     }
 }
 

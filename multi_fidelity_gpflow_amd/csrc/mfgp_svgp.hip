@@ -509,19 +509,18 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
     hipStream_t sk = svgp_fork(s);
     const int blocks = (int)std::min<long>((mm + 255) / 256, 2048);
     hipLaunchKernelGGL(k_zero_upper_tiles, dim3(blocks, 1, L), dim3(256), 0, s, S.Xo, NB, S.mpad, mm);
-    (void)hipMemsetAsync(info, 0, sizeof(int) * L, sk);
-    // Kuu_l (+ jitter) by the lean Gram launch, then the first diagonal factor of every latent as a
-    // launch of its own (fused into the Gram it set that launch's register allocation: 3.3% of a
-    // single-bin iteration for a 300 x 300 Gram per latent); RHS = I
+    // Kuu_l (+ jitter) and RHS = I by one Gram launch, then the first diagonal factor of every
+    // latent as a launch of its own (fused into the Gram it set that launch's register allocation:
+    // 3.3% of a single-bin iteration for a 300 x 300 Gram per latent); the first factor is the
+    // first writer of info (no memset)
     {
-        hipLaunchKernelGGL(k_rhs_init, dim3(blocks, 1, L), dim3(256), 0, sk, S.R, (long)S.mpad, mm, S.mpad, 0,
-                           (const double*)nullptr, 0L, 0L, m, 0);
         GramArgs g{};
         g.X1 = Z; g.ldx1 = ldz; g.sx1 = 0; g.n1 = m;
         g.X2 = Z; g.ldx2 = ldz; g.sx2 = 0; g.n2 = m;
         g.theta = thetas; g.stheta = S.G; g.D = d; g.rbf_only = 0;
         g.out = S.Kuu; g.ldo = S.mpad; g.so = mm;
         g.padded = 1; g.npad = S.mpad; g.tiles_c = S.Tm; g.add_noise = 0; g.diag_add = jitter;
+        g.R = S.R; g.ldr = S.mpad; g.sR = mm;
         // the dense-layout Gram (64 x 64 entries a workgroup, both triangles): the lean tile
         // launch took 56-66 us for 64 latents of 300 x 300 on the chain's critical path
         launch_gram_dense(g, L, S.mpad, S.mpad, sk);
