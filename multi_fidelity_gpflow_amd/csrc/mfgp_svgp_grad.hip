@@ -910,11 +910,26 @@ static int svgp_grad_run(hipStream_t s, int n, int m, int L, int p, int d, const
     if (W) hipLaunchKernelGGL(k_gw, dim3(cdv(p * L, NTHREADS / 64)), dim3(NTHREADS), 0, s, g.r, g_mu, g_var, W, n, p, L,
                               noise_dev, scale, gW);
     hipLaunchKernelGGL(k_qmu_pad, dim3(cdv(mpad, 256), 1, L), dim3(256), 0, s, q_mu, m, L, mpad, g.qm);
-    // Side branch (svgp_fork): dE/dm, dE/dLq and the K_diag term need only the forward's A, B and
-    // the VE backward's alpha / beta; they run beside gA -> Gb / Sigma_bar / Kbar -> the derivative
-    // sums.  (A second dependency, Kbar and the (Z, X) sums handed to the side after gA, measured
-    // 2.20 -> 2.11 ms alone but 2.23 -> 2.76 in a process with more streams than the 4 hardware
-    // queues: the graph's cross-queue waits stalled ~40 us at a time.)
+    // Two branches after gA (ONE fork, one join): the side takes dE/dm, dE/dLq, Kbar -> the (Z, X)
+    // derivative sums and the K_diag term; the caller's stream Gb -> Sigma_bar -> the (Z, Z) sums.
+    // (Forking before gA to run dE/dm / dE/dLq beside it, then handing Kbar to the side after gA
+    // with a second edge, measured 2.11 ms alone but 2.76 in a process holding more streams than
+    // the 4 hardware queues: that graph's cross-queue waits stalled ~40 us at a time; this one
+    // edge pair: 2.15 -> 2.08 alone, 2.18 -> 2.09 in the default bench process.)
+    // 3. gA = (2 Lq B - 2 A) diag(beta) + m alpha^T
+    {
+        BgemmArgs a{};
+        a.amask = 1;   // Lq lower
+        a.A = Lq; a.lda = mpad; a.sA = mm;
+        a.B = g.B; a.ldb = npad; a.sB = mn;
+        a.Cin = g.A; a.ldc = npad; a.sC = mn; a.beta = -2.0;
+        a.colscale = g.beta; a.scs = npad;
+        a.x = g.qm; a.sx = mpad; a.y = g.alpha; a.sy = npad;
+        a.D = g.gA; a.ldd = npad; a.sD = mn;
+        a.alpha = 2.0;
+        a.Mt = Tm; a.Nt = Tn; a.Kt = Tm;
+        bgemm<NB>(s, 0, 0, a, L);
+    }
     hipStream_t sb = svgp_fork(s);
     // 2. dE/dm = A alpha - m  (folding its row products into step 3's epilogue, which reads A as
     //    Cin, measured slower: +45 us there and an 18 us partial reduction against this 51 us pass)
@@ -932,21 +947,7 @@ static int svgp_grad_run(hipStream_t s, int n, int m, int L, int p, int d, const
         a.Mt = Tm; a.Nt = Tm; a.Kt = Tn; a.tril = 1;
         bgemm<NB>(sb, 0, 1, a, L);
     }
-    // 3. gA = (2 Lq B - 2 A) diag(beta) + m alpha^T
-    {
-        BgemmArgs a{};
-        a.amask = 1;   // Lq lower
-        a.A = Lq; a.lda = mpad; a.sA = mm;
-        a.B = g.B; a.ldb = npad; a.sB = mn;
-        a.Cin = g.A; a.ldc = npad; a.sC = mn; a.beta = -2.0;
-        a.colscale = g.beta; a.scs = npad;
-        a.x = g.qm; a.sx = mpad; a.y = g.alpha; a.sy = npad;
-        a.D = g.gA; a.ldd = npad; a.sD = mn;
-        a.alpha = 2.0;
-        a.Mt = Tm; a.Nt = Tn; a.Kt = Tm;
-        bgemm<NB>(s, 0, 0, a, L);
-    }
-    // 6. Kbar = dE/dKuf = Li^T gA
+    // 6. Kbar = dE/dKuf = Li^T gA (side)
     {
         BgemmArgs a{};
         a.amask = 2;   // Li^T upper
@@ -955,7 +956,7 @@ static int svgp_grad_run(hipStream_t s, int n, int m, int L, int p, int d, const
         a.D = g.Kbar; a.ldd = npad; a.sD = mn;
         a.alpha = 1.0;
         a.Mt = Tm; a.Nt = Tn; a.Kt = Tm;
-        bgemm<NB>(s, 1, 0, a, L);
+        bgemm<NB>(sb, 1, 0, a, L);
     }
     // 4. dE/dLi = tril(gA Kuf^T)
     {
@@ -996,11 +997,11 @@ static int svgp_grad_run(hipStream_t s, int n, int m, int L, int p, int d, const
     } else {
         sq<NB>(s, Tm, L, mm, mpad, 1, Li, 0, g.T1, g.Sig, -1.0, nullptr, 0.0, 0, nullptr, nullptr, 0, 2, 0);   // Li^T upper
     }
-    // 8. kernel / inducing-point derivative sums
+    // 8. kernel / inducing-point derivative sums: (Z, X) on the side, (Z, Z) here
     // compile-time bound on d: the per-dimension accumulators stay in registers
     auto kgrad = [&](auto dc) {
         constexpr int DC = decltype(dc)::value;
-        launch_kgrad<DC>(s, Z, ldz, m, X, ldx, n, g.Kbar, npad, mn, thetas, G, d, 1.0, g.n_at, g.nbc_uf, L, g.gth_uf,
+        launch_kgrad<DC>(sb, Z, ldz, m, X, ldx, n, g.Kbar, npad, mn, thetas, G, d, 1.0, g.n_at, g.nbc_uf, L, g.gth_uf,
                          g.gz_uf);
         launch_kgrad<DC>(s, Z, ldz, m, Z, ldz, m, g.Sig, mpad, mm, thetas, G, d, 2.0, g.n_at, g.nbc_uu, L, g.gth_uu,
                          g.gz_uu);
