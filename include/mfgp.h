@@ -52,6 +52,9 @@ typedef struct mfgp_handle_s* mfgp_handle_t;
 #define MFGP_FLOW_TIMEOUT (-100)
 
 int mfgp_version(void);
+/* Hash of the sources this library was built from (every file of csrc/ and include/mfgp.h:
+ * multi_fidelity_gpflow_amd/build.py source_hash()); "unknown" for a build made without it. */
+const char* mfgp_build_id(void);
 const char* mfgp_error_string(int code);
 
 /* Handle: device + stream + tile size (32 or 64).  No reference analogue

@@ -22,6 +22,7 @@ _sz = C.c_size_t
 # name -> argtypes (restype is int everywhere except noted)
 SIGNATURES = {
     "mfgp_version": [],
+    "mfgp_build_id": [],
     "mfgp_error_string": [_i],
     "mfgp_create": [_i, C.POINTER(_p)],
     "mfgp_destroy": [_p],
@@ -145,9 +146,28 @@ def load(path: str = None):
                     continue
                 fn = getattr(lib, name)
                 fn.argtypes = args
-                fn.restype = C.c_char_p if name == "mfgp_error_string" else C.c_int
+                fn.restype = C.c_char_p if name in ("mfgp_error_string", "mfgp_build_id") else C.c_int
             _lib = lib
     return _lib
+
+
+def build_id() -> str:
+    """The source hash the loaded library was built from (include/mfgp.h mfgp_build_id)."""
+    lib = load()
+    return lib.mfgp_build_id().decode() if hasattr(lib, "mfgp_build_id") else "unknown"
+
+
+def check_provenance():
+    """Raise unless the loaded libmfgp.so was built from the sources checked out beside it
+    (build.source_hash() of csrc/ + include/mfgp.h).  Diagnostic builds (MFGP_LIB_PATH) pass."""
+    from .build import source_hash
+    path = os.environ.get("MFGP_LIB_PATH")
+    if path and path != LIB_PATH:
+        return
+    want, got = source_hash(), build_id()
+    if got != want:
+        raise MFGPError(f"libmfgp.so was built from other sources (build id {got}, sources {want}): "
+                        "rebuild with `python -c 'import __graft_entry__ as g; g.build()'`")
 
 
 def check(code: int, what: str):

@@ -196,11 +196,8 @@ static int fence_wait(int dev, hipStream_t s, bool hold = false) {
     return MFGP_OK;
 }
 
-static int fence_record(int dev, hipStream_t s, bool release = false) {
-    if (dev < 0 || dev >= FENCE_MAX_DEVICES || stream_capturing(s)) return MFGP_OK;
-    FlowFence& f = g_fence[dev];
-    std::unique_lock<std::mutex> lk(f.mu);
-    if (!fence_enter(f, lk)) return MFGP_ERR_FENCE;
+// with f.mu locked: record the fence event on s (created on first use)
+static void fence_arm(FlowFence& f, int dev, hipStream_t s) {
     if (!f.ev) {
         int cur = -1;
         (void)hipGetDevice(&cur);
@@ -209,6 +206,14 @@ static int fence_record(int dev, hipStream_t s, bool release = false) {
         if (cur >= 0 && cur != dev) (void)hipSetDevice(cur);
     }
     if (f.ev && hipEventRecord(f.ev, s) == hipSuccess) f.armed = true;
+}
+
+static int fence_record(int dev, hipStream_t s, bool release = false) {
+    if (dev < 0 || dev >= FENCE_MAX_DEVICES || stream_capturing(s)) return MFGP_OK;
+    FlowFence& f = g_fence[dev];
+    std::unique_lock<std::mutex> lk(f.mu);
+    if (!fence_enter(f, lk)) return MFGP_ERR_FENCE;
+    fence_arm(f, dev, s);
     if (release && f.held && --f.depth <= 0) {   // the outermost RECORD of the holder
         f.held = false;
         f.depth = 0;
@@ -217,6 +222,38 @@ static int fence_record(int dev, hipStream_t s, bool release = false) {
     }
     return MFGP_OK;
 }
+
+// An eager flow launch's turn at the fence.  Taken before the first launch of the
+// sequence: the bounded host wait happens here, so a fence held past its bound by another thread
+// fails the call with NOTHING enqueued.  The fence's mutex is then kept until commit(), which
+// follows the flow launch and records the event unconditionally: no other thread's flow, WAIT or
+// hold can be ordered between this launch's wait and its record, and a launch that was enqueued
+// always becomes the fence's last flow.
+struct FenceTurn {
+    FlowFence* f = nullptr;
+    std::unique_lock<std::mutex> lk;
+    int dev = -1;
+    int rc = MFGP_OK;
+    FenceTurn(int device, hipStream_t s) {
+        if (device < 0 || device >= FENCE_MAX_DEVICES || stream_capturing(s)) return;
+        FlowFence& ff = g_fence[device];
+        lk = std::unique_lock<std::mutex>(ff.mu);
+        if (!fence_enter(ff, lk)) {
+            rc = MFGP_ERR_FENCE;
+            lk.unlock();
+            return;
+        }
+        if (ff.armed) (void)hipStreamWaitEvent(s, ff.ev, 0);
+        f = &ff;
+        dev = device;
+    }
+    void commit(hipStream_t s) {
+        if (!f) return;
+        fence_arm(*f, dev, s);
+        f = nullptr;
+        lk.unlock();
+    }
+};
 
 // k_gram (LML layout) with more lower tiles than CUs: one workgroup per CU, tile (0,0) and its
 // fused factor alone on workgroup 0 (beside two other tile workgroups it took ~2x as long, and
@@ -280,9 +317,9 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
     }
     if (pm) pm->mark(s);
     // the flow fence before any launch of the sequence: a fence held past its bound by another
-    // host thread fails the call with nothing enqueued
-    int fence_rc = L.flow_wgs ? fence_wait(h->device, s) : MFGP_OK;
-    if (fence_rc != MFGP_OK) return fence_rc;
+    // host thread fails the call with nothing enqueued; once past it, the flow is always recorded
+    FenceTurn fence(L.flow_wgs ? h->device : -1, s);
+    if (fence.rc != MFGP_OK) return fence.rc;
     // The AR1 flow path (NB = 32, nlf = 0): the Gram is formed inside k_chol_flow, so the launch
     // in front of it only sets up the workspace (sentinel fill, schedule tables, item slots) --
     // and a value+grad call leaves exactly that set-up behind (k_grad's tail).  In resident mode
@@ -332,7 +369,7 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
         fa.X = X; fa.ldxi = ldx; fa.Y = Y; fa.ldy = ldy; fa.theta = theta; fa.D = d;
         fa.gram = flow_gram ? 1 : 0;
         launch_chol_flow(fa, L.flow_wgs, s);
-        fence_rc = fence_record(h->device, s);
+        fence.commit(s);
     } else {
         CholArgs c{};
         c.A = L.A; c.lda = L.npad; c.sA = 0;
@@ -369,7 +406,6 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
     f.abortw = L.flow_wgs ? L.flags : nullptr;
     hipLaunchKernelGGL(k_reduce_items, dim3(2 + (want_grad ? L.G : 0)), dim3(NTHREADS), 0, s, f);
     if (pm) pm->mark(s);
-    if (fence_rc != MFGP_OK) return fence_rc;
     if (last() != hipSuccess) return MFGP_ERR_LAUNCH;
     if (leaves_setup) {
         h->res.ws = ws; h->res.n = n; h->res.p = p; h->res.d = d; h->res.flow_wgs = L.flow_wgs;
@@ -697,6 +733,15 @@ using namespace mfgp;
 extern "C" {
 
 int mfgp_version(void) { return 100; }
+
+// Build provenance: build.py passes the hash of the sources the library is compiled from (every
+// file of csrc/ and include/mfgp.h, build.source_hash()); the marker string also lets the builder
+// read the id from the file without loading it.
+#ifndef MFGP_BUILD_ID
+#define MFGP_BUILD_ID "unknown"
+#endif
+__attribute__((used)) static const char k_build_marker[] = "mfgp-build-id:" MFGP_BUILD_ID;
+const char* mfgp_build_id(void) { return k_build_marker + 14; }
 
 const char* mfgp_error_string(int code) {
     switch (code) {

@@ -228,7 +228,7 @@ class Engine:
         recorded graphs; the shared grow-only buffers may be replaced under them)."""
         return torch.empty(int(nbytes), dtype=torch.uint8, device=self.device)
 
-    def gpr_lml(self, X, Y, theta, want_grad=False, ws=None):
+    def gpr_lml(self, X, Y, theta, want_grad=False, ws=None, out=None, info=None):
         n, dp1 = X.shape
         p = Y.shape[1]
         d = dp1 - 1
@@ -239,8 +239,10 @@ class Engine:
             raise MFGPError("gpr_lml: private workspace too small")
         if Y.dtype != X.dtype:
             raise MFGPError("gpr_lml: X and Y must share a dtype")
-        out = torch.empty((1 + theta_size(d),), dtype=torch.float64, device=self.device)
-        info = torch.empty((1,), dtype=torch.int32, device=self.device)
+        if out is None:
+            out = torch.empty((1 + theta_size(d),), dtype=torch.float64, device=self.device)
+        if info is None:
+            info = torch.empty((1,), dtype=torch.int32, device=self.device)
         check(self.lib.mfgp_gpr_lml_ex(self.h, dtype_code(X), n, p, d, ptr(X), dp1, ptr(Y), p, ptr(theta),
                                        int(want_grad), ptr(ws), ws.numel(), ptr(out), ptr(info)), "mfgp_gpr_lml_ex")
         return out, info

@@ -17,6 +17,18 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running CPU oracle check")
 
 
+_provenance_checked = []
+
+
+def pytest_runtest_setup(item):
+    """Before the first GPU test: the loaded libmfgp.so must be the one built from the sources
+    checked out here (mfgp_build_id against build.source_hash(); VERDICT r5 #7)."""
+    if "gpu" in item.keywords and not _provenance_checked:
+        from multi_fidelity_gpflow_amd import _lib
+        _lib.check_provenance()
+        _provenance_checked.append(True)
+
+
 @pytest.fixture(scope="session")
 def kats():
     import json

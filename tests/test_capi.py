@@ -34,6 +34,15 @@ def test_python_binding_covers_header(lib):
     assert set(SIGNATURES) == set(_declared())
 
 
+def test_library_built_from_checked_out_sources(lib):
+    """Build provenance: the library carries the hash of the sources it was compiled
+    from, and it is the hash of csrc/ + include/mfgp.h as checked out now."""
+    from multi_fidelity_gpflow_amd import _lib
+    from multi_fidelity_gpflow_amd.build import built_id, source_hash
+    assert lib.mfgp_build_id().decode() == source_hash() == built_id()
+    _lib.check_provenance()
+
+
 def test_host_only_entry_points(lib):
     assert lib.mfgp_version() >= 100
     assert lib.mfgp_error_string(-2).decode() == "workspace too small"

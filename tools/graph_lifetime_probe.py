@@ -1,0 +1,141 @@
+"""Diagnostic: which graph-lifetime order crashes hipGraphLaunch.
+
+Round 5's knob sweep segfaulted in the first replay of its fifth configuration when each
+configuration's session (and its captured fp32 lookahead graphs) was dropped only after the next
+session had been created.  Each scenario below runs in a child process with faulthandler on; the
+driver prints the child's exit status and the tail of its stderr (the Python stack of a crash).
+
+  python tools/graph_lifetime_probe.py            # every scenario, one child each
+  python tools/graph_lifetime_probe.py NAME       # one scenario in this process
+"""
+import faulthandler
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+SCENARIOS = ["torch_forkjoin", "f32_small_abrb", "f32_sweep_nolook", "f32_sweep_same", "f32_sweep_old"]
+
+
+def _log(msg):
+    print(msg, flush=True)
+
+
+def _model(n_lf, n_hf, p):
+    import numpy as np
+    import multi_fidelity_gpflow_amd as M
+    from multi_fidelity_gpflow_amd.data import synthetic_multifidelity
+    X, Y, _, _ = synthetic_multifidelity(n_lf=n_lf, n_hf=n_hf, p=p)
+    d = X.shape[1] - 1
+    return M.MultiFidelityGPModel(X, Y, M.SquaredExponential(lengthscales=np.ones(d)),
+                                  M.SquaredExponential(lengthscales=np.ones(d)), dtype="float32")
+
+
+def torch_forkjoin():
+    """No library: graphs with a side-stream fork / join (torch matmuls), each dropped only after the
+    next one was created and warmed up, as the sweep did."""
+    import torch
+    a = torch.randn(2048, 2048, device="cuda")
+    side = torch.cuda.Stream(priority=-1)
+    g_old = None
+    for i in range(8):
+        g = torch.cuda.CUDAGraph()
+        b = torch.empty_like(a)
+        with torch.cuda.graph(g):
+            cur = torch.cuda.current_stream()
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                c = a @ a
+            b.copy_(a @ a.T)
+            cur.wait_stream(side)
+            b.add_(c)
+        g_old = None   # the previous graph dies after the new capture
+        g.replay()
+        torch.cuda.synchronize()
+        g_old = g
+        _log(f"torch_forkjoin {i}: ok")
+
+
+def _sweep(configs, lookahead=True, n=(16384, 2048, 512)):
+    import torch
+    from multi_fidelity_gpflow_amd.engine import Engine
+    torch.cuda.set_device(0)
+    eng = Engine.get()
+    eng.set_f32_lookahead(lookahead)
+    m = _model(*n)
+    sess = None
+    for i, (panel, rv) in enumerate(configs):
+        eng.set_f32_panel(panel)
+        eng.set_f32_reserve(rv)
+        # round 5's original order: the previous session (and its graphs) dies at this reassignment,
+        # i.e. after the new session was created and warmed up, before it captures
+        sess = m.adam_session(0.1, 8, graph=True, graph_chunk=2)
+        sess.run(2)
+        sess.prepare(4)
+        sess.sync()
+        t0 = time.time()
+        sess.run(4)
+        sess.sync()
+        _log(f"config {i} panel={panel} reserve={rv}: {(time.time() - t0) / 4 * 1e3:.1f} ms/step")
+
+
+def f32_sweep_old():
+    _sweep([(4, 32), (6, 32), (8, 32), (4, 48), (8, 48), (2, 32)])
+
+
+def f32_sweep_same():
+    _sweep([(6, 32)] * 6)
+
+
+def f32_sweep_nolook():
+    _sweep([(4, 32), (6, 32), (8, 32), (4, 48), (8, 48), (2, 32)], lookahead=False)
+
+
+def f32_small_abrb():
+    """VERDICT's order at a small fp32 size with the lookahead: capture A, capture B, release A,
+    replay B (several rounds)."""
+    import torch
+    torch.cuda.set_device(0)
+    m = _model(3584, 512, 64)
+    for i in range(6):
+        a = m.adam_session(0.1, 8, graph=True, graph_chunk=2)
+        a.run(2)
+        a.prepare(4)
+        a.run(4)
+        b = m.adam_session(0.1, 8, graph=True, graph_chunk=2)
+        b.run(2)
+        b.prepare(4)
+        a.close()
+        del a
+        b.run(4)
+        b.sync()
+        _log(f"f32_small_abrb {i}: ok")
+        del b
+
+
+def driver():
+    outdir = os.path.join(ROOT, "gpurun_out", "graph_probe")
+    os.makedirs(outdir, exist_ok=True)
+    for name in (sys.argv[2:] or SCENARIOS):
+        t0 = time.time()
+        with open(os.path.join(outdir, name + ".log"), "w") as f:
+            r = subprocess.run([sys.executable, "-u", "-X", "faulthandler", os.path.abspath(__file__), name],
+                               stdout=f, stderr=subprocess.STDOUT, timeout=300)
+        tail = open(os.path.join(outdir, name + ".log")).read().splitlines()[-25:]
+        _log(f"== {name}: exit {r.returncode} after {time.time() - t0:.1f} s")
+        for ln in tail:
+            _log("   " + ln)
+        if r.returncode not in (0, -11, 139):
+            _log("stopping: not a clean exit or a host segfault")
+            break
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] != "--all":
+        faulthandler.enable()
+        globals()[sys.argv[1]]()
+    else:
+        driver()
