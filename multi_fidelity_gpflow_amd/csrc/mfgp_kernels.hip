@@ -1674,28 +1674,12 @@ void launch_pred(const PredAArgs& pa, const PredOutArgs& po, int T, hipStream_t 
 //   Z = L^{-1} Y, alpha = L^{-T} Z, S_ij = sum_m L^{-1}_mi^T L^{-1}_mj - alpha_i alpha_j^T / P, and
 //   k_grad's epilogue (W = -P S against dK/dtheta recomputed from the inputs) on the three lower
 //   tiles; then finalize_body's LML / gradient output and adam_body's step.
-// LDS hazard check (a debug build, -DTINY_POISON=1; tools/tiny_poison.sh): at every slot reuse the
-// dead slots are overwritten with a signalling NaN between two extra barriers, so a read that was
-// not ordered before the reuse by the barrier named at that point returns NaN instead of stale data
-// (the parity tests then fail).  Off in the library: no code.
-#ifndef TINY_POISON
-#define TINY_POISON 0
-#endif
+// LDS hazards: every workgroup barrier of the kernel is TINY_BARRIER(k), k = 1 .. 19 in source
+// order; tests/test_tiny_schedule.py restates which LDS doubles each wave reads and writes between
+// them (every shape the kernel takes) and checks on the CPU that no two waves touch a double in one
+// interval unless both only read, and that each of the 19 barriers orders some such pair.
+#define TINY_BARRIER(k) __syncthreads()
 constexpr int TINY_MAXD = 16, TINY_XS = TINY_MAXD + 1, TINY_N = 64, TINY_P = 64;
-
-// slots in `mask` (bit i: LDS tile slot i of k_gpr_tiny) := signalling NaN
-__device__ __forceinline__ void tiny_poison(double* smem, unsigned mask) {
-    constexpr int E = TileCfg<32>::ELEMS;
-    const double snan = __builtin_bit_cast(double, 0x7FF4000000000000ull);
-    for (int sl = 0; sl < 16; ++sl)
-        if (mask & (1u << sl))
-            for (int e = threadIdx.x; e < E; e += NTHREADS) smem[(long)sl * E + e] = snan;
-}
-#if TINY_POISON
-#define TINY_REUSE(mask) do { __syncthreads(); tiny_poison(smem, (mask)); __syncthreads(); } while (0)
-#else
-#define TINY_REUSE(mask) do { } while (0)
-#endif
 
 struct TinyArgs {
     const double* X; long ldx;
@@ -1793,7 +1777,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
 #pragma unroll
     for (int q = 0; q < XPER; ++q)
         if (t + q * NTHREADS < TINY_N * TINY_XS) xr[t + q * NTHREADS] = xv0[q];
-    __syncthreads();
+    TINY_BARRIER(1);
     for (int e = t; e < TINY_N * TINY_XS; e += NTHREADS) {
         const int r = e / TINY_XS, d = e % TINY_XS;
         const double x = (d < D) ? xr[e] : 0.0;
@@ -1801,9 +1785,9 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
         aD[e] = (d < D4 && d < D) ? x * il[TINY_MAXD + d] : 0.0;
     }
     if (t < TINY_N) fl[t] = (t < n) ? xr[t * TINY_XS + D] : -1.0;
-    __syncthreads();
+    TINY_BARRIER(2);
     if (t < TINY_N) { nL[t] = dot4(aL + t * TINY_XS, aL + t * TINY_XS, D4); nD[t] = dot4(aD + t * TINY_XS, aD + t * TINY_XS, D4); }
-    __syncthreads();
+    TINY_BARRIER(3);
     // ---- K tiles (0,0), (1,0), (1,1): k_gram's padded-entry arithmetic, the dot products a_i . a_j
     //      of the expanded r^2 on the matrix core (16 x 16 blocks, three per wave, D4 / 4
     //      v_mfma_f64_16x16x4 each) instead of a dot4 chain of 2 D4 LDS reads an entry
@@ -1839,9 +1823,8 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
             }
         }
     }
-    __syncthreads();
+    TINY_BARRIER(4);
     // reuse: the Gram staging (slots 6-8) is dead after the barrier above; slots 6-9 become Y tiles
-    TINY_REUSE(0x7C0u);
     // ---- factor: D_0; L_10, K_11 update, D_1, L^{-1}_10
     if (w == 0) tile_potrf_inv_w1_wave(K00, S, K00, D0, dg, &bad[0]);
     else if (w == 1 && f.adam && aown) {   // adam_body's step-size and SoftplusGrad factors
@@ -1849,30 +1832,26 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
         a_alpha = f.lr * sqrt(1.0 - pow(f.b2, tt)) / (1.0 - pow(f.b1, tt));
         a_eu = exp(-pu) + 1.0;
     }
-    __syncthreads();
+    TINY_BARRIER(5);
     // reuse: K00 (slot 0, the factor's in-place scratch) is dead after the barrier above (Ki00 later)
-    TINY_REUSE(0x1u);
     if (T > 1) {
         Acc<32> acc;
         acc_zero(acc);
         tile_mma<32, false, true>(acc, K10, D0, 1.0);      // L_10 = K_10 D_0^T
         acc_to_lds(acc, L10);
-        __syncthreads();
+        TINY_BARRIER(6);
         // reuse: K10 (slot 1) was last read by the product above, before this barrier; T goes there
-        TINY_REUSE(0x2u);
         acc_load<32>(acc, K11, S);
         tile_mma<32, false, true>(acc, L10, L10, -1.0);    // K_11 - L_10 L_10^T
-        __syncthreads();   // every read of K11 (acc_load) is done before K11 is rewritten
-        acc_to_lds(acc, K11);
+        acc_to_lds(acc, K11);   // each wave rewrites the block it read: no barrier in between
         acc_zero(acc);
         tile_mma<32, false, false>(acc, L10, D0, 1.0);     // T = L_10 D_0 (into K10's slot)
         acc_to_lds(acc, K10);
-        __syncthreads();
+        TINY_BARRIER(7);
         if (w == 0) tile_potrf_inv_w1_wave(K11, S, K11, D1, dg + 32, &bad[1]);
-        __syncthreads();
+        TINY_BARRIER(8);
         // reuse: K11 (slot 2, the factor's scratch) and L_10 (slot 5, last read by T = L_10 D_0
         // before the barrier ahead of the factor) are dead; L^{-1}_10 is written over L_10 below
-        TINY_REUSE(0x24u);
         acc_zero(acc);
         tile_mma<32, false, false>(acc, D1, K10, -1.0);    // L^{-1}_10 = -D_1 T (over L10)
         acc_to_lds(acc, L10);   // (read, and T's slot 1 rewritten as Ki10, only after the barrier below)
@@ -1887,9 +1866,8 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
     //      is the LML's quadratic term in the step path's form) and K^{-1} = L^{-T} L^{-1} (lower
     //      tiles, over the consumed K00 / T / K11 slots); then alpha = L^{-T} Z, each column tile's
     //      results replacing its Y tiles (all read first)
-    __syncthreads();   // the Y tiles and every wave's block of L^{-1}_10 are in; every read of T is done
+    TINY_BARRIER(9);   // the Y tiles and every wave's block of L^{-1}_10 are in; every read of T is done
     // reuse: T (slot 1) is dead after the barrier above; Ki10 (or, in PRED, K(X, X*)) goes there
-    TINY_REUSE(T > 1 ? 0x2u : 0x0u);
     double* Ki00 = slot(0); double* Ki10 = slot(1); double* Ki11 = slot(2);
     double z2 = 0.0;
     Acc<32> zc[2][2];
@@ -1923,16 +1901,15 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
             acc_to_lds(acc, Ki11);
         }
     }
-    __syncthreads();
+    TINY_BARRIER(10);
     // reuse: the Y tiles (slots 6-9) were last read by the Z products, before the barrier above
-    TINY_REUSE(0x3C0u);
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
         if (c >= Tp) break;
         acc_to_lds(zc[c][0], Yt(0, c));
         if (T > 1) acc_to_lds(zc[c][1], Yt(1, c));
     }
-    __syncthreads();
+    TINY_BARRIER(11);
     if constexpr (PRED) {
         const int ns = a.ns, Ts = (ns + 31) / 32;
         const double rho = sc.rho();
@@ -1942,9 +1919,8 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
             const int r = e / TINY_XS, d = e % TINY_XS;
             xs[e] = (r < ns && d <= D) ? a.Xs[(long)r * a.ldxs + d] : 0.0;
         }
-        __syncthreads();
+        TINY_BARRIER(12);
         // reuse: slots 0, 1, 2 (K00 / T / K11, consumed) and 10 become K(X, X*)
-        TINY_REUSE(0x407u);
         for (int e = t; e < T * Ts * 1024; e += NTHREADS) {   // K(X, X*): the AR1 kernel, exact masks
             const int tl = e >> 10, r = (e >> 5) & 31, c = e & 31;
             const int ti = tl / Ts, tc = tl % Ts;
@@ -1966,7 +1942,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
             }
             Km(ti, tc)[r * S + c] = v;
         }
-        __syncthreads();
+        TINY_BARRIER(13);
         Acc<32> A0[2], A1[2];   // A = L^{-1} Kmn, column tile c
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
@@ -1979,16 +1955,15 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
                 tile_mma<32, false, false>(A1[c], D1, Km(1, c), 1.0);
             }
         }
-        __syncthreads();
+        TINY_BARRIER(14);
         // reuse: K(X, X*) (slots 0, 1, 2, 10) was last read by the A products, before the barrier above
-        TINY_REUSE(0x407u);
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             if (c >= Ts) break;
             acc_to_lds(A0[c], Km(0, c));
             if (T > 1) acc_to_lds(A1[c], Km(1, c));
         }
-        __syncthreads();
+        TINY_BARRIER(15);
         for (int cs = 0; cs < Ts; ++cs)   // mean tile (cs, cy) = sum_i A(i, cs)^T Z(i, cy)
             for (int cy = 0; cy < Tp; ++cy) {
                 Acc<32> m;
@@ -2033,9 +2008,8 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
             tile_mma<32, true, false>(ac[c][1], D1, Yt(1, c), 1.0);
         }
     }
-    __syncthreads();
+    TINY_BARRIER(16);
     // reuse: the Z tiles (slots 6-9) were last read by the alpha products, before the barrier above
-    TINY_REUSE(0x3C0u);
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
         if (c >= Tp) break;
@@ -2045,7 +2019,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
     auto At = [&](int r, int c) { return Yt(r, c); };
     double ld = 0.0;
     if (t < n) ld = log(dg[t]);
-    __syncthreads();
+    TINY_BARRIER(17);
     // ---- gradient: S tiles and k_grad's epilogue (per element: its weights; per dimension: the
     //      lengthscale sums, reduced at once, so no per-thread array is indexed at run time)
     double cLe[12], cDe[12];
@@ -2116,10 +2090,8 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
     }
     // ---- reductions (L^{-1} is consumed: its slots hold 64 quad partials per quantity): quantity
     //      q < G the gradient entry q, G the quadratic term, G + 1 sum log L_ii
-    __syncthreads();
     // reuse: D_0, D_1, L^{-1}_10 (slots 3-5) were last read by the K^{-1} / Z / alpha products, before
-    // the barriers above; the reduction buffer RB spans them
-    TINY_REUSE(0x38u);
+    // TINY_BARRIER(16); the reduction buffer RB spans them (the gradient above reads none of them)
     double* RB = slot(3);
     auto put = [&](int q, double v) {
         v = quad_sum(v);
@@ -2144,7 +2116,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
             put(2 + D + d, td);
         }
     }
-    __syncthreads();
+    TINY_BARRIER(18);
     for (int g0 = 0; g0 < G + 2; g0 += NTHREADS / 8) {
         const int qx = g0 + (t >> 3), sub = t & 7;
         double v = 0.0;
@@ -2166,7 +2138,7 @@ __global__ __launch_bounds__(NTHREADS) void k_gpr_tiny(TinyArgs a) {
         const int b0 = bad[0], b1 = (T > 1) ? bad[1] : 0;
         a.info[0] = b0 ? b0 : (b1 ? 32 + b1 : 0);
     }
-    __syncthreads();
+    TINY_BARRIER(19);
     // ---- finalize_body / adam_body (LDS staging instead of the item round trip)
     const double LOG2PI = 1.8378770664093453;
     const int info0 = (bad[0] != 0 || (T > 1 && bad[1] != 0)) ? 1 : 0;
