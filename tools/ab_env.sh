@@ -1,13 +1,17 @@
 #!/bin/bash
-# A/B of an environment knob on the Goku bench line (run on the GPU box from the repo root):
-#   bash tools/ab_env.sh VAR "v1 v2 ..."   -> interleaved rounds, evals/s and the flow launch time
+# Interleaved A/B of environment settings on the Goku headline step (GPU box, repo root):
+#   bash tools/ab_env.sh OUTDIR ROUNDS "ENV_A" "ENV_B" ...   (ENV: space-separated VAR=value, or "-")
+# Each round runs every setting once (bench.py --no-extras, 300 steps); prints ms/step per run.
 set -o pipefail
-mkdir -p gpurun_out
-var=$1; shift
-for round in 1 2 3; do
-  for v in $1; do
-    env "$var=$v" timeout -k 10 120 python bench.py --no-cpu-baseline --no-train-predict --no-extras \
-      > gpurun_out/abe_$v.json 2> gpurun_out/abe_$v.err || exit $?
-    python -c "import json; d=json.load(open('gpurun_out/abe_$v.json')); print('$var=$v', round(d['value'],1), d['roofline']['avg_launch_us'], d['roofline']['phase_ms'])"
+O=${1:?}; R=${2:?}; shift 2
+mkdir -p "$O"
+for r in $(seq 1 "$R"); do
+  k=0
+  for e in "$@"; do
+    k=$((k + 1))
+    envs=""; [ "$e" != "-" ] && envs="$e"
+    env $envs timeout -k 10 300 python bench.py --no-extras --no-cpu-baseline --no-train-predict \
+      > "$O/ab_${k}_$r.json" 2> "$O/ab_${k}_$r.err" || exit 3
+    python -c "import json,sys; d=json.load(open('$O/ab_${k}_$r.json')); print('round $r [$e]', d['value'], 'evals/s', d['ms_per_step'], 'ms', 'flow', d['roofline'].get('avg_launch_us'))"
   done
 done
