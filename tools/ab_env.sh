@@ -12,6 +12,6 @@ for r in $(seq 1 "$R"); do
     envs=""; [ "$e" != "-" ] && envs="$e"
     env $envs timeout -k 10 300 python bench.py --no-extras --no-cpu-baseline --no-train-predict \
       > "$O/ab_${k}_$r.json" 2> "$O/ab_${k}_$r.err" || exit 3
-    python -c "import json,sys; d=json.load(open('$O/ab_${k}_$r.json')); print('round $r [$e]', d['value'], 'evals/s', d['ms_per_step'], 'ms', 'flow', d['roofline'].get('avg_launch_us'))"
+    python -c "import json,sys; d=json.load(open('$O/ab_${k}_$r.json')); print('round $r [$e]', d['value'], 'evals/s', d['ms_per_step'], 'ms', 'phases', d['roofline'].get('phase_ms'))"
   done
 done
