@@ -240,6 +240,13 @@ int mfgp_svgp_elbo_grad(mfgp_handle_t h, int n, int m, int l, int p, int d, cons
                         double scale, double kl_mult, double jitter, void* ws, size_t ws_bytes, double* out, double* g_mu,
                         double* g_var, double* gZ, double* gtheta, double* gq_mu, double* gq_sqrt, double* gW,
                         double* gnoise, int* info);
+/* Layout of mfgp_svgp_elbo_grad's q_sqrt (input) and gq_sqrt (output) on this handle: 0 (default)
+ * [L][M][M] (lower part used / written, upper zero), 1 packed lower triangles [L][M(M+1)/2], entry
+ * (i, j <= i) at i(i+1)/2 + j -- the size of GPflow's unconstrained q_sqrt variable (the
+ * FillTriangular bijector's vector; q_sqrt of singlebin_svgp.py:57-62 and GPflow SVGP), so a training
+ * state's parameter, gradient and Adam moments hold no upper halves.  Other entry points always
+ * take [L][M][M]. */
+int mfgp_set_svgp_qs_packed(mfgp_handle_t h, int packed);
 
 /* One Keras-2.10 (legacy) Adam step on a packed parameter vector (the apply_gradients of
  * the SVGP optimize loops, linear_svgp.py:190 / singlebin_svgp.py:86): u unconstrained,

@@ -65,6 +65,7 @@ SIGNATURES = {
     "mfgp_svgp_grad_workspace_size": [_p, _i, _i, _i, _i, _i, C.POINTER(_sz)],
     "mfgp_svgp_elbo_grad": [_p, _i, _i, _i, _i, _i, _p, _i, _p, _i, _p, _i, _p, _p, _p, _p, _p, _d, _d, _d, _p,
                             _sz, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
+    "mfgp_set_svgp_qs_packed": [_p, _i],
     "mfgp_adam_packed": [_p, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _d, _d, _d, _p, _d, _p, _p],
     "mfgp_adam_packed_ex": [_p, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _d, _d, _d, _p, _d, _p, _p, _p, _i],
     "mfgp_gmf_gram": [_p, _i, _i, _i, _i, _p, _i, _p, _i, _p, _d, _p, _i],

@@ -37,6 +37,7 @@ struct mfgp_handle_s {
     int tiny;                   // small problems (n, p <= 64, D <= 16, AR1 kernel): one-launch LML step (default on; MFGP_TINY=0 / mfgp_set_tiny(h, 0) disables)
     hipStream_t side;           // its high-priority side stream + fork / join events (created with the handle)
     hipEvent_t ev_fork, ev_join;
+    int svgp_qs_packed;         // mfgp_set_svgp_qs_packed: mfgp_svgp_elbo_grad's q_sqrt / gq_sqrt as packed triangles
     int resident;               // mfgp_set_resident: fp64 value+grad flow calls may skip the set-up launch
     struct {                    // the last fp64 LML call on this handle, when it left its workspace set
         const void* ws;         // up for the next one (k_grad's grad_next_setup); ws == nullptr: none
@@ -1169,10 +1170,17 @@ int mfgp_svgp_elbo_grad(mfgp_handle_t h, int n, int m, int l, int p, int d, cons
     if (W == nullptr && l != p) return MFGP_ERR_ARG;
     if (W != nullptr && gW == nullptr) return MFGP_ERR_ARG;
     if (ldx < d + 1 || ldz < d + 1 || ldy < p) return MFGP_ERR_ARG;
-    svgp_set_side(SvgpSide{h->side, h->ev_fork, h->ev_join});
+    svgp_set_side(SvgpSide{h->side, h->ev_fork, h->ev_join, h->svgp_qs_packed});
     return svgp_grad_impl(h->stream, h->nb, n, m, l, p, d, X, ldx, Y, ldy, Z, ldz, thetas, q_mu, q_sqrt, W, noise, 0.0,
                           scale, kl_mult, jitter, ws, ws_bytes, out, g_mu, g_var, gZ, gtheta, gq_mu, gq_sqrt, gW,
                           gnoise, info);
+}
+
+int mfgp_set_svgp_qs_packed(mfgp_handle_t h, int packed) {
+    CHECK_H(h);
+    if (packed != 0 && packed != 1) return MFGP_ERR_ARG;
+    h->svgp_qs_packed = packed;
+    return MFGP_OK;
 }
 
 int mfgp_adam_packed(mfgp_handle_t h, int n, double* u, double* c, const double* g, double* m, double* v,

@@ -186,7 +186,10 @@ void launch_bgemm(int nb, hipStream_t st, int ta, int tb, const BgemmArgs& a, in
 // K_uu factorization beside the K_uf Gram; the reverse pass's dE/dm, dE/dLq and K_diag terms beside
 // the gA -> Sigma_bar / K_bar -> kernel-derivative chain).  Set by the C-ABI entry points for the
 // calling thread; side == nullptr: everything on the caller's stream.
-struct SvgpSide { hipStream_t side; hipEvent_t fork, join; };
+// per-call SVGP settings of the calling thread (svgp_set_side, from the handle at each entry):
+// its side stream and fork / join events; qs_packed: q_sqrt / gq_sqrt of the gradient entry as packed
+// lower triangles [L][M(M+1)/2] (mfgp_set_svgp_qs_packed)
+struct SvgpSide { hipStream_t side; hipEvent_t fork, join; int qs_packed = 0; };
 void svgp_set_side(const SvgpSide& sd);
 const SvgpSide& svgp_side();
 

@@ -101,13 +101,17 @@ __global__ void k_zero_upper_tiles(double* Xo, int nb, int mpad, long mm) {
     }
 }
 
-// tril(q_sqrt_l) into a zero-padded Mpad x Mpad buffer
-__global__ void k_lq_pad(const double* q_sqrt, int m, int mpad, double* Lq) {
+// tril(q_sqrt_l) into a zero-padded Mpad x Mpad buffer (packed: q_sqrt_l as its lower triangle,
+// (r, c <= r) at r (r + 1) / 2 + c)
+__global__ void k_lq_pad(const double* q_sqrt, int m, int mpad, double* Lq, int packed) {
     const int l = blockIdx.z;
-    const long tot = (long)mpad * mpad;
+    const long tot = (long)mpad * mpad, tri = (long)m * (m + 1) / 2;
     for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < tot; e += (long)gridDim.x * blockDim.x) {
         const int r = (int)(e / mpad), c = (int)(e % mpad);
-        Lq[l * tot + e] = (r < m && c <= r) ? q_sqrt[(long)l * m * m + (long)r * m + c] : 0.0;
+        double v = 0.0;
+        if (r < m && c <= r)
+            v = packed ? q_sqrt[l * tri + (long)r * (r + 1) / 2 + c] : q_sqrt[(long)l * m * m + (long)r * m + c];
+        Lq[l * tot + e] = v;
     }
 }
 
@@ -446,22 +450,35 @@ __global__ void k_svgp_mix(const double* g_mu, const double* g_var, const double
 // per (l, s); the -M L / 2 term is added in k_svgp_final.
 constexpr int KL_SLICES = 8;
 __global__ __launch_bounds__(NTHREADS) void k_svgp_kl(const double* q_mu, const double* q_sqrt, int m, int L,
-                                                      double* kl_part) {
+                                                      double* kl_part, int packed) {
     __shared__ double red[4];
     const int sl = blockIdx.x, l = blockIdx.y;
     const int r0 = (int)((long)m * sl / KL_SLICES), r1 = (int)((long)m * (sl + 1) / KL_SLICES);
-    const double* base = q_sqrt + (long)l * m * m + (long)r0 * m;
     double maha = 0.0, tr = 0.0, ld = 0.0;
     for (int r = r0 + threadIdx.x; r < r1; r += NTHREADS) {
         const double q = q_mu[(long)r * L + l];
         maha += q * q;
     }
-    const long ne = (long)(r1 - r0) * m;
-    for (long e = threadIdx.x; e < ne; e += NTHREADS) {
-        const int r = r0 + (int)(e / m), c = (int)(e % m);
-        const double v = base[e];
-        if (c <= r) tr += v * v;
-        if (c == r) ld += log(v * v);
+    if (packed) {   // the rows' lower triangles are one contiguous range; the diagonal one per row
+        const double* base = q_sqrt + (long)l * m * (m + 1) / 2;
+        const long e0 = (long)r0 * (r0 + 1) / 2, e1 = (long)r1 * (r1 + 1) / 2;
+        for (long e = e0 + threadIdx.x; e < e1; e += NTHREADS) {
+            const double v = base[e];
+            tr += v * v;
+        }
+        for (int r = r0 + threadIdx.x; r < r1; r += NTHREADS) {
+            const double v = base[(long)r * (r + 1) / 2 + r];
+            ld += log(v * v);
+        }
+    } else {
+        const double* base = q_sqrt + (long)l * m * m + (long)r0 * m;
+        const long ne = (long)(r1 - r0) * m;
+        for (long e = threadIdx.x; e < ne; e += NTHREADS) {
+            const int r = r0 + (int)(e / m), c = (int)(e % m);
+            const double v = base[e];
+            if (c <= r) tr += v * v;
+            if (c == r) ld += log(v * v);
+        }
     }
     maha = block_sum(maha, red);
     tr = block_sum(tr, red);
@@ -543,8 +560,9 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
         g.padded = 0; g.tiles_c = S.Tn; g.diag_add = 0.0;
         launch_gram_dense(g, L, S.mpad, S.npad, s);   // zero padding written by the kernel
     }
-    hipLaunchKernelGGL(k_lq_pad, dim3(blocks, 1, L), dim3(256), 0, s, q_sqrt, m, S.mpad, S.Lq);
-    if (!f_mu) hipLaunchKernelGGL(k_svgp_kl, dim3(KL_SLICES, L), dim3(NTHREADS), 0, s, q_mu, q_sqrt, m, L, S.kl_part);
+    const int qp = t_side.qs_packed;
+    hipLaunchKernelGGL(k_lq_pad, dim3(blocks, 1, L), dim3(256), 0, s, q_sqrt, m, S.mpad, S.Lq, qp);
+    if (!f_mu) hipLaunchKernelGGL(k_svgp_kl, dim3(KL_SLICES, L), dim3(NTHREADS), 0, s, q_mu, q_sqrt, m, L, S.kl_part, qp);
     svgp_join(s);
     if (!two_gemm)   // C = Lq^T Li (the fused conditional's B = C Kuf), after Lq and Li
         hipLaunchKernelGGL(k_lqt_linv<NB>, dim3(S.Tm * S.Tm, 1, L), dim3(NTHREADS), 2 * sizeof(double) * NB * (NB + 2),

@@ -355,10 +355,12 @@ __global__ void k_psi(const double* H, double* P, int mpad, long mm) {
     }
 }
 
-// dE/dLq := G - klm (Lq - diag(1/Lq_ii)) on the m x m lower part; zero elsewhere.  Out: [L][m][m]
-__global__ void k_glq_final(const double* G, const double* Lq, int m, int mpad, long mm, double klm, double* out) {
+// dE/dLq := G - klm (Lq - diag(1/Lq_ii)) on the m x m lower part; zero elsewhere.  Out: [L][m][m],
+// or (packed) the lower triangles [L][m (m + 1) / 2], (i, j <= i) at i (i + 1) / 2 + j
+__global__ void k_glq_final(const double* G, const double* Lq, int m, int mpad, long mm, double klm, double* out,
+                            int packed) {
     const int b = blockIdx.z;
-    const long tot = (long)m * m;
+    const long tot = (long)m * m, tri = (long)m * (m + 1) / 2;
     for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < tot; e += (long)gridDim.x * blockDim.x) {
         const int i = (int)(e / m), j = (int)(e % m);
         double v = 0.0;
@@ -367,7 +369,8 @@ __global__ void k_glq_final(const double* G, const double* Lq, int m, int mpad, 
             v = G[b * mm + (long)i * mpad + j] - klm * lq;
             if (i == j) v += klm / lq;
         }
-        out[(long)b * tot + e] = v;
+        if (!packed) out[(long)b * tot + e] = v;
+        else if (j <= i) out[(long)b * tri + (long)i * (i + 1) / 2 + j] = v;
     }
 }
 
@@ -1013,7 +1016,7 @@ static int svgp_grad_run(hipStream_t s, int n, int m, int L, int p, int d, const
     else kgrad(std::integral_constant<int, 32>{});
     // the side's short tail
     hipLaunchKernelGGL(k_glq_final, dim3(std::min(cdv(m * m, 256), 1024), 1, L), dim3(256), 0, sb, g.gLq, Lq, m, mpad,
-                       mm, kl_mult, gq_sqrt);
+                       mm, kl_mult, gq_sqrt, svgp_side().qs_packed);
     hipLaunchKernelGGL(k_kff_grad, dim3(L), dim3(NTHREADS), 0, sb, X, (long)ldx, n, g.beta, npad, thetas, G, d,
                        g.gth_kff);
     svgp_join(s);

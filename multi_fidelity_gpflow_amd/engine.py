@@ -389,9 +389,10 @@ class Engine:
         return self._size(self.lib.mfgp_svgp_grad_workspace_size, n, m, L, p, d)
 
     def svgp_elbo_grad(self, X, Y, Z, thetas, q_mu, q_sqrt, W, noise, scale, kl_mult, jitter, out, g_mu, g_var,
-                       gZ, gtheta, gq_mu, gq_sqrt, gW, gnoise, info, ws=None):
+                       gZ, gtheta, gq_mu, gq_sqrt, gW, gnoise, info, ws=None, qs_packed=False):
         """Gradient of VE*scale - kl_mult*KL w.r.t. the constrained SVGP parameters (all device
-        tensors, written in place; noise is a device scalar)."""
+        tensors, written in place; noise is a device scalar).  qs_packed: q_sqrt and gq_sqrt are
+        packed lower triangles [L, M(M+1)/2] (mfgp_set_svgp_qs_packed), else [L, M, M]."""
         n, dp1 = X.shape
         d = dp1 - 1
         p = Y.shape[1]
@@ -402,11 +403,16 @@ class Engine:
             ws = self.workspace("svgp_grad", nbytes)
         elif ws.numel() < nbytes:
             raise MFGPError("svgp_elbo_grad: private workspace too small")
-        check(self.lib.mfgp_svgp_elbo_grad(self.h, n, m, L, p, d, ptr(X), dp1, ptr(Y), Y.stride(0), ptr(Z), dp1,
-                                           ptr(thetas), ptr(q_mu), ptr(q_sqrt), ptr(W), ptr(noise), float(scale),
-                                           float(kl_mult), float(jitter), ptr(ws), ws.numel(), ptr(out), ptr(g_mu),
-                                           ptr(g_var), ptr(gZ), ptr(gtheta), ptr(gq_mu), ptr(gq_sqrt), ptr(gW),
-                                           ptr(gnoise), ptr(info)), "mfgp_svgp_elbo_grad")
+        h = self.h
+        check(self.lib.mfgp_set_svgp_qs_packed(h, 1 if qs_packed else 0), "mfgp_set_svgp_qs_packed")
+        try:
+            check(self.lib.mfgp_svgp_elbo_grad(h, n, m, L, p, d, ptr(X), dp1, ptr(Y), Y.stride(0), ptr(Z), dp1,
+                                               ptr(thetas), ptr(q_mu), ptr(q_sqrt), ptr(W), ptr(noise), float(scale),
+                                               float(kl_mult), float(jitter), ptr(ws), ws.numel(), ptr(out),
+                                               ptr(g_mu), ptr(g_var), ptr(gZ), ptr(gtheta), ptr(gq_mu), ptr(gq_sqrt),
+                                               ptr(gW), ptr(gnoise), ptr(info)), "mfgp_svgp_elbo_grad")
+        finally:
+            check(self.lib.mfgp_set_svgp_qs_packed(h, 0), "mfgp_set_svgp_qs_packed")
 
     def adam_packed(self, u, c, g, m, v, trainable, transform, span, step, lr_sched, b1, b2, eps, out, kl_mult,
                     loss_hist, kl_hist, info=None):

@@ -275,9 +275,13 @@ class _SVGPTrainer:
         qm = model.q_mu
         segs.append(("q_mu", (m, L), qm.numpy(), qm.unconstrained_variable, np.full((m, L), qm.trainable), 0, None))
         qs = model.q_sqrt
-        low = np.tril(np.ones((m, m), bool))[None].repeat(L, axis=0)
-        segs.append(("q_sqrt", (L, m, m), np.tril(qs.numpy()), np.tril(qs.unconstrained_variable),
-                     low & qs.trainable, 0, None))
+        # q_sqrt as packed lower triangles [L][M(M+1)/2] (row-major (i, j <= i) at i(i+1)/2 + j;
+        # mfgp_set_svgp_qs_packed): GPflow's unconstrained variable has no upper half either, and
+        # the packed Adam then moves half the bytes
+        self._tril = np.tril_indices(m)
+        ti, tj = self._tril
+        segs.append(("q_sqrt", (L, ti.size), qs.numpy()[:, ti, tj], np.asarray(qs.unconstrained_variable)[:, ti, tj],
+                     np.full((L, ti.size), qs.trainable), 0, None))
         if Wp is not None:
             segs.append(("W", (p, L), Wp.numpy(), Wp.unconstrained_variable, np.full((p, L), Wp.trainable), 0, None))
         nv = model.likelihood.variance
@@ -333,7 +337,13 @@ class _SVGPTrainer:
         return buf[off:off + int(np.prod(shape))].view(*shape)
 
     def grad_views(self):
-        return {k: self.view(self.g, k) for k in self.layout}
+        """Gradient views by parameter; q_sqrt's unpacked to [L, M, M] (lower part)."""
+        g = {k: self.view(self.g, k) for k in self.layout}
+        ti, tj = self._tril
+        dense = torch.zeros((self.L, self.m, self.m), dtype=torch.float64, device=self.g.device)
+        dense[:, torch.as_tensor(ti, device=dense.device), torch.as_tensor(tj, device=dense.device)] = g["q_sqrt"]
+        g["q_sqrt"] = dense
+        return g
 
     def grad(self):
         """One gradient evaluation at the current parameters, ordered on the trainer's stream."""
@@ -348,7 +358,7 @@ class _SVGPTrainer:
                                 self.view(c, "q_sqrt"), W, self.view(c, "noise"), self.scale, self.klm,
                                 DEFAULT_JITTER, self.out, self.g_mu, self.g_var, self.view(g, "Z"),
                                 self.view(g, "theta"), self.view(g, "q_mu"), self.view(g, "q_sqrt"), gW,
-                                self.view(g, "noise"), self.info, ws=self.ws)
+                                self.view(g, "noise"), self.info, ws=self.ws, qs_packed=True)
 
     def _step(self):
         self._grad()
@@ -399,8 +409,9 @@ class _SVGPTrainer:
 
         model.inducing_variable.unconstrained_variable = seg("Z")
         model.q_mu.unconstrained_variable = seg("q_mu")
-        qs = model.q_sqrt.unconstrained_variable
-        model.q_sqrt.unconstrained_variable = np.where(np.tril(np.ones(qs.shape[-2:], bool)), seg("q_sqrt"), qs)
+        qs = np.array(model.q_sqrt.unconstrained_variable)
+        qs[:, self._tril[0], self._tril[1]] = seg("q_sqrt")
+        model.q_sqrt.unconstrained_variable = qs
         if "W" in self.layout:
             model.kernel.W.unconstrained_variable = seg("W")
         model.likelihood.variance.unconstrained_variable = np.reshape(seg("noise"), model.likelihood.variance.shape)
