@@ -64,4 +64,5 @@ def test_resident_matches_nonresident_under_interleavings(goku, eng):
     refs = {"a": ref_a, "b": ref_b, "v": ref_v}
     for i, (k, (o, info)) in enumerate(seq):
         assert info == 0, (i, k, info)
-        np.testing.assert_array_equal(o, refs[k], err_msg=f"call {i} ({k})")
+        nv = 1 if k == "v" else o.size   # a value-only call writes out[0] only
+        np.testing.assert_array_equal(o[:nv], refs[k][:nv], err_msg=f"call {i} ({k})")
