@@ -171,7 +171,7 @@ class SharedThetaTrainer:
             def _adam(out):
                 # the reduced LML is NaN on every rank when any rank's evaluation failed (its
                 # finalize writes NaN): all ranks then skip the update and keep the step counter
-                torch.isnan(out[:1], out=self._isnan)
+                torch.ne(out[:1], out[:1], out=self._isnan)   # NaN test, no allocation
                 self.bad.copy_(self._isnan)
                 eng.adam_packed(self.u, self.theta, out[1:], self.m, self.v, self.trainable, self.transform,
                                 self.span, self.step_t, self.lr, self.b1, self.b2, 1e-7, out, 1.0, self.hist_t,

@@ -17,7 +17,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-SCENARIOS = ["torch_forkjoin", "f32_small_abrb", "f32_sweep_nolook", "f32_sweep_same", "f32_sweep_old"]
+SCENARIOS = ["f32_keep_all", "f32_small_sweep", "f32_destroy_after_capture", "f32_sweep_same"]
 
 
 def _log(msg):
@@ -63,27 +63,49 @@ def torch_forkjoin():
         _log(f"torch_forkjoin {i}: ok")
 
 
-def _sweep(configs, lookahead=True, n=(16384, 2048, 512)):
+def _sweep(configs, lookahead=True, n=(16384, 2048, 512), order="reassign"):
+    """order: "reassign" (round 5: the previous session dies when the next one is assigned, after
+    its creation and warm-up, before its capture), "keep" (no session is ever dropped), "after"
+    (the previous session is dropped after the next one captured, before its first replay)."""
     import torch
     from multi_fidelity_gpflow_amd.engine import Engine
     torch.cuda.set_device(0)
     eng = Engine.get()
     eng.set_f32_lookahead(lookahead)
     m = _model(*n)
-    sess = None
+    sess, kept = None, []
     for i, (panel, rv) in enumerate(configs):
         eng.set_f32_panel(panel)
         eng.set_f32_reserve(rv)
-        # round 5's original order: the previous session (and its graphs) dies at this reassignment,
-        # i.e. after the new session was created and warmed up, before it captures
+        prev = sess
         sess = m.adam_session(0.1, 8, graph=True, graph_chunk=2)
+        if order == "reassign":
+            prev = None
+        elif order == "keep":
+            kept.append(prev)
+            prev = None
         sess.run(2)
         sess.prepare(4)
+        if order == "after":
+            prev = None
         sess.sync()
         t0 = time.time()
         sess.run(4)
         sess.sync()
-        _log(f"config {i} panel={panel} reserve={rv}: {(time.time() - t0) / 4 * 1e3:.1f} ms/step")
+        _log(f"config {i} panel={panel} reserve={rv} stream {sess.stream.cuda_stream:#x}: "
+             f"{(time.time() - t0) / 4 * 1e3:.1f} ms/step")
+
+
+def f32_keep_all():
+    _sweep([(6, 32)] * 7, order="keep")
+
+
+def f32_destroy_after_capture():
+    _sweep([(6, 32)] * 7, order="after")
+
+
+def f32_small_sweep():
+    _sweep([(6, 32)] * 8, n=(3584, 512, 64))
 
 
 def f32_sweep_old():
