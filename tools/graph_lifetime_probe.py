@@ -142,6 +142,20 @@ def f32_small_abrb():
         del b
 
 
+def hip_only():
+    """The same orders with the HIP runtime alone (tools/ubench_graph_lifetime.hip), one child per
+    mode; stops at the first crash."""
+    exe = os.path.join(ROOT, "tools", "ubench_graph_lifetime")
+    for mode in (sys.argv[2:] or ["after", "nofork", "samestream", "reassign", "reassign_free"]):
+        r = subprocess.run([exe, mode], capture_output=True, text=True, timeout=120)
+        _log(f"== hip {mode}: exit {r.returncode}")
+        for ln in (r.stdout + r.stderr).splitlines()[-6:]:
+            _log("   " + ln)
+        if r.returncode not in (0, 1):
+            _log("stopping: the child crashed, aborted or timed out")
+            break
+
+
 def driver():
     outdir = os.path.join(ROOT, "gpurun_out", "graph_probe")
     os.makedirs(outdir, exist_ok=True)
@@ -161,7 +175,9 @@ def driver():
 
 
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] != "--all":
+    if len(sys.argv) > 1 and sys.argv[1] == "--hip":
+        hip_only()
+    elif len(sys.argv) > 1 and sys.argv[1] != "--all":
         faulthandler.enable()
         globals()[sys.argv[1]]()
     else:
