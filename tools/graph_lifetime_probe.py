@@ -146,7 +146,8 @@ def hip_only():
     """The same orders with the HIP runtime alone (tools/ubench_graph_lifetime.hip), one child per
     mode; stops at the first crash."""
     exe = os.path.join(ROOT, "tools", "ubench_graph_lifetime")
-    for mode in (sys.argv[2:] or ["after", "nofork", "samestream", "reassign", "reassign_free"]):
+    for mode in (sys.argv[2:] or ["after", "nofork", "samestream", "reassign", "reassign_free", "after_cs",
+                                  "reassign_cs"]):
         r = subprocess.run([exe, mode], capture_output=True, text=True, timeout=120)
         _log(f"== hip {mode}: exit {r.returncode}")
         for ln in (r.stdout + r.stderr).splitlines()[-6:]:

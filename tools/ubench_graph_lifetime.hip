@@ -10,6 +10,9 @@
 //   samestream     reassign, every session on one stream
 //   reassign_free  reassign + a hipFree of a fresh 64 MB buffer before each capture (torch's
 //                  empty_cache at torch.cuda.graph entry)
+//   reassign_cs    reassign, every capture on ONE capture stream (torch's default capture stream),
+//                  the eager runs and the replays on the session's stream s_k
+//   after_cs       after, with the capture stream
 //   hipcc --offload-arch=gfx950 -O3 tools/ubench_graph_lifetime.hip -o tools/ubench_graph_lifetime
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -33,8 +36,9 @@ int main(int argc, char** argv) {
     const char* mode = argc > 1 ? argv[1] : "reassign";
     const bool fork = strcmp(mode, "nofork") != 0;
     const bool same = strcmp(mode, "samestream") == 0;
-    const bool after = strcmp(mode, "after") == 0;
+    const bool after = strncmp(mode, "after", 5) == 0;
     const bool dofree = strcmp(mode, "reassign_free") == 0;
+    const bool cs = strstr(mode, "_cs") != nullptr;
     const int sessions = 8, panels = 20, n = 1 << 16;
     int lo = 0, hi = 0;
     CK(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -60,8 +64,9 @@ int main(int argc, char** argv) {
             }
         }
     };
-    hipStream_t one = nullptr;
+    hipStream_t one = nullptr, cap = nullptr;
     if (same) CK(hipStreamCreateWithFlags(&one, hipStreamNonBlocking));
+    if (cs) CK(hipStreamCreateWithFlags(&cap, hipStreamNonBlocking));
     hipGraphExec_t prev = nullptr;
     for (int k = 0; k < sessions; ++k) {
         hipStream_t s = one;
@@ -75,10 +80,19 @@ int main(int argc, char** argv) {
             CK(hipFree(t));
         }
         hipGraph_t g;
-        CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
-        pattern(s);
-        pattern(s);                       // two steps a graph
-        CK(hipStreamEndCapture(s, &g));
+        hipStream_t c = cs ? cap : s;
+        if (cs) {   // the capture stream follows the session's work (torch's wait_stream)
+            hipEvent_t e;
+            CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            CK(hipEventRecord(e, s));
+            CK(hipStreamWaitEvent(c, e, 0));
+            CK(hipStreamSynchronize(c));
+            CK(hipEventDestroy(e));
+        }
+        CK(hipStreamBeginCapture(c, hipStreamCaptureModeGlobal));
+        pattern(c);
+        pattern(c);                       // two steps a graph
+        CK(hipStreamEndCapture(c, &g));
         hipGraphExec_t ex;
         CK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
         CK(hipGraphDestroy(g));
