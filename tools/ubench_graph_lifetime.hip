@@ -13,6 +13,8 @@
 //   reassign_cs    reassign, every capture on ONE capture stream (torch's default capture stream),
 //                  the eager runs and the replays on the session's stream s_k
 //   after_cs       after, with the capture stream
+//   *_af           (suffix) instantiated with hipGraphInstantiateFlagAutoFreeOnLaunch, as torch's
+//                  CUDAGraph::capture_end does
 //   hipcc --offload-arch=gfx950 -O3 tools/ubench_graph_lifetime.hip -o tools/ubench_graph_lifetime
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -39,6 +41,7 @@ int main(int argc, char** argv) {
     const bool after = strncmp(mode, "after", 5) == 0;
     const bool dofree = strcmp(mode, "reassign_free") == 0;
     const bool cs = strstr(mode, "_cs") != nullptr;
+    const bool af = strstr(mode, "_af") != nullptr;
     const int sessions = 8, panels = 20, n = 1 << 16;
     int lo = 0, hi = 0;
     CK(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -94,7 +97,8 @@ int main(int argc, char** argv) {
         pattern(c);                       // two steps a graph
         CK(hipStreamEndCapture(c, &g));
         hipGraphExec_t ex;
-        CK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+        if (af) CK(hipGraphInstantiateWithFlags(&ex, g, hipGraphInstantiateFlagAutoFreeOnLaunch));
+        else CK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
         CK(hipGraphDestroy(g));
         if (after && prev) { CK(hipGraphExecDestroy(prev)); prev = nullptr; }
         printf("session %d: launching\n", k);
