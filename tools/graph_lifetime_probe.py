@@ -17,7 +17,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-SCENARIOS = ["f32_keep_all", "f32_small_sweep", "f32_destroy_after_capture", "f32_sweep_same"]
+SCENARIOS = ["small_close_before", "small_buffers_after", "small_graphs_after", "f32_small_sweep"]
 
 
 def _log(msg):
@@ -94,6 +94,52 @@ def _sweep(configs, lookahead=True, n=(16384, 2048, 512), order="reassign"):
         sess.sync()
         _log(f"config {i} panel={panel} reserve={rv} stream {sess.stream.cuda_stream:#x}: "
              f"{(time.time() - t0) / 4 * 1e3:.1f} ms/step")
+
+
+def _small_sweep(variant, count=8):
+    """Bisection of the reassign order at a small fp32 size (lookahead on):
+      close_before   the previous session's graphs closed before the next session is created
+                     (round 5's fix), its buffers dropped after
+      graphs_after   the next session created and warmed up, then the previous session's graphs
+                     closed (its buffers kept alive), then the capture
+      buffers_after  the previous session's graphs closed before the next session is created, its
+                     buffers dropped after the next session's warm-up (before the capture)"""
+    import torch
+    from multi_fidelity_gpflow_amd.engine import Engine
+    torch.cuda.set_device(0)
+    eng = Engine.get()
+    eng.set_f32_lookahead(True)
+    m = _model(3584, 512, 64)
+    prev, kept = None, []
+    for i in range(count):
+        if prev is not None and variant in ("close_before", "buffers_after"):
+            prev.close()
+        sess = m.adam_session(0.1, 8, graph=True, graph_chunk=2)
+        sess.run(2)
+        if prev is not None:
+            if variant == "graphs_after":
+                prev.close()
+                kept.append(prev)
+            prev = None          # close_before / buffers_after: the buffers go here
+        sess.prepare(4)
+        sess.sync()
+        sess.run(4)
+        sess.sync()
+        _log(f"{variant} {i}: ok")
+        prev = sess
+        del sess
+
+
+def small_close_before():
+    _small_sweep("close_before")
+
+
+def small_graphs_after():
+    _small_sweep("graphs_after")
+
+
+def small_buffers_after():
+    _small_sweep("buffers_after")
 
 
 def f32_keep_all():
