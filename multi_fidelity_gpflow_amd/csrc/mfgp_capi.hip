@@ -8,6 +8,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include <chrono>
 #include <condition_variable>
 #include <mutex>
@@ -48,6 +52,22 @@ struct mfgp_handle_s {
 };
 
 namespace mfgp {
+
+// Diagnostic: with MFGP_SEGV_TRACE=1 in the environment when the library loads, a host SIGSEGV prints
+// the native call stack (symbol names from the dynamic tables) to stderr before the default action.
+static void segv_trace(int sig) {
+    void* fr[64];
+    const int n = backtrace(fr, 64);
+    static const char msg[] = "\nlibmfgp: SIGSEGV, native stack:\n";
+    (void)!write(2, msg, sizeof(msg) - 1);
+    backtrace_symbols_fd(fr, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+__attribute__((constructor)) static void segv_trace_install() {
+    const char* e = getenv("MFGP_SEGV_TRACE");
+    if (e && atoi(e) != 0) signal(SIGSEGV, segv_trace);
+}
 
 static inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 

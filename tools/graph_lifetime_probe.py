@@ -200,7 +200,7 @@ def hip_only():
             _log("   " + ln)
         if r.returncode not in (0, 1):
             _log("stopping: the child crashed, aborted or timed out")
-            break
+            sys.exit(3)
 
 
 def driver():
@@ -218,7 +218,7 @@ def driver():
         if r.returncode not in (0, 1):
             # a crash, abort or time limit: nothing more runs on the GPU in this call
             _log("stopping: the child crashed, aborted or timed out")
-            break
+            sys.exit(3)
 
 
 if __name__ == "__main__":
