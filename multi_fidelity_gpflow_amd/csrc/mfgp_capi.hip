@@ -41,8 +41,6 @@ struct mfgp_handle_s {
     int tiny;                   // small problems (n, p <= 64, D <= 16, AR1 kernel): one-launch LML step (default on; MFGP_TINY=0 / mfgp_set_tiny(h, 0) disables)
     hipStream_t side;           // its high-priority side stream + fork / join events (created with the handle)
     hipEvent_t ev_fork, ev_join;
-    struct CapEv { unsigned long long id; hipEvent_t fork, join; } * cap_ev;   // one pair per stream capture
-    int n_cap_ev, cap_ev_len;
     int svgp_qs_packed;         // mfgp_set_svgp_qs_packed: mfgp_svgp_elbo_grad's q_sqrt / gq_sqrt as packed triangles
     int resident;               // mfgp_set_resident: fp64 value+grad flow calls may skip the set-up launch
     struct {                    // the last fp64 LML call on this handle, when it left its workspace set
@@ -195,53 +193,6 @@ static FlowFence g_fence[FENCE_MAX_DEVICES];
 static bool stream_capturing(hipStream_t s) {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
-}
-
-// The fork / join event pair of a two-stream launch sequence (the fp32 lookahead, the SVGP side
-// stream) enqueued on s.  Eagerly: the handle's pair.  Inside a stream capture: a pair created for
-// THAT capture and never recorded outside it (kept until mfgp_destroy; a capture of a whole step
-// uses one pair).  One pair shared by eager runs and by every capture crashed hipGraphLaunch in
-// the replay of a later capture: with a graph exec holding that pair's capture-time edges destroyed
-// after the pair was recorded eagerly again (tools/graph_lifetime_probe.py small_graphs_after: the
-// fifth session's first replay segfaulted; destroying it before the eager use, or never, did not).
-static void fork_events(mfgp_handle_t h, hipStream_t s, hipEvent_t& fork, hipEvent_t& join) {
-    fork = h->ev_fork;
-    join = h->ev_join;
-    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    unsigned long long id = 0;
-    if (hipStreamGetCaptureInfo(s, &st, &id) != hipSuccess || st != hipStreamCaptureStatusActive) return;
-    for (int i = h->n_cap_ev - 1; i >= 0; --i)
-        if (h->cap_ev[i].id == id) {
-            fork = h->cap_ev[i].fork;
-            join = h->cap_ev[i].join;
-            return;
-        }
-    hipEvent_t f = nullptr, j = nullptr;
-    if (hipEventCreateWithFlags(&f, hipEventDisableTiming) != hipSuccess) return;
-    if (hipEventCreateWithFlags(&j, hipEventDisableTiming) != hipSuccess) {
-        (void)hipEventDestroy(f);
-        return;
-    }
-    if (h->n_cap_ev == h->cap_ev_len) {
-        const int len = h->cap_ev_len ? 2 * h->cap_ev_len : 16;
-        void* p = realloc(h->cap_ev, sizeof(*h->cap_ev) * (size_t)len);
-        if (!p) {
-            (void)hipEventDestroy(f);
-            (void)hipEventDestroy(j);
-            return;
-        }
-        h->cap_ev = static_cast<decltype(h->cap_ev)>(p);
-        h->cap_ev_len = len;
-    }
-    h->cap_ev[h->n_cap_ev++] = {id, f, j};
-    fork = f;
-    join = j;
-}
-
-static SvgpSide svgp_side_of(mfgp_handle_t h, int qs_packed = 0) {
-    hipEvent_t ef, ej;
-    fork_events(h, h->stream, ef, ej);
-    return SvgpSide{h->side, ef, ej, qs_packed};
 }
 
 // with f.mu locked: wait (bounded) until no other thread holds the fence
@@ -755,13 +706,8 @@ static int f32_value_grad(mfgp_handle_t h, int n, int p, int d, const float* X, 
     F32Args& a = L.a;
     a.info = info; a.X = X; a.ldx = ldx; a.Y = Y; a.ldy = ldy; a.theta = theta;
     a.upd_slots = (h->f32_reserve > 0 && h->ncu > h->f32_reserve) ? 2 * (h->ncu - h->f32_reserve) : 0;
-    if (h->f32_lookahead) {
-        hipEvent_t ef, ej;
-        fork_events(h, s, ef, ej);
-        launch_f32_sweep(a, s, mk, h->side, ef, ej);
-    } else {
-        launch_f32_sweep(a, s, mk);
-    }
+    if (h->f32_lookahead) launch_f32_sweep(a, s, mk, h->side, h->ev_fork, h->ev_join);
+    else launch_f32_sweep(a, s, mk);
     if (want_grad) launch_f32_grad(a, s, mk);
     if (mk) mk->begin(s, F32_FIN);
     if (refine) launch_f32_refine_lml(a, L.r, s);   // q = Y.a0 + a0.R + |L~^-1 R|^2 partials into zpart
@@ -790,13 +736,8 @@ static int f32_predict(mfgp_handle_t h, int n, int p, int d, int ns, const float
     F32Args& a = L.a;
     a.info = info; a.X = X; a.ldx = ldx; a.Y = Y; a.ldy = ldy; a.Xs = Xs; a.ldxs = ldxs; a.theta = theta;
     a.upd_slots = (h->f32_reserve > 0 && h->ncu > h->f32_reserve) ? 2 * (h->ncu - h->f32_reserve) : 0;
-    if (h->f32_lookahead) {
-        hipEvent_t ef, ej;
-        fork_events(h, h->stream, ef, ej);
-        launch_f32_sweep(a, h->stream, nullptr, h->side, ef, ej);
-    } else {
-        launch_f32_sweep(a, h->stream);
-    }
+    if (h->f32_lookahead) launch_f32_sweep(a, h->stream, nullptr, h->side, h->ev_fork, h->ev_join);
+    else launch_f32_sweep(a, h->stream);
     launch_f32_predict(a, mean, ldm, var, h->stream);   // variance (and the unrefined mean)
     if (h->f32_refine) launch_f32_refine_mean(a, L.r, mean, ldm, h->f32_refine, h->stream);
     if (cov) launch_f32_predict_cov(a, cov, ldc, h->stream);
@@ -891,11 +832,6 @@ int mfgp_destroy(mfgp_handle_t h) {
         if (h->side) (void)hipStreamDestroy(h->side);
         if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
         if (h->ev_join) (void)hipEventDestroy(h->ev_join);
-        for (int i = 0; i < h->n_cap_ev; ++i) {
-            (void)hipEventDestroy(h->cap_ev[i].fork);
-            (void)hipEventDestroy(h->cap_ev[i].join);
-        }
-        free(h->cap_ev);
     }
     free(h);
     return MFGP_OK;
@@ -1227,7 +1163,7 @@ int mfgp_svgp_elbo(mfgp_handle_t h, int n, int m, int l, int p, int d, const dou
     if (n < 1 || m < 1 || l < 1 || p < 1 || !X || !Y || !Z || !thetas || !q_mu || !q_sqrt || !ws || !out || !info)
         return MFGP_ERR_ARG;
     if (!W && l != p) return MFGP_ERR_ARG;
-    svgp_set_side(svgp_side_of(h));
+    svgp_set_side(SvgpSide{h->side, h->ev_fork, h->ev_join});
     return svgp_elbo_impl(h->stream, h->nb, n, m, l, p, d, X, ldx, Y, ldy, Z, ldz, thetas, q_mu, q_sqrt, W, noise,
                           scale, jitter, ws, ws_bytes, out, g_mu, g_var, info, nullptr);
 }
@@ -1254,7 +1190,7 @@ int mfgp_svgp_elbo_grad(mfgp_handle_t h, int n, int m, int l, int p, int d, cons
     if (W == nullptr && l != p) return MFGP_ERR_ARG;
     if (W != nullptr && gW == nullptr) return MFGP_ERR_ARG;
     if (ldx < d + 1 || ldz < d + 1 || ldy < p) return MFGP_ERR_ARG;
-    svgp_set_side(svgp_side_of(h, h->svgp_qs_packed));
+    svgp_set_side(SvgpSide{h->side, h->ev_fork, h->ev_join, h->svgp_qs_packed});
     return svgp_grad_impl(h->stream, h->nb, n, m, l, p, d, X, ldx, Y, ldy, Z, ldz, thetas, q_mu, q_sqrt, W, noise, 0.0,
                           scale, kl_mult, jitter, ws, ws_bytes, out, g_mu, g_var, gZ, gtheta, gq_mu, gq_sqrt, gW,
                           gnoise, info);
@@ -1301,7 +1237,7 @@ int mfgp_svgp_predict(mfgp_handle_t h, int nstar, int m, int l, int p, int d, co
         !g_var || !f_mu || !f_var || !info)
         return MFGP_ERR_ARG;
     if (!W && l != p) return MFGP_ERR_ARG;
-    svgp_set_side(svgp_side_of(h));
+    svgp_set_side(SvgpSide{h->side, h->ev_fork, h->ev_join});
     return svgp_predict_impl(h->stream, h->nb, nstar, m, l, p, d, Xs, ldxs, Z, ldz, thetas, q_mu, q_sqrt, W, jitter,
                              ws, ws_bytes, g_mu, g_var, f_mu, f_var, info);
 }
@@ -1324,7 +1260,7 @@ int mfgp_svgp_predict_cov(mfgp_handle_t h, int mode, int nstar, int m, int l, in
         !ws || !g_mu || !g_var || !f_mu || !f_var || !f_cov || !info)
         return MFGP_ERR_ARG;
     if (!W && l != p) return MFGP_ERR_ARG;
-    svgp_set_side(svgp_side_of(h));
+    svgp_set_side(SvgpSide{h->side, h->ev_fork, h->ev_join});
     const int rc = svgp_predict_cov_impl(h->stream, h->nb, mode, nstar, m, l, p, d, Xs, ldxs, Z, ldz, thetas, q_mu,
                                          q_sqrt, W, jitter, ws, ws_bytes, g_mu, g_var, f_mu, f_var, f_cov, info);
     return rc == -2 ? MFGP_ERR_WORKSPACE : (rc ? MFGP_ERR_LAUNCH : MFGP_OK);
