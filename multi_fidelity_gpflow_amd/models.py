@@ -368,8 +368,41 @@ def _pool_take(key):
         return _pool.pop(key, None)
 
 
+atexit.register(lambda: release_retired_graphs())
 atexit.register(clear_session_pool)
 Engine._mode_listeners.append(lambda eng: clear_session_pool())
+
+
+# ---------------------------------------------------------------- retired step graphs
+# The captured step graphs of a closed, released or dropped session are not destroyed before the
+# interpreter exits; they are kept here (no buffers: a graph holds no reference to the tensors it
+# was captured on).  Reason: in the HIP runtime this image ships (libamdhip64 of
+# ROCm 7.0.2, GPU_MAX_HW_QUEUES = 4), instantiating a graph with parallel branches (the fp32
+# lookahead's and the SVGP gradient's fork / join) acquires hardware queues for its internal branch
+# streams, shared by reference count with user streams; destroying such a graph exec after a later
+# user stream came to share one of those queues made the next hipGraphLaunch on it segfault
+# (tools/graph_lifetime_probe.py small_graphs_after: the fifth session's first replay, every run,
+# with AMD_LOG_LEVEL=3 showing the exec's releaseQueue on the queue the new session's stream
+# holds; never with the graphs kept).  A retired graph costs its exec's host nodes and kernel
+# arguments (a few hundred KB at the Synth size); release_retired_graphs() frees them when the
+# caller knows that no captured graph will be launched again in the process.
+_retired_graphs: list = []
+
+
+def _retire_graphs(graphs: dict):
+    if graphs:
+        _retired_graphs.extend(graphs.values())
+        graphs.clear()
+
+
+def release_retired_graphs():
+    """Destroy the retired step graphs now (see above: only when no captured graph is launched in
+    this process afterwards).  Returns how many were destroyed."""
+    n = len(_retired_graphs)
+    if n and torch.cuda.is_available():
+        torch.cuda.synchronize()
+    _retired_graphs.clear()
+    return n
 
 
 class _AdamCore:
@@ -414,9 +447,12 @@ class _AdamCore:
         self.nbytes = self.ws_bytes + 2 * o["end"] + X.numel() * X.element_size() + Y.numel() * Y.element_size()
         self.warm = False
 
+    def __del__(self):
+        _retire_graphs(getattr(self, "graphs", None))
+
     def release(self):
-        """Destroy the captured graphs and drop every buffer (an evicted or cleared pool entry)."""
-        self.graphs.clear()
+        """Retire the captured graphs and drop every buffer (an evicted or cleared pool entry)."""
+        _retire_graphs(self.graphs)
         self.X = self.Y = self.st = self.ws = self.d_in = self.h_in = self.h_out = None
         self.hist = self.si = self.info = self.out = None
 
@@ -577,6 +613,7 @@ class _StepRunner:
     def __init__(self, step, chunk: int, graphs: dict = None):
         self._step = weakref.WeakMethod(step) if hasattr(step, "__self__") else (lambda f=step: f)
         self.chunk = chunk
+        self._owns = graphs is None
         self.graphs = {} if graphs is None else graphs
 
     def step(self):
@@ -586,8 +623,14 @@ class _StepRunner:
         fn()
 
     def close(self):
-        """Destroy the captured graphs now (outside any capture)."""
-        self.graphs.clear()
+        """Release the captured graphs now (retired until exit, see release_retired_graphs)."""
+        _retire_graphs(self.graphs)
+
+    def __del__(self):
+        # a dropped runner's own graphs are retired too, not destroyed by reference counting (a
+        # session's graphs belong to its _AdamCore, which retires them itself)
+        if getattr(self, "_owns", False):
+            _retire_graphs(self.graphs)
 
     def _graph(self, n):
         g = self.graphs.get(n)

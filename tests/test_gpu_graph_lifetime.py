@@ -53,6 +53,36 @@ def test_f32_lookahead_release_earlier_graphs_then_replay():
         del b
 
 
+def test_f32_release_after_next_session_warmup():
+    """The order that crashed (tools/graph_lifetime_probe.py small_graphs_after): the
+    next session is created and runs its eager fp32 lookahead step on a new stream, THEN the
+    previous session's graphs are released, then the next session captures and replays.  Without
+    the graph retirement the fifth session's first replay segfaulted in hipGraphLaunch, every run."""
+    from multi_fidelity_gpflow_amd import models as MM
+    eng = Engine.get()
+    eng.set_f32_lookahead(True)
+    m = _f32_model()
+    ref = m.adam_session(0.1, 6, graph=False)
+    ref.run(6)
+    h_ref = _hist(ref, 6)
+    ref.close()
+    del ref
+    n0 = len(MM._retired_graphs)
+    prev = None
+    for _ in range(7):
+        sess = m.adam_session(0.1, 6, graph=True, graph_chunk=2)
+        sess.run(2)                   # eager, on the new session's stream
+        if prev is not None:
+            prev.close()              # release the previous session's graphs now
+            prev = None
+        sess.prepare(4)
+        sess.run(4)
+        np.testing.assert_array_equal(_hist(sess, 6), h_ref)
+        prev = sess
+    prev.close()
+    assert len(MM._retired_graphs) >= n0 + 7
+
+
 def test_svgp_release_earlier_graphs_then_replay(hbs):
     from multi_fidelity_gpflow_amd.svgp import _SVGPTrainer
     X, Y = hbs["X"], hbs["Y"]

@@ -32,8 +32,3 @@ for panel, rv in [(int(a), int(b)) for a, b in (x.split(":") for x in sys.argv[1
     sess.run(4)
     sess.sync()
     print(f"panel={panel} reserve={rv}: {(time.time() - t0) / 4 * 1e3:.1f} ms/step", flush=True)
-    # release this session's graphs before the next session captures: left to the reassignment
-    # below (the old graphs destroyed after the new session's warm-up), the fifth configuration's
-    # first graph replay segfaulted inside hipGraphLaunch (round 5; not seen with the release here)
-    sess.close()
-    del sess
