@@ -27,7 +27,6 @@ struct mfgp_handle_s {
     hipStream_t stream;
     int nb;
     int grad_chunk;
-    int grad_bchunk;            // k_grad_blk m-rows per task (NB = 32, AR1 kernel; 0: k_grad's one-tile tasks)
     int flow_wgs;   // k_chol_flow grid (one workgroup per CU); 0: launch-per-step Cholesky
     int flow_min_t; // fewest 32-tiles a factorization needs to take the flow (below: the step launches)
     int ncu;        // compute units of the device
@@ -110,7 +109,7 @@ static int flow_grid(int nb, int T, int Tp, int flow_wgs, int min_t) {
 }
 
 static GprLayout gpr_layout(int nb, int n, int p, int d, void* ws, int grad_chunk, int nlf = 0, int flow_wgs = 0,
-                            int flow_min_t = 0, int grad_bchunk = 0) {
+                            int flow_min_t = 0) {
     GprLayout L;
     L.nb = nb;
     L.T = ceil_div(n, nb);
@@ -120,8 +119,7 @@ static GprLayout gpr_layout(int nb, int n, int p, int d, void* ws, int grad_chun
     L.G = kernel_theta_size(nlf, d);
     L.gstride = (L.G + 3) & ~3;
     L.flow_wgs = flow_grid(nb, L.T, L.Tp, flow_wgs, flow_min_t);
-    // the blocked gradient (k_grad_blk: 2 x 2 output tiles a task) for the AR1 kernel on 32-tiles
-    L.gchunk = (nb == 32 && nlf == 0 && grad_bchunk > 0) ? -grad_bchunk : grad_chunk;
+    L.gchunk = grad_chunk;
     L.ng = grad_tasks(L.T, L.gchunk);
     Carve c(ws);
     const size_t ldr = (size_t)L.npad + L.ppad;
@@ -321,7 +319,7 @@ template <int NB>
 static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X, int ldx, const double* Y, int ldy,
                           double* theta, int want_grad, void* ws, size_t ws_bytes, double* out, int* info,
                           const FinArgs* adam, PhaseMarks* pm = nullptr, int nlf = 0) {
-    const GprLayout L = gpr_layout(NB, n, p, d, ws, h->grad_chunk, nlf, h->flow_wgs, h->flow_min_t, h->grad_bchunk);
+    const GprLayout L = gpr_layout(NB, n, p, d, ws, h->grad_chunk, nlf, h->flow_wgs, h->flow_min_t);
     if (ws_bytes < L.bytes) return MFGP_ERR_WORKSPACE;
     if (L.G > FIN_MAXG) return MFGP_ERR_ARG;   // finalize_body stages theta in LDS
     hipStream_t s = h->stream;
@@ -364,7 +362,7 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
         g.Dd = L.Dd; g.sD = 0; g.ldiag = L.ldiag; g.sL = 0; g.info = info; g.nlf = nlf;
         g.cnt = L.cnt; g.ncnt = L.ncnt;
         if (MFGP_REDUCE_FLAG) { g.isent = L.items; g.nisent = L.G + 2; }
-        const bool order = want_grad && std::abs(L.gchunk) + L.T + L.Tp < 2048;   // gram LDS holds the histogram
+        const bool order = want_grad && L.gchunk + L.T + L.Tp < 2048;   // gram LDS holds the histogram
         if (order) { g.gorder = L.gorder; g.gT = L.T; g.gchunk = L.gchunk; g.gTp = L.Tp; }
         if (L.flow_wgs) { g.fown = L.own; g.fW = FLOW_WAVES * (L.flow_wgs - 1); g.fflags = L.flags; g.nfflags = L.nflags; g.fpub = L.pub; g.npub = L.npub; }
         const int extra = (order ? 1 : 0) + (L.flow_wgs ? 1 : 0);
@@ -406,7 +404,7 @@ static int gpr_value_grad(mfgp_handle_t h, int n, int p, int d, const double* X,
     if (pm) pm->mark(s);
     if (want_grad) {
         GradArgs ga{L.Xo, ldr, X, (long)ldx, theta, L.gpart, L.gstride, L.T, L.Tp, n, p, d,
-                    L.gchunk, nlf, std::abs(L.gchunk) + L.T + L.Tp < 2048 ? L.gorder : nullptr};
+                    L.gchunk, nlf, L.gchunk + L.T + L.Tp < 2048 ? L.gorder : nullptr};
         if (leaves_setup) {   // the next evaluation's set-up, after the flow
             ga.fpub = L.pub; ga.npub = L.npub;
             ga.isent = L.items; ga.nisent = L.G + 2;
@@ -819,8 +817,6 @@ int mfgp_create(int device, mfgp_handle_t* out) {
     if (const char* fp = getenv("MFGP_F32_PANEL")) h->f32_panel = std::max(1, atoi(fp));
     if (const char* fl = getenv("MFGP_FLOW")) if (atoi(fl) == 0) h->flow_wgs = 0;
     if (const char* gc = getenv("MFGP_GRAD_CHUNK")) h->grad_chunk = std::max(1, atoi(gc));
-    h->grad_bchunk = 6;   // k_grad_blk m-rows per task (Goku T = 37: 511 tasks, all resident at two per CU)
-    if (const char* gb = getenv("MFGP_GRAD_BCHUNK")) h->grad_bchunk = std::max(0, atoi(gb));
     const char* env = getenv("MFGP_TILE");
     if (env && atoi(env) == 64) h->nb = 64;
     *out = h;
@@ -873,7 +869,7 @@ int mfgp_gpr_flow_trace(mfgp_handle_t h, int n, int p, int d, size_t* offset, in
     CHECK_D(d);
     if (n < 1 || p < 1 || !offset || !count) return MFGP_ERR_ARG;
     char* const base = reinterpret_cast<char*>((uintptr_t)1 << 20);   // any 256-B aligned stand-in
-    const GprLayout L = gpr_layout(h->nb, n, p, d, base, h->grad_chunk, 0, h->flow_wgs, h->flow_min_t, h->grad_bchunk);
+    const GprLayout L = gpr_layout(h->nb, n, p, d, base, h->grad_chunk, 0, h->flow_wgs, h->flow_min_t);
     *offset = (size_t)(reinterpret_cast<char*>(L.trace) - base);
     *count = L.ntrace;
     return MFGP_OK;
@@ -978,7 +974,7 @@ int mfgp_gmf_gpr_workspace_size(mfgp_handle_t h, int nlf, int n, int p, int d, s
     CHECK_D(d);
     CHECK_LF(nlf);
     if (n < 1 || p < 1 || !bytes) return MFGP_ERR_ARG;
-    *bytes = gpr_layout(h->nb, n, p, d, nullptr, h->grad_chunk, nlf, h->flow_wgs, h->flow_min_t, h->grad_bchunk).bytes;
+    *bytes = gpr_layout(h->nb, n, p, d, nullptr, h->grad_chunk, nlf, h->flow_wgs, h->flow_min_t).bytes;
     return MFGP_OK;
 }
 
@@ -1024,7 +1020,7 @@ int mfgp_gpr_workspace_size(mfgp_handle_t h, int n, int p, int d, size_t* bytes)
     CHECK_H(h);
     CHECK_D(d);
     if (n < 1 || p < 1 || !bytes) return MFGP_ERR_ARG;
-    *bytes = gpr_layout(h->nb, n, p, d, nullptr, h->grad_chunk, 0, h->flow_wgs, h->flow_min_t, h->grad_bchunk).bytes;
+    *bytes = gpr_layout(h->nb, n, p, d, nullptr, h->grad_chunk, 0, h->flow_wgs, h->flow_min_t).bytes;
     return MFGP_OK;
 }
 

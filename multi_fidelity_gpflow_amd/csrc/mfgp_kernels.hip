@@ -915,38 +915,15 @@ __host__ __device__ inline int grad_row_chunks(int T, int i, int ch) { return (T
 __host__ __device__ inline int grad_m0(int T, int i, int ch, int c) { (void)T; return i + c * ch; }
 __host__ __device__ inline int grad_m1(int T, int m0, int ch) { return min(T, m0 + ch); }
 
-// Blocked form (chunk < 0, k_grad_blk): a task is the 2 x 2 block of output tiles (2I, 2I+1) x
-// (2J, 2J+1), J <= I, over -chunk consecutive m-rows starting at 2I (rows m < 2I of those columns
-// of L^{-1} are zero).  Block row I has T - 2I m-rows.
-__host__ __device__ inline int gblk_chunks(int T, int I, int bch) { return (T - 2 * I + bch - 1) / bch; }
-
 __host__ __device__ int grad_tasks(int T, int ch) {
     int s = 0;
-    if (ch < 0) {
-        for (int I = 0; 2 * I < T; ++I) s += (I + 1) * gblk_chunks(T, I, -ch);
-        return s;
-    }
     for (int i = 0; i < T; ++i) s += (i + 1) * grad_row_chunks(T, i, ch);
     return s;
 }
 
 // k_grad task -> (row i, column j, chunk ch) in the natural order (rows, then columns,
 // then m-chunks); returns the task's item count (m tiles + the alpha items of chunk 0).
-// Blocked form: (block row I, block column J, chunk) and its count of 2 x 2 block steps.
 __device__ __forceinline__ int grad_decode(int t, int T, int chunk, int Tp, int& i, int& j, int& ch) {
-    if (chunk < 0) {
-        const int bch = -chunk;
-        for (i = 0;; ++i) {
-            const int cnt = (i + 1) * gblk_chunks(T, i, bch);
-            if (t < cnt) break;
-            t -= cnt;
-        }
-        const int nch = gblk_chunks(T, i, bch);
-        j = t / nch;
-        ch = t % nch;
-        const int m0 = 2 * i + ch * bch;
-        return min(T, m0 + bch) - m0 + (ch == 0 ? Tp : 0);
-    }
     for (i = 0;; ++i) {
         const int cnt = (i + 1) * grad_row_chunks(T, i, chunk);
         if (t < cnt) break;
@@ -993,7 +970,7 @@ __device__ __forceinline__ void grad_next_setup(const GradArgs& a) {
 constexpr int GRAD_ORDER_MAGIC = 0x4F524431;
 __device__ void build_grad_order(int T, int chunk, int Tp, int* order, int* hist) {
     const int ntask = grad_tasks(T, chunk);
-    const int lmax = (chunk < 0 ? -chunk : chunk) + Tp;
+    const int lmax = chunk + Tp;
     unsigned* hs = reinterpret_cast<unsigned*>(hist + lmax + 1);
     if (sched_cached(order, ntask, GRAD_ORDER_MAGIC, T, chunk, Tp, hs)) return;
     for (int l = threadIdx.x; l <= lmax; l += NTHREADS) hist[l] = 0;
@@ -1352,269 +1329,6 @@ __global__ __launch_bounds__(NTHREADS) void k_grad(GradArgs a) {
     grad_next_setup(a);
 }
 
-// ---- K5, blocked form (NB = 32, the AR1 kernel; GradArgs::chunk = -bch).  A workgroup owns the
-// 2 x 2 block of output tiles (i0, i0+1) x (j0, j0+1) = (2I, 2I+1) x (2J, 2J+1) and a chunk of bch
-// m-rows: per m it stages the four column tiles L^{-1}_{m,i0}, L^{-1}_{m,i1}, L^{-1}_{m,j0},
-// L^{-1}_{m,j1} once and runs the four tile products that contract them (k_grad: two tiles staged
-// per product), 32 MFMAs a wave per barrier instead of 8.  Tiles that are zero (L^{-1}_{m,i1} at
-// m = i0), above the diagonal ((i0, j1) of a diagonal block) or past the last tile are neither
-// loaded nor multiplied.  Its epilogue is k_grad's, run over the block's tiles with the partial
-// sums accumulated in place, so each task writes one partial per gradient entry.
-constexpr int GBLK_REGION = 8 * TileCfg<32>::ELEMS;        // 2 buffers x 4 operand tiles
-constexpr int GBLK_RAW = 4 * 32 * XS;                      // raw rows of i0, i1, j0, j1 (epilogue)
-constexpr int GBLK_RED_OFF = (GBLK_RAW + 4 * 32 + 1) & ~1; // after the rows and the 4 x 32 flags
-
-__global__ __launch_bounds__(NTHREADS, 2) void k_grad_blk(GradArgs a) {
-    constexpr int NB = 32, S = TileCfg<32>::S, E = TileCfg<32>::ELEMS;
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    const int G = kernel_theta_size(0, a.D);
-    double* xr = smem;                        // 4 x NB x XS raw rows (epilogue)
-    double* fl = smem + GBLK_RAW;             // 4 x NB flags
-    double* R = smem + GBLK_RED_OFF;          // G x GRAD_RLD quad partials
-    double* il2 = R + G * GRAD_RLD;           // 2 x D 1 / l^2
-    const MFTheta th{a.theta, a.D};
-    const int bch = -a.chunk;
-
-    const int task = a.order ? a.order[blockIdx.x] : (int)blockIdx.x;
-    int I, J, ch;
-    grad_decode(task, a.T, a.chunk, a.Tp, I, J, ch);
-    const int i0 = 2 * I, i1 = i0 + 1, j0 = 2 * J, j1 = j0 + 1;
-    const bool diag = I == J;
-    const bool vi1 = i1 < a.T, vj1 = j1 < a.T;
-    const bool t01 = vj1 && !diag, t10 = vi1, t11 = vi1 && vj1;
-    const int m0 = i0 + ch * bch, m1 = min(a.T, m0 + bch);
-    const int nm = m1 - m0;
-    const int nq = nm + (ch == 0 ? a.Tp : 0);
-    const int tcol[4] = {i0, i1, j0, j1};
-
-    // the epilogue's raw rows and lengthscales, loaded under the operand stream
-    constexpr int GPRE = 2;
-    const int nraw = NB * (a.D + 1);
-    double pv[4][GPRE];
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int s2 = 0; s2 < GPRE; ++s2) {
-            const int e = threadIdx.x + s2 * NTHREADS;
-            const int r = e / (a.D + 1), d = e % (a.D + 1);
-            const int g = tcol[u] * NB + r;
-            pv[u][s2] = (e < nraw && g < a.n) ? a.X[(long)g * a.ldxx + d] : 0.0;
-        }
-    double pl = 1.0;
-    if (threadIdx.x < 2 * a.D) {
-        const int src = threadIdx.x / a.D, d = threadIdx.x % a.D;
-        pl = src == 0 ? th.lL(d) : th.lD(d);
-    }
-
-    // acc[u]: output tile u = 2 * (row in block) + (column in block): (i0,j0) (i0,j1) (i1,j0) (i1,j1)
-    Acc<NB> acc[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) acc_zero(acc[u]);
-    const double negP = -(double)a.P;
-    {
-        const long rs = (long)NB * a.ldx;
-        // item q: the m-row of the A side (columns i0, i1) and of the B side (columns j0, j1);
-        // which of the four column tiles are nonzero
-        auto rows = [&](int q, int& ra, int& rb) {
-            ra = q < nm ? m0 + q : a.T + q - nm;
-            rb = q < nm ? ra : ra + a.Tp;
-        };
-        auto live = [&](int q, bool& a1, bool& b1) {
-            int ra, rb;
-            rows(q, ra, rb);
-            a1 = vi1 && (q >= nm || ra >= i1);
-            b1 = vj1 && (q >= nm || rb >= j1) && !(diag && !t11);
-        };
-        auto fetch = [&](TileRegs<NB> (&r)[4], int q) {
-            int ra, rb;
-            rows(q, ra, rb);
-            bool a1, b1;
-            live(q, a1, b1);
-            tile_fetch<NB>(r[0], a.Xo + ra * rs + (long)i0 * NB, a.ldx);
-            if (a1) tile_fetch<NB>(r[1], a.Xo + ra * rs + (long)i1 * NB, a.ldx);
-            tile_fetch<NB>(r[2], a.Xo + rb * rs + (long)j0 * NB, a.ldx);
-            if (b1) tile_fetch<NB>(r[3], a.Xo + rb * rs + (long)j1 * NB, a.ldx);
-        };
-        auto put = [&](double* buf, const TileRegs<NB> (&r)[4], int q) {
-            bool a1, b1;
-            live(q, a1, b1);
-            tile_put<NB>(buf, r[0]);
-            if (a1) tile_put<NB>(buf + E, r[1]);
-            tile_put<NB>(buf + 2 * E, r[2]);
-            if (b1) tile_put<NB>(buf + 3 * E, r[3]);
-        };
-        auto products = [&](const double* buf, int q) {
-            bool a1, b1;
-            live(q, a1, b1);
-            tile_mma<NB, true, false>(acc[0], buf, buf + 2 * E, 1.0);
-            if (t01 && b1) tile_mma<NB, true, false>(acc[1], buf, buf + 3 * E, 1.0);
-            if (t10 && a1) tile_mma<NB, true, false>(acc[2], buf + E, buf + 2 * E, 1.0);
-            if (t11 && a1 && b1) tile_mma<NB, true, false>(acc[3], buf + E, buf + 3 * E, 1.0);
-        };
-        // two LDS buffers + two register sets, as k_grad: at even q buffer 0 holds item q,
-        // set 1 item q+1, set 0 item q+2
-        TileRegs<NB> r0[4], r1[4];
-        double* B0 = smem;
-        double* B1 = smem + 4 * E;
-        fetch(r0, 0);
-        put(B0, r0, 0);
-        if (nq > 1) fetch(r1, 1);
-        if (nq > 2) fetch(r0, 2);
-        __syncthreads();
-        for (int q = 0; q < nq; q += 2) {
-            products(B0, q);
-            if (q + 1 < nq) {
-                put(B1, r1, q + 1);
-                if (q + 3 < nq) fetch(r1, q + 3);
-            }
-            __syncthreads();
-            if (q + 1 < nq) {
-                products(B1, q + 1);
-                if (q + 2 < nq) {
-                    put(B0, r0, q + 2);
-                    if (q + 4 < nq) fetch(r0, q + 4);
-                }
-                __syncthreads();
-            }
-        }
-    }
-
-    // stage the raw rows and flags of the four row tiles (operand buffers are free now)
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        auto stage = [&](int e, double v) {
-            const int r = e / (a.D + 1), d = e % (a.D + 1);
-            if (d < a.D) xr[(u * NB + r) * XS + d] = v;
-            else fl[u * NB + r] = (tcol[u] * NB + r < a.n) ? v : -1.0;
-        };
-#pragma unroll
-        for (int s2 = 0; s2 < GPRE; ++s2) {
-            const int e = threadIdx.x + s2 * NTHREADS;
-            if (e < nraw) stage(e, pv[u][s2]);
-        }
-        for (int e = threadIdx.x + GPRE * NTHREADS; e < nraw; e += NTHREADS) {
-            const int r = e / (a.D + 1), d = e % (a.D + 1);
-            const int g = tcol[u] * NB + r;
-            stage(e, g < a.n ? a.X[(long)g * a.ldxx + d] : 0.0);
-        }
-    }
-    if (threadIdx.x < 2 * a.D) il2[threadIdx.x] = 1.0 / (pl * pl);
-    for (int e = threadIdx.x + NTHREADS; e < 2 * a.D; e += NTHREADS) {
-        const int src = e / a.D, d = e % a.D;
-        const double l = src == 0 ? th.lL(d) : th.lD(d);
-        il2[e] = 1.0 / (l * l);
-    }
-    __syncthreads();
-
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    // partial of entry qidx: quad-summed, one LDS slot per quad; a slot is written by one lane
-    // only, so the tiles of the block accumulate into it without barriers
-    auto put = [&](int qidx, double v, bool first) {
-        v = quad_sum(v);
-        if ((lane & 3) == 0) {
-            double& dst = R[qidx * GRAD_RLD + wv * 16 + (lane >> 2)];
-            dst = first ? v : dst + v;
-        }
-    };
-    const double rho = th.rho();
-    double gvL = 0.0, gvD = 0.0, grho = 0.0, gnoise = 0.0;
-    bool first = true;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const bool valid = u == 0 || (u == 1 && t01) || (u == 2 && t10) || (u == 3 && t11);
-        if (!valid) continue;
-        const int ti = tcol[u >> 1], tj = tcol[2 + (u & 1)];
-        const double* xi = xr + (u >> 1) * NB * XS;
-        const double* xj = xr + (2 + (u & 1)) * NB * XS;
-        const double* fi = fl + (u >> 1) * NB;
-        const double* fj = fl + (2 + (u & 1)) * NB;
-        const double wscale = ((ti == tj) ? 0.5 : 1.0) * negP;
-        const int ri[4] = {acc_row<NB>(0, 0), acc_row<NB>(0, 1), acc_row<NB>(0, 2), acc_row<NB>(0, 3)};
-        const int cj = acc_col<NB>(0);
-        bool L1[4], H1[4], L2, H2;
-        double s2[4], s2d[4];
-        const double f2 = fj[cj];
-        L2 = f2 == 0.0; H2 = f2 == 1.0;
-        bool anyHH = false;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const double f1 = fi[ri[r]];
-            L1[r] = f1 == 0.0; H1[r] = f1 == 1.0;
-            anyHH |= H1[r] && H2;
-            s2[r] = 0.0;
-            s2d[r] = 0.0;
-        }
-        for (int d = 0; d < a.D; ++d) {
-            const double il = il2[d], ild = il2[a.D + d];
-            const double xjd = xj[cj * XS + d];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const double df = xi[ri[r] * XS + d] - xjd;
-                const double d2 = df * df;
-                s2[r] += d2 * il;
-                s2d[r] += d2 * ild;
-            }
-        }
-        double cL[4], cD[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const double w = acc[u].v[0][r] * wscale;
-            const bool lv = (L1[r] || H1[r]) && (L2 || H2);
-            const double eL = lv ? exp_lib(-0.5 * s2[r]) : 0.0;
-            const double kL = th.vL() * eL;
-            double eD = 0.0;
-            if (anyHH && H1[r] && H2) eD = exp_lib(-0.5 * s2d[r]);
-            const double kD = th.vD() * eD;
-            const double si = L1[r] ? 1.0 : (H1[r] ? rho : 0.0), sj = L2 ? 1.0 : (H2 ? rho : 0.0);
-            const double hi = H1[r] ? 1.0 : 0.0, hj = H2 ? 1.0 : 0.0;
-            cL[r] = w * si * sj * kL;
-            cD[r] = w * hi * hj * kD;
-            gvL += w * si * sj * eL;
-            gvD += w * hi * hj * eD;
-            grho += w * (hi * sj + si * hj) * kL;
-            if (ti == tj && ri[r] == cj && ti * NB + ri[r] < a.n) gnoise += w;
-        }
-        for (int d = 0; d < a.D; ++d) {
-            double tl = 0.0, td = 0.0;
-            const double xjd = xj[cj * XS + d];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const double df = xi[ri[r] * XS + d] - xjd;
-                tl += cL[r] * df * df;
-                td += cD[r] * df * df;
-            }
-            put(1 + d, tl, first);
-            put(2 + a.D + d, td, first);
-        }
-        first = false;
-    }
-    put(0, gvL, true);
-    put(1 + a.D, gvD, true);
-    put(2 + 2 * a.D, grho, true);
-    put(3 + 2 * a.D, gnoise, true);
-    __syncthreads();
-    for (int g0 = 0; g0 < G; g0 += NTHREADS / 8) {   // gpart [quantity][task]
-        const int qx = g0 + (threadIdx.x >> 3), sub = threadIdx.x & 7;
-        double v = 0.0;
-        if (qx < G) {
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v += R[qx * GRAD_RLD + sub * 8 + u];
-        }
-        v = quad_sum(v);
-        v += __shfl_xor(v, 4, 64);
-        if (sub == 0 && qx < G) {
-            if (qx >= 1 && qx <= a.D) { const double l = th.lL(qx - 1); v /= l * l * l; }
-            else if (qx >= 2 + a.D && qx <= 1 + 2 * a.D) { const double l = th.lD(qx - 2 - a.D); v /= l * l * l; }
-            a.gpart[(long)qx * gridDim.x + task] = v;
-        }
-    }
-    grad_next_setup(a);
-}
-
-size_t grad_blk_smem_bytes(int G, int D) {
-    return sizeof(double) * std::max((size_t)GBLK_REGION, (size_t)GBLK_RED_OFF + (size_t)G * GRAD_RLD + 2 * D);
-}
-
 size_t grad_smem_bytes(int nb, int G, int nil2) {
     const size_t region = 2 * (size_t)(nb == 32 ? GRAD_NBUF<32> : GRAD_NBUF<64>) * nb * (nb + 2);
     const size_t epi = (size_t)(nb == 32 ? GRAD_RED_OFF<32> : GRAD_RED_OFF<64>) + (size_t)G * GRAD_RLD + nil2;
@@ -1936,17 +1650,6 @@ void launch_chol_steps(CholArgs c, int batch, hipStream_t s) {
 }
 template <int NB>
 void launch_grad(const GradArgs& g, hipStream_t s) {
-    if (NB == 32 && g.chunk < 0 && !g.nlf) {   // blocked form
-        static bool attr = false;
-        const size_t lds = grad_blk_smem_bytes(kernel_theta_size(0, g.D), g.D);
-        if (!attr) {
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_grad_blk),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-            attr = true;
-        }
-        hipLaunchKernelGGL(k_grad_blk, dim3(grad_tasks(g.T, g.chunk)), dim3(NTHREADS), lds, s, g);
-        return;
-    }
     const size_t lds = grad_smem_bytes(NB, kernel_theta_size(g.nlf, g.D), (g.nlf ? g.nlf + 1 : 2) * g.D);
     if (g.nlf)
         hipLaunchKernelGGL((k_grad<NB, true>), dim3(grad_tasks(g.T, g.chunk)), dim3(NTHREADS), lds, s, g);
