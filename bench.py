@@ -651,7 +651,15 @@ def shared_theta_leg(X, Yr, steps, warmup, device):
     return {"mode": "shared", "scaling": "strong", "steps": steps, "warmup": warmup,
             "ms_per_step": round(dt / steps * 1e3, 4), "value": round(steps / dt, 3), "unit": "evals/s",
             "parallelism": f"bins{world}-shared-theta",
-            "collective": "one all-reduce of 1 + G doubles per step (eager launches, no graph replay)"}
+            "collective": collective_label(sess)}
+
+
+def collective_label(sess) -> str:
+    """How a shared-theta trainer ran its per-step all-reduce."""
+    backend = dist.get_backend() if dist.is_available() and dist.is_initialized() else "none"
+    how = (f"replayed from hipGraphs of {sess.graph_chunk} steps, the all-reduce captured inside"
+           if getattr(sess, "graph_chunk", 0) else "eager launches")
+    return f"one {backend} all-reduce of 1 + G doubles per step ({how})"
 
 
 def dist_device_index() -> int:
@@ -730,7 +738,10 @@ def main():
     local = dist_device_index()
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
-    if world > 1:
+    # MFGP_DIST_WS1=1: a process group even at world size 1 (the RCCL code path on one GPU: its
+    # broadcast, all-reduce and captured collectives; not a scaling figure)
+    ws1 = world == 1 and os.environ.get("MFGP_DIST_WS1", "0") == "1"
+    if world > 1 or ws1:
         init_dist(device)
 
     from multi_fidelity_gpflow_amd.engine import Engine
@@ -755,7 +766,6 @@ def main():
     if args.mode == "shared":
         from multi_fidelity_gpflow_amd.distributed import SharedThetaTrainer
         sess = SharedThetaTrainer(model, 0.1, K + W)
-        sess.sync = torch.cuda.synchronize
     else:
         sess = model.adam_session(0.1, K + W, graph=True, graph_chunk=50 if args.config == "goku" else 2)
     sess.run(W)
@@ -843,13 +853,15 @@ def main():
         }
         if shared_sub is not None:
             line["shared_theta"] = shared_sub
+        if args.mode == "shared":
+            line["collective"] = collective_label(sess)
         if world == 1 and args.config == "goku" and not args.no_extras:
             # every other BASELINE config, measured in this process after the headline timing
             line["hbs"] = hbs_leg()
             line["goku_svgp"] = svgp_leg(X, Yr, Xt, 20, 5)
             line["synth"] = synth_leg()
         print(json.dumps(line))
-    if world > 1:
+    if world > 1 or ws1:
         dist.destroy_process_group()
 
 
