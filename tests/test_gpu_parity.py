@@ -348,8 +348,10 @@ def test_lbfgs_forrester_kat(kats, eng, flow):
     # rounding of K itself moves the LML there.  The line search also visits nearly
     # singular K (noise at its 1e-6 floor, long lengthscales), where any fp64 Cholesky differs from
     # another by far more than 1e-11; the reference for "rounding level" at a point is the spread
-    # of the oracle's own LML under relative 2^-52 perturbations of K (four draws).  So the endpoint's
-    # spread between schedules is the line search's sensitivity, not a different objective.
+    # of the oracle's own LML under symmetric relative perturbations of K of size n 2^-52 (four
+    # draws): the backward error of an n x n Cholesky, |dK| <= gamma_{n+1} |L||L^T|.  So the
+    # endpoint's spread between schedules is the line search's sensitivity, not a different
+    # objective.
     rng = np.random.default_rng(0)
     worst, well, dg, nwell = 0.0, 0.0, 0.0, 0
     N, P = Y.shape
@@ -361,7 +363,7 @@ def test_lbfgs_forrester_kat(kats, eng, flow):
         spread = 0.0
         for _ in range(4):
             U = rng.uniform(-1, 1, K.shape)
-            Kp = K * (1.0 + 2.0 ** -52 * (U + U.T) / 2)
+            Kp = K * (1.0 + N * 2.0 ** -52 * (U + U.T) / 2)
             Lp = np.linalg.cholesky(Kp)
             Ap = np.linalg.solve(Lp, Y)
             lp = -0.5 * np.sum(Ap * Ap) - P * np.sum(np.log(np.diag(Lp))) - 0.5 * N * P * np.log(2 * np.pi)
@@ -373,7 +375,7 @@ def test_lbfgs_forrester_kat(kats, eng, flow):
             well = max(well, d / abs(lo))
             gov = np.concatenate([[go["vL"]], go["lL"], [go["vD"]], go["lD"], [go["rho0"]], [go["noise"]]])
             dg = max(dg, np.abs(g - gov).max() / max(np.abs(gov).max(), 1e-300))
-    print(f"  {len(visits)} evaluations: |device - oracle| <= {worst:.1f} x the oracle's own rounding spread; "
+    print(f"  {len(visits)} evaluations: |device - oracle| <= {worst:.2f} x the oracle's rounding spread; "
           f"at the {nwell} well-conditioned points value {well:.1e}, gradient {dg:.1e}")
     assert len(visits) > 20 and nwell > 10
     assert worst < 50.0 and well < 1e-11 and dg < 1e-7
