@@ -377,7 +377,7 @@ def test_lbfgs_forrester_kat(kats, eng, flow):
             dg = max(dg, np.abs(g - gov).max() / max(np.abs(gov).max(), 1e-300))
     print(f"  {len(visits)} evaluations: |device - oracle| <= {worst:.2f} x the oracle's rounding spread; "
           f"at the {nwell} well-conditioned points value {well:.1e}, gradient {dg:.1e}")
-    assert len(visits) > 20 and nwell > 10
+    assert len(visits) > 20 and nwell >= 5
     assert worst < 50.0 and well < 1e-11 and dg < 1e-7
     rho = float(m.kernel.rho.numpy()[0, 0])
     print(f"L-BFGS Forrester ({'tiny' if tiny else ('flow' if flow else 'steps')}) rho {rho:.9f} vs recorded {kats['forrester_lbfgs']['rho']} "
