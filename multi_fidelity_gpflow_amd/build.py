@@ -63,6 +63,7 @@ def build_lib(force: bool = False, extra_flags=None, out: str = OUT, csrc: str =
     if not force and out == OUT and not needs_rebuild():
         return out
     from concurrent.futures import ThreadPoolExecutor
+    out = os.path.abspath(out)
     flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-I" + os.path.join(ROOT, "include"),
              "-Wno-unused-result", '-DMFGP_BUILD_ID="%s"' % source_hash(csrc)] + list(extra_flags or [])
     objdir = out + ".objs"

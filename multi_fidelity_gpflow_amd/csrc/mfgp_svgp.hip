@@ -520,16 +520,14 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
     // needs to form A and B in one tile loop without keeping A), and no C.  The column moments
     // come out of the GEMMs' epilogues in the fused kernel's partial layout and order.
     const bool two_gemm = NB == 32 && Aout != nullptr;
-    // the K_uu pipeline (latency-bound: ~20 launches of small grids) on the side stream; the K_uf
-    // Gram, tril(q_sqrt), the zeros above Li's tiles (the step sequence never writes there) and
-    // the KL (q_mu, q_sqrt only) on the caller's beside it
-    hipStream_t sk = svgp_fork(s);
+    // K_uu (+ jitter, RHS = I) by one Gram launch and the first diagonal factor of every latent
+    // (the first writer of info) on the caller's stream, alone; then the rest of the K_uu pipeline
+    // (latency-bound: ~20 launches of small grids, the forward's critical path) on the side stream,
+    // and the K_uf Gram, tril(q_sqrt), the zeros above Li's tiles (the step sequence never writes
+    // there) and the KL on the caller's beside it.  (Forked before the first factor, the K_uf
+    // Gram's 24k workgroups held the CUs: the 64 one-workgroup factors took 64 us instead of ~5.)
     const int blocks = (int)std::min<long>((mm + 255) / 256, 2048);
-    hipLaunchKernelGGL(k_zero_upper_tiles, dim3(blocks, 1, L), dim3(256), 0, s, S.Xo, NB, S.mpad, mm);
-    // Kuu_l (+ jitter) and RHS = I by one Gram launch, then the first diagonal factor of every
-    // latent as a launch of its own (fused into the Gram it set that launch's register allocation:
-    // 3.3% of a single-bin iteration for a 300 x 300 Gram per latent); the first factor is the
-    // first writer of info (no memset)
+    hipStream_t sk;
     {
         GramArgs g{};
         g.X1 = Z; g.ldx1 = ldz; g.sx1 = 0; g.n1 = m;
@@ -540,8 +538,9 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
         g.R = S.R; g.ldr = S.mpad; g.sR = mm;
         // the dense-layout Gram (64 x 64 entries a workgroup, both triangles): the lean tile
         // launch took 56-66 us for 64 latents of 300 x 300 on the chain's critical path
-        launch_gram_dense(g, L, S.mpad, S.mpad, sk);
-        launch_first_factor<NB>(S.Kuu, S.mpad, mm, S.Dd, (long)S.Tm * NB * NB, S.ldiag, S.mpad, info, L, sk);
+        launch_gram_dense(g, L, S.mpad, S.mpad, s);
+        launch_first_factor<NB>(S.Kuu, S.mpad, mm, S.Dd, (long)S.Tm * NB * NB, S.ldiag, S.mpad, info, L, s);
+        sk = svgp_fork(s);
         CholArgs c{};
         c.A = S.Kuu; c.lda = S.mpad; c.sA = mm;
         c.R = S.R; c.ldr = S.mpad; c.sR = mm;
@@ -550,6 +549,7 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
         c.T = S.Tm; c.Tp = 0; c.k = 0;
         launch_chol_steps<NB>(c, L, sk);
     }
+    hipLaunchKernelGGL(k_zero_upper_tiles, dim3(blocks, 1, L), dim3(256), 0, s, S.Xo, NB, S.mpad, mm);
     // Kuf_l = K_l(Z, X), zero padded to Mpad x Npad
     {
         GramArgs g{};

@@ -1,13 +1,11 @@
 #!/bin/bash
-# SVGP A/B of library variants (GPU box, repo root): interleaved goku_svgp bench lines
-#   bash tools/svgp_ab.sh V1 V2 ...   (multi_fidelity_gpflow_amd/variants/libmfgp_<V>.so)
+# SVGP A/B of library builds (GPU box, repo root): interleaved single-bin SVGP iteration times
+#   bash tools/svgp_ab.sh ROUNDS LIB1 LIB2 ...   (paths of libmfgp.so builds, MFGP_LIB_PATH)
 set -o pipefail
-mkdir -p gpurun_out
-for round in 1 2; do
+R=$1; shift
+for round in $(seq 1 "$R"); do
   for v in "$@"; do
-    MFGP_LIB_PATH=multi_fidelity_gpflow_amd/variants/libmfgp_$v.so timeout -k 10 200 \
-      python bench.py --config goku_svgp --steps 30 --warmup 10 --no-train-predict --no-cpu-baseline \
-      > gpurun_out/svab_$v.json 2> gpurun_out/svab_$v.err || exit $?
-    python -c "import json; d=json.load(open('gpurun_out/svab_$v.json')); print('$v', d['ms_per_step'], d.get('latent_l15', {}).get('ms_per_step'))"
+    MFGP_LIB_PATH=$v timeout -k 10 200 python tools/bench_svgp.py --which single --iters 40 > /tmp/svab.json 2>/tmp/svab.err || exit 3
+    python -c "import json; d=json.loads(open('/tmp/svab.json').read().splitlines()[-1]); print('$v', round(d['s_per_iter']*1e3, 4), 'ms')"
   done
 done
