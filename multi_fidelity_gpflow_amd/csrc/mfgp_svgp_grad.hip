@@ -517,7 +517,7 @@ template <int DC>
 __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(KG_WAVES))) void k_kgrad(const double* P1, long ld1, int n1, const double* P2, long ld2,
                                                     int n2, const double* Wt, long ldw, long sW, const double* thetas,
                                                     int G, int D, double zf, int nbc, double* gth_part,
-                                                    double* gz_part, const double* Kp) {
+                                                    double* gz_part) {
     constexpr int NCB = kg_ncb<DC>(), SC = NCB * 16 + 1, XS = DC + 1, NS = DC / 4;
     static_assert(DC % 4 == 0, "dimension chunks of the distance MFMA");
     constexpr int BS = NCB * 16 + 1;                                   // [1 | x | x^2] row stride
@@ -560,13 +560,6 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(KG_WAV
     const int bbase = bc * KG_COLS;
     const int bend = min(n2, bbase + KG_COLS);
     const double* wrow = Wt + lat * sW + (long)a * ldw;
-    // Kp (the (Z, X) pass): the forward's K_uf in Wt's layout.  A pair that is not HF x HF has
-    // K_uf(a, b) = sa sb kL(a, b), so its LF weight wl = Wt K_uf and its dk/dvL, dk/drho terms come
-    // from that entry: one load instead of the distance and the exp (blocks holding an HF x HF pair
-    // take the distance path).  Needs vL, rho != 0 (softplus-constrained: always, in training).
-    const bool kuse = Kp != nullptr && vL != 0.0 && rho != 0.0;
-    const double* krow = kuse ? Kp + lat * sW + (long)a * ldw : wrow;
-    const double ivL = kuse ? 1.0 / vL : 0.0, irho = kuse ? 1.0 / rho : 0.0;
     // Pairs in 16 x 16 blocks (16 a rows of the wave x 16 b rows of its half): the distances
     // |za - xb|^2 / l^2 = |za/l|^2 + |xb/l|^2 - 2 (za/l).(xb/l) with the dot products on the matrix
     // core (NS = DC / 4 steps of v_mfma_f64_16x16x4; lane (li, lq) then holds the pairs (a = li,
@@ -585,10 +578,6 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(KG_WAV
             wv[r] = (aval && b < bend) ? w : 0.0;
         }
     };
-    auto kload = [&](int b0, double* kv) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) kv[r] = krow[min(b0 + 4 * r + lk, bend - 1)];
-    };
     double zl[NS], zd[NS];
     double na = 0.0, nad = 0.0;
 #pragma unroll
@@ -605,9 +594,8 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(KG_WAV
     double* xsb = lds_buf;                                  // [2][KG_CHUNK][XS]
     double* nrm = xsb + 2 * KG_CHUNK * XS;                  // [2][KG_CHUNK][2]
     double* bop = nrm + 2 * KG_CHUNK * 2;                   // [2][KG_CHUNK][BS]
-    double wc[4], wn[4], kc[4], kn[4];
+    double wc[4], wn[4];
     wload(bhalf, wc);
-    if (kuse) kload(bhalf, kc);
     for (int c0 = 0; c0 < KG_COLS / 2; c0 += KG_CHUNK) {
         __syncthreads();   // the previous chunk is consumed
         for (int e = t; e < 2 * KG_CHUNK * XS; e += NTHREADS) {
@@ -657,30 +645,6 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(KG_WAV
             const int rb = 16 * blk;
             if (bhalf + c0 + rb >= bend) break;             // wave-uniform: past the last b row
             wload(bhalf + c0 + rb + 16, wn);                 // the next block's weights, in flight meanwhile
-            if (kuse) {
-                kload(bhalf + c0 + rb + 16, kn);
-                bool hh = false;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) hh |= Ha && xs[(rb + lk + 4 * r) * XS + DC] == 1.0;
-                if (__ballot(hh) == 0) {   // wave-uniform: no HF x HF pair, K_uf gives the weights
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int bl = rb + lk + 4 * r;
-                        const double fb = xs[bl * XS + DC];
-                        const bool Lb = (fb == 0.0), Hb = (fb == 1.0);
-                        const double wl = (Lb || Hb) ? wc[r] * kc[r] : 0.0;   // wv sa sb kL
-                        gvL += wl * ivL;
-                        grho += wl * ((Ha ? 1.0 : 0.0) + (Hb ? 1.0 : 0.0)) * irho;
-#pragma unroll
-                        for (int c = 0; c < NCB; ++c)
-                            accL[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(wl, bo[(rb + 4 * r + lk) * BS + 16 * c + li], accL[c], 0, 0, 0);
-                        __builtin_amdgcn_sched_barrier(0);
-                    }
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) { wc[r] = wn[r]; kc[r] = kn[r]; }
-                    continue;
-                }
-            }
             f64x4 dl = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int q = 0; q < NS; ++q)
@@ -706,7 +670,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(KG_WAV
                 __builtin_amdgcn_sched_barrier(0);
             }
 #pragma unroll
-            for (int r = 0; r < 4; ++r) { wc[r] = wn[r]; kc[r] = kn[r]; }
+            for (int r = 0; r < 4; ++r) wc[r] = wn[r];
         }
         // HF x HF pairs (the delta kernel), in a pass of their own: few blocks hold any (Goku: X's
         // HF rows are its last 36), and the hot pass above keeps its accumulators in place
@@ -942,9 +906,9 @@ void svgp_forward_buffers(int nb, int n, int m, int l, int p, int d, void* ws, d
 template <int DC>
 static void launch_kgrad(hipStream_t s, const double* P1, long ld1, int n1, const double* P2, long ld2, int n2,
                          const double* Wt, long ldw, long sW, const double* thetas, int G, int D, double zf, int nat,
-                         int nbc, int L, double* gth, double* gz, const double* Kp = nullptr) {
+                         int nbc, int L, double* gth, double* gz) {
     hipLaunchKernelGGL(k_kgrad<DC>, dim3(nat * nbc, 1, L), dim3(NTHREADS), 0, s, P1, ld1, n1, P2, ld2, n2, Wt, ldw,
-                       sW, thetas, G, D, zf, nbc, gth, gz, Kp);
+                       sW, thetas, G, D, zf, nbc, gth, gz);
 }
 
 template <int NB>
@@ -1067,7 +1031,7 @@ static int svgp_grad_run(hipStream_t s, int n, int m, int L, int p, int d, const
     auto kgrad = [&](auto dc) {
         constexpr int DC = decltype(dc)::value;
         launch_kgrad<DC>(sb, Z, ldz, m, X, ldx, n, g.Kbar, npad, mn, thetas, G, d, 1.0, g.n_at, g.nbc_uf, L, g.gth_uf,
-                         g.gz_uf, Kuf);
+                         g.gz_uf);
         launch_kgrad<DC>(s, Z, ldz, m, Z, ldz, m, g.Sig, mpad, mm, thetas, G, d, 2.0, g.n_at, g.nbc_uu, L, g.gth_uu,
                          g.gz_uu);
     };
