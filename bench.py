@@ -275,6 +275,22 @@ def host_cpus():
     return aff, src
 
 
+def cpu_protocol_measured():
+    """The CPU baseline's full protocol (1000 Adam steps + predict_f on the box's cores), timed once
+    by tools/cpu_protocol.py into profiles/rNN/cpu_protocol.json (the latest round that has one)."""
+    import glob
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", "cpu_protocol.json")))
+    if not found:
+        return None
+    try:
+        with open(found[-1]) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    return {"train_predict_s": d.get("train_predict_s"), "steps": d.get("steps"), "cores": d.get("cores"),
+            "source": os.path.relpath(found[-1], ROOT) + " (tools/cpu_protocol.py, timed once on a GPU box host)"}
+
+
 def cpu_baseline(X, Y):
     """fp64 torch-CPU restatement of the reference path (oracle/torch_oracle.py, checked against
     the KAT-pinned oracle/mfgp_oracle.py) on this host: all threads and 1 thread, value-only and
@@ -301,6 +317,7 @@ def cpu_baseline(X, Y):
             "value_only_evals_s": legs["all"]["value_evals_s"],
             "one_core": legs["one"],
             "train_1000_adam_s_est": round(1000.0 / legs["all"]["value_grad_evals_s"], 2),
+            "protocol_measured": cpu_protocol_measured(),
             "sample": (f"Goku (N={X.shape[0]}, P={Y.shape[1]}) fp64 LML value+grad and value-only evaluations at "
                        f"the initial theta, oracle/torch_oracle.py (MKL Cholesky/TRSM/GEMM), median of >=20 "
                        f"after warm-up (fewer if a leg exceeds ~6 s), torch threads {nthreads} (the cores available: "
