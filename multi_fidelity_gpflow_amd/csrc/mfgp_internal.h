@@ -179,11 +179,6 @@ struct BgemmArgs {
     // qv, csq2 likewise of D[i][j] qv[i qs + b] over rows i < qn (the SVGP conditional's moments)
     double* csq; double* csq2; long ldcs;
     const double* qv; long qs; int qn;
-    // split k (k_bgemm2 only; ksplit <= 1: none): ksplit workgroups per 64 x 64 output block, each a
-    // contiguous part of the block's k-range; every part stores its partial block (sc1) into kpart
-    // and counts itself in kcnt[block] (zero on entry, reset by the last arrival); the last arrival
-    // sums the parts in part order and runs the epilogue (deterministic whatever the arrival order)
-    int ksplit; double* kpart; int* kcnt;
 };
 void launch_bgemm(int nb, hipStream_t st, int ta, int tb, const BgemmArgs& a, int batch);
 

@@ -110,9 +110,6 @@ __global__ __launch_bounds__(NTHREADS) void k_bgemm2(BgemmArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     int bx, b;
     xcd_swizzle(bx, b);
-    const int ks = a.ksplit > 1 ? a.ksplit : 1;
-    const int part = bx % ks;
-    bx /= ks;
     const int Nb = (a.Nt + 1) >> 1;
     const int bi = bx / Nb, bj = bx % Nb;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
@@ -139,17 +136,6 @@ __global__ __launch_bounds__(NTHREADS) void k_bgemm2(BgemmArgs a) {
         int k0, k1;
         krange(r, c, k0, k1);
         if (k1 > k0) { kb0 = min(kb0, k0); kb1 = max(kb1, k1); }
-    }
-    if (ks > 1 && kb1 <= kb0 && part != 0) return;   // nothing to multiply: part 0 writes the block
-    const bool split = ks > 1 && kb1 > kb0;
-    if (split) {   // this part's contiguous share of the block's k-range
-        const int chunk = (kb1 - kb0 + ks - 1) / ks;
-        const int p0 = kb0 + part * chunk;
-        kb1 = min(kb1, p0 + chunk);
-        kb0 = p0;
-        kw0 = max(kw0, kb0);
-        kw1 = min(kw1, kb1);
-        if (kw1 < kw0) kw1 = kw0;
     }
     const double* A = a.A + b * a.sA;
     const double* B = a.B + b * a.sB;
@@ -226,39 +212,6 @@ __global__ __launch_bounds__(NTHREADS) void k_bgemm2(BgemmArgs a) {
             __syncthreads();
         }
     }
-    if (split) {
-        // partial block -> kpart[block][part][lane-major 16 doubles]; the last arrival sums the parts
-        const long nblk = (long)((a.Mt + 1) >> 1) * Nb;
-        const long blk = (long)b * nblk + bx;
-        double* slot = a.kpart + (blk * ks) * (NTHREADS * 16);
-#pragma unroll
-        for (int p = 0; p < 2; ++p)
-#pragma unroll
-            for (int q = 0; q < 2; ++q)
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    st_coherent(slot + (long)part * NTHREADS * 16 + (long)((p * 2 + q) * 4 + r) * NTHREADS + threadIdx.x,
-                                acc[p][q][r]);
-        drain_stores();
-        __syncthreads();
-        int* last = reinterpret_cast<int*>(smem);   // the operand buffer is free (all LDS dynamic)
-        if (threadIdx.x == 0) *last = arrive(a.kcnt + blk) == ks - 1;
-        __syncthreads();
-        if (!*last) return;
-#pragma unroll
-        for (int p = 0; p < 2; ++p)
-#pragma unroll
-            for (int q = 0; q < 2; ++q)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const long e = (long)((p * 2 + q) * 4 + r) * NTHREADS + threadIdx.x;
-                    double v = 0.0;
-                    for (int pp = 0; pp < ks; ++pp)   // part order: the same sum whoever arrives last
-                        v += (pp == part) ? acc[p][q][r] : ld_coherent(slot + (long)pp * NTHREADS * 16 + e);
-                    acc[p][q][r] = v;
-                }
-        if (threadIdx.x == 0) __hip_atomic_store(a.kcnt + blk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
     if (!live) return;
     double* Dt = a.D + b * a.sD;
     if (a.sym) {   // tiles ti >= tj only (tril): v (Psi: 0.5 v) at (i, j) and (j, i)
@@ -331,7 +284,7 @@ static void bgemm(hipStream_t st, int ta, int tb, const BgemmArgs& a, int batch)
                 (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bgemm2_smem());
             attr = true;
         }
-        dim3 g(((a.Mt + 1) >> 1) * ((a.Nt + 1) >> 1) * (a.ksplit > 1 ? a.ksplit : 1), 1, batch);
+        dim3 g(((a.Mt + 1) >> 1) * ((a.Nt + 1) >> 1), 1, batch);
         const size_t sm = bgemm2_smem();
         if (!ta && !tb) hipLaunchKernelGGL((k_bgemm2<false, false>), g, dim3(NTHREADS), sm, st, a);
         else if (!ta && tb) hipLaunchKernelGGL((k_bgemm2<false, true>), g, dim3(NTHREADS), sm, st, a);
@@ -880,24 +833,8 @@ struct SvgpGradLayout {
     double *qm, *alpha, *beta, *A, *B, *gA, *Gb, *H, *P, *Sig, *Kbar, *T1, *gLq, *gqm, *r, *gnp, *gth_uu, *gth_uf,
         *gth_kff, *gz_uu, *gz_uf;
     int nbc_uu, nbc_uf, n_at, nb_uu, nb_uf, nnoise;
-    int ksplit, Tm;
-    long nblk;
-    double *kpart_lq, *kpart_li;
-    int* kcnt;
     size_t bytes;
 };
-
-// k-parts of the two M x M products whose k-range is all of N (dE/dLq, dE/dLi): at Goku's M = 300
-// only the 15 lower 64 x 64 blocks a latent have work, 960 workgroups of 37 k-tiles each
-// (env MFGP_SVGP_KSPLIT, 1 = no split)
-static int svgp_ksplit() {
-    static int v = [] {
-        const char* e = getenv("MFGP_SVGP_KSPLIT");
-        const int k = e ? atoi(e) : 2;
-        return k < 1 ? 1 : (k > 8 ? 8 : k);
-    }();
-    return v;
-}
 
 static SvgpGradLayout grad_layout(int nb, int n, int m, int L, int p, int d, size_t base_off, void* ws) {
     SvgpGradLayout g;
@@ -939,14 +876,6 @@ static SvgpGradLayout grad_layout(int nb, int n, int m, int L, int p, int d, siz
     g.gth_kff = take((size_t)L * G);
     g.gz_uu = take((size_t)L * g.nb_uu * KG_ROWS * d + 8);
     g.gz_uf = take((size_t)L * g.nb_uf * KG_ROWS * d + 8);
-    // split-k scratch of the two M x M products with K = N (dE/dLq, dE/dLi): partial blocks + counters
-    g.Tm = mpad / nb;
-    g.ksplit = nb == 32 ? svgp_ksplit() : 1;
-    const long nblk = (long)((g.Tm + 1) / 2) * ((g.Tm + 1) / 2) * L;
-    g.kpart_lq = take(g.ksplit > 1 ? (size_t)nblk * g.ksplit * NTHREADS * 16 : 0);
-    g.kpart_li = take(g.ksplit > 1 ? (size_t)nblk * g.ksplit * NTHREADS * 16 : 0);
-    g.kcnt = reinterpret_cast<int*>(take(g.ksplit > 1 ? (size_t)nblk : 0));   // 2 x nblk ints
-    g.nblk = nblk;
     g.bytes = off + 256;
     return g;
 }
@@ -1045,10 +974,6 @@ static int svgp_grad_run(hipStream_t s, int n, int m, int L, int p, int d, const
         a.D = g.gLq; a.ldd = mpad; a.sD = mm;
         a.alpha = 2.0;
         a.Mt = Tm; a.Nt = Tm; a.Kt = Tn; a.tril = 1;
-        if (g.ksplit > 1) {
-            a.ksplit = g.ksplit; a.kpart = g.kpart_lq; a.kcnt = g.kcnt;
-            (void)hipMemsetAsync(g.kcnt, 0, sizeof(int) * g.nblk, sb);
-        }
         bgemm<NB>(sb, 0, 1, a, L);
     }
     // 6. Kbar = dE/dKuf = Li^T gA (side)
@@ -1070,10 +995,6 @@ static int svgp_grad_run(hipStream_t s, int n, int m, int L, int p, int d, const
         a.D = g.Gb; a.ldd = mpad; a.sD = mm;
         a.alpha = 1.0;
         a.Mt = Tm; a.Nt = Tm; a.Kt = Tn; a.tril = 1;
-        if (g.ksplit > 1) {
-            a.ksplit = g.ksplit; a.kpart = g.kpart_li; a.kcnt = g.kcnt + g.nblk;
-            (void)hipMemsetAsync(g.kcnt + g.nblk, 0, sizeof(int) * g.nblk, s);
-        }
         bgemm<NB>(s, 0, 1, a, L);
     }
     // 5. Sigma_bar = -Li^T Psi(Gb Li^T) Li
