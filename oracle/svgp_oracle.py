@@ -108,7 +108,12 @@ def mix_cov(g_cov, g_var, W, full_cov, full_output_cov):
 
 
 def elbo_t(X, Y, Z, kps, q_mu, q_sqrt, W, noise, num_data=None):
-    """GPflow SVGP.elbo (Gaussian likelihood, whiten=True). W=None -> SeparateIndependent."""
+    """GPflow SVGP.elbo (Gaussian likelihood, whiten=True). W=None -> SeparateIndependent.
+
+    noise must be an fp64 tensor: a torch.tensor(python_float) is fp32 and turns the constant
+    -0.5 log(2 pi) - 0.5 log(noise) into an fp32 scalar (1.6e-8 off a term, 1.2e-3 over Goku's N P)."""
+    if not (torch.is_tensor(noise) and noise.dtype == torch.float64):
+        raise TypeError("elbo_t: noise must be a float64 tensor")
     gm, gv = latent_moments(X, Z, kps, q_mu, q_sqrt)
     if W is not None:
         fm, fv = gm @ W.T, gv @ (W * W).T

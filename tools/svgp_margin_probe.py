@@ -79,16 +79,31 @@ def main():
                         lD=torch.tensor(t[2 + D:2 + 2 * D]), rho=torch.tensor(t[2 + 2 * D])))
     q_mu = torch.tensor(m.q_mu.numpy())
     q_sqrt = torch.tensor(m.q_sqrt.numpy())
-    noise = torch.tensor(float(m.likelihood.variance.numpy()))
+    noise = torch.tensor(float(m.likelihood.variance.numpy()), dtype=torch.float64)
+    noise32 = torch.tensor(float(m.likelihood.variance.numpy()))   # the old test helper's fp32 scalar
     Xt, Yt = torch.tensor(X), torch.tensor(Y)
     e_or, _, _ = S.elbo_t(Xt, Yt, Z, kps, q_mu, q_sqrt, None, noise)
     e_or = float(e_or)
     gm_o, gv_o = S.latent_moments(Xt, Z, kps, q_mu, q_sqrt)
     out, gmu_d, gvar_d, info = cap["res"]
+    e_o, kl_o, ve_o = [float(v) for v in S.elbo_t(Xt, Yt, Z, kps, q_mu, q_sqrt, None, noise)]
+    nz = float(noise)
+    ve_np = float((-0.5 * S.LOG2PI - 0.5 * np.log(nz) - 0.5 * ((Y - gmu_d.T) ** 2 + gvar_d.T) / nz).sum())
+    ve_onp = float((-0.5 * S.LOG2PI - 0.5 * np.log(nz) - 0.5 * ((Y - gm_o.numpy()) ** 2 + gv_o.numpy()) / nz).sum())
+    Lq = np.tril(q_sqrt.numpy())
+    kl_np = 0.5 * float((q_mu.numpy() ** 2).sum() - Mi * L + (Lq ** 2).sum()
+                        - np.log(np.diagonal(Lq, axis1=1, axis2=2) ** 2).sum())
+    parts = {"device": {"elbo": float(out[0]), "kl": float(out[1]), "ve": float(out[2])},
+             "oracle": {"elbo": e_o, "kl": kl_o, "ve": ve_o},
+             "numpy_from_device_moments": {"ve": ve_np}, "numpy_from_oracle_moments": {"ve": ve_onp},
+             "numpy_kl": kl_np, "noise": nz,
+             # what torch.tensor(python_float) (fp32) made of the oracle's per-term constant, times N P
+             "fp32_noise_constant_shift": float(Y.size * (float(-0.5 * S.LOG2PI - 0.5 * torch.log(noise32))
+                                                          - (-0.5 * S.LOG2PI - 0.5 * np.log(nz))))}
     rep = {"elbo_dev": e_dev, "elbo_oracle": e_or, "elbo_rel": abs(e_dev - e_or) / abs(e_or),
            "g_var_abs_max": float(np.abs(gvar_d.T - gv_o.numpy()).max()),
            "g_var_sum_err": float((gvar_d.T - gv_o.numpy()).sum()),
-           "g_mu_abs_max": float(np.abs(gmu_d.T - gm_o.numpy()).max())}
+           "g_mu_abs_max": float(np.abs(gmu_d.T - gm_o.numpy()).max()), "parts": parts}
     w = cap["wsd"]
     n = X.shape[0]
     lay, mpad, npad = layout(32, n, Mi, L)
