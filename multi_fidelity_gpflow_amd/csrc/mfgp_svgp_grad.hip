@@ -507,25 +507,27 @@ __global__ __launch_bounds__(NTHREADS) void k_gw(const double* r, const double* 
 // Workgroup: 32 a rows x KG_COLS b columns; wave w: rows 16 (w & 1) .., b half w >> 1; the b rows
 // go through LDS KG_CHUNK per half at a time, W is loaded one step ahead.
 constexpr int KG_ROWS = 32, KG_COLS = 256, KG_CHUNK = 32;
-// Registers held to three waves per SIMD (168 VGPRs, no spills; unbounded the allocator took 148
+// Registers held to three waves per SIMD for D <= 12 (168 VGPRs; unbounded the allocator took 148
 // VGPRs + AGPRs, two waves): 2.714 -> 2.672 ms a Goku SVGP step; four waves (10 spills) 2.675.
+// Wider rows (DC 16 / 32) get two / one waves per SIMD: held to three they spill 21 / 194 VGPRs.
 constexpr int KG_WAVES = 3;
 template <int DC>
 constexpr int kg_ncb() { return (2 * DC + 1 + 15) / 16; }
 
 template <int DC>
-__global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(KG_WAVES))) void k_kgrad(const double* P1, long ld1, int n1, const double* P2, long ld2,
+__global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(DC <= 12 ? KG_WAVES : (DC <= 16 ? 2 : 1)))) void k_kgrad(const double* P1, long ld1, int n1, const double* P2, long ld2,
                                                     int n2, const double* Wt, long ldw, long sW, const double* thetas,
                                                     int G, int D, double zf, int nbc, double* gth_part,
                                                     double* gz_part) {
     constexpr int NCB = kg_ncb<DC>(), SC = NCB * 16 + 1, XS = DC + 1, NS = DC / 4;
     static_assert(DC % 4 == 0, "dimension chunks of the distance MFMA");
-    constexpr int BS = NCB * 16 + 1;                                   // [1 | x | x^2] row stride
-    constexpr int SACC = (NTHREADS / 64) * 16 * SC, XST = 2 * KG_CHUNK * (XS + 2 + BS);
-    __shared__ double il[DC], id[DC], cz[DC];
+    constexpr int SACC = (NTHREADS / 64) * 16 * SC, XST = 2 * KG_CHUNK * (XS + 2);
+    __shared__ double il[DC], id[DC];
+    // the workgroup's 32 Z rows ([row][XS]: coordinates, the fidelity at DC), loaded once for the
+    // prologue and the epilogue; coordinates are centred on row 0 (cz = zsm[0][d])
+    __shared__ double zsm[KG_ROWS * XS];
     // the b rows of a chunk during the pair loop -- [half][row][XS] centred coordinates (column DC
-    // the fidelity), [half][row][2] their scaled squared norms, [half][row][BS] the B operand rows
-    // [1 | x | x^2] of the moment GEMM -- and the moment accumulators after it
+    // the fidelity), [half][row][2] their scaled squared norms -- and the moment accumulators after it
     __shared__ double lds_buf[SACC > XST ? SACC : XST];
     auto sacc = reinterpret_cast<double(*)[16][SC]>(lds_buf);
     __shared__ double wred[NTHREADS / 64][4];
@@ -537,20 +539,29 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(KG_WAV
     const int li = l & 15, lk = l >> 4;
     const MFTheta th{thetas + (long)lat * G, D};
     const double vL = th.vL(), vD = th.vD(), rho = th.rho();
+    for (int e = t; e < KG_ROWS * XS; e += NTHREADS) {
+        const int r = e / XS, d = e % XS, ag = at * KG_ROWS + r;
+        double v = (d == DC) ? -1.0 : 0.0;
+        if (ag < n1) {
+            if (d < D) v = P1[(long)ag * ld1 + d];
+            else if (d == DC) v = P1[(long)ag * ld1 + D];
+        }
+        zsm[e] = v;
+    }
     if (t < DC) {
         il[t] = (t < D) ? 1.0 / th.lL(t) : 0.0;
         id[t] = (t < D) ? 1.0 / th.lD(t) : 0.0;
-        cz[t] = (t < D) ? P1[(long)(at * KG_ROWS) * ld1 + t] : 0.0;
         dsum[0][t] = 0.0;
         dsum[1][t] = 0.0;
     }
     __syncthreads();
-    const int a = at * KG_ROWS + 16 * (w & 1) + li;
-    const double fa = (a < n1) ? P1[(long)a * ld1 + D] : -1.0;
+    const double* cz = zsm;   // row 0 (at * KG_ROWS < n1 always)
+    const int ar = 16 * (w & 1) + li, a = at * KG_ROWS + ar;
+    const double fa = zsm[ar * XS + DC];
     const bool La = (fa == 0.0), Ha = (fa == 1.0), aval = La || Ha;
     double za[DC];
 #pragma unroll
-    for (int d = 0; d < DC; ++d) za[d] = (aval && d < D) ? P1[(long)a * ld1 + d] - cz[d] : 0.0;
+    for (int d = 0; d < DC; ++d) za[d] = (aval && d < D) ? zsm[ar * XS + d] - cz[d] : 0.0;
     f64x4 accL[NCB], accD[NCB];
 #pragma unroll
     for (int c = 0; c < NCB; ++c) { accL[c] = f64x4{0.0, 0.0, 0.0, 0.0}; accD[c] = accL[c]; }
@@ -566,9 +577,13 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(KG_WAV
     // b = lq + 4 r)), which are exactly the A-operand positions of the moment GEMM's step r: the
     // VALU keeps one exp per pair (two for HF x HF pairs) and the weights.  (The direct-difference
     // loop spent ~157 VALU instructions per 64 pairs; k_kgrad was 12.9% of a Goku SVGP step.)
-    // b rows are staged KG_CHUNK per half at a time.  The pair weights of the next chunk are loaded
-    // (into registers) while this chunk's pairs are processed.
-    const int bhalf = bbase + (KG_COLS / 2) * half;
+    // b rows are staged one chunk of KG_CHUNK rows per half at a time: iteration i gives chunk 2 i + h
+    // of the workgroup's columns to half h, and the loop stops after the last chunk that holds a
+    // column (a workgroup over the last 44 of 300 columns runs one iteration, not four, and both
+    // halves share the columns of a ragged last block).  The next block's pair weights are loaded
+    // (into registers) while this block's pairs are processed.
+    const int nit = (bend - bbase + 2 * KG_CHUNK - 1) / (2 * KG_CHUNK);
+    auto bstart = [&](int i) { return bbase + (2 * i + half) * KG_CHUNK; };
     // the 4 weights (b = b0 + 4 r + lk) of a block: unconditional loads (W is padded), then the mask
     auto wload = [&](int b0, double* wv) {
 #pragma unroll
@@ -593,80 +608,78 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(KG_WAV
     }
     double* xsb = lds_buf;                                  // [2][KG_CHUNK][XS]
     double* nrm = xsb + 2 * KG_CHUNK * XS;                  // [2][KG_CHUNK][2]
-    double* bop = nrm + 2 * KG_CHUNK * 2;                   // [2][KG_CHUNK][BS]
-    double wc[4], wn[4];
-    wload(bhalf, wc);
-    for (int c0 = 0; c0 < KG_COLS / 2; c0 += KG_CHUNK) {
-        __syncthreads();   // the previous chunk is consumed
-        for (int e = t; e < 2 * KG_CHUNK * XS; e += NTHREADS) {
-            const int hf = e / (KG_CHUNK * XS), rem = e % (KG_CHUNK * XS);
-            const int r = rem / XS, d = rem % XS;
-            const int b = bbase + (KG_COLS / 2) * hf + c0 + r;
-            double v = (d == DC) ? -1.0 : 0.0;
-            if (b < bend) {
-                if (d < D) v = P2[(long)b * ld2 + d] - cz[d];
-                else if (d == DC) v = P2[(long)b * ld2 + D];
-            }
-            xsb[e] = v;
-        }
-        __syncthreads();
-        for (int e = t; e < 2 * KG_CHUNK * NCB * 16; e += NTHREADS) {
-            const int hr = e / (NCB * 16), j = e % (NCB * 16);   // hr = hf * KG_CHUNK + r
-            const int hf = hr / KG_CHUNK, r = hr % KG_CHUNK;
-            const int b = bbase + (KG_COLS / 2) * hf + c0 + r;
-            const double* xr = xsb + hr * XS;
-            double bv = 0.0;
-            if (j == 0) bv = (b < bend) ? 1.0 : 0.0;
-            else if (j <= D) bv = xr[j - 1];
-            else if (j <= 2 * D) {
-                const double x = xr[j - 1 - D];
-                bv = x * x;
-            }
-            bop[hr * BS + j] = bv;
-        }
-        if (t < 2 * KG_CHUNK) {   // wave 0: the scaled squared norms of the chunk's rows
-            const double* xr = xsb + t * XS;
-            double nl = 0.0, nd = 0.0;
+    // The moment GEMM's B operand [1 | x | x^2] of b row k, column j = 16 c + li of the lane, is
+    // formed from the staged row (j = 0: 1, whatever the row: its weights are 0 where it is not a
+    // pair; 1 <= j <= D: x_{j-1}; D < j <= 2D: x_{j-1-D}^2; above: 0).  (A staged [1 | x | x^2]
+    // copy cost a pass over the chunk and a barrier: 1.6 us of a 5 us chunk.)
+    int bkind[NCB], bdim[NCB];
 #pragma unroll
+    for (int c = 0; c < NCB; ++c) {
+        const int j = 16 * c + li;
+        bkind[c] = (j == 0) ? 0 : (j <= D ? 1 : (j <= 2 * D ? 2 : 3));
+        bdim[c] = (bkind[c] == 1) ? j - 1 : (bkind[c] == 2 ? j - 1 - D : 0);
+    }
+    auto bval = [&](const double* xrow, int c) {
+        const double v = xrow[bdim[c]];
+        return bkind[c] == 0 ? 1.0 : (bkind[c] == 1 ? v : (bkind[c] == 2 ? v * v : 0.0));
+    };
+    double wc[4], wn[4];
+    wload(bstart(0), wc);
+    for (int it = 0; it < nit; ++it) {
+        __syncthreads();   // the previous chunk is consumed
+        if (t < 2 * KG_CHUNK) {   // wave 0: the two chunks' 64 b rows (centred) and their scaled squared norms
+            const int hf = t / KG_CHUNK, r = t % KG_CHUNK;
+            const int b = bbase + (2 * it + hf) * KG_CHUNK + r;
+            double* xq = xsb + t * XS;
+            double nl = 0.0, nd = 0.0;
+#pragma unroll 4
             for (int d = 0; d < DC; ++d) {
-                const double u = xr[d] * il[d], v = xr[d] * id[d];
+                const double v = (b < bend && d < D) ? P2[(long)b * ld2 + d] - cz[d] : 0.0;
+                xq[d] = v;
+                const double u = v * il[d], q = v * id[d];
                 nl = fma(u, u, nl);
-                nd = fma(v, v, nd);
+                nd = fma(q, q, nd);
             }
+            xq[DC] = (b < bend) ? P2[(long)b * ld2 + D] : -1.0;
             nrm[t * 2] = nl;
             nrm[t * 2 + 1] = nd;
         }
         __syncthreads();
         const double* xs = xsb + half * KG_CHUNK * XS;
         const double* nr = nrm + half * KG_CHUNK * 2;
-        const double* bo = bop + half * KG_CHUNK * BS;
+        const int b0 = bstart(it);
 #pragma unroll
         for (int blk = 0; blk < KG_CHUNK / 16; ++blk) {
             const int rb = 16 * blk;
-            if (bhalf + c0 + rb >= bend) break;             // wave-uniform: past the last b row
-            wload(bhalf + c0 + rb + 16, wn);                 // the next block's weights, in flight meanwhile
+            if (b0 + rb >= bend) break;                      // wave-uniform: past the last b row
+            wload(rb + 16 < KG_CHUNK ? b0 + rb + 16 : bstart(it + 1), wn);   // the next block's weights, in flight meanwhile
             f64x4 dl = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int q = 0; q < NS; ++q)
                 dl = __builtin_amdgcn_mfma_f64_16x16x4f64(xs[(rb + li) * XS + 4 * q + lk] * il[4 * q + lk], zl[q], dl, 0, 0, 0);
             // step r: the lane's pair (a = li, b = rb + 4 r + lk); its weight is the A operand of
             // the moment GEMM's step r, B = [1 | x | x^2] of b
+            // the four pairs' exps as four interleaved chains (exp4: each polynomial step issued
+            // for all four before the next; one exp_lib chain at a time left the 13 dependent
+            // f64 FMAs of each exp exposed), then the accumulations in r order
+            double eL[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) eL[r] = -0.5 * fmax(na + nr[2 * (rb + lk + 4 * r)] - 2.0 * dl[r], 0.0);
+            exp4(eL);   // dk/dvL (TF form: finite where vL underflows); bitwise exp_lib for x <= 0
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int bl = rb + lk + 4 * r;
                 const double fb = xs[bl * XS + DC];
                 const bool Lb = (fb == 0.0), Hb = (fb == 1.0);
                 const double wv = (Lb || Hb) ? wc[r] : 0.0;
-                const double rL = fmax(na + nr[2 * bl] - 2.0 * dl[r], 0.0);
                 const double sb = Lb ? 1.0 : rho;
-                const double eL = exp_lib(-0.5 * rL);   // dk/dvL (TF form: finite where vL underflows)
-                const double kL = vL * eL;
+                const double kL = vL * eL[r];
                 const double wl = wv * sa * sb * kL;
-                gvL += wv * sa * sb * eL;
+                gvL += wv * sa * sb * eL[r];
                 grho += wv * ((Ha ? sb : 0.0) + (Hb ? sa : 0.0)) * kL;
 #pragma unroll
                 for (int c = 0; c < NCB; ++c)
-                    accL[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(wl, bo[(rb + 4 * r + lk) * BS + 16 * c + li], accL[c], 0, 0, 0);
+                    accL[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(wl, bval(xs + bl * XS, c), accL[c], 0, 0, 0);
                 __builtin_amdgcn_sched_barrier(0);
             }
 #pragma unroll
@@ -677,13 +690,13 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(KG_WAV
 #pragma unroll
         for (int blk = 0; blk < KG_CHUNK / 16; ++blk) {
             const int rb = 16 * blk;
-            if (bhalf + c0 + rb >= bend) break;
+            if (b0 + rb >= bend) break;
             bool hany = false;
 #pragma unroll
             for (int r = 0; r < 4; ++r) hany |= Ha && xs[(rb + lk + 4 * r) * XS + DC] == 1.0;
             if (__ballot(hany) == 0) continue;   // wave-uniform
             double wh[4];
-            wload(bhalf + c0 + rb, wh);
+            wload(b0 + rb, wh);
             f64x4 dd = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int q = 0; q < NS; ++q)
@@ -697,7 +710,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(KG_WAV
                 gvD += we;
 #pragma unroll
                 for (int c = 0; c < NCB; ++c)
-                    accD[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(we * vD, bo[(rb + 4 * r + lk) * BS + 16 * c + li], accD[c], 0, 0, 0);
+                    accD[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(we * vD, bval(xs + bl * XS, c), accD[c], 0, 0, 0);
             }
         }
     }
@@ -728,7 +741,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(KG_WAV
                 const int ag = at * KG_ROWS + r;
                 auto S = [&](int col) { return sacc[hw][rr][col] + sacc[2 + hw][rr][col]; };
                 const double s0 = S(0), s1 = S(1 + d), s2 = S(1 + D + d);
-                const double z = (ag < n1) ? P1[(long)ag * ld1 + d] - cz[d] : 0.0;
+                const double z = (ag < n1) ? zsm[r * XS + d] - cz[d] : 0.0;
                 const double ic = ph ? id[d] : il[d];
                 const double ic2 = ic * ic;
                 term = (z * z * s0 - 2.0 * z * s1 + s2) * ic2 * ic;   // d k / d l = k (za - xb)^2 / l^3
