@@ -595,6 +595,8 @@ def hbs_leg(steps=200, warmup=20):
                      "achieved": round(fl / (us * 1e-6) / 1e12, 6),
                      "frac": round(fl / (us * 1e-6) / 1e12 / FP64_PEAK_TFLOPS, 8),
                      "flop_source": "SURVEY §8(d) value+grad unit (step_flops)"})
+        # the live figures are the same measurement here (no rocprofv3 average for this kernel)
+        roof["achieved_live"], roof["frac_live"] = roof["achieved"], roof["frac"]
     return {
         "config": {"workload": "hbs_multibin_adam_step", "n_lf": int((X[:, -1] == 0).sum()),
                    "n_hf": int((X[:, -1] == 1).sum()), "d": d, "p": P},
