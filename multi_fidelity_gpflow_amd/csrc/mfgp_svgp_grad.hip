@@ -98,8 +98,9 @@ size_t bgemm_smem(int nb) { return 2 * sizeof(double) * (size_t)nb * (nb + 2); }
 // (k_bgemm: one 16 x 16 chain per wave), and each k-tile's two A tiles and two B tiles are staged
 // in LDS once for all four waves (twice k_bgemm's operand reuse), one buffer, the next k-tile's
 // global loads issued into registers before the current products.  Every 16 x 16 block
-// runs the same MFMA sequence as tile_mma<32> (k-tiles ascending, 4-deep steps ascending, alpha
-// on the A operand), so the results are bitwise k_bgemm's.  Edge blocks (odd Mt / Nt) load a
+// runs the same MFMA sequence as tile_mma<32> (k-tiles ascending, 4-deep steps ascending; alpha, a
+// power of two, on the accumulated tile instead of the A operand: the same bits), so the results
+// are bitwise k_bgemm's.  Edge blocks (odd Mt / Nt) load a
 // clamped in-range tile for the missing half and store nothing from it.
 constexpr int BG2_E = 32 * 34;   // one 32-tile in LDS (TileCfg<32>)
 size_t bgemm2_smem() { return 4 * sizeof(double) * (size_t)BG2_E; }
@@ -188,7 +189,7 @@ __global__ __launch_bounds__(NTHREADS) void k_bgemm2(BgemmArgs a) {
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
                 const int i = 16 * t + li, j = 16 * t + li;
-                av[t] = a.alpha * (TA ? As[k * S + i] : As[i * S + k]);
+                av[t] = TA ? As[k * S + i] : As[i * S + k];
                 bv[t] = TB ? Bs[j * S + k] : Bs[k * S + j];
             }
 #pragma unroll
@@ -213,6 +214,15 @@ __global__ __launch_bounds__(NTHREADS) void k_bgemm2(BgemmArgs a) {
         }
     }
     if (!live) return;
+    // alpha on the accumulated tile, not on every A operand (a VALU multiply feeding each MFMA):
+    // every caller's alpha is a power of two (1, -1, 2), so the scaled sums are bit for bit those
+    // of scaled operands
+    if (a.alpha != 1.0) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) acc[p][q] *= a.alpha;
+    }
     double* Dt = a.D + b * a.sD;
     if (a.sym) {   // tiles ti >= tj only (tril): v (Psi: 0.5 v) at (i, j) and (j, i)
         if (tj > ti) return;
