@@ -92,26 +92,42 @@ void svgp_forward_buffers(int nb, int n, int m, int l, int p, int d, void* ws, d
 }
 
 // Zeros in the strictly-upper tiles of L^{-1} (the step sequence writes only tiles (i, c <= i)):
-// the matvecs and the E = Lq C - Li input read whole rows of it
+// the matvecs and the E = Lq C - Li input read whole rows of it.  One workgroup per 8 rows, 16-B
+// stores of each row's part right of its tile (a thread per element with a division by mpad took
+// 23 us for 64 latents, beside the K_uu chain on the critical path).
+constexpr int ZU_ROWS = 8;
 __global__ void k_zero_upper_tiles(double* Xo, int nb, int mpad, long mm) {
     const int l = blockIdx.z;
-    for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < mm; e += (long)gridDim.x * blockDim.x) {
-        const int r = (int)(e / mpad), c = (int)(e % mpad);
-        if (r / nb < c / nb) Xo[l * mm + e] = 0.0;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int rr = w; rr < ZU_ROWS; rr += blockDim.x >> 6) {   // a wave per row
+        const int r = blockIdx.x * ZU_ROWS + rr;
+        if (r >= mpad) break;
+        const int c0 = (r / nb + 1) * nb;                      // first column right of the tile (even)
+        double* row = Xo + l * mm + (long)r * mpad;
+        for (int c = c0 + 2 * lane; c < mpad; c += 128)
+            *reinterpret_cast<f64x2*>(row + c) = f64x2{0.0, 0.0};
     }
 }
 
 // tril(q_sqrt_l) into a zero-padded Mpad x Mpad buffer (packed: q_sqrt_l as its lower triangle,
-// (r, c <= r) at r (r + 1) / 2 + c)
+// (r, c <= r) at r (r + 1) / 2 + c).  A wave per row: its packed segment read in order, the row
+// written in order (16-B stores; the per-element form with two divisions took 33 us for 64 latents)
 __global__ void k_lq_pad(const double* q_sqrt, int m, int mpad, double* Lq, int packed) {
     const int l = blockIdx.z;
     const long tot = (long)mpad * mpad, tri = (long)m * (m + 1) / 2;
-    for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < tot; e += (long)gridDim.x * blockDim.x) {
-        const int r = (int)(e / mpad), c = (int)(e % mpad);
-        double v = 0.0;
-        if (r < m && c <= r)
-            v = packed ? q_sqrt[l * tri + (long)r * (r + 1) / 2 + c] : q_sqrt[(long)l * m * m + (long)r * m + c];
-        Lq[l * tot + e] = v;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int rr = w; rr < ZU_ROWS; rr += blockDim.x >> 6) {
+        const int r = blockIdx.x * ZU_ROWS + rr;
+        if (r >= mpad) break;
+        const double* src = (r < m) ? (packed ? q_sqrt + l * tri + (long)r * (r + 1) / 2 : q_sqrt + (long)l * m * m + (long)r * m)
+                                    : nullptr;
+        double* row = Lq + l * tot + (long)r * mpad;
+        for (int c = 2 * lane; c < mpad; c += 128) {
+            f64x2 v = {0.0, 0.0};
+            if (src && c <= r) v.x = src[c];
+            if (src && c + 1 <= r) v.y = src[c + 1];
+            *reinterpret_cast<f64x2*>(row + c) = v;
+        }
     }
 }
 
@@ -526,7 +542,6 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
     // and the K_uf Gram, tril(q_sqrt), the zeros above Li's tiles (the step sequence never writes
     // there) and the KL on the caller's beside it.  (Forked before the first factor, the K_uf
     // Gram's 24k workgroups held the CUs: the 64 one-workgroup factors took 64 us instead of ~5.)
-    const int blocks = (int)std::min<long>((mm + 255) / 256, 2048);
     hipStream_t sk;
     {
         GramArgs g{};
@@ -549,7 +564,7 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
         c.T = S.Tm; c.Tp = 0; c.k = 0;
         launch_chol_steps<NB>(c, L, sk);
     }
-    hipLaunchKernelGGL(k_zero_upper_tiles, dim3(blocks, 1, L), dim3(256), 0, s, S.Xo, NB, S.mpad, mm);
+    hipLaunchKernelGGL(k_zero_upper_tiles, dim3(cdiv(S.mpad, ZU_ROWS), 1, L), dim3(256), 0, s, S.Xo, NB, S.mpad, mm);
     // Kuf_l = K_l(Z, X), zero padded to Mpad x Npad
     {
         GramArgs g{};
@@ -561,7 +576,7 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
         launch_gram_dense(g, L, S.mpad, S.npad, s);   // zero padding written by the kernel
     }
     const int qp = t_side.qs_packed;
-    hipLaunchKernelGGL(k_lq_pad, dim3(blocks, 1, L), dim3(256), 0, s, q_sqrt, m, S.mpad, S.Lq, qp);
+    hipLaunchKernelGGL(k_lq_pad, dim3(cdiv(S.mpad, ZU_ROWS), 1, L), dim3(256), 0, s, q_sqrt, m, S.mpad, S.Lq, qp);
     if (!f_mu) hipLaunchKernelGGL(k_svgp_kl, dim3(KL_SLICES, L), dim3(NTHREADS), 0, s, q_mu, q_sqrt, m, L, S.kl_part, qp);
     svgp_join(s);
     if (!two_gemm)   // C = Lq^T Li (the fused conditional's B = C Kuf), after Lq and Li
