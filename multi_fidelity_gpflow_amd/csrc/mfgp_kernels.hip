@@ -876,6 +876,87 @@ __global__ __launch_bounds__(NTHREADS) void k_chol_update(CholArgs a) {
     acc_store(acc, Ric, a.ldr);
 }
 
+// Batched step k with the panel folded in (NB = 32, batch > 1, k < T - 1): each task forms the
+// panel tiles it needs itself -- L_ik = A_ik D_k^T (and L_jk, or X_kc = D_k R_kc) -- from the
+// unscaled tiles, then does its update, with the same tile products in the same order as the
+// k_chol_panel + k_chol_update pair (bitwise the same results).  The tasks of row k + 1 store
+// X_kc (row k of L^{-1}) for the step after; L_ik itself is not stored (nothing reads the factor's
+// off-diagonal tiles after step k).  Saves the panel launch and its hand-off through memory on
+// the K_uu chain of the SVGP forward (10 steps at Goku).
+template <int NB>
+__global__ __launch_bounds__(NTHREADS) void k_chol_fused(CholArgs a) {
+    constexpr int E = TileCfg<NB>::ELEMS;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    double* Ds = smem;           // D_k
+    double* T0 = Ds + E;         // A_ik, later factor scratch
+    double* T1 = T0 + E;         // A_jk or R_kc
+    double* Pi = T1 + E;         // L_ik
+    double* Pj = Pi + E;         // L_jk or X_kc, later D_{k+1}
+    double* dg = Pj + E;
+    int& bad = *reinterpret_cast<int*>(dg + NB);
+    const int k = a.k, T = a.T, Tp = a.Tp;
+    const int rem = T - k - 1, nA = rem * (rem + 1) / 2, ncol = k + 1 + Tp;
+    int t, b;
+    chol_update_order(gridDim.x, t, b);
+    double* A = a.A + b * a.sA;
+    auto At = [&](int i, int j) { return A + (long)i * NB * a.lda + (long)j * NB; };
+    tile_load<NB>(Ds, a.Dd + b * a.sD + (long)k * NB * NB, NB);
+    Acc<NB> acc, lp;
+    if (t < nA) {    // A_ij -= L_ik L_jk^T
+        int ii, jj;
+        tri_decode(t, ii, jj);
+        const int i = k + 1 + ii, j = k + 1 + jj;
+        tile_load<NB>(T0, At(i, k), a.lda);
+        if (j != i) tile_load<NB>(T1, At(j, k), a.lda);
+        acc_load(acc, At(i, j), a.lda);
+        __syncthreads();
+        acc_zero(lp);
+        tile_mma<NB, false, true>(lp, T0, Ds, 1.0);
+        acc_to_lds(lp, Pi);
+        if (j != i) {
+            acc_zero(lp);
+            tile_mma<NB, false, true>(lp, T1, Ds, 1.0);
+            acc_to_lds(lp, Pj);
+        }
+        __syncthreads();
+        tile_mma<NB, false, true>(acc, Pi, j != i ? Pj : Pi, -1.0);
+        if (i == j && i == k + 1) {
+            __syncthreads();   // T0 / Pj are reused below
+            if constexpr (NB == 32) {
+                tile_potrf_inv_w1_acc(acc.v[0], T0, Pj, dg, &bad);
+            } else {
+                acc_to_lds(acc, T0);
+                __syncthreads();
+                tile_potrf_inv<NB>(T0, Pj, dg, &bad);
+            }
+            tile_store<NB>(a.Dd + b * a.sD + (long)(k + 1) * NB * NB, NB, Pj);
+            for (int r = threadIdx.x; r < NB; r += NTHREADS) a.ldiag[b * a.sL + (k + 1) * NB + r] = dg[r];
+            if (threadIdx.x == 0 && bad && a.info[b] == 0) a.info[b] = (k + 1) * NB + bad;
+        } else {
+            acc_store(acc, At(i, j), a.lda);
+        }
+        return;
+    }
+    t -= nA;         // R_ic -= L_ik X_kc
+    const int i = k + 1 + t / ncol, cc = t % ncol;
+    const int c = (cc <= k) ? cc : T + (cc - k - 1);
+    double* Ric = a.R + b * a.sR + (long)i * NB * a.ldr + (long)c * NB;
+    tile_load<NB>(T0, At(i, k), a.lda);
+    tile_load<NB>(T1, a.R + b * a.sR + (long)k * NB * a.ldr + (long)c * NB, a.ldr);
+    acc_load(acc, Ric, a.ldr);
+    __syncthreads();
+    acc_zero(lp);
+    tile_mma<NB, false, true>(lp, T0, Ds, 1.0);
+    acc_to_lds(lp, Pi);
+    acc_zero(lp);
+    tile_mma<NB, false, false>(lp, Ds, T1, 1.0);
+    acc_to_lds(lp, Pj);
+    if (i == k + 1) acc_store(lp, a.Xo + b * a.sX + (long)k * NB * a.ldx + (long)c * NB, a.ldx);
+    __syncthreads();
+    tile_mma<NB, false, false>(acc, Pi, Pj, -1.0);
+    acc_store(acc, Ric, a.ldr);
+}
+
 int chol_step_blocks(int T, int Tp, int k, bool alpha) {
     const int rem = T - k - 1;
     return rem * (rem + 1) / 2 + rem * (k + 1 + Tp) + (alpha ? (k + 1) * Tp : 0) + ((k == T - 1) ? (T + Tp) : 0);
@@ -1628,6 +1709,27 @@ void launch_first_factor(const double* A, long lda, long sA, double* Dd, long sD
 }
 template <int NB>
 void launch_chol_steps(CholArgs c, int batch, hipStream_t s) {
+    if constexpr (NB == 32) if (batch != 1) {   // one fused launch a step (k_chol_fused), the last row by a panel
+        c.alpha = nullptr;
+        static bool attr = false;
+        const size_t lds = sizeof(double) * (5 * (size_t)TileCfg<NB>::ELEMS + NB + 2);
+        if (!attr) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_chol_fused<NB>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            attr = true;
+        }
+        for (int k = 0; k < c.T; ++k) {
+            c.k = k;
+            const int rem = c.T - k - 1, ncol = k + 1 + c.Tp;
+            if (rem > 0)
+                hipLaunchKernelGGL(k_chol_fused<NB>, dim3(rem * (rem + 1) / 2 + rem * ncol, 1, batch), dim3(NTHREADS),
+                                   lds, s, c);
+            else   // the last step: X_{T-1, c} only
+                hipLaunchKernelGGL(k_chol_panel<NB>, dim3(ncol, 1, batch), dim3(NTHREADS),
+                                   2 * sizeof(double) * TileCfg<NB>::ELEMS, s, c);
+        }
+        return;
+    }
     if (batch != 1) {   // panel + update launches a step (k_chol_panel); no fused alpha
         c.alpha = nullptr;
         for (int k = 0; k < c.T; ++k) {
