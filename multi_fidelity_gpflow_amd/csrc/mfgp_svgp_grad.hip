@@ -1226,13 +1226,16 @@ __global__ void k_adam_packed(int n, double* u, double* c, const double* g, doub
     // the step size (two pow)
     __shared__ double s_alpha;
     __shared__ int s_ok;
-    if (threadIdx.x == 0) {
-        int ok = 1;
-        for (int i = 0; i < ninfo; ++i) ok &= info[i] == 0;
-        const int s = *step;
-        const double t = (double)(s + 1);
-        s_alpha = lr_sched[s] * sqrt(1.0 - pow(b2, t)) / (1.0 - pow(b1, t));
-        s_ok = ok;
+    if (threadIdx.x < 64) {   // wave 0: the info words a lane each (one round trip, not ninfo)
+        int bad = 0;
+        for (int i = threadIdx.x; i < ninfo; i += 64) bad |= info[i] != 0;
+        const bool ok = __ballot(bad) == 0;
+        if (threadIdx.x == 0) {
+            const int s = *step;
+            const double t = (double)(s + 1);
+            s_alpha = lr_sched[s] * sqrt(1.0 - pow(b2, t)) / (1.0 - pow(b1, t));
+            s_ok = ok ? 1 : 0;
+        }
     }
     __syncthreads();
     if (!s_ok) return;
