@@ -83,6 +83,10 @@ struct CholArgs {
     double* ldiag; long sL;              // diag(L)
     int* info;
     int T, Tp, k;
+    // Batched steps (k_chol_fused / k_chol_panel): R = [I | ...] is implicit -- the identity tile
+    // R_kk and the untouched strictly-lower tiles (zero until the step c == k that first updates
+    // R_ic) are formed in the kernels, so R needs no initialisation (the Gram skips writing it)
+    int r_implicit;
     // Optional (batch 1, LML path): alpha = L^{-T} Z accumulated row by row as rows of
     // [L^{-1} | Z] become final, and the sum Z^2 partials.  nullptr: skipped.
     double* alpha; long ldal;            // Npad x Ppad

@@ -779,6 +779,16 @@ __global__ __launch_bounds__(NTHREADS) void k_chol_step(CholArgs a) {
 // stored to Xo) once, and the update launch does one product per tile (the trailing task of
 // tile (k+1, k+1) then factors it).  The same products in the same order: bitwise k_chol_step's
 // results.  (Goku SVGP, 64 latents x 10 tiles: 9 x 20.5 us of steps.)
+// LDS tile <- the NB x NB identity (CholArgs::r_implicit: the RHS's R_kk)
+template <int NB>
+__device__ __forceinline__ void tile_identity(double* __restrict__ s) {
+    constexpr int S = TileCfg<NB>::S;
+    for (int p = threadIdx.x; p < NB * NB; p += NTHREADS) {
+        const int r = p / NB, c = p % NB;
+        s[r * S + c] = (r == c) ? 1.0 : 0.0;
+    }
+}
+
 template <int NB>
 __global__ __launch_bounds__(NTHREADS) void k_chol_panel(CholArgs a) {
     constexpr int E = TileCfg<NB>::ELEMS;
@@ -801,7 +811,8 @@ __global__ __launch_bounds__(NTHREADS) void k_chol_panel(CholArgs a) {
     }
     t -= rem;        // X_kc = D_k R_kc, c = 0..k, then the Y tiles
     const int c = (t <= k) ? t : T + (t - k - 1);
-    tile_load<NB>(T0, a.R + b * a.sR + (long)k * NB * a.ldr + (long)c * NB, a.ldr);
+    if (a.r_implicit && c == k) tile_identity<NB>(T0);
+    else tile_load<NB>(T0, a.R + b * a.sR + (long)k * NB * a.ldr + (long)c * NB, a.ldr);
     __syncthreads();
     tile_mma<NB, false, false>(acc, Ds, T0, 1.0);
     acc_store(acc, a.Xo + b * a.sX + (long)k * NB * a.ldx + (long)c * NB, a.ldx);
@@ -942,8 +953,14 @@ __global__ __launch_bounds__(NTHREADS) void k_chol_fused(CholArgs a) {
     const int c = (cc <= k) ? cc : T + (cc - k - 1);
     double* Ric = a.R + b * a.sR + (long)i * NB * a.ldr + (long)c * NB;
     tile_load<NB>(T0, At(i, k), a.lda);
-    tile_load<NB>(T1, a.R + b * a.sR + (long)k * NB * a.ldr + (long)c * NB, a.ldr);
-    acc_load(acc, Ric, a.ldr);
+    const bool first = a.r_implicit && c == k;   // R_kk = I; R_ic (i > k) untouched until now: 0
+    if (first) {
+        tile_identity<NB>(T1);
+        acc_zero(acc);
+    } else {
+        tile_load<NB>(T1, a.R + b * a.sR + (long)k * NB * a.ldr + (long)c * NB, a.ldr);
+        acc_load(acc, Ric, a.ldr);
+    }
     __syncthreads();
     acc_zero(lp);
     tile_mma<NB, false, true>(lp, T0, Ds, 1.0);

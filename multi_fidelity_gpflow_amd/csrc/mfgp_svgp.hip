@@ -550,7 +550,9 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
         g.theta = thetas; g.stheta = S.G; g.D = d; g.rbf_only = 0;
         g.out = S.Kuu; g.ldo = S.mpad; g.so = mm;
         g.padded = 1; g.npad = S.mpad; g.tiles_c = S.Tm; g.add_noise = 0; g.diag_add = jitter;
-        g.R = S.R; g.ldr = S.mpad; g.sR = mm;
+        // NB = 32: R = I stays implicit in the batched steps (CholArgs::r_implicit); the Gram
+        // wrote 52 MB of identity at Goku on the chain's critical path
+        g.R = NB == 32 ? nullptr : S.R; g.ldr = S.mpad; g.sR = mm;
         // the dense-layout Gram (64 x 64 entries a workgroup, both triangles): the lean tile
         // launch took 56-66 us for 64 latents of 300 x 300 on the chain's critical path
         launch_gram_dense(g, L, S.mpad, S.mpad, s);
@@ -562,6 +564,7 @@ static int svgp_run(hipStream_t s, int n, int m, int L, int p, int d, const doub
         c.Xo = S.Xo; c.ldx = S.mpad; c.sX = mm;
         c.Dd = S.Dd; c.sD = (long)S.Tm * NB * NB; c.ldiag = S.ldiag; c.sL = S.mpad; c.info = info;
         c.T = S.Tm; c.Tp = 0; c.k = 0;
+        c.r_implicit = NB == 32 ? 1 : 0;   // k_chol_fused (NB = 32) forms R's identity and zeros itself
         launch_chol_steps<NB>(c, L, sk);
     }
     hipLaunchKernelGGL(k_zero_upper_tiles, dim3(cdiv(S.mpad, ZU_ROWS), 1, L), dim3(256), 0, s, S.Xo, NB, S.mpad, mm);
