@@ -720,7 +720,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-train-predict", action="store_true")
     ap.add_argument("--no-latent", action="store_true",
-                    help="--config goku_svgp: time the single-bin model only (the PMC passes of tools/profile_all.sh)")
+                    help="--config goku_svgp: time the single-bin model only (the PMC passes of tools/gpu_run.sh profile:goku_svgp)")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the hbs / synth / goku_svgp sub-objects of the default (Goku, N=1) line")
     ap.add_argument("--mode", choices=["shard", "shared"], default="shard",

@@ -1,6 +1,6 @@
 """Build A/B variants of libmfgp.so in parallel (CPU, in this container):
     python tools/build_variants.py name=-DFLAG[,-DFLAG2] ...
--> multi_fidelity_gpflow_amd/variants/libmfgp_<name>.so (tools/ab_bench.sh runs them)."""
+-> multi_fidelity_gpflow_amd/variants/libmfgp_<name>.so (tools/ab.sh runs them)."""
 import concurrent.futures as cf
 import os
 import sys

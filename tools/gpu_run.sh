@@ -9,6 +9,10 @@
 #   dist2:CFG        two gloo ranks sharing the GPU, bench.py --gpus 2 --config CFG
 #   profile:CFG      tools/profile_round.sh (trace + PMC passes)  -> OUTDIR/CFG/
 #   py:SCRIPT[,ARGS] python SCRIPT ARGS                           -> OUTDIR/py_N.log
+#   rccl             one rank, world-size-1 nccl group, shared-theta line -> OUTDIR/rccl_ws1_shared.json
+#   svgptrace        kernel trace of 30 single-bin SVGP iterations  -> OUTDIR/svgp_single_trace/
+#   cpuproto         the CPU baseline's full 1000-step protocol    -> OUTDIR/cpu_protocol.json
+# (A/B runs: tools/ab.sh.)
 set -o pipefail
 export TMPDIR=/tmp
 O=${1:?usage: gpu_run.sh OUTDIR STEP...}
@@ -49,6 +53,19 @@ for step in "$@"; do
                 "--steps 50 --warmup 20 --no-train-predict --no-cpu-baseline" ;;
         *) echo "unknown profile config $arg"; false ;;
       esac; rc=$? ;;
+    rccl)
+      MFGP_DIST_WS1=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+        --master-addr 127.0.0.1 --master-port 29555 bench.py --mode shared --no-extras --no-cpu-baseline \
+        --no-train-predict --steps 300 > "$O/rccl_ws1_shared.out" 2> "$O/rccl_ws1_shared.err"; rc=$?
+      [ $rc -eq 0 ] && { grep '^{' "$O/rccl_ws1_shared.out" > "$O/rccl_ws1_shared.json"; rc=$?; }
+      head -c 700 "$O/rccl_ws1_shared.json"; echo ;;
+    svgptrace)
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/svgp_single_trace" -o run -- \
+        python3 tools/bench_svgp.py --which single --iters 30 > "$O/svgp_single.json" 2> "$O/svgp_single.err"; rc=$?
+      cat "$O/svgp_single.json" ;;
+    cpuproto)
+      timeout -k 10 300 python tools/cpu_protocol.py "$O/cpu_protocol.json" > "$O/cpu_protocol.log" 2>&1; rc=$?
+      cat "$O/cpu_protocol.json" ;;
     py)
       timeout -k 10 600 python -u $arg > "$O/py_$i.log" 2>&1; rc=$?; tail -30 "$O/py_$i.log" ;;
     *)
