@@ -514,9 +514,12 @@ __global__ __launch_bounds__(NTHREADS) void k_gw(const double* r, const double* 
 // wd = Wt kD (HF x HF pairs, only when the wave holds one).  Coordinates are taken relative to
 // the block's first Z row, which keeps the expansion's cancellation at the data's spread.
 // The per-pair work left on the VALU is r^2 and one exp (two for HF x HF pairs).
-// Workgroup: 32 a rows x KG_COLS b columns; wave w: rows 16 (w & 1) .., b half w >> 1; the b rows
+// Workgroup: 32 a rows x cpb <= KG_COLS b columns; wave w: rows 16 (w & 1) .., b half w >> 1; the b rows
 // go through LDS KG_CHUNK per half at a time, W is loaded one step ahead.
 constexpr int KG_ROWS = 32, KG_COLS = 256, KG_CHUNK = 32;
+#ifndef MFGP_KG_EQUAL
+#define MFGP_KG_EQUAL 1
+#endif
 // Registers held to three waves per SIMD for D <= 12 (168 VGPRs; unbounded the allocator took 148
 // VGPRs + AGPRs, two waves): 2.714 -> 2.672 ms a Goku SVGP step; four waves (10 spills) 2.675.
 // Wider rows (DC 16 / 32) get two / one waves per SIMD: held to three they spill 21 / 194 VGPRs.
@@ -527,7 +530,7 @@ constexpr int kg_ncb() { return (2 * DC + 1 + 15) / 16; }
 template <int DC>
 __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(DC <= 12 ? KG_WAVES : (DC <= 16 ? 2 : 1)))) void k_kgrad(const double* P1, long ld1, int n1, const double* P2, long ld2,
                                                     int n2, const double* Wt, long ldw, long sW, const double* thetas,
-                                                    int G, int D, double zf, int nbc, double* gth_part,
+                                                    int G, int D, double zf, int nbc, int cpb, double* gth_part,
                                                     double* gz_part) {
     constexpr int NCB = kg_ncb<DC>(), SC = NCB * 16 + 1, XS = DC + 1, NS = DC / 4;
     static_assert(DC % 4 == 0, "dimension chunks of the distance MFMA");
@@ -578,8 +581,8 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(DC <= 
     double gvL = 0.0, gvD = 0.0, grho = 0.0;
     const double sa = La ? 1.0 : rho;
     const int half = w >> 1;
-    const int bbase = bc * KG_COLS;
-    const int bend = min(n2, bbase + KG_COLS);
+    const int bbase = bc * cpb;
+    const int bend = min(n2, bbase + cpb);
     const double* wrow = Wt + lat * sW + (long)a * ldw;
     // Pairs in 16 x 16 blocks (16 a rows of the wave x 16 b rows of its half): the distances
     // |za - xb|^2 / l^2 = |za/l|^2 + |xb/l|^2 - 2 (za/l).(xb/l) with the dot products on the matrix
@@ -930,8 +933,11 @@ template <int DC>
 static void launch_kgrad(hipStream_t s, const double* P1, long ld1, int n1, const double* P2, long ld2, int n2,
                          const double* Wt, long ldw, long sW, const double* thetas, int G, int D, double zf, int nat,
                          int nbc, int L, double* gth, double* gz) {
+    // the nbc = ceil(n2 / KG_COLS) column blocks of a row tile cut EQUAL (to a multiple of KG_CHUNK):
+    // K_uu's 300 columns as 160 + 140, not 256 + 44 (the long blocks set the (Z, Z) sums' length)
+    const int cpb = std::min(KG_COLS, cdv(cdv(n2, nbc), KG_CHUNK) * KG_CHUNK);
     hipLaunchKernelGGL(k_kgrad<DC>, dim3(nat * nbc, 1, L), dim3(NTHREADS), 0, s, P1, ld1, n1, P2, ld2, n2, Wt, ldw,
-                       sW, thetas, G, D, zf, nbc, gth, gz);
+                       sW, thetas, G, D, zf, nbc, MFGP_KG_EQUAL ? cpb : KG_COLS, gth, gz);
 }
 
 template <int NB>
