@@ -111,8 +111,16 @@ __global__ __launch_bounds__(NTHREADS) void k_bgemm2(BgemmArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     int bx, b;
     xcd_swizzle(bx, b);
-    const int Nb = (a.Nt + 1) >> 1;
-    const int bi = bx / Nb, bj = bx % Nb;
+    const int Nb = (a.Nt + 1) >> 1, Mb = (a.Mt + 1) >> 1;
+    // longest blocks first (placement only): a lower-masked A (k < ti + 1) or upper-masked B
+    // (k < tj + 1) gives the last row / column blocks the longest k-ranges, so those are dealt first
+    // and the launch does not end on them
+#ifndef MFGP_BG2_LPT
+#define MFGP_BG2_LPT 1
+#endif
+    int bi = bx / Nb, bj = bx % Nb;
+    if (MFGP_BG2_LPT && a.amask == 1) bi = Mb - 1 - bi;
+    if (MFGP_BG2_LPT && a.bmask == 2) bj = Nb - 1 - bj;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
     const int ti = 2 * bi + (w >> 1), tj = 2 * bj + (w & 1);   // this wave's output tile
     const bool live = ti < a.Mt && tj < a.Nt;
